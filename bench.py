@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Throughput bench: LiDAR frames/s of the fused ground-removal + cone-detection HIP path.
+
+Workload (BASELINE.json configs[2], and configs[3]'s per-GPU share at 8 GPUs): a batch of
+256 synthetic cone-field frames x 65,536 points (64 rings x 1024 columns, xyzi float32,
+point_step 16) resident in HBM, simulation params. One step = one cg_run_batch over the
+batch. Frames are independent units: each rank processes its own batch (weak scaling, no
+data-path collective); the timed region is bracketed by barrier + synchronize and the max
+over ranks is reported.
+
+The roofline object prices the dominant (only) kernel, cg_frame_kernel, by its algorithmic
+bytes B = 16 N + 20 V + 8 C + 64 per frame over its average duration from
+HIP events recorded on the launch stream. cpu_baseline times the CPU restatement
+(oracle/, single core, same frames) on a bounded sample on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--rings", type=int, default=64)
+    ap.add_argument("--cols", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--single-frame", action="store_true", help="also time C2 single-frame latency")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import cones_perception_amd as cp
+    params = cp.load_params("simulation")
+    F, N = args.frames, args.rings * args.cols
+    # each rank owns frames [rank*F, (rank+1)*F): distinct synthetic scenes per rank
+    raw = cp.synth_frames(F, first_frame=rank * F, rings=args.rings, cols=args.cols,
+                          threads=min(16, os.cpu_count() or 1))
+    d_in = torch.from_numpy(raw).to(dev)
+    eng = cp.BatchEngine(params, device=local)
+    # a dedicated stream: the default stream's handle is 0, which the C-ABI reads as "use the
+    # handle's own stream"; events and kernel must share one stream
+    stream = torch.cuda.Stream(dev)
+    sh = stream.cuda_stream
+    assert sh != 0
+
+    def step():
+        eng.run(d_in.data_ptr(), F, N, 16, stream=sh)
+
+    torch.cuda.synchronize(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        evs[s][0].record(stream)
+        step()
+        evs[s][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    avg_kernel_ms = sum(kern_ms) / len(kern_ms)
+
+    # algorithmic bytes of one launch, from the frames' own V and C
+    res = eng.results()
+    hdr_np = fetch_headers(res, F)
+    V = hdr_np[:, 3].astype(np.float64)
+    Cn = hdr_np[:, 4].astype(np.float64)
+    bytes_per_launch = float((16.0 * N + 20.0 * V + 8.0 * Cn + 64.0).sum())
+    achieved_gbs = bytes_per_launch / (avg_kernel_ms * 1e-3) / 1e9
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_frames = F * args.steps * world
+    fps = total_frames / elapsed
+
+    single = None
+    if args.single_frame and rank == 0:
+        single = single_frame_latency(cp, params, raw, local)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(cp, params, raw, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "LiDAR frames/sec @64k pts/frame, 1/2/4/8 MI355X; cluster-set match vs PCL",
+            "value": fps,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"C3/C4: {F} frames x {N} pts per GPU per step (xyzi f32, "
+                                   "simulation params), ground_removal + cone_detection fused",
+                       "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
+                       "parallelism": f"frame-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "cg_frame_kernel", "avg_kernel_ms": avg_kernel_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "cpu_baseline": cpu,
+        }
+        if single is not None:
+            line["single_frame"] = single
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def fetch_headers(res, F):
+    """Copy the per-frame header words of the last batch to host."""
+    import ctypes
+    import numpy as np
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.zeros((F, 8), np.uint32)
+    rc = hip.hipMemcpy(out.ctypes.data, res.d_header, F * 32, 2)   # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise RuntimeError(f"hipMemcpy failed: {rc}")
+    return out
+
+
+def single_frame_latency(cp, params, raw, device, reps=200):
+    """C2: one 64k frame through the synchronous ROS drop-in call (H2D + kernel + D2H)."""
+    pipe = cp.ConePipeline(params, device=device)
+    msg = cp.frame_cloud(raw[0])
+    for _ in range(10):
+        pipe.cloud_handler(msg)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pipe.cloud_handler(msg)
+    dt = (time.perf_counter() - t0) / reps
+    return {"latency_ms": dt * 1e3, "frames_per_s": 1.0 / dt, "includes": "PCIe H2D of 1 MiB + D2H of results"}
+
+
+def cpu_baseline(cp, params, raw, budget_s):
+    """The CPU restatement (oracle/, -O2, one core) on the first frames of this rank's batch."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        O.run(params, cp.frame_cloud(raw[n % raw.shape[0]]), O.MODE_PIPELINE)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and n >= 20:
+            break
+    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames of this bench's 64k-point synthetic batch, sequential, "
+                      f"{el:.1f} s, oracle/cg_oracle.cpp (g++ -O2 -ffp-contract=off)"}
+
+
+if __name__ == "__main__":
+    main()

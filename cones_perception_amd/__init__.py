@@ -1,0 +1,324 @@
+"""cones_perception_amd — MI355X (gfx950) LiDAR cone-detection hot path.
+
+Python mirror of the reference's two ROS node interfaces over the C-ABI
+(include/cones_gpu.h). The names follow the reference:
+
+  GroundRemover.cloud_handler   src/ground_removal.cpp:50-89
+  ConeDetector.cloud_handler    src/cone_detection.cpp:130-187 (up to the pre-tracking centroids)
+  ConePipeline.cloud_handler    launch/cones_perception.launch:17-37 (ground_removal:=true)
+
+Parameters use the YAML keys of config/*.yaml verbatim. All compute runs in the HIP library;
+this module only marshals PointCloud2 bytes. Importing it without the built library raises.
+"""
+from dataclasses import dataclass, field
+import ctypes as C
+from typing import List, Optional
+
+import numpy as np
+
+from . import _abi
+from ._abi import (CG_MODE_DETECT, CG_MODE_PIPELINE, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL,
+                   CG_F_VOXEL_PASSTHROUGH, CgError, check, lib)
+
+lib()   # fail loudly at import if the gfx950 library is missing
+
+__all__ = ["PROFILES", "load_params", "PointField", "PointCloud2", "Detection", "GroundRemover",
+           "ConeDetector", "ConePipeline", "BatchEngine", "synth_frames", "CgError"]
+
+# ---------------------------------------------------------------------------------------
+# Parameter profiles: the reference's config/*.yaml (keys verbatim, misspellings kept).
+GROUND_PARAMS = {"num_of_sectors": 16, "default_lowest_point": -0.1}   # ground_removal_params.yaml
+PROFILES = {
+    # config/cones_detection_params_simulation.yaml:1-11 (the metric's profile)
+    "simulation": {"cones_matching_dist_theshold": 0.5, "cone_position_extension_length": 0.05,
+                   "distance_treshold_max": 10.0, "distance_treshold_min": 1.0,
+                   "level_threshold": -5.0, "angle_threshold": 160.0,
+                   "min_cluster_size": 2, "max_cluster_size": 500,
+                   "voxel_filter_leaf_size_x": 0.04, "voxel_filter_leaf_size_y": 0.04,
+                   "voxel_filter_leaf_size_z": 0.04},
+    # config/cones_detection_params_our.yaml:1-11
+    "our": {"cones_matching_dist_theshold": 0.5, "cone_position_extension_length": 0.05,
+            "distance_treshold_max": 7.0, "distance_treshold_min": 0.7, "level_threshold": -0.5,
+            "angle_threshold": 90.0, "min_cluster_size": 3, "max_cluster_size": 50,
+            "voxel_filter_leaf_size_x": 0.04, "voxel_filter_leaf_size_y": 0.04,
+            "voxel_filter_leaf_size_z": 0.04},
+    # config/cones_detection_params_fsai.yaml:1-11
+    "fsai": {"cones_matching_dist_theshold": 0.5, "cone_position_extension_length": 0.05,
+             "distance_treshold_max": 6.0, "distance_treshold_min": 1.0, "level_threshold": -0.09,
+             "angle_threshold": 160.0, "min_cluster_size": 3, "max_cluster_size": 500,
+             "voxel_filter_leaf_size_x": 0.04, "voxel_filter_leaf_size_y": 0.04,
+             "voxel_filter_leaf_size_z": 0.04},
+}
+
+
+def load_params(profile: Optional[str] = "simulation", *overrides) -> _abi.cg_params:
+    """cg_params from the reference defaults, a named profile, then YAML files / dicts.
+
+    Missing keys keep the reference's class-member defaults (cg_params_init), as a missing
+    ROS param does in the nodes. Unknown keys are ignored like unused ROS params.
+    """
+    p = _abi.cg_params()
+    lib().cg_params_init(C.byref(p))
+    layers = [GROUND_PARAMS]
+    if profile:
+        layers.append(PROFILES[profile])
+    for o in overrides:
+        if isinstance(o, str):
+            import yaml
+            with open(o) as fh:
+                o = yaml.safe_load(fh) or {}
+        layers.append(o)
+    names = {n for n, _ in _abi.cg_params._fields_}
+    for layer in layers:
+        for k, v in layer.items():
+            if k in names:
+                setattr(p, k, v)
+    return p
+
+
+# ---------------------------------------------------------------------------------------
+# sensor_msgs/PointCloud2 (ROS-free)
+FLOAT32 = 7
+
+
+@dataclass
+class PointField:
+    name: str
+    offset: int
+    datatype: int = FLOAT32
+    count: int = 1
+
+
+@dataclass
+class PointCloud2:
+    width: int
+    height: int
+    fields: List[PointField]
+    point_step: int
+    row_step: int
+    data: np.ndarray            # uint8 buffer
+    is_dense: bool = True
+    header: dict = field(default_factory=dict)
+
+    @staticmethod
+    def from_xyzi(points: np.ndarray, layout: int = 16, height: int = 1, intensity: bool = True):
+        """Pack an (N, 4) float32 array as xyzi (point_step 16) or PCL PointXYZI (32)."""
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 4)
+        n = pts.shape[0]
+        if layout == 16:
+            buf = pts.copy()
+            fields = [PointField("x", 0), PointField("y", 4), PointField("z", 8)]
+            if intensity:
+                fields.append(PointField("intensity", 12))
+        elif layout == 32:
+            buf = np.zeros((n, 8), np.float32)
+            buf[:, 0:3] = pts[:, 0:3]
+            buf[:, 3] = 1.0
+            buf[:, 4] = pts[:, 3]
+            fields = [PointField("x", 0), PointField("y", 4), PointField("z", 8)]
+            if intensity:
+                fields.append(PointField("intensity", 16))
+        else:
+            raise ValueError("layout must be 16 or 32")
+        width = n // height if height else n
+        return PointCloud2(width, height, fields, layout, layout * width,
+                           buf.view(np.uint8).reshape(-1), True)
+
+    def offset_of(self, name: str) -> int:
+        for f in self.fields:
+            if f.name == name and f.datatype == FLOAT32 and f.count == 1:
+                return f.offset
+        return -1
+
+    def has_field(self, name: str) -> bool:
+        return any(f.name == name for f in self.fields)
+
+    def view(self, intensity_offset: Optional[int] = None) -> _abi.cg_cloud_view:
+        data = np.ascontiguousarray(self.data, dtype=np.uint8)
+        self.data = data
+        v = _abi.cg_cloud_view()
+        v.data = data.ctypes.data if data.size else None
+        v.width, v.height = self.width, self.height
+        v.point_step, v.row_step = self.point_step, self.row_step
+        v.off_x, v.off_y, v.off_z = self.offset_of("x"), self.offset_of("y"), self.offset_of("z")
+        v.off_intensity = self.offset_of("intensity") if intensity_offset is None else intensity_offset
+        v.is_dense = 1 if self.is_dense else 0
+        return v
+
+    def xyzi(self) -> np.ndarray:
+        """Decode to (N, 4) float32 like pcl::fromROSMsg (missing fields read as 0)."""
+        n = self.width * self.height
+        out = np.zeros((n, 4), np.float32)
+        raw = np.ascontiguousarray(self.data, dtype=np.uint8)
+        rows = raw[: self.height * self.row_step].reshape(self.height, self.row_step)
+        for a, name in enumerate(("x", "y", "z", "intensity")):
+            off = self.offset_of(name)
+            if off < 0:
+                continue
+            cols = rows[:, : self.width * self.point_step].reshape(self.height, self.width, self.point_step)
+            out[:, a] = cols[:, :, off:off + 4].copy().view(np.float32).reshape(-1)
+        return out
+
+
+@dataclass
+class Detection:
+    """Hot-path output of one frame (what get_centroid_clouds receives, plus centroids)."""
+    n_points: int
+    n_kept: int
+    n_filtered: int
+    voxels: np.ndarray              # (V, 4) x, y, z, intensity
+    labels: np.ndarray              # (V,) cluster rank or -1
+    cluster_offsets: np.ndarray     # (C + 1,)
+    cluster_indices: np.ndarray     # (offsets[C],)
+    centroids: np.ndarray           # (C, 2) after the radial push
+    flags: int = 0
+
+    @property
+    def clusters(self) -> List[np.ndarray]:
+        o = self.cluster_offsets
+        return [self.cluster_indices[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+def _detection(r: _abi.cg_detect_result) -> Detection:
+    V, Cn = r.n_voxels, r.n_clusters
+    vox = np.ctypeslib.as_array(r.voxels, (V * 4,)).reshape(V, 4).copy() if V else np.zeros((0, 4), np.float32)
+    lab = np.ctypeslib.as_array(r.labels, (V,)).copy() if V else np.zeros(0, np.int32)
+    offs = np.ctypeslib.as_array(r.cluster_offsets, (Cn + 1,)).copy()
+    nidx = int(offs[-1]) if Cn else 0
+    idx = np.ctypeslib.as_array(r.cluster_indices, (nidx,)).copy() if nidx else np.zeros(0, np.int32)
+    cen = np.ctypeslib.as_array(r.centroids, (Cn * 2,)).reshape(Cn, 2).copy() if Cn else np.zeros((0, 2), np.float32)
+    return Detection(r.n_points, r.n_kept, r.n_filtered, vox, lab, offs, idx, cen, r.flags)
+
+
+class _Handle:
+    def __init__(self, params=None, device: int = 0):
+        self.params = params if params is not None else load_params()
+        h = C.c_void_p()
+        check(lib().cg_create(C.byref(self.params), device, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().cg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+
+class GroundRemover(_Handle):
+    """GroundRemover::cloud_handler (src/ground_removal.cpp:50-89) on the GPU."""
+
+    def cloud_handler(self, msg: PointCloud2) -> PointCloud2:
+        v = msg.view(intensity_offset=msg.offset_of("intensity"))
+        r = _abi.cg_ground_result()
+        check(lib().cg_ground_remove(self._h, C.byref(v), C.byref(r)))
+        n = r.n_points
+        data = np.ctypeslib.as_array(r.data, (n * 32,)).copy() if n else np.zeros(0, np.uint8)
+        out = PointCloud2(r.width, r.height,
+                          [PointField("x", 0), PointField("y", 4), PointField("z", 8),
+                           PointField("intensity", 16)], 32, 32 * r.width, data, msg.is_dense,
+                          dict(msg.header))
+        out.n_kept = r.n_kept
+        return out
+
+
+class ConeDetector(_Handle):
+    """ConeDetector::cloud_handler (src/cone_detection.cpp:130-175) up to the centroids.
+
+    Reproduces the intensity probe (lines 131-151): the first cloud decides, once, whether
+    clouds carry an intensity field; if not, a fake FLOAT32 field at offset 0 is appended,
+    so intensity reads the bytes of x.
+    """
+    _mode = "detect"
+
+    def __init__(self, params=None, device: int = 0):
+        super().__init__(params, device)
+        self.intensity_in_cloud_checked = False
+        self.intensity_in_cloud = True
+
+    def cloud_handler(self, msg: PointCloud2) -> Detection:
+        if not self.intensity_in_cloud_checked:
+            if not msg.has_field("intensity"):
+                self.intensity_in_cloud = False
+            self.intensity_in_cloud_checked = True
+        off_i = msg.offset_of("intensity") if self.intensity_in_cloud else 0
+        v = msg.view(intensity_offset=off_i)
+        r = _abi.cg_detect_result()
+        fn = lib().cg_detect if self._mode == "detect" else lib().cg_pipeline
+        check(fn(self._h, C.byref(v), C.byref(r)))
+        return _detection(r)
+
+
+class ConePipeline(ConeDetector):
+    """ground_removal -> cone_detection (launch/cones_perception.launch:17-37), fused."""
+    _mode = "pipeline"
+
+    def cloud_handler(self, msg: PointCloud2) -> Detection:
+        off_i = msg.offset_of("intensity")   # ground node: missing intensity reads 0
+        v = msg.view(intensity_offset=off_i)
+        r = _abi.cg_detect_result()
+        check(lib().cg_pipeline(self._h, C.byref(v), C.byref(r)))
+        return _detection(r)
+
+
+class BatchEngine(_Handle):
+    """Device-resident batch engine (cg_run_batch): frames already in HBM."""
+
+    def run(self, d_ptr: int, n_frames: int, n_points: int, point_step: int = 16,
+            frame_stride: Optional[int] = None, mode: int = CG_MODE_PIPELINE, stream: int = 0,
+            offsets=(0, 4, 8, 12), is_dense: bool = True):
+        b = _abi.cg_batch()
+        b.d_data = d_ptr
+        b.frame_stride = frame_stride if frame_stride is not None else n_points * point_step
+        b.n_frames, b.n_points, b.point_step = n_frames, n_points, point_step
+        b.off_x, b.off_y, b.off_z, b.off_intensity = offsets
+        b.is_dense = 1 if is_dense else 0
+        check(lib().cg_run_batch(self._h, C.byref(b), mode, C.c_void_p(stream) if stream else None))
+
+    def results(self) -> _abi.cg_batch_results:
+        r = _abi.cg_batch_results()
+        check(lib().cg_batch_results_get(self._h, C.byref(r)))
+        return r
+
+    def fetch(self, frame: int) -> Detection:
+        r = _abi.cg_detect_result()
+        check(lib().cg_batch_fetch(self._h, frame, C.byref(r)))
+        return _detection(r)
+
+
+# ---------------------------------------------------------------------------------------
+def synth_config(rings=64, cols=1024, point_step=16, seed=0x00C0FFEE, cones_per_row=5, clutter=0,
+                 column_major=True) -> _abi.cg_synth_cfg:
+    c = _abi.cg_synth_cfg()
+    lib().cg_synth_default(C.byref(c))
+    c.rings, c.cols, c.point_step, c.seed = rings, cols, point_step, seed
+    c.cones_per_row, c.clutter, c.column_major = cones_per_row, clutter, 1 if column_major else 0
+    return c
+
+
+def synth_frames(n_frames=1, first_frame=0, threads=8, out: Optional[np.ndarray] = None, **kw) -> np.ndarray:
+    """Deterministic synthetic cone-field frames as a (n_frames, N*point_step) uint8 array."""
+    cfg = synth_config(**kw)
+    stride = cfg.rings * cfg.cols * cfg.point_step
+    if out is None:
+        out = np.empty((n_frames, stride), np.uint8)
+    check(lib().cg_synth_frames(C.byref(cfg), first_frame, n_frames, out.ctypes.data, stride, threads))
+    return out
+
+
+def frame_cloud(raw: np.ndarray, point_step=16) -> PointCloud2:
+    """Wrap one synthetic frame's bytes as a PointCloud2."""
+    n = raw.size // point_step
+    if point_step == 16:
+        fields = [PointField("x", 0), PointField("y", 4), PointField("z", 8), PointField("intensity", 12)]
+    else:
+        fields = [PointField("x", 0), PointField("y", 4), PointField("z", 8), PointField("intensity", 16)]
+    return PointCloud2(n, 1, fields, point_step, n * point_step, raw.reshape(-1), True)

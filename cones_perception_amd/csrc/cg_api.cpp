@@ -1,0 +1,494 @@
+// cg_api.cpp — host side of the C-ABI (include/cones_gpu.h): handle, parameter preparation,
+// staging, kernel launches and result download. No compute happens here: every per-point
+// operation of the hot path runs in cg_kernels.hip. The host only (1) resolves the
+// reference's parameter expressions into exact device thresholds once per cg_set_params,
+// (2) copies PointCloud2 bytes in and results out.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "../../include/cones_gpu.h"
+#include "cg_internal.h"
+#include "cg_math.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(e_ == hipErrorOutOfMemory ? CG_E_OOM : CG_E_DEVICE, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);               \
+    } while (0)
+
+// Smallest S >= 0 (a double) with pred(S) true; pred must be monotone in S. Returns
+// `none` if pred(+inf) is false.
+template <class F>
+double min_double_where(F pred, double none) {
+    const uint64_t inf_bits = cg_dbits(INFINITY);
+    if (!pred(INFINITY)) return none;
+    if (pred(0.0)) return 0.0;
+    uint64_t lo = 0, hi = inf_bits;   // pred(lo) false, pred(hi) true
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (pred(cg_bitsd(mid))) hi = mid; else lo = mid;
+    }
+    return cg_bitsd(hi);
+}
+
+// euclidan_dist(p, 0) as a function of S = (x^2 + y^2) + z^2 (src/perception_handling/utils.cpp:33)
+float dist_of_sumsq(double S) { return (float)std::sqrt(S); }
+
+int prepare(const cg_params& p, CgDevParams& d) {
+    if (!(p.voxel_filter_leaf_size_x > 0) || !(p.voxel_filter_leaf_size_y > 0) ||
+        !(p.voxel_filter_leaf_size_z > 0))
+        return fail(CG_E_INVALID, "voxel_filter_leaf_size_* must be > 0");
+    std::memset(&d, 0, sizeof(d));
+    d.default_low = p.default_lowest_point;
+    // (double)z < level_threshold
+    d.level_f = cg_ceil_to_float(p.level_threshold);
+    // euclidan_dist(...) > distance_treshold_max  <=>  S >= s_far
+    const double dmax = p.distance_treshold_max, dmin = p.distance_treshold_min;
+    d.s_far = (dmax != dmax) ? NAN
+                             : min_double_where([&](double S) { return (double)dist_of_sumsq(S) > dmax; }, NAN);
+    // euclidan_dist(...) < distance_treshold_min  <=>  S < s_near
+    d.s_near = (dmin != dmin) ? 0.0
+                              : min_double_where([&](double S) { return (double)dist_of_sumsq(S) >= dmin; },
+                                                 INFINITY);
+    // -angle*pi/180 >= atan2f  <=>  a <= ang_lo ;  atan2f >= angle*pi/180  <=>  a >= ang_hi
+    const double theta = p.angle_threshold * M_PI / 180;
+    const double ntheta = -p.angle_threshold * M_PI / 180;
+    d.ang_lo = cg_floor_to_float(ntheta);
+    d.ang_hi = cg_ceil_to_float(theta);
+    // pcl::VoxelGrid::setLeafSize(float, float, float): inverse = 1.0f / leaf
+    d.inv_leaf[0] = 1.0f / (float)p.voxel_filter_leaf_size_x;
+    d.inv_leaf[1] = 1.0f / (float)p.voxel_filter_leaf_size_y;
+    d.inv_leaf[2] = 1.0f / (float)p.voxel_filter_leaf_size_z;
+    // tolerance (src/cone_detection.cpp:22-23,212): const float members promoted by pow
+    const float cone_width = 0.228, cone_height = 0.325;
+    const double tol = std::sqrt(std::pow(cone_height, 2) + std::pow(cone_width, 2));
+    const float tol_f = (float)tol;                               // extract(): float tolerance
+    d.r2 = (float)((double)tol_f * (double)tol_f);                 // KdTreeFLANN::radiusSearch
+    d.cell_inv = 1.0f / (tol_f * 1.0625f);
+    d.min_cl = (uint32_t)p.min_cluster_size;
+    d.max_cl = (uint32_t)p.max_cluster_size;
+    d.ext = p.cone_position_extension_length;
+    // does PointXYZI() (0,0,0) survive filter_points_position?
+    const float a0 = cg_atan2f(0.0f, 0.0f);
+    const double S0 = 0.0;
+    const bool rm = (0.0f < d.level_f) || (S0 >= d.s_far) || (S0 < d.s_near) || (a0 <= d.ang_lo) ||
+                    (a0 >= d.ang_hi);
+    d.zero_pass = rm ? 0 : 1;
+    return CG_OK;
+}
+
+}  // namespace
+
+struct cg_handle {
+    int device = 0;
+    cg_params params{};
+    CgDevParams dp{};
+    hipStream_t stream = nullptr;
+    // batch result buffers
+    uint32_t cap_frames = 0, cap_points = 0;
+    uint32_t* d_hdr = nullptr;
+    float4* d_vox = nullptr;
+    int32_t* d_lab = nullptr;
+    int32_t* d_offs = nullptr;
+    int32_t* d_idx = nullptr;
+    float2* d_cen = nullptr;
+    uint8_t* d_ground = nullptr;
+    uint8_t* d_scratch = nullptr;
+    uint64_t scratch_stride = 0;
+    // single-frame staging
+    uint8_t* d_in = nullptr;
+    size_t d_in_bytes = 0;
+    uint8_t* h_stage = nullptr;   // pinned
+    size_t h_stage_bytes = 0;
+    // last batch
+    uint32_t last_frames = 0, last_points = 0;
+    int last_mode = -1;
+    hipStream_t last_stream = nullptr;
+    // host results
+    uint32_t h_hdr[CG_HDR_WORDS] = {};
+    std::vector<float> h_vox, h_cen;
+    std::vector<int32_t> h_lab, h_offs, h_idx;
+    uint8_t* h_ground = nullptr;  // pinned
+    size_t h_ground_bytes = 0;
+};
+
+namespace {
+
+void free_batch(cg_handle* h) {
+    hipFree(h->d_hdr); hipFree(h->d_vox); hipFree(h->d_lab); hipFree(h->d_offs);
+    hipFree(h->d_idx); hipFree(h->d_cen); hipFree(h->d_ground); hipFree(h->d_scratch);
+    h->d_hdr = nullptr; h->d_vox = nullptr; h->d_lab = nullptr; h->d_offs = nullptr;
+    h->d_idx = nullptr; h->d_cen = nullptr; h->d_ground = nullptr; h->d_scratch = nullptr;
+    h->cap_frames = h->cap_points = 0;
+}
+
+int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
+    const uint32_t pts = std::max<uint32_t>(points, 1);
+    const bool need_ground = ground && h->d_ground == nullptr;
+    if (frames <= h->cap_frames && pts <= h->cap_points && !need_ground) return CG_OK;
+    const uint32_t nf = std::max(frames, h->cap_frames), np = std::max(pts, h->cap_points);
+    const bool had_ground = h->d_ground != nullptr || ground;
+    free_batch(h);
+    const uint64_t F = nf, C = np;
+    HIPCHK(hipMalloc(&h->d_hdr, F * CG_HDR_WORDS * 4));
+    HIPCHK(hipMalloc(&h->d_vox, F * C * 16));
+    HIPCHK(hipMalloc(&h->d_lab, F * C * 4));
+    HIPCHK(hipMalloc(&h->d_offs, F * (C + 1) * 4));
+    HIPCHK(hipMalloc(&h->d_idx, F * C * 4));
+    HIPCHK(hipMalloc(&h->d_cen, F * C * 8));
+    h->scratch_stride = (cg_scratch_bytes(np) + 255) & ~255ull;
+    HIPCHK(hipMalloc(&h->d_scratch, F * h->scratch_stride));
+    if (had_ground) HIPCHK(hipMalloc(&h->d_ground, F * C * 32));
+    h->cap_frames = nf;
+    h->cap_points = np;
+    return CG_OK;
+}
+
+int check_view(const cg_cloud_view* v) {
+    if (!v) return fail(CG_E_INVALID, "null cloud view");
+    const uint64_t n = (uint64_t)v->width * v->height;
+    if (n > CG_MAX_POINTS)
+        return fail(CG_E_CAPACITY, "cloud has %llu points; the frame engine supports <= %d",
+                    (unsigned long long)n, CG_MAX_POINTS);
+    if (n == 0) return CG_OK;
+    if (!v->data) return fail(CG_E_INVALID, "null cloud data");
+    if (v->point_step == 0) return fail(CG_E_INVALID, "point_step is 0");
+    if ((uint64_t)v->row_step < (uint64_t)v->width * v->point_step)
+        return fail(CG_E_INVALID, "row_step < width * point_step");
+    const int32_t offs[4] = {v->off_x, v->off_y, v->off_z, v->off_intensity};
+    for (int32_t o : offs)
+        if (o >= 0 && (uint64_t)o + 4 > v->point_step)
+            return fail(CG_E_INVALID, "field offset %d outside point_step %u", o, v->point_step);
+    return CG_OK;
+}
+
+// Stage a PointCloud2 data block as one contiguous device frame. Aligned, unpadded rows are
+// uploaded verbatim; padded rows or unaligned fields are re-packed (pure byte moves, the
+// memcpy half of pcl::fromROSMsg) to x,y,z,intensity at 0,4,8,12.
+int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L) {
+    const uint32_t n = v->width * v->height;
+    const bool aligned = v->point_step % 4 == 0 && (v->off_x < 0 || v->off_x % 4 == 0) &&
+                         (v->off_y < 0 || v->off_y % 4 == 0) && (v->off_z < 0 || v->off_z % 4 == 0) &&
+                         (v->off_intensity < 0 || v->off_intensity % 4 == 0);
+    const bool contiguous = v->height <= 1 || v->row_step == v->width * v->point_step;
+    const bool verbatim = aligned && contiguous;
+    const uint32_t step = verbatim ? v->point_step : 16;
+    const size_t bytes = std::max<size_t>((size_t)n * step, 16);
+    if (bytes > h->h_stage_bytes) {
+        if (h->h_stage) hipHostFree(h->h_stage);
+        h->h_stage = nullptr;
+        HIPCHK(hipHostMalloc(&h->h_stage, bytes, hipHostMallocDefault));
+        h->h_stage_bytes = bytes;
+    }
+    if (bytes > h->d_in_bytes) {
+        if (h->d_in) hipFree(h->d_in);
+        h->d_in = nullptr;
+        HIPCHK(hipMalloc(&h->d_in, bytes));
+        h->d_in_bytes = bytes;
+    }
+    const uint8_t* src = (const uint8_t*)v->data;
+    if (verbatim) {
+        if (n) std::memcpy(h->h_stage, src, (size_t)n * step);
+        L.point_step = v->point_step;
+        L.off_x = v->off_x; L.off_y = v->off_y; L.off_z = v->off_z; L.off_i = v->off_intensity;
+    } else {
+        const int32_t offs[4] = {v->off_x, v->off_y, v->off_z, v->off_intensity};
+        for (uint32_t r = 0; r < v->height; r++)
+            for (uint32_t c = 0; c < v->width; c++) {
+                const uint8_t* p = src + (size_t)r * v->row_step + (size_t)c * v->point_step;
+                uint8_t* q = h->h_stage + ((size_t)r * v->width + c) * 16;
+                for (int a = 0; a < 4; a++) {
+                    if (offs[a] >= 0) std::memcpy(q + 4 * a, p + offs[a], 4);
+                    else std::memset(q + 4 * a, 0, 4);
+                }
+            }
+        L.point_step = 16;
+        L.off_x = 0; L.off_y = 4; L.off_z = 8; L.off_i = 12;
+    }
+    if (n) HIPCHK(hipMemcpyAsync(h->d_in, h->h_stage, (size_t)n * step, hipMemcpyHostToDevice, h->stream));
+    L.in = h->d_in;
+    L.frame_stride = (uint64_t)n * step;
+    L.n_frames = 1;
+    L.n_points = n;
+    L.is_dense = v->is_dense;
+    return CG_OK;
+}
+
+void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
+    L.cap = h->cap_points;
+    L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
+    L.idx = h->d_idx; L.cen = h->d_cen; L.ground = h->d_ground;
+    L.scratch = h->d_scratch; L.scratch_stride = h->scratch_stride;
+}
+
+int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
+    const uint64_t cap = h->cap_points;
+    HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, CG_HDR_WORDS * 4,
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint32_t V = h->h_hdr[CG_HDR_V], C = h->h_hdr[CG_HDR_C];
+    h->h_vox.resize((size_t)V * 4 + 4);
+    h->h_lab.resize((size_t)V + 1);
+    h->h_offs.resize((size_t)C + 2);
+    h->h_cen.resize((size_t)C * 2 + 2);
+    h->h_idx.resize((size_t)V + 1);
+    if (V) {
+        HIPCHK(hipMemcpyAsync(h->h_vox.data(), h->d_vox + frame * cap, (size_t)V * 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(h->h_lab.data(), h->d_lab + frame * cap, (size_t)V * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipMemcpyAsync(h->h_offs.data(), h->d_offs + frame * (cap + 1), (size_t)(C + 1) * 4,
+                          hipMemcpyDeviceToHost, s));
+    if (C) {
+        HIPCHK(hipMemcpyAsync(h->h_cen.data(), h->d_cen + frame * cap, (size_t)C * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    const uint32_t nidx = C ? (uint32_t)h->h_offs[C] : 0u;
+    if (nidx) {
+        HIPCHK(hipMemcpyAsync(h->h_idx.data(), h->d_idx + frame * cap, (size_t)nidx * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    out->n_points = h->h_hdr[CG_HDR_N];
+    out->n_kept = h->h_hdr[CG_HDR_K];
+    out->n_filtered = h->h_hdr[CG_HDR_M];
+    out->n_voxels = V;
+    out->n_clusters = C;
+    out->flags = h->h_hdr[CG_HDR_FLAGS];
+    out->voxels = h->h_vox.data();
+    out->labels = h->h_lab.data();
+    out->cluster_offsets = h->h_offs.data();
+    out->cluster_indices = h->h_idx.data();
+    out->centroids = h->h_cen.data();
+    return CG_OK;
+}
+
+int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_result* dres,
+               cg_ground_result* gres) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    int rc = check_view(in);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(h->device));
+    const uint32_t n = in->width * in->height;
+    rc = ensure_batch(h, 1, n, kmode == CG_KMODE_GROUND);
+    if (rc) return rc;
+    CgLaunch L{};
+    rc = stage_frame(h, in, L);
+    if (rc) return rc;
+    fill_launch_outputs(h, L);
+    HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, h->stream));
+    h->last_frames = 1; h->last_points = n; h->last_mode = kmode; h->last_stream = h->stream;
+    if (kmode == CG_KMODE_GROUND) {
+        const size_t bytes = std::max<size_t>((size_t)n * 32, 32);
+        if (bytes > h->h_ground_bytes) {
+            if (h->h_ground) hipHostFree(h->h_ground);
+            h->h_ground = nullptr;
+            HIPCHK(hipHostMalloc(&h->h_ground, bytes, hipHostMallocDefault));
+            h->h_ground_bytes = bytes;
+        }
+        if (n) HIPCHK(hipMemcpyAsync(h->h_ground, h->d_ground, (size_t)n * 32, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr, CG_HDR_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        gres->n_points = n;
+        gres->n_kept = h->h_hdr[CG_HDR_K];
+        gres->width = in->width;
+        gres->height = in->height;
+        gres->data = h->h_ground;
+        return CG_OK;
+    }
+    return fetch_frame(h, h->stream, 0, dres);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cg_last_error(void) { return g_err.c_str(); }
+const char* cg_version(void) { return "cones_gpu 0.1.0 (gfx950)"; }
+
+void cg_params_init(cg_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->num_of_sectors = 16;                 // src/ground_removal.cpp:18
+    p->default_lowest_point = -0.1f;        // src/ground_removal.cpp:19
+    p->distance_treshold_max = 7.0;         // src/cone_detection.cpp:27
+    p->distance_treshold_min = 0.7;         // :28
+    p->level_threshold = -0.5;              // :29
+    p->angle_threshold = 90.0;              // :30
+    p->min_cluster_size = 3;                // :32
+    p->max_cluster_size = 50;               // :33
+    p->cones_matching_dist_theshold = 0.5;  // :39
+    p->cone_position_extension_length = 0.05;  // :40
+    p->voxel_filter_leaf_size_x = 0.04;     // :41-43
+    p->voxel_filter_leaf_size_y = 0.04;
+    p->voxel_filter_leaf_size_z = 0.04;
+}
+
+int cg_create(const cg_params* params, int device, cg_handle** out) {
+    if (!out) return fail(CG_E_INVALID, "null output handle pointer");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(CG_E_DEVICE, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(CG_E_DEVICE, "device %d out of range (%d)", device, ndev);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(CG_E_DEVICE, "device %d is %s; this library is built for gfx950", device, prop.gcnArchName);
+    cg_params p;
+    if (params) p = *params; else cg_params_init(&p);
+    CgDevParams dp;
+    int rc = prepare(p, dp);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(device));
+    cg_handle* h = new cg_handle();
+    h->device = device;
+    h->params = p;
+    h->dp = dp;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(CG_E_DEVICE, "hipStreamCreate failed");
+    }
+    *out = h;
+    return CG_OK;
+}
+
+int cg_destroy(cg_handle* h) {
+    if (!h) return CG_OK;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    free_batch(h);
+    if (h->d_in) hipFree(h->d_in);
+    if (h->h_stage) hipHostFree(h->h_stage);
+    if (h->h_ground) hipHostFree(h->h_ground);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return CG_OK;
+}
+
+int cg_set_params(cg_handle* h, const cg_params* params) {
+    if (!h || !params) return fail(CG_E_INVALID, "null argument");
+    CgDevParams dp;
+    int rc = prepare(*params, dp);
+    if (rc) return rc;
+    h->params = *params;
+    h->dp = dp;
+    return CG_OK;
+}
+
+int cg_ground_remove(cg_handle* h, const cg_cloud_view* in, cg_ground_result* out) {
+    if (!out) return fail(CG_E_INVALID, "null result");
+    return run_single(h, in, CG_KMODE_GROUND, nullptr, out);
+}
+int cg_detect(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out) {
+    if (!out) return fail(CG_E_INVALID, "null result");
+    return run_single(h, in, CG_KMODE_DETECT, out, nullptr);
+}
+int cg_pipeline(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out) {
+    if (!out) return fail(CG_E_INVALID, "null result");
+    return run_single(h, in, CG_KMODE_PIPELINE, out, nullptr);
+}
+
+int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
+    if (!h || !b) return fail(CG_E_INVALID, "null argument");
+    if (mode != CG_MODE_PIPELINE && mode != CG_MODE_DETECT) return fail(CG_E_INVALID, "bad mode %d", mode);
+    if (b->n_points > CG_MAX_POINTS)
+        return fail(CG_E_CAPACITY, "frames of %u points; the frame engine supports <= %d", b->n_points,
+                    CG_MAX_POINTS);
+    if (b->n_frames && b->n_points && !b->d_data) return fail(CG_E_INVALID, "null batch data");
+    if (b->point_step == 0 || b->point_step % 4 || b->frame_stride % 4 ||
+        b->frame_stride < (uint64_t)b->n_points * b->point_step)
+        return fail(CG_E_INVALID, "bad point_step / frame_stride");
+    const int32_t offs[4] = {b->off_x, b->off_y, b->off_z, b->off_intensity};
+    for (int32_t o : offs)
+        if (o >= 0 && (o % 4 || (uint32_t)o + 4 > b->point_step))
+            return fail(CG_E_INVALID, "field offset %d invalid for point_step %u", o, b->point_step);
+    HIPCHK(hipSetDevice(h->device));
+    int rc = ensure_batch(h, b->n_frames, b->n_points, false);
+    if (rc) return rc;
+    CgLaunch L{};
+    L.in = (const uint8_t*)b->d_data;
+    L.frame_stride = b->frame_stride;
+    L.n_frames = b->n_frames;
+    L.n_points = b->n_points;
+    L.point_step = b->point_step;
+    L.off_x = b->off_x; L.off_y = b->off_y; L.off_z = b->off_z; L.off_i = b->off_intensity;
+    L.is_dense = b->is_dense;
+    fill_launch_outputs(h, L);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    HIPCHK((hipError_t)cg_launch_batch(L, h->dp, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s));
+    h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
+    return CG_OK;
+}
+
+int cg_batch_results_get(cg_handle* h, cg_batch_results* out) {
+    if (!h || !out) return fail(CG_E_INVALID, "null argument");
+    out->n_frames = h->last_frames;
+    out->capacity = h->cap_points;
+    out->d_header = h->d_hdr;
+    out->d_voxels = (const float*)h->d_vox;
+    out->d_labels = h->d_lab;
+    out->d_cluster_offsets = h->d_offs;
+    out->d_cluster_indices = h->d_idx;
+    out->d_centroids = (const float*)h->d_cen;
+    return CG_OK;
+}
+
+int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out) {
+    if (!h || !out) return fail(CG_E_INVALID, "null argument");
+    if (frame >= h->last_frames) return fail(CG_E_INVALID, "frame %u >= %u", frame, h->last_frames);
+    HIPCHK(hipSetDevice(h->device));
+    return fetch_frame(h, h->last_stream, frame, out);
+}
+
+int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out, uint32_t n) {
+    if (!h || (n && (!y || !x || !out))) return fail(CG_E_INVALID, "null argument");
+    if (!n) return CG_OK;
+    HIPCHK(hipSetDevice(h->device));
+    float *dy = nullptr, *dx = nullptr, *dout = nullptr;
+    HIPCHK(hipMalloc(&dy, (size_t)n * 4));
+    HIPCHK(hipMalloc(&dx, (size_t)n * 4));
+    HIPCHK(hipMalloc(&dout, (size_t)n * 8));
+    HIPCHK(hipMemcpy(dy, y, (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dx, x, (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPCHK((hipError_t)cg_launch_selftest_atan2f(dy, dx, dout, n, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+    hipFree(dy); hipFree(dx); hipFree(dout);
+    return CG_OK;
+}
+
+int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n) {
+    if (!h || (n && (!s || !out))) return fail(CG_E_INVALID, "null argument");
+    if (!n) return CG_OK;
+    HIPCHK(hipSetDevice(h->device));
+    double *din = nullptr, *dout = nullptr;
+    HIPCHK(hipMalloc(&din, (size_t)n * 8));
+    HIPCHK(hipMalloc(&dout, (size_t)n * 8));
+    HIPCHK(hipMemcpy(din, s, (size_t)n * 8, hipMemcpyHostToDevice));
+    HIPCHK((hipError_t)cg_launch_selftest_sqrt(din, dout, n, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+    hipFree(din); hipFree(dout);
+    return CG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// cg_internal.h — structures shared by the HIP kernels (cg_kernels.hip) and the host side of
+// the C-ABI (cg_api.cpp). Not part of the public boundary (include/cones_gpu.h).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+// Device form of cg_params: the reference's float-vs-double comparisons pre-resolved on the
+// host into exact float / double thresholds (see cg_math.h and DESIGN.md §Numerics).
+struct CgDevParams {
+    float  default_low;     // default_lowest_point (src/ground_removal.cpp:19,58)
+    float  level_f;         // remove iff z < level_f    <=> (double)z < level_threshold
+    double s_far;           // remove iff S >= s_far      <=> euclidan_dist > distance_treshold_max
+    double s_near;          // remove iff S <  s_near     <=> euclidan_dist < distance_treshold_min
+    float  ang_lo;          // remove iff a <= ang_lo     <=> -theta >= atan2f(y,x)
+    float  ang_hi;          // remove iff a >= ang_hi     <=> atan2f(y,x) >= theta
+    float  inv_leaf[3];     // VoxelGrid inverse_leaf_size_ = 1.0f / (float)leaf
+    float  r2;              // float(tol * tol), tol = float(sqrt(0.325f^2 + 0.228f^2))
+    float  cell_inv;        // 1 / neighbour-grid cell size (cell = 1.0625 * tol)
+    uint32_t min_cl, max_cl;// cluster size limits as PCL's unsigned compares see them
+    double ext;             // cone_position_extension_length
+    int32_t zero_pass;      // a (0,0,0,i=0) pad point survives filter_points_position
+    int32_t pad_;
+};
+
+// One batch launch: uniform frames, device-resident input and outputs.
+struct CgLaunch {
+    const uint8_t* in;
+    uint64_t frame_stride;
+    uint32_t n_frames, n_points, point_step;
+    int32_t off_x, off_y, off_z, off_i;
+    uint32_t is_dense;
+    // outputs (per frame slots of `cap` points)
+    uint32_t cap;
+    uint32_t* hdr;      // n_frames x 8
+    float4*  vox;       // n_frames x cap
+    int32_t* lab;       // n_frames x cap
+    int32_t* offs;      // n_frames x (cap + 1)
+    int32_t* idx;       // n_frames x cap
+    float2*  cen;       // n_frames x cap
+    uint8_t* ground;    // n_frames x n_points x 32 B (ground-only mode)
+    // HBM scratch for frames whose survivors do not fit the LDS path
+    uint8_t* scratch;
+    uint64_t scratch_stride;
+};
+
+#define CG_BLOCK 1024          // one workgroup (16 waves) per frame
+#define CG_MMAX 2048           // LDS-path capacity (points surviving the filter)
+#define CG_MAX_POINTS 65536    // 64 points per lane
+
+enum { CG_LAYOUT_GENERIC = 0, CG_LAYOUT_XYZI16 = 1, CG_LAYOUT_PCL32 = 2 };
+enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };
+
+// Bytes of HBM scratch one frame of n points needs for the global (non-LDS) path.
+uint64_t cg_scratch_bytes(uint32_t n_points);
+// Enqueue the batch kernel. Returns a hipError_t.
+int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
+int cg_launch_selftest_atan2f(const float* y, const float* x, float* out, uint32_t n, hipStream_t s);
+int cg_launch_selftest_sqrt(const double* in, double* out, uint32_t n, hipStream_t s);

@@ -1,0 +1,791 @@
+// cg_kernels.hip — gfx950 kernels for the LiDAR cone-detection hot path.
+//
+// One 1024-lane workgroup (16 waves) owns one frame end to end; a batch launch is a grid of
+// n_frames workgroups. Per frame:
+//
+//  frontend (HBM-streaming, ~all of the frame's bytes)
+//    pass 1  coalesced point loads (lane t handles points k*1024 + t), glibc-exact atan2f,
+//            22-degree sector, position-filter bit; z kept on chip (32 points per lane in VGPRs,
+//            the rest in LDS); running per-lane sector minimum flushed into 17 LDS bins with
+//            ds_min_u32 on order-preserving keys        (src/ground_removal.cpp:58-68)
+//    pass 2  ground threshold per sector, keep bits, ballot counts per (k, wave)
+//                                                       (src/ground_removal.cpp:70-77, and
+//                                                        src/cone_detection.cpp:189-204)
+//    scan    one exclusive scan over the 1024 (k, wave) counts = stable compaction offsets
+//    pass 3  re-gather the few survivors (x, y, z, intensity) into LDS (or HBM scratch)
+//  backend (LDS-resident, latency-bound; M ~ 1e3 points)
+//    voxel   min/max, PCL idx key, bitonic sort of (idx, position), run heads, centroid sums
+//            in ascending position order             (pcl::VoxelGrid, src/cone_detection.cpp:240-249)
+//    cluster neighbour grid (cell >= tolerance), binary-searched cell rows, exact float
+//            L2_Simple predicate, lock-free union-find hooking larger roots under smaller
+//            ones so a component's root is its lowest voxel index = PCL's seed
+//                                                    (KdTree + ECE, src/cone_detection.cpp:206-220)
+//    order   size filter, PCL's std::sort(rbegin, rend) order (restated, cg_sort.h),
+//            stable counting sort into CSR, per-cluster centroid + radial push
+//                                                    (src/cone_detection.cpp:261-279)
+//
+// Compiled with -ffp-contract=off: every float/double expression must round like the
+// reference's non-FMA x86-64 build.
+#include <hip/hip_runtime.h>
+#include "cg_internal.h"
+#include "../../include/cones_gpu.h"
+#include "cg_math.h"
+#include "cg_sort.h"
+
+#define WAVES (CG_BLOCK / 64)
+
+// ------------------------------------------------------------------------------------------
+// LDS map. The frontend stores z for points k >= 32 in `zl`, which overlays the backend arrays
+// (dead until pass 3 begins, and pass 2 keeps its decisions in registers).
+struct FrontShared {
+    uint32_t sec_key[CG_NUM_BINS + 1];
+    float thr[CG_NUM_BINS + 1];
+    uint32_t cnt[CG_BLOCK];        // survivors per (k, wave), then exclusive offsets
+    uint32_t red[8 * WAVES];       // wave partials
+    uint32_t scal[64];             // broadcast scalars
+    int32_t stk[3 * CG_SORT_STACK];// introsort stack (cluster order)
+};
+#define FRONT_BYTES ((sizeof(FrontShared) + 255) & ~(size_t)255)
+
+struct BackLds {
+    float4 P[CG_MMAX];
+    uint64_t KEY[CG_MMAX];
+    float4 VOX[CG_MMAX];
+    uint32_t A[CG_MMAX + 4];
+    uint32_t PAR[CG_MMAX];
+    uint32_t CNT[CG_MMAX];
+    uint32_t UK[CG_MMAX];
+    int32_t LAB[CG_MMAX];
+    uint32_t ORD[CG_MMAX];
+    uint32_t IDX[CG_MMAX];
+    uint32_t OFF[CG_MMAX + 4];
+};
+#define SMEM_BYTES (FRONT_BYTES + sizeof(BackLds))
+static_assert(SMEM_BYTES <= 163840, "LDS budget");
+static_assert(sizeof(BackLds) >= 32 * CG_BLOCK * sizeof(float), "z overlay must fit");
+
+// Scalar slots in FrontShared::scal
+enum {
+    S_K = 0, S_MS, S_M, S_MF, S_V, S_C, S_U, S_FLAGS, S_PASS,
+    S_MINB0, S_MINB1, S_MINB2, S_MUL1, S_MUL2,
+    S_ORGX, S_ORGY, S_ORGZ, S_TMP
+};
+
+struct Work {
+    float4* P; uint64_t* KEY; float4* VOX; uint32_t* A; uint32_t* PAR; uint32_t* CNT;
+    uint32_t* UK; int32_t* LAB; uint32_t* ORD; uint32_t* IDX; uint32_t* OFF;
+};
+
+uint64_t cg_scratch_bytes(uint32_t n) {
+    uint64_t n2 = 1; while (n2 < n) n2 <<= 1;
+    uint64_t c = (uint64_t)n + 4;
+    return 16 * c + 8 * n2 + 16 * c + 4 * c * 8 + 256;
+}
+
+__device__ __forceinline__ Work global_work(uint8_t* base, uint32_t n) {
+    uint64_t n2 = 1; while (n2 < n) n2 <<= 1;
+    const uint64_t c = (uint64_t)n + 4;
+    Work w;
+    uint8_t* p = base;
+    w.P = (float4*)p; p += 16 * c;
+    w.VOX = (float4*)p; p += 16 * c;
+    w.KEY = (uint64_t*)p; p += 8 * n2;
+    w.A = (uint32_t*)p; p += 4 * c;
+    w.PAR = (uint32_t*)p; p += 4 * c;
+    w.CNT = (uint32_t*)p; p += 4 * c;
+    w.UK = (uint32_t*)p; p += 4 * c;
+    w.LAB = (int32_t*)p; p += 4 * c;
+    w.ORD = (uint32_t*)p; p += 4 * c;
+    w.IDX = (uint32_t*)p; p += 4 * c;
+    w.OFF = (uint32_t*)p; p += 4 * c;
+    return w;
+}
+
+// ------------------------------------------------------------------------------------------
+// Wave / block primitives (wave = 64 lanes).
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint32_t wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Exclusive scan over i in [0, n) in chunks of 1024: val(i) -> emit(i, excl). Returns total.
+// Every thread of the block must call it.
+template <class FV, class FE>
+__device__ __forceinline__ uint32_t block_scan(uint32_t n, FV val, FE emit, uint32_t* red) {
+    uint32_t carry = 0;
+    const uint32_t l = lane_id(), w = wave_id();
+    for (uint32_t base = 0; base < n; base += CG_BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < n ? val(i) : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (l == 63) red[w] = inc;
+        __syncthreads();
+        if (w == 0) {
+            uint32_t t = l < WAVES ? red[l] : 0u;
+            uint32_t ti = wave_incl_scan(t);
+            if (l < WAVES) red[WAVES + l] = ti - t;
+            if (l == WAVES - 1) red[2 * WAVES] = ti;
+        }
+        __syncthreads();
+        if (i < n) emit(i, carry + red[WAVES + w] + inc - v);
+        const uint32_t tot = red[2 * WAVES];
+        __syncthreads();
+        carry += tot;
+    }
+    return carry;
+}
+
+// Ascending bitonic sort of S[0, n2), n2 a power of two.
+__device__ __forceinline__ void bitonic_sort(uint64_t* S, uint32_t n2) {
+    for (uint32_t k = 2; k <= n2; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < (n2 >> 1); t += CG_BLOCK) {
+                const uint32_t l = 2 * t - (t & (j - 1)), r = l + j;
+                const bool up = (l & k) == 0;
+                const uint64_t a = S[l], b = S[r];
+                if ((a > b) == up) { S[l] = b; S[r] = a; }
+            }
+            __syncthreads();
+        }
+}
+
+__device__ __forceinline__ uint32_t ld_rlx(uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Union-find with path halving; roots only ever point to smaller indices.
+__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
+    while (true) {
+        uint32_t p = ld_rlx(par + x);
+        if (p == x) return x;
+        uint32_t gp = ld_rlx(par + p);
+        if (gp == p) return p;
+        st_rlx(par + x, gp);
+        x = gp;
+    }
+}
+__device__ __forceinline__ void uf_union(uint32_t* par, uint32_t a, uint32_t b) {
+    while (true) {
+        a = uf_find(par, a);
+        b = uf_find(par, b);
+        if (a == b) return;
+        if (a > b) { uint32_t t = a; a = b; b = t; }
+        if (atomicCAS(par + b, b, a) == b) return;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Point access.
+template <int LAYOUT>
+__device__ __forceinline__ void load_xyz(const uint8_t* fb, uint32_t i, const CgLaunch& L,
+                                         float& x, float& y, float& z) {
+    if (LAYOUT == CG_LAYOUT_XYZI16) {
+        const float4 v = *(const float4*)(fb + (uint64_t)i * 16);
+        x = v.x; y = v.y; z = v.z;
+    } else if (LAYOUT == CG_LAYOUT_PCL32) {
+        const float4 v = *(const float4*)(fb + (uint64_t)i * 32);
+        x = v.x; y = v.y; z = v.z;
+    } else {
+        const uint8_t* p = fb + (uint64_t)i * L.point_step;
+        x = L.off_x >= 0 ? *(const float*)(p + L.off_x) : 0.f;
+        y = L.off_y >= 0 ? *(const float*)(p + L.off_y) : 0.f;
+        z = L.off_z >= 0 ? *(const float*)(p + L.off_z) : 0.f;
+    }
+}
+template <int LAYOUT>
+__device__ __forceinline__ float4 load_xyzi(const uint8_t* fb, uint32_t i, const CgLaunch& L) {
+    if (LAYOUT == CG_LAYOUT_XYZI16) return *(const float4*)(fb + (uint64_t)i * 16);
+    if (LAYOUT == CG_LAYOUT_PCL32) {
+        const float4 v = *(const float4*)(fb + (uint64_t)i * 32);
+        const float in = *(const float*)(fb + (uint64_t)i * 32 + 16);
+        return make_float4(v.x, v.y, v.z, in);
+    }
+    float x, y, z;
+    load_xyz<CG_LAYOUT_GENERIC>(fb, i, L, x, y, z);
+    const uint8_t* p = fb + (uint64_t)i * L.point_step;
+    const float in = L.off_i >= 0 ? *(const float*)(p + L.off_i) : 0.f;
+    return make_float4(x, y, z, in);
+}
+
+// filter_points_position (src/cone_detection.cpp:195-201): true = keep.
+__device__ __forceinline__ bool position_keep(const CgDevParams& P, float x, float y, float z, float a) {
+    const double S = cg_sumsq_d(x, y, z);
+    const bool rm = (z < P.level_f) || (S >= P.s_far) || (S < P.s_near) || (a <= P.ang_lo) ||
+                    (a >= P.ang_hi);
+    return !rm;
+}
+
+// ------------------------------------------------------------------------------------------
+// Backend: voxel grid + Euclidean clustering + centroids for one frame of M survivors in W.P.
+__device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* fs, const CgLaunch& L,
+                                        const CgDevParams& P, uint32_t f, uint32_t flags) {
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    uint32_t* red = fs->red;
+    // ---- voxel grid: getMinMax3D over finite points ----
+    {
+        float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        uint32_t nf = 0;
+        for (uint32_t j = tid; j < M; j += CG_BLOCK) {
+            const float4 p = W.P[j];
+            if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+                mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+                mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+                nf++;
+            }
+        }
+        float r[6];
+#pragma unroll
+        for (int a = 0; a < 3; a++) { r[a] = wave_min(mn[a]); r[3 + a] = wave_max(mx[a]); }
+        nf = wave_sum(nf);
+        if (l == 0) {
+#pragma unroll
+            for (int a = 0; a < 6; a++) red[8 * w + a] = __float_as_uint(r[a]);
+            red[8 * w + 6] = nf;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t nfin = 0;
+            for (int q = 0; q < WAVES; q++) {
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    bmn[a] = fminf(bmn[a], __uint_as_float(red[8 * q + a]));
+                    bmx[a] = fmaxf(bmx[a], __uint_as_float(red[8 * q + 3 + a]));
+                }
+                nfin += red[8 * q + 6];
+            }
+            uint32_t pass = 0;
+            int min_b[3] = {0, 0, 0}, div_b[3] = {1, 1, 1};
+            if (nfin > 0) {
+                double prod = 1.0;
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    const float span = (bmx[a] - bmn[a]) * P.inv_leaf[a];
+                    const double d = span >= 9.0e18f ? 9.0e18 : (double)((int64_t)span + 1);
+                    prod *= d;
+                }
+                if (prod > 2147483647.0) pass = 1;
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    min_b[a] = (int)floorf(bmn[a] * P.inv_leaf[a]);
+                    const int max_b = (int)floorf(bmx[a] * P.inv_leaf[a]);
+                    div_b[a] = max_b - min_b[a] + 1;
+                }
+            }
+            fs->scal[S_PASS] = pass;
+            fs->scal[S_MF] = nfin;
+            fs->scal[S_MINB0] = (uint32_t)min_b[0];
+            fs->scal[S_MINB1] = (uint32_t)min_b[1];
+            fs->scal[S_MINB2] = (uint32_t)min_b[2];
+            fs->scal[S_MUL1] = (uint32_t)div_b[0];
+            fs->scal[S_MUL2] = (uint32_t)div_b[0] * (uint32_t)div_b[1];
+        }
+        __syncthreads();
+    }
+    const uint32_t pass = fs->scal[S_PASS];
+    uint32_t V;
+    float4* const vox_out = L.vox + (uint64_t)f * L.cap;
+    if (pass) {
+        // overflow guard: output = *input_ (all M points, in order)
+        for (uint32_t j = tid; j < M; j += CG_BLOCK) { W.VOX[j] = W.P[j]; vox_out[j] = W.P[j]; }
+        V = M;
+        flags |= 0x1u;
+        __syncthreads();
+    } else {
+        const float mnb0 = (float)(int)fs->scal[S_MINB0], mnb1 = (float)(int)fs->scal[S_MINB1],
+                    mnb2 = (float)(int)fs->scal[S_MINB2];
+        const uint32_t mul1 = fs->scal[S_MUL1], mul2 = fs->scal[S_MUL2];
+        uint32_t n2 = 1;
+        while (n2 < M) n2 <<= 1;
+        for (uint32_t j = tid; j < n2; j += CG_BLOCK) {
+            uint64_t key = ~0ull;
+            if (j < M) {
+                const float4 p = W.P[j];
+                if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+                    const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
+                    const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
+                    const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
+                    const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+                    key = ((uint64_t)idx << 32) | j;
+                }
+            }
+            W.KEY[j] = key;
+        }
+        __syncthreads();
+        bitonic_sort(W.KEY, n2);
+        const uint32_t Mf = fs->scal[S_MF];
+        V = block_scan(
+            Mf,
+            [&](uint32_t j) -> uint32_t { return (j == 0 || (W.KEY[j] >> 32) != (W.KEY[j - 1] >> 32)) ? 1u : 0u; },
+            [&](uint32_t j, uint32_t e) {
+                if (j == 0 || (W.KEY[j] >> 32) != (W.KEY[j - 1] >> 32)) W.A[e] = j;
+            },
+            red);
+        if (tid == 0) W.A[V] = Mf;
+        __syncthreads();
+        // CentroidPoint<PointXYZI>: float sums in ascending point position, / float(n)
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+            const uint32_t s = W.A[v], e = W.A[v + 1];
+            float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+            for (uint32_t j = s; j < e; j++) {
+                const float4 p = W.P[(uint32_t)W.KEY[j]];
+                sx += p.x; sy += p.y; sz += p.z; si += p.w;
+            }
+            const float n = (float)(e - s);
+            const float4 c = make_float4(sx / n, sy / n, sz / n, si / n);
+            W.VOX[v] = c;
+            vox_out[v] = c;
+        }
+        __syncthreads();
+    }
+    // ---- Euclidean clustering over the V voxel points ----
+    uint32_t C = 0;
+    if (V > 0) {
+        {   // neighbour-grid origin
+            float mn[3] = {INFINITY, INFINITY, INFINITY};
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+                const float4 p = W.VOX[v];
+                mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+            }
+#pragma unroll
+            for (int a = 0; a < 3; a++) mn[a] = wave_min(mn[a]);
+            if (l == 0) {
+#pragma unroll
+                for (int a = 0; a < 3; a++) red[8 * w + a] = __float_as_uint(mn[a]);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                float o[3] = {INFINITY, INFINITY, INFINITY};
+                for (int q = 0; q < WAVES; q++)
+#pragma unroll
+                    for (int a = 0; a < 3; a++) o[a] = fminf(o[a], __uint_as_float(red[8 * q + a]));
+#pragma unroll
+                for (int a = 0; a < 3; a++) if (!isfinite(o[a])) o[a] = 0.f;
+                fs->scal[S_ORGX] = __float_as_uint(o[0]);
+                fs->scal[S_ORGY] = __float_as_uint(o[1]);
+                fs->scal[S_ORGZ] = __float_as_uint(o[2]);
+            }
+            __syncthreads();
+        }
+        const float ox = __uint_as_float(fs->scal[S_ORGX]), oy = __uint_as_float(fs->scal[S_ORGY]),
+                    oz = __uint_as_float(fs->scal[S_ORGZ]);
+        auto cell = [&](float c, float o) -> uint32_t {
+            const float q = floorf((c - o) * P.cell_inv);
+            if (!(q >= 0.f)) return 0u;           // NaN or below origin
+            return q >= 1023.f ? 1023u : (uint32_t)q;
+        };
+        auto cell_key = [&](const float4& p) -> uint32_t {
+            return (cell(p.z, oz) << 20) | (cell(p.y, oy) << 10) | cell(p.x, ox);
+        };
+        uint32_t n2 = 1;
+        while (n2 < V) n2 <<= 1;
+        for (uint32_t j = tid; j < n2; j += CG_BLOCK)
+            W.KEY[j] = j < V ? (((uint64_t)cell_key(W.VOX[j]) << 16) | j) : ~0ull;
+        __syncthreads();
+        bitonic_sort(W.KEY, n2);
+        const uint32_t U = block_scan(
+            V,
+            [&](uint32_t j) -> uint32_t { return (j == 0 || (W.KEY[j] >> 16) != (W.KEY[j - 1] >> 16)) ? 1u : 0u; },
+            [&](uint32_t j, uint32_t e) {
+                const uint64_t k = W.KEY[j];
+                W.ORD[j] = (uint32_t)(k & 0xffffu);
+                if (j == 0 || (k >> 16) != (W.KEY[j - 1] >> 16)) { W.UK[e] = (uint32_t)(k >> 16); W.A[e] = j; }
+            },
+            red);
+        if (tid == 0) W.A[U] = V;
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) { W.PAR[v] = v; W.CNT[v] = 0; }
+        __syncthreads();
+        // union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple)
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+            const float4 q = W.VOX[v];
+            const uint32_t cx = cell(q.x, ox), cy = cell(q.y, oy), cz = cell(q.z, oz);
+            const uint32_t xlo = cx > 0 ? cx - 1 : 0, xhi = cx < 1023 ? cx + 1 : 1023;
+            for (int dz = -1; dz <= 1; dz++) {
+                const int zz = (int)cz + dz;
+                if (zz < 0 || zz > 1023) continue;
+                for (int dy = -1; dy <= 1; dy++) {
+                    const int yy = (int)cy + dy;
+                    if (yy < 0 || yy > 1023) continue;
+                    const uint32_t lo = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xlo;
+                    const uint32_t hi = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xhi;
+                    uint32_t a = 0, b = U;
+                    while (a < b) {
+                        const uint32_t m = (a + b) >> 1;
+                        if (W.UK[m] < lo) a = m + 1; else b = m;
+                    }
+                    for (uint32_t u = a; u < U && W.UK[u] <= hi; u++) {
+                        const uint32_t e = W.A[u + 1];
+                        for (uint32_t j = W.A[u]; j < e; j++) {
+                            const uint32_t o = W.ORD[j];
+                            if (o <= v) continue;
+                            const float4 p = W.VOX[o];
+                            const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+                            float acc = ddx * ddx;
+                            acc = acc + ddy * ddy;
+                            acc = acc + ddz * ddz;
+                            if (acc < P.r2) uf_union(W.PAR, v, o);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+            W.LAB[v] = (int32_t)uf_find(W.PAR, v);
+            W.ORD[v] = 0xffffffffu;   // becomes root -> output rank
+        }
+        __syncthreads();
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) atomicAdd(&W.CNT[W.LAB[v]], 1u);
+        __syncthreads();
+        // kept components in discovery (seed) order; DROOT/DSZ/RANK/FIN overlay W.P (dead)
+        uint32_t* const DROOT = (uint32_t*)W.P;
+        uint32_t* const DSZ = DROOT + V;
+        uint32_t* const RANK = DSZ + V;
+        uint32_t* const FIN = RANK + V;
+        C = block_scan(
+            V,
+            [&](uint32_t v) -> uint32_t {
+                const uint32_t c = W.CNT[v];
+                return ((uint32_t)W.LAB[v] == v && c >= P.min_cl && c <= P.max_cl) ? 1u : 0u;
+            },
+            [&](uint32_t v, uint32_t d) {
+                const uint32_t c = W.CNT[v];
+                if ((uint32_t)W.LAB[v] == v && c >= P.min_cl && c <= P.max_cl) { DROOT[d] = v; DSZ[d] = c; }
+            },
+            red);
+        // cluster order: PCL sorts the reversed discovery list ascending by size with std::sort
+        if (C > CG_SORT_THRESHOLD) {
+            if (tid == 0) {
+                uint64_t* rec = W.KEY;
+                for (uint32_t i = 0; i < C; i++) {
+                    const uint32_t d = C - 1 - i;
+                    rec[i] = ((uint64_t)DSZ[d] << 32) | d;
+                }
+                cg_std_sort(rec, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, fs->stk);
+                for (uint32_t k = 0; k < C; k++) {
+                    const uint32_t d = (uint32_t)rec[C - 1 - k];
+                    FIN[k] = d;
+                    RANK[d] = k;
+                }
+            }
+        } else {
+            // <= 16 clusters: insertion sort is stable, so order = (size desc, seed asc)
+            for (uint32_t d = tid; d < C; d += CG_BLOCK) {
+                const uint32_t sd = DSZ[d];
+                uint32_t r = 0;
+                for (uint32_t e = 0; e < C; e++) {
+                    const uint32_t se = DSZ[e];
+                    r += (se > sd) || (se == sd && e < d);
+                }
+                RANK[d] = r;
+                FIN[r] = d;
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = block_scan(
+            C, [&](uint32_t k) -> uint32_t { return DSZ[FIN[k]]; },
+            [&](uint32_t k, uint32_t e) { W.OFF[k] = e; }, red);
+        if (tid == 0) W.OFF[C] = tot;
+        for (uint32_t d = tid; d < C; d += CG_BLOCK) W.ORD[DROOT[d]] = RANK[d];
+        for (uint32_t k = tid; k < C; k += CG_BLOCK) W.CNT[k] = 0;   // CSR cursors
+        __syncthreads();
+        int32_t* const lab_out = L.lab + (uint64_t)f * L.cap;
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+            const int32_t lb = (int32_t)W.ORD[(uint32_t)W.LAB[v]];
+            W.LAB[v] = lb;
+            lab_out[v] = lb;
+        }
+        __syncthreads();
+        // stable counting sort of voxel indices by cluster rank (one wave, ascending v)
+        int32_t* const idx_out = L.idx + (uint64_t)f * L.cap;
+        if (w == 0) {
+            for (uint32_t base = 0; base < V; base += 64) {
+                const uint32_t v = base + l;
+                const int32_t k = v < V ? W.LAB[v] : -1;
+                uint64_t pending = __ballot(k >= 0);
+                while (pending) {
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
+                    const int32_t kk = __shfl(k, (int)leader, 64);
+                    const uint64_t same = __ballot(k == kk) & pending;
+                    uint32_t cur = 0;
+                    if (l == leader) cur = atomicAdd(&W.CNT[kk], (uint32_t)__popcll(same));
+                    cur = __shfl(cur, (int)leader, 64);
+                    if (k == kk) {
+                        const uint32_t pos = W.OFF[kk] + cur + (uint32_t)__popcll(same & ((1ull << l) - 1ull));
+                        W.IDX[pos] = v;
+                        idx_out[pos] = (int32_t)v;
+                    }
+                    pending &= ~same;
+                }
+            }
+        }
+        __syncthreads();
+        // src/cone_detection.cpp:261-279: xy mean (float, ascending index, starts at 0), then
+        // p += p / len * ext with len = float(sqrt((double)x^2 + (double)y^2 + 0))
+        float2* const cen_out = L.cen + (uint64_t)f * L.cap;
+        int32_t* const off_out = L.offs + (uint64_t)f * (L.cap + 1);
+        for (uint32_t k = tid; k < C; k += CG_BLOCK) {
+            const uint32_t s = W.OFF[k], e = W.OFF[k + 1];
+            float x = 0.0f, y = 0.0f;
+            for (uint32_t i = s; i < e; i++) {
+                const float4 p = W.VOX[W.IDX[i]];
+                x += p.x;
+                y += p.y;
+            }
+            const int j = (int)(e - s);
+            const float px = x / (float)j, py = y / (float)j;
+            const double S = ((double)px * (double)px + (double)py * (double)py) + 0.0;
+            const float len = (float)__builtin_sqrt(S);
+            const float qx = (float)((double)px + (double)(px / len) * P.ext);
+            const float qy = (float)((double)py + (double)(py / len) * P.ext);
+            cen_out[k] = make_float2(qx, qy);
+        }
+        for (uint32_t k = tid; k <= C; k += CG_BLOCK) off_out[k] = (int32_t)W.OFF[k];
+    } else if (tid == 0) {
+        L.offs[(uint64_t)f * (L.cap + 1)] = 0;
+    }
+    if (tid == 0) {
+        uint32_t* h = L.hdr + (uint64_t)f * 8;
+        h[CG_HDR_M] = M;
+        h[CG_HDR_V] = V;
+        h[CG_HDR_C] = C;
+        h[CG_HDR_FLAGS] = flags;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused per-frame kernel. PPT points per lane (PPT_REG of their z in VGPRs, the rest in LDS).
+template <int PPT, int LAYOUT, int KMODE>
+__global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
+    constexpr int PPT_REG = PPT < 32 ? PPT : 32;
+    constexpr int NSW = (PPT + 5) / 6;
+    constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
+    constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+    FrontShared* fs = (FrontShared*)smem;
+    BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
+    float* zl = (float*)bl;                       // z overlay for k >= PPT_REG
+
+    const uint32_t f = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
+    const uint32_t N = L.n_points;
+
+    if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
+    if (tid < 64) fs->scal[tid] = 0;
+    __syncthreads();
+
+    // ---- pass 1 ----
+    float zr[PPT_REG];
+    uint32_t sw[NSW];
+    uint64_t posm = 0;
+#pragma unroll
+    for (int q = 0; q < NSW; q++) sw[q] = 0;
+    int cur_s = -1;
+    float cur_m = 0.f;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
+        const bool valid = i < N;
+        float x = 0.f, y = 0.f, z = 0.f;
+        if (valid) load_xyz<LAYOUT>(fb, i, L, x, y, z);
+        const float a = cg_atan2f(y, x);
+        if (FILTER) posm |= (uint64_t)(valid && position_keep(P, x, y, z, a)) << k;
+        if (GROUND) {
+            const int s = cg_sector(a);
+            sw[k / 6] |= (uint32_t)s << (5 * (k % 6));
+            if (k < PPT_REG) zr[k < PPT_REG ? k : 0] = z;
+            else zl[(k - PPT_REG) * CG_BLOCK + tid] = z;
+            if (valid && s < CG_NUM_BINS && z == z) {
+                if (s != cur_s) {
+                    if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+                    cur_s = s;
+                    cur_m = z;
+                } else {
+                    cur_m = fminf(cur_m, z);
+                }
+            }
+        }
+    }
+    if (GROUND && cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+    __syncthreads();
+    if (GROUND && tid < CG_NUM_BINS + 1) {
+        // (double)z < (double)low + 0.1  <=>  z < ceil_to_float(low + 0.1)  (ground_removal.cpp:75)
+        const float low = cg_fkey_inv(fs->sec_key[tid]);
+        fs->thr[tid] = cg_ceil_to_float((double)low + 0.1);
+    }
+    __syncthreads();
+
+    // ---- pass 2: keep bits and ballot counts ----
+    uint64_t keepm = 0;
+    uint32_t kground = 0;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
+        const bool valid = i < N;
+        bool keep_g = valid;
+        if (GROUND) {
+            const float z = k < PPT_REG ? zr[k < PPT_REG ? k : 0] : zl[(k - PPT_REG) * CG_BLOCK + tid];
+            const uint32_t s = (sw[k / 6] >> (5 * (k % 6))) & 31u;
+            keep_g = valid && !(z < fs->thr[s]);
+            kground += (uint32_t)__popcll(__ballot(keep_g));
+        }
+        const bool keep = FILTER ? (keep_g && ((posm >> k) & 1ull)) : keep_g;
+        keepm |= (uint64_t)keep << k;
+        const uint64_t b = __ballot(keep);
+        if (l == 0) fs->cnt[k * WAVES + w] = (uint32_t)__popcll(b);
+    }
+    if (GROUND && l == 0) atomicAdd(&fs->scal[S_K], kground);
+    __syncthreads();
+    // stable compaction offsets over (k, wave) in point order
+    const uint32_t Ms = block_scan(
+        PPT * WAVES, [&](uint32_t i) -> uint32_t { return fs->cnt[i]; },
+        [&](uint32_t i, uint32_t e) { fs->cnt[i] = e; }, fs->red);
+    const uint32_t K = GROUND ? fs->scal[S_K] : N;
+
+    if (KMODE == CG_KMODE_GROUND) {
+        // groundless cloud: K kept points in order, then N-K PointXYZI() (ground_removal.cpp:70-79)
+        float4* out = (float4*)(L.ground + (uint64_t)f * N * 32);
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint64_t b = __ballot((keepm >> k) & 1ull);
+            if ((keepm >> k) & 1ull) {
+                const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
+                const uint32_t dst = fs->cnt[k * WAVES + w] + (uint32_t)__popcll(b & ((1ull << l) - 1ull));
+                const float4 p = load_xyzi<LAYOUT>(fb, i, L);
+                out[2 * dst] = make_float4(p.x, p.y, p.z, 1.0f);
+                out[2 * dst + 1] = make_float4(p.w, 0.f, 0.f, 0.f);
+            }
+        }
+        for (uint32_t j = Ms + tid; j < N; j += CG_BLOCK) {
+            out[2 * j] = make_float4(0.f, 0.f, 0.f, 1.0f);
+            out[2 * j + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (tid == 0) {
+            uint32_t* h = L.hdr + (uint64_t)f * 8;
+            h[0] = N; h[1] = K; h[2] = N; h[3] = 0; h[4] = 0; h[5] = 0;
+        }
+        return;
+    }
+
+    // pipeline: the detector input is the groundless cloud, whose N-K trailing
+    // PointXYZI() points survive the filter iff P.zero_pass (src/cone_detection.cpp:195-201)
+    const uint32_t npad = (KMODE == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
+    const uint32_t M = Ms + npad;
+    const bool use_lds = M <= CG_MMAX;
+    uint32_t flags = use_lds ? 0u : 0x2u;
+    if (tid == 0) {
+        uint32_t* h = L.hdr + (uint64_t)f * 8;
+        h[0] = N;
+        h[1] = K;
+    }
+    __syncthreads();   // z overlay in LDS is dead from here on
+
+    Work W;
+    if (use_lds) {
+        W.P = bl->P; W.KEY = bl->KEY; W.VOX = bl->VOX; W.A = bl->A; W.PAR = bl->PAR; W.CNT = bl->CNT;
+        W.UK = bl->UK; W.LAB = bl->LAB; W.ORD = bl->ORD; W.IDX = bl->IDX; W.OFF = bl->OFF;
+    } else {
+        W = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
+    }
+    // ---- pass 3: gather survivors in point order ----
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const uint64_t b = __ballot((keepm >> k) & 1ull);
+        if ((keepm >> k) & 1ull) {
+            const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
+            const uint32_t dst = fs->cnt[k * WAVES + w] + (uint32_t)__popcll(b & ((1ull << l) - 1ull));
+            W.P[dst] = load_xyzi<LAYOUT>(fb, i, L);
+        }
+    }
+    for (uint32_t j = tid; j < npad; j += CG_BLOCK) W.P[Ms + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    if (use_lds) {
+        Work WL;
+        WL.P = bl->P; WL.KEY = bl->KEY; WL.VOX = bl->VOX; WL.A = bl->A; WL.PAR = bl->PAR; WL.CNT = bl->CNT;
+        WL.UK = bl->UK; WL.LAB = bl->LAB; WL.ORD = bl->ORD; WL.IDX = bl->IDX; WL.OFF = bl->OFF;
+        backend(WL, M, fs, L, P, f, flags);
+    } else {
+        backend(W, M, fs, L, P, f, flags);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Launchers.
+template <int PPT, int LAYOUT>
+static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
+    const dim3 grid(L.n_frames), block(CG_BLOCK);
+    switch (kmode) {
+        case CG_KMODE_PIPELINE:
+            hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
+            break;
+        case CG_KMODE_DETECT:
+            hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
+            break;
+        default:
+            hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_GROUND>), grid, block, 0, s, L, P);
+            break;
+    }
+    return hipGetLastError();
+}
+
+int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
+    if (L.n_frames == 0) return hipSuccess;
+    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 &&
+                        L.off_i == 12;
+    if (L.n_points <= 16 * CG_BLOCK) {
+        return xyzi16 ? launch3<16, CG_LAYOUT_XYZI16>(L, P, kmode, s)
+                      : launch3<16, CG_LAYOUT_GENERIC>(L, P, kmode, s);
+    }
+    return xyzi16 ? launch3<64, CG_LAYOUT_XYZI16>(L, P, kmode, s)
+                  : launch3<64, CG_LAYOUT_GENERIC>(L, P, kmode, s);
+}
+
+// ------------------------------------------------------------------------------------------
+// Self-test kernels: the device restatements, evaluated element-wise for host comparison.
+__global__ void cg_selftest_atan2f_kernel(const float* y, const float* x, float* out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float a = cg_atan2f(y[i], x[i]);
+        out[2 * i] = a;
+        out[2 * i + 1] = (float)cg_sector(a);
+    }
+}
+__global__ void cg_selftest_sqrt_kernel(const double* in, double* out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = __builtin_sqrt(in[i]);
+}
+int cg_launch_selftest_atan2f(const float* y, const float* x, float* out, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(cg_selftest_atan2f_kernel, dim3((n + 255) / 256), dim3(256), 0, s, y, x, out, n);
+    return hipGetLastError();
+}
+int cg_launch_selftest_sqrt(const double* in, double* out, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(cg_selftest_sqrt_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, out, n);
+    return hipGetLastError();
+}

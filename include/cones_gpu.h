@@ -1,0 +1,191 @@
+/* cones_gpu.h — C-ABI of the MI355X (gfx950) LiDAR cone-detection hot path.
+ *
+ * Drop-in for the bodies of the two ROS callbacks of dmn-sjk/cones_perception
+ * (reference paths relative to its repository root):
+ *   - GroundRemover::cloud_handler   src/ground_removal.cpp:50-89  (lines 51-79 replaced)
+ *   - ConeDetector::cloud_handler    src/cone_detection.cpp:130-187 (lines 138-167 and the
+ *     centroid arithmetic 261-279 replaced; tracking 282-339, colour RPC 342-363 and the
+ *     4-topic publish 177-186 stay in the node)
+ * The reference has no plugin API; its seam is those callback bodies, which call PCL
+ * (fromROSMsg, VoxelGrid, search::KdTree, EuclideanClusterExtraction, toROSMsg) and libm.
+ * INTEGRATION.md shows the patched callbacks. Plain C types only: no torch, no C++ in
+ * signatures, no exceptions across the boundary.
+ *
+ * Threading: a handle is not thread-safe (the reference runs one callback at a time under
+ * ros::spin, src/ground_removal.cpp:47, src/cone_detection.cpp:127). Single-frame calls are
+ * synchronous. Batch calls are asynchronous on the given HIP stream.
+ */
+#ifndef CONES_GPU_H
+#define CONES_GPU_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------- */
+#define CG_OK          0
+#define CG_E_INVALID   1   /* bad argument / unsupported cloud layout */
+#define CG_E_DEVICE    2   /* HIP runtime error or no gfx950 device */
+#define CG_E_OOM       3   /* device or pinned host allocation failed */
+#define CG_E_CAPACITY  4   /* frame larger than the batch engine supports (N > 65536) */
+
+/* result flags (cg_detect_result.flags, batch header word CG_HDR_FLAGS) */
+#define CG_F_VOXEL_PASSTHROUGH 0x1u  /* PCL VoxelGrid overflow guard hit: voxel cloud = input */
+#define CG_F_GLOBAL_SCRATCH    0x2u  /* frame too large for the LDS path; ran from HBM scratch */
+#define CG_F_ORDER_CANONICAL   0x4u  /* >16 clusters: order is (size desc, seed asc); PCL's
+                                        std::sort may order equal-size clusters differently */
+
+/* ---- parameters --------------------------------------------------------------------- */
+/* Field names are the YAML keys, misspellings kept (config/*.yaml). */
+typedef struct cg_params {
+    /* config/ground_removal_params.yaml; defaults src/ground_removal.cpp:18-19 */
+    int32_t num_of_sectors;          /* read but inert: sector width is fixed at 22 deg (G1) */
+    float   default_lowest_point;
+    /* config/cones_detection_params_*.yaml; defaults src/cone_detection.cpp:27-43 */
+    double  distance_treshold_max;
+    double  distance_treshold_min;
+    double  level_threshold;
+    double  angle_threshold;         /* degrees */
+    int32_t min_cluster_size;
+    int32_t max_cluster_size;
+    double  cone_position_extension_length;
+    double  voxel_filter_leaf_size_x;
+    double  voxel_filter_leaf_size_y;
+    double  voxel_filter_leaf_size_z;
+    double  cones_matching_dist_theshold;  /* tracking only (out of path); carried for the node */
+} cg_params;
+
+/* Class-member defaults of the reference (src/ground_removal.cpp:18-19,
+ * src/cone_detection.cpp:27-43), i.e. what a node uses for a missing ROS param. */
+void cg_params_init(cg_params* p);
+
+/* ---- input cloud -------------------------------------------------------------------- */
+/* Borrowed description of a sensor_msgs/PointCloud2. Fields are located by byte offset; pass
+ * -1 for a field that is absent or not FLOAT32 x1 (pcl::fromROSMsg then leaves it at 0).
+ * Reproducing src/cone_detection.cpp:142-151 (detector input without an intensity field gets
+ * a fake FLOAT32 field at offset 0) is the caller's job: pass off_intensity = 0. */
+typedef struct cg_cloud_view {
+    const void* data;        /* PointCloud2::data (host memory for the single-frame calls) */
+    uint32_t width, height;  /* N = width * height */
+    uint32_t point_step, row_step;
+    int32_t  off_x, off_y, off_z, off_intensity;
+    uint8_t  is_dense;
+} cg_cloud_view;
+
+/* ---- handle ------------------------------------------------------------------------- */
+typedef struct cg_handle cg_handle;
+
+/* Create a handle on HIP device `device` (one stream, lazily grown device buffers). */
+int  cg_create(const cg_params* params, int device, cg_handle** out);
+int  cg_destroy(cg_handle* h);
+int  cg_set_params(cg_handle* h, const cg_params* params);
+/* Thread-local message for the last failing call on this thread ("" if none). */
+const char* cg_last_error(void);
+
+/* ---- single-frame calls (ROS drop-in) ------------------------------------------------ */
+/* GroundRemover::cloud_handler body (src/ground_removal.cpp:51-79): per-22-degree-sector
+ * lowest z, keep points with !(z < low + 0.1), stable, then zero-pad back to N points
+ * (pcl::PointXYZI() = x=y=z=0, data[3]=1, intensity=0). Output data is N x 32 B in PCL
+ * PointXYZI layout (x,y,z @0,4,8; 1.0f @12; intensity @16; 12 zero bytes) — the bytes
+ * toROSMsg would publish. Library-owned; valid until the next call on the handle. */
+typedef struct cg_ground_result {
+    uint32_t n_points;       /* N, preserved (G5) */
+    uint32_t n_kept;         /* K */
+    uint32_t width, height;  /* organized shape preserved (resize keeps width*height == N) */
+    const uint8_t* data;     /* N * 32 bytes */
+} cg_ground_result;
+int cg_ground_remove(cg_handle* h, const cg_cloud_view* in, cg_ground_result* out);
+
+/* ConeDetector::cloud_handler hot part (src/cone_detection.cpp:156-175, 189-220, 240-279):
+ * filter_points_position -> VoxelGrid -> KdTree + EuclideanClusterExtraction -> per-cluster
+ * xy centroid pushed 0.05 m outward. Arrays are library-owned, valid until the next call. */
+typedef struct cg_detect_result {
+    uint32_t n_points;           /* N of the input */
+    uint32_t n_kept;             /* K (pipeline only; = N for cg_detect) */
+    uint32_t n_filtered;         /* M, points surviving filter_points_position */
+    uint32_t n_voxels;           /* V, points of the VoxelGrid output */
+    uint32_t n_clusters;         /* C */
+    uint32_t flags;              /* CG_F_* */
+    const float*   voxels;           /* V x 4: x, y, z, intensity (PCL output order) */
+    const int32_t* labels;           /* V: cluster rank in output order, or -1 */
+    const int32_t* cluster_offsets;  /* C + 1 */
+    const int32_t* cluster_indices;  /* cluster_offsets[C] voxel indices, ascending per cluster */
+    const float*   centroids;        /* C x 2: x, y after the radial push (z = 0) */
+} cg_detect_result;
+int cg_detect(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out);
+
+/* ground_removal -> cone_detection composition of launch/cones_perception.launch:17-37
+ * (ground_removal:=true), fused: the detector sees exactly the groundless cloud the ground
+ * node would publish (K kept points in order, then N-K zero points). */
+int cg_pipeline(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out);
+
+/* ---- batch engine (device-resident frames) ------------------------------------------ */
+/* n_frames uniform frames of n_points PointCloud2 points each, contiguous rows
+ * (row_step = n_points * point_step), frame f at d_data + f * frame_stride (device memory). */
+typedef struct cg_batch {
+    const void* d_data;
+    uint64_t frame_stride;
+    uint32_t n_frames, n_points, point_step;
+    int32_t  off_x, off_y, off_z, off_intensity;
+    uint8_t  is_dense;
+} cg_batch;
+
+#define CG_MODE_PIPELINE 0   /* ground removal + detector (cg_pipeline semantics) */
+#define CG_MODE_DETECT   1   /* detector only (cg_detect semantics) */
+
+/* Enqueue one pass of the hot path over the batch on `hip_stream` (hipStream_t; NULL = the
+ * handle's own stream). Results stay on the device until the next batch call. */
+int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream);
+
+/* Per-frame header words in the device result buffer. */
+#define CG_HDR_N      0
+#define CG_HDR_K      1
+#define CG_HDR_M      2
+#define CG_HDR_V      3
+#define CG_HDR_C      4
+#define CG_HDR_FLAGS  5
+#define CG_HDR_WORDS  8
+
+typedef struct cg_batch_results {
+    uint32_t n_frames;
+    uint32_t capacity;                 /* per-frame slot length (points) of each array */
+    const uint32_t* d_header;          /* n_frames x CG_HDR_WORDS */
+    const float*    d_voxels;          /* n_frames x capacity x 4 */
+    const int32_t*  d_labels;          /* n_frames x capacity */
+    const int32_t*  d_cluster_offsets; /* n_frames x (capacity + 1) */
+    const int32_t*  d_cluster_indices; /* n_frames x capacity */
+    const float*    d_centroids;       /* n_frames x capacity x 2 */
+} cg_batch_results;
+int cg_batch_results_get(cg_handle* h, cg_batch_results* out);
+/* Synchronise the batch stream and copy one frame's results to handle-owned host buffers. */
+int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out);
+
+/* ---- device self-checks (tests) ------------------------------------------------------ */
+/* Evaluate the device atan2f / sector / sqrt restatements on n host inputs (device round
+ * trip), for comparison with the host libm in tests. */
+int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out, uint32_t n);
+int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
+
+/* Exported library version string. */
+const char* cg_version(void);
+
+/* ---- synthetic frames (harness; src-free of any GPU call) ---------------------------- */
+typedef struct cg_synth_cfg {
+    uint32_t rings, cols;            /* N = rings * cols */
+    float    elev_min_deg, elev_max_deg, mount_height, wall_radius, range_noise;
+    uint32_t point_step;             /* 16 (xyzi) or 32 (PCL PointXYZI layout) */
+    uint32_t column_major;           /* 1: point = col*rings + ring; 0: ring*cols + col */
+    uint32_t cones_per_row;
+    uint32_t clutter;                /* extra posts (dense scenes) */
+    uint64_t seed;
+} cg_synth_cfg;
+void cg_synth_default(cg_synth_cfg* c);
+int  cg_synth_frames(const cg_synth_cfg* cfg, uint64_t first_frame, uint32_t n_frames,
+                     void* out, uint64_t frame_stride, uint32_t n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CONES_GPU_H */

@@ -1,0 +1,409 @@
+// cg_oracle.cpp — CPU restatement of the dmn-sjk/cones_perception LiDAR hot path.
+//
+// TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// leg may load this library, and only as the checker / the timed CPU baseline. The product
+// (cones_perception_amd, libcones_gpu.so) never links or calls it.
+//
+// PARITY UNPINNED: the reference ships no tests, golden vectors or fixtures (SURVEY.md §4,
+// §8c), and it cannot be built here (ROS, PCL 1.10, FLANN 1.9.1, Eigen and Boost are absent).
+// This file restates, from the reference sources and from PCL 1.10 / FLANN 1.9.1 as shipped
+// with ROS Noetic (not present here, restated from their published algorithms):
+//   decode            pcl::fromROSMsg field mapping by name           src/ground_removal.cpp:54
+//   ground removal    GroundRemover::cloud_handler                    src/ground_removal.cpp:56-79
+//   position filter   ConeDetector::filter_points_position            src/cone_detection.cpp:189-204
+//   distance          perception_handling::euclidan_dist              src/perception_handling/utils.cpp:32-34
+//   voxel grid        pcl::VoxelGrid<PointXYZI>::applyFilter (1.10)   called src/cone_detection.cpp:240-249
+//   clustering        pcl::extractEuclideanClusters + KdTreeFLANN     called src/cone_detection.cpp:206-220
+//   cluster order     std::sort(clusters.rbegin(), rend(), size<)     (EuclideanClusterExtraction::extract)
+//   centroid          ConeDetector::get_centroid_clouds (centroid)    src/cone_detection.cpp:261-279
+// libm calls (atan2f, sqrt, pow, floorf) go to the host glibc, as in the reference build.
+// Compiled with -O2 -ffp-contract=off and no -march flags (a stock x86-64 Noetic build has no
+// FMA). Defined divergences from the reference's undefined behaviour:
+//   G3  sector 16 (angles in [352,360) deg) is its own bin initialised to default_lowest_point;
+//       a NaN angle uses a never-updated bin (the reference indexes with int(NaN)).
+//   C1  the first cluster's x sum starts at 0 (uninitialised in src/cone_detection.cpp:264).
+// Voxel summation order: VOXEL_ORDER_PCL sorts with std::sort exactly as PCL (unstable
+// introsort order); VOXEL_ORDER_STABLE sums each voxel in ascending point index (the device
+// path's order). Both are exposed so tests can count where they differ.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+namespace {
+
+struct Params {
+    int32_t num_of_sectors;
+    float default_lowest_point;
+    double distance_treshold_max, distance_treshold_min, level_threshold, angle_threshold;
+    int32_t min_cluster_size, max_cluster_size;
+    double cone_position_extension_length;
+    double voxel_filter_leaf_size_x, voxel_filter_leaf_size_y, voxel_filter_leaf_size_z;
+    double cones_matching_dist_theshold;
+};  // layout-identical to cg_params (include/cones_gpu.h)
+
+struct View {
+    const void* data;
+    uint32_t width, height, point_step, row_step;
+    int32_t off_x, off_y, off_z, off_intensity;
+    uint8_t is_dense;
+};  // layout-identical to cg_cloud_view
+
+// pcl::PointXYZI: x,y,z, data[3] = 1, intensity, padding (32 bytes).
+struct Pt {
+    float x = 0.f, y = 0.f, z = 0.f, w = 1.f;
+    float intensity = 0.f, pad[3] = {0.f, 0.f, 0.f};
+};
+
+float read_f32(const uint8_t* p, int32_t off) {
+    if (off < 0) return 0.f;
+    float v;
+    std::memcpy(&v, p + off, 4);
+    return v;
+}
+
+// pcl::fromROSMsg: row-major over height x width, fields copied by offset.
+std::vector<Pt> decode(const View& v) {
+    std::vector<Pt> out((size_t)v.width * v.height);
+    const uint8_t* base = (const uint8_t*)v.data;
+    for (uint32_t r = 0; r < v.height; r++)
+        for (uint32_t c = 0; c < v.width; c++) {
+            const uint8_t* p = base + (size_t)r * v.row_step + (size_t)c * v.point_step;
+            Pt& q = out[(size_t)r * v.width + c];
+            q.x = read_f32(p, v.off_x);
+            q.y = read_f32(p, v.off_y);
+            q.z = read_f32(p, v.off_z);
+            q.intensity = read_f32(p, v.off_intensity);
+        }
+    return out;
+}
+
+// ---------------- ground removal: src/ground_removal.cpp:56-79 ----------------
+const float kSectorAngleRad = (float)((360 / 16) * M_PI / 180);  // member init, ground_removal.cpp:20
+
+int sector_of(float y, float x) {
+    float atan_angle = atan2f(y, x);
+    float angle = (atan_angle < 0) ? atan_angle += 2 * M_PI : atan_angle;
+    if (std::isnan(angle)) return 17;                     // defined: NaN bin, never updated
+    return (int)std::floor(angle / kSectorAngleRad);      // 0..16
+}
+
+size_t ground_remove(std::vector<Pt>& cloud, const Params& prm) {
+    const size_t n = cloud.size();
+    std::vector<float> lowest(18, prm.default_lowest_point);   // 17 addressed bins + NaN bin
+    for (const Pt& p : cloud) {
+        int s = sector_of(p.y, p.x);
+        if (s < 17 && lowest[s] > p.z) lowest[s] = p.z;
+    }
+    auto it = std::remove_if(cloud.begin(), cloud.end(), [&](const Pt& p) {
+        return p.z < lowest[sector_of(p.y, p.x)] + 0.1;   // float + double -> double compare
+    });
+    cloud.erase(it, cloud.end());
+    size_t kept = cloud.size();
+    cloud.resize(n);    // PointCloud::resize(n): appends PointXYZI()
+    return kept;
+}
+
+// ---------------- detector: src/cone_detection.cpp:189-204 ----------------
+float euclidan_dist(float x1, float y1, float z1, float x2, float y2, float z2) {
+    return std::sqrt(std::pow(x1 - x2, 2) + std::pow(y1 - y2, 2) + std::pow(z1 - z2, 2));
+}
+
+void filter_points_position(std::vector<Pt>& cloud, const Params& prm) {
+    auto it = std::remove_if(cloud.begin(), cloud.end(), [&](const Pt& p) {
+        return p.z < prm.level_threshold ||
+               euclidan_dist(p.x, p.y, p.z, 0, 0, 0) > prm.distance_treshold_max ||
+               euclidan_dist(p.x, p.y, p.z, 0, 0, 0) < prm.distance_treshold_min ||
+               -prm.angle_threshold * M_PI / 180 >= atan2f(p.y, p.x) ||
+               atan2f(p.y, p.x) >= prm.angle_threshold * M_PI / 180;
+    });
+    cloud.erase(it, cloud.end());
+}
+
+// ---------------- pcl::VoxelGrid<PointXYZI>::applyFilter (PCL 1.10) ----------------
+struct IdxPair {
+    unsigned int idx, cloud_point_index;
+    bool operator<(const IdxPair& o) const { return idx < o.idx; }
+};
+
+bool voxel_grid(const std::vector<Pt>& in, bool is_dense, const Params& prm, int order,
+                std::vector<Pt>& out) {
+    // setLeafSize(float,float,float): inverse = Ones / leaf (float division)
+    const float leaf[3] = {(float)prm.voxel_filter_leaf_size_x, (float)prm.voxel_filter_leaf_size_y,
+                           (float)prm.voxel_filter_leaf_size_z};
+    const float inv[3] = {1.0f / leaf[0], 1.0f / leaf[1], 1.0f / leaf[2]};
+    auto finite = [](const Pt& p) {
+        return std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z);
+    };
+    // getMinMax3D (skips non-finite when !is_dense; our inputs treat NaN that way always)
+    float mn[3] = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(),
+                   std::numeric_limits<float>::max()};
+    float mx[3] = {-std::numeric_limits<float>::max(), -std::numeric_limits<float>::max(),
+                   -std::numeric_limits<float>::max()};
+    size_t nfin = 0;
+    for (const Pt& p : in) {
+        if (!finite(p)) continue;
+        nfin++;
+        const float c[3] = {p.x, p.y, p.z};
+        for (int a = 0; a < 3; a++) { mn[a] = std::min(mn[a], c[a]); mx[a] = std::max(mx[a], c[a]); }
+    }
+    (void)is_dense;
+    out.clear();
+    if (nfin == 0) return false;
+    // overflow guard: output = *input_
+    int64_t d[3];
+    for (int a = 0; a < 3; a++) {
+        float span = (mx[a] - mn[a]) * inv[a];
+        d[a] = span >= 9.0e18f ? (int64_t)9e18 : (int64_t)span + 1;
+    }
+    const double prod = (double)d[0] * (double)d[1] * (double)d[2];
+    if (prod > (double)std::numeric_limits<int32_t>::max()) {
+        out = in;
+        return true;
+    }
+    int min_b[3], max_b[3], div_b[3];
+    for (int a = 0; a < 3; a++) {
+        min_b[a] = (int)std::floor(mn[a] * inv[a]);
+        max_b[a] = (int)std::floor(mx[a] * inv[a]);
+        div_b[a] = max_b[a] - min_b[a] + 1;
+    }
+    const int mul[3] = {1, div_b[0], div_b[0] * div_b[1]};
+    std::vector<IdxPair> index_vector;
+    index_vector.reserve(in.size());
+    for (size_t i = 0; i < in.size(); i++) {
+        const Pt& p = in[i];
+        if (!finite(p)) continue;
+        int ijk0 = (int)(std::floor(p.x * inv[0]) - (float)min_b[0]);
+        int ijk1 = (int)(std::floor(p.y * inv[1]) - (float)min_b[1]);
+        int ijk2 = (int)(std::floor(p.z * inv[2]) - (float)min_b[2]);
+        unsigned int idx = (unsigned int)ijk0 * (unsigned)mul[0] + (unsigned int)ijk1 * (unsigned)mul[1] +
+                           (unsigned int)ijk2 * (unsigned)mul[2];
+        index_vector.push_back({idx, (unsigned int)i});
+    }
+    if (order == 1) std::sort(index_vector.begin(), index_vector.end(), std::less<IdxPair>());
+    else std::stable_sort(index_vector.begin(), index_vector.end(), std::less<IdxPair>());
+    size_t index = 0;
+    while (index < index_vector.size()) {
+        size_t i = index + 1;
+        while (i < index_vector.size() && index_vector[i].idx == index_vector[index].idx) ++i;
+        // CentroidPoint<PointXYZI>: float sums of x,y,z and intensity, then / float(n)
+        float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+        for (size_t li = index; li < i; li++) {
+            const Pt& p = in[index_vector[li].cloud_point_index];
+            sx += p.x; sy += p.y; sz += p.z; si += p.intensity;
+        }
+        const float n = (float)(i - index);
+        Pt c;
+        c.x = sx / n; c.y = sy / n; c.z = sz / n; c.intensity = si / n;
+        out.push_back(c);
+        index = i;
+    }
+    return false;
+}
+
+// ---------------- radius search: KdTreeFLANN / FLANN KDTreeSingleIndex ----------------
+// Leaf size 15 as PCL configures FLANN. Distances are FLANN L2_Simple<float>:
+// acc = 0; acc += (q-p)^2 over x, y, z in float; neighbour iff acc < r2 (strict).
+// Results sorted by (distance, index) (KdTree(sorted = true)). Pruning is conservative so the
+// result is the exact float predicate over all points.
+struct KdTree {
+    struct Node { int lo, hi, left, right, dim; float split; };
+    const std::vector<Pt>* pts = nullptr;
+    std::vector<int> idx;
+    std::vector<Node> nodes;
+
+    int build(int lo, int hi) {
+        Node nd{lo, hi, -1, -1, 0, 0.f};
+        if (hi - lo > 15) {
+            float bmin[3] = {INFINITY, INFINITY, INFINITY}, bmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = lo; i < hi; i++) {
+                const Pt& p = (*pts)[idx[i]];
+                const float c[3] = {p.x, p.y, p.z};
+                for (int a = 0; a < 3; a++) { bmin[a] = std::min(bmin[a], c[a]); bmax[a] = std::max(bmax[a], c[a]); }
+            }
+            int dim = 0;
+            for (int a = 1; a < 3; a++) if (bmax[a] - bmin[a] > bmax[dim] - bmin[dim]) dim = a;
+            int mid = (lo + hi) / 2;
+            auto key = [&](int i) { const Pt& p = (*pts)[i]; return dim == 0 ? p.x : dim == 1 ? p.y : p.z; };
+            std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi,
+                             [&](int a, int b) { return key(a) < key(b); });
+            nd.dim = dim;
+            nd.split = key(idx[mid]);
+            int me = (int)nodes.size();
+            nodes.push_back(nd);
+            int l = build(lo, mid), r = build(mid, hi);
+            nodes[me].left = l; nodes[me].right = r;
+            return me;
+        }
+        nodes.push_back(nd);
+        return (int)nodes.size() - 1;
+    }
+    void init(const std::vector<Pt>& p) {
+        pts = &p;
+        idx.resize(p.size());
+        for (size_t i = 0; i < p.size(); i++) idx[i] = (int)i;
+        nodes.clear();
+        if (!p.empty()) build(0, (int)p.size());
+    }
+    void search(int node, const Pt& q, float r2, double rr, std::vector<std::pair<float, int>>& res) const {
+        const Node& nd = nodes[node];
+        if (nd.left < 0) {
+            for (int i = nd.lo; i < nd.hi; i++) {
+                const Pt& p = (*pts)[idx[i]];
+                float acc = 0.f, diff;
+                diff = q.x - p.x; acc += diff * diff;
+                diff = q.y - p.y; acc += diff * diff;
+                diff = q.z - p.z; acc += diff * diff;
+                if (acc < r2) res.push_back({acc, idx[i]});
+            }
+            return;
+        }
+        const float qv = nd.dim == 0 ? q.x : nd.dim == 1 ? q.y : q.z;
+        const double gap = (double)qv - (double)nd.split;     // exact in double
+        const int first = gap < 0 ? nd.left : nd.right, second = gap < 0 ? nd.right : nd.left;
+        search(first, q, r2, rr, res);
+        if (gap * gap <= rr) search(second, q, r2, rr, res);
+    }
+    void radius(const Pt& q, float r2, std::vector<std::pair<float, int>>& res) const {
+        res.clear();
+        if (nodes.empty()) return;
+        search(0, q, r2, (double)r2 * 1.0001 + 1e-12, res);
+        std::sort(res.begin(), res.end());   // (dist, index)
+    }
+};
+
+// pcl::extractEuclideanClusters (PCL 1.10) + EuclideanClusterExtraction::extract ordering.
+std::vector<std::vector<int>> euclidean_clusters(const std::vector<Pt>& cloud, float tolerance,
+                                                 unsigned min_pts, unsigned max_pts) {
+    std::vector<std::vector<int>> clusters;
+    if (cloud.empty()) return clusters;
+    KdTree tree;
+    tree.init(cloud);
+    const float r2 = (float)((double)tolerance * (double)tolerance);   // KdTreeFLANN::radiusSearch
+    const size_t nn_start_idx = 1;                                     // sorted results
+    std::vector<bool> processed(cloud.size(), false);
+    std::vector<std::pair<float, int>> nn;
+    for (size_t i = 0; i < cloud.size(); i++) {
+        if (processed[i]) continue;
+        std::vector<int> seed_queue{(int)i};
+        processed[i] = true;
+        for (size_t sq = 0; sq < seed_queue.size(); sq++) {
+            tree.radius(cloud[seed_queue[sq]], r2, nn);
+            for (size_t j = nn_start_idx; j < nn.size(); j++) {
+                int k = nn[j].second;
+                if (processed[k]) continue;
+                seed_queue.push_back(k);
+                processed[k] = true;
+            }
+        }
+        if (seed_queue.size() >= min_pts && seed_queue.size() <= max_pts) {
+            std::sort(seed_queue.begin(), seed_queue.end());
+            seed_queue.erase(std::unique(seed_queue.begin(), seed_queue.end()), seed_queue.end());
+            clusters.push_back(seed_queue);
+        }
+    }
+    std::sort(clusters.rbegin(), clusters.rend(),
+              [](const std::vector<int>& a, const std::vector<int>& b) { return a.size() < b.size(); });
+    return clusters;
+}
+
+struct Out {
+    uint32_t* hdr;      // [8]: N, K, M, V, C, flags, duplicate voxel points, 0
+    float* ground;      // N x 8 floats (mode 2) or null
+    float* voxels;      // V x 4
+    int32_t* labels;    // V
+    int32_t* offsets;   // C + 1
+    int32_t* indices;   // offsets[C]
+    float* centroids;   // C x 2
+};
+
+void detect(std::vector<Pt>& cloud, bool is_dense, const Params& prm, int order, Out& o) {
+    filter_points_position(cloud, prm);
+    o.hdr[2] = (uint32_t)cloud.size();
+    std::vector<Pt> vox;
+    bool passthrough = voxel_grid(cloud, is_dense, prm, order, vox);
+    o.hdr[3] = (uint32_t)vox.size();
+    o.hdr[5] = passthrough ? 1u : 0u;
+    // ConeDetector constants (src/cone_detection.cpp:22-23) and tolerance (line 212)
+    const float CONE_WIDTH = 0.228, CONE_HEIGHT = 0.325;
+    const double tol = std::sqrt(std::pow(CONE_HEIGHT, 2) + std::pow(CONE_WIDTH, 2));
+    auto clusters = euclidean_clusters(vox, (float)tol, (unsigned)prm.min_cluster_size,
+                                       (unsigned)prm.max_cluster_size);
+    o.hdr[4] = (uint32_t)clusters.size();
+    // duplicate (bit-identical) voxel points break the nn_start_idx = 1 assumption (rule E2)
+    {
+        std::vector<std::tuple<uint32_t, uint32_t, uint32_t>> keys;
+        keys.reserve(vox.size());
+        for (const Pt& p : vox) {
+            uint32_t a, b, c;
+            std::memcpy(&a, &p.x, 4); std::memcpy(&b, &p.y, 4); std::memcpy(&c, &p.z, 4);
+            keys.emplace_back(a, b, c);
+        }
+        std::sort(keys.begin(), keys.end());
+        uint32_t dups = 0;
+        for (size_t i = 1; i < keys.size(); i++) dups += keys[i] == keys[i - 1];
+        o.hdr[6] = dups;
+    }
+    for (size_t v = 0; v < vox.size(); v++) {
+        o.voxels[4 * v + 0] = vox[v].x; o.voxels[4 * v + 1] = vox[v].y;
+        o.voxels[4 * v + 2] = vox[v].z; o.voxels[4 * v + 3] = vox[v].intensity;
+        o.labels[v] = -1;
+    }
+    int32_t off = 0;
+    for (size_t c = 0; c < clusters.size(); c++) {
+        o.offsets[c] = off;
+        // src/cone_detection.cpp:261-279 (x starts at 0: rule C1)
+        float x = 0.0f, y = 0.0f;
+        int j = 0;
+        for (int idx : clusters[c]) {
+            x += vox[idx].x;
+            y += vox[idx].y;
+            j++;
+            o.indices[off++] = idx;
+            o.labels[idx] = (int32_t)c;
+        }
+        float px = x / j, py = y / j, pz = 0.0f;
+        float vector_len = euclidan_dist(px, py, pz, 0, 0, 0);
+        px = px + px / vector_len * prm.cone_position_extension_length;
+        py = py + py / vector_len * prm.cone_position_extension_length;
+        o.centroids[2 * c + 0] = px;
+        o.centroids[2 * c + 1] = py;
+    }
+    o.offsets[clusters.size()] = off;
+}
+
+}  // namespace
+
+extern "C" {
+
+// mode: 0 = pipeline (ground removal then detector), 1 = detector only, 2 = ground only.
+// order: 0 = stable voxel sums (device order), 1 = PCL std::sort order.
+// All output arrays must hold N entries (N+1 for offsets; 8N floats for ground).
+int oracle_run(const void* params, const void* view, int mode, int order, uint32_t* hdr,
+               float* ground, float* voxels, int32_t* labels, int32_t* offsets, int32_t* indices,
+               float* centroids) {
+    const Params& prm = *(const Params*)params;
+    const View& v = *(const View*)view;
+    std::vector<Pt> cloud = decode(v);
+    std::memset(hdr, 0, 8 * sizeof(uint32_t));
+    hdr[0] = (uint32_t)cloud.size();
+    hdr[1] = (uint32_t)cloud.size();
+    if (mode == 0 || mode == 2) hdr[1] = (uint32_t)ground_remove(cloud, prm);
+    if (mode == 2) {
+        for (size_t i = 0; i < cloud.size(); i++) std::memcpy(ground + 8 * i, &cloud[i], 32);
+        return 0;
+    }
+    Out o{hdr, ground, voxels, labels, offsets, indices, centroids};
+    detect(cloud, v.is_dense != 0, prm, order, o);
+    return 0;
+}
+
+// Host libm probes for the device-restatement checks.
+float oracle_atan2f(float y, float x) { return atan2f(y, x); }
+int oracle_sector(float y, float x) { return sector_of(y, x); }
+double oracle_sqrt(double s) { return std::sqrt(s); }
+float oracle_euclid(float x, float y, float z) { return euclidan_dist(x, y, z, 0, 0, 0); }
+
+}  // extern "C"
