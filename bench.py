@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--single-frame", action="store_true", help="also time C2 single-frame latency")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic: per-phase in-kernel timing")
     args = ap.parse_args()
 
     import numpy as np
@@ -104,6 +105,9 @@ def main():
     total_frames = F * args.steps * world
     fps = total_frames / elapsed
 
+    if args.stamps and rank == 0:
+        phase_stamps(eng, step, F)
+
     single = None
     if args.single_frame and rank == 0:
         single = single_frame_latency(cp, params, raw, local)
@@ -155,6 +159,29 @@ def fetch_headers(res, F):
     if rc != 0:
         raise RuntimeError(f"hipMemcpy failed: {rc}")
     return out
+
+
+def phase_stamps(eng, step, F):
+    """Diagnostic build of one batch: s_memrealtime stamps at phase boundaries (not timed)."""
+    import ctypes
+    import numpy as np
+    from cones_perception_amd import _abi
+    lib = _abi.lib()
+    _abi.check(lib.cg_debug_stamps(eng.handle, 1))
+    step()
+    st = np.zeros((F, 16), np.uint64)
+    _abi.check(lib.cg_debug_stamps_fetch(eng.handle, st.ctypes.data, F))
+    _abi.check(lib.cg_debug_stamps(eng.handle, 0))
+    names = ["pass1 stream", "pass2+scan", "pass3 gather", "voxel", "cluster-union", "order+csr+centroid"]
+    t = st[:, :7].astype(np.int64)
+    t0 = t[:, 0].min()
+    out = {"wg_start_spread_us": float((t[:, 0].max() - t0) / 100.0),
+           "wg_end_spread_us": float((t[:, 6].max() - t[:, 6].min()) / 100.0),
+           "batch_span_us": float((t[:, 6].max() - t0) / 100.0)}
+    for i, n in enumerate(names):
+        d = (t[:, i + 1] - t[:, i]) / 100.0
+        out[n] = {"median_us": float(np.median(d)), "max_us": float(d.max())}
+    print("STAMPS " + json.dumps(out), flush=True)
 
 
 def single_frame_latency(cp, params, raw, device, reps=200):

@@ -89,6 +89,11 @@ int prepare(const cg_params& p, CgDevParams& d) {
     d.min_cl = (uint32_t)p.min_cluster_size;
     d.max_cl = (uint32_t)p.max_cluster_size;
     d.ext = p.cone_position_extension_length;
+    // float certificates for the distance compares: |fl((x^2+y^2)+z^2) - S| <= 4 ulp(S)
+    d.sfar_lo = cg_floor_to_float(d.s_far * (1.0 - 1e-6));
+    d.sfar_hi = cg_ceil_to_float(d.s_far * (1.0 + 1e-6));
+    d.snear_lo = cg_floor_to_float(d.s_near * (1.0 - 1e-6));
+    d.snear_hi = cg_ceil_to_float(d.s_near * (1.0 + 1e-6));
     // does PointXYZI() (0,0,0) survive filter_points_position?
     const float a0 = cg_atan2f(0.0f, 0.0f);
     const double S0 = 0.0;
@@ -131,6 +136,10 @@ struct cg_handle {
     std::vector<int32_t> h_lab, h_offs, h_idx;
     uint8_t* h_ground = nullptr;  // pinned
     size_t h_ground_bytes = 0;
+    // diagnostics
+    bool stamps_on = false;
+    uint64_t* d_stamps = nullptr;
+    uint32_t stamps_frames = 0;
 };
 
 namespace {
@@ -240,6 +249,22 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
     L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
     L.idx = h->d_idx; L.cen = h->d_cen; L.ground = h->d_ground;
     L.scratch = h->d_scratch; L.scratch_stride = h->scratch_stride;
+    L.stamps = nullptr;
+    if (h->stamps_on) {
+        if (h->stamps_frames < h->cap_frames) {
+            hipFree(h->d_stamps);
+            h->d_stamps = nullptr;
+            if (hipMalloc(&h->d_stamps, (size_t)h->cap_frames * 16 * 8) == hipSuccess)
+                h->stamps_frames = h->cap_frames;
+            else
+                h->stamps_frames = 0;
+        }
+        if (h->d_stamps) {
+            hipMemsetAsync(h->d_stamps, 0, (size_t)h->stamps_frames * 16 * 8, h->stream);
+            hipStreamSynchronize(h->stream);
+        }
+        L.stamps = h->d_stamps;
+    }
 }
 
 int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
@@ -376,6 +401,7 @@ int cg_destroy(cg_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     free_batch(h);
+    if (h->d_stamps) hipFree(h->d_stamps);
     if (h->d_in) hipFree(h->d_in);
     if (h->h_stage) hipHostFree(h->h_stage);
     if (h->h_ground) hipHostFree(h->h_ground);
@@ -457,6 +483,27 @@ int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out) {
     if (frame >= h->last_frames) return fail(CG_E_INVALID, "frame %u >= %u", frame, h->last_frames);
     HIPCHK(hipSetDevice(h->device));
     return fetch_frame(h, h->last_stream, frame, out);
+}
+
+int cg_debug_stamps(cg_handle* h, int enable) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    HIPCHK(hipSetDevice(h->device));
+    h->stamps_on = enable != 0;
+    if (!h->stamps_on && h->d_stamps) {
+        hipFree(h->d_stamps);
+        h->d_stamps = nullptr;
+        h->stamps_frames = 0;
+    }
+    return CG_OK;
+}
+
+int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames) {
+    if (!h || !out) return fail(CG_E_INVALID, "null argument");
+    if (!h->d_stamps || n_frames > h->stamps_frames) return fail(CG_E_INVALID, "stamps not enabled");
+    HIPCHK(hipSetDevice(h->device));
+    if (h->last_stream) HIPCHK(hipStreamSynchronize(h->last_stream));
+    HIPCHK(hipMemcpy(out, h->d_stamps, (size_t)n_frames * 16 * 8, hipMemcpyDeviceToHost));
+    return CG_OK;
 }
 
 int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out, uint32_t n) {

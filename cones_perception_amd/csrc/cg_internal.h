@@ -19,6 +19,9 @@ struct CgDevParams {
     uint32_t min_cl, max_cl;// cluster size limits as PCL's unsigned compares see them
     double ext;             // cone_position_extension_length
     int32_t zero_pass;      // a (0,0,0,i=0) pad point survives filter_points_position
+    // fast-path certificates (float bounds around the exact double thresholds): a float
+    // sum of squares below *_lo / above *_hi decides the compare without the double path
+    float sfar_lo, sfar_hi, snear_lo, snear_hi;
     int32_t pad_;
 };
 
@@ -41,6 +44,8 @@ struct CgLaunch {
     // HBM scratch for frames whose survivors do not fit the LDS path
     uint8_t* scratch;
     uint64_t scratch_stride;
+    // diagnostics: per-workgroup phase timestamps (16 slots per frame) or null
+    uint64_t* stamps;
 };
 
 #define CG_BLOCK 1024          // one workgroup (16 waves) per frame

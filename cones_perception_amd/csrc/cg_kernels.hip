@@ -33,13 +33,15 @@
 #include "cg_sort.h"
 
 #define WAVES (CG_BLOCK / 64)
+#define CG_BRUTE_V 384        // voxel count up to which clustering tests all pairs
 
 // ------------------------------------------------------------------------------------------
-// LDS map. The frontend stores z for points k >= 32 in `zl`, which overlays the backend arrays
-// (dead until pass 3 begins, and pass 2 keeps its decisions in registers).
+// LDS map. The frontend's 16-bit z-key prefixes (zq) overlay the backend arrays, which are
+// dead until pass 3 begins; pass 2 leaves its decisions in registers.
 struct FrontShared {
     uint32_t sec_key[CG_NUM_BINS + 1];
     float thr[CG_NUM_BINS + 1];
+    uint32_t tkey[CG_NUM_BINS + 1];
     uint32_t cnt[CG_BLOCK];        // survivors per (k, wave), then exclusive offsets
     uint32_t red[8 * WAVES];       // wave partials
     uint32_t scal[64];             // broadcast scalars
@@ -62,14 +64,21 @@ struct BackLds {
 };
 #define SMEM_BYTES (FRONT_BYTES + sizeof(BackLds))
 static_assert(SMEM_BYTES <= 163840, "LDS budget");
-static_assert(sizeof(BackLds) >= 32 * CG_BLOCK * sizeof(float), "z overlay must fit");
+static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint16_t), "z-key overlay must fit");
 
 // Scalar slots in FrontShared::scal
 enum {
     S_K = 0, S_MS, S_M, S_MF, S_V, S_C, S_U, S_FLAGS, S_PASS,
     S_MINB0, S_MINB1, S_MINB2, S_MUL1, S_MUL2,
-    S_ORGX, S_ORGY, S_ORGZ, S_TMP
+    S_ORGX, S_ORGY, S_ORGZ, S_TKMIN, S_TKMAX, S_TOUCHED, S_TMP
 };
+
+// Diagnostic phase stamps (s_memtime by lane 0 of each workgroup), only when L.stamps != 0.
+#define STAMP(ph)                                                                          \
+    do {                                                                                   \
+        if (L.stamps && threadIdx.x == 0)                                                  \
+            L.stamps[(uint64_t)blockIdx.x * 16 + (ph)] = __builtin_amdgcn_s_memrealtime();     \
+    } while (0)
 
 struct Work {
     float4* P; uint64_t* KEY; float4* VOX; uint32_t* A; uint32_t* PAR; uint32_t* CNT;
@@ -174,6 +183,23 @@ __device__ __forceinline__ void bitonic_sort(uint64_t* S, uint32_t n2) {
         }
 }
 
+// Sort n <= CG_RANK_SORT_MAX distinct keys: out[rank(in[j])] = in[j], rank by a broadcast
+// sweep (every lane reads the same in[i]). Ends with a barrier.
+#define CG_RANK_SORT_MAX 512
+__device__ __forceinline__ void rank_sort(const uint64_t* in, uint64_t* out, uint32_t n) {
+    for (uint32_t j = threadIdx.x; j < n; j += CG_BLOCK) {
+        const uint64_t kj = in[j];
+        uint32_t r = 0;
+        uint32_t i = 0;
+        for (; i + 4 <= n; i += 4) {
+            r += (in[i] < kj) + (in[i + 1] < kj) + (in[i + 2] < kj) + (in[i + 3] < kj);
+        }
+        for (; i < n; i++) r += in[i] < kj;
+        out[r] = kj;
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ uint32_t ld_rlx(uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -220,6 +246,21 @@ __device__ __forceinline__ void load_xyz(const uint8_t* fb, uint32_t i, const Cg
     }
 }
 template <int LAYOUT>
+__device__ __forceinline__ float3 load_xyz3(const uint8_t* fb, uint32_t i, const CgLaunch& L) {
+    if (LAYOUT == CG_LAYOUT_XYZI16) return *(const float3*)(fb + (uint64_t)i * 16);
+    if (LAYOUT == CG_LAYOUT_PCL32) return *(const float3*)(fb + (uint64_t)i * 32);
+    float x, y, z;
+    load_xyz<CG_LAYOUT_GENERIC>(fb, i, L, x, y, z);
+    return make_float3(x, y, z);
+}
+// Order-preserving key with -0 folded onto +0 and every NaN onto one key above +inf, so
+// that for non-NaN T:  z < T  <=>  cg_zkey(z) < cg_zkey(T)  (NaN z: never below, as in C).
+__device__ __forceinline__ uint32_t cg_zkey(float z) {
+    if (z != z) return 0xffffffffu;
+    if (z == 0.0f) z = 0.0f;
+    return cg_fkey(z);
+}
+template <int LAYOUT>
 __device__ __forceinline__ float4 load_xyzi(const uint8_t* fb, uint32_t i, const CgLaunch& L) {
     if (LAYOUT == CG_LAYOUT_XYZI16) return *(const float4*)(fb + (uint64_t)i * 16);
     if (LAYOUT == CG_LAYOUT_PCL32) {
@@ -234,12 +275,66 @@ __device__ __forceinline__ float4 load_xyzi(const uint8_t* fb, uint32_t i, const
     return make_float4(x, y, z, in);
 }
 
-// filter_points_position (src/cone_detection.cpp:195-201): true = keep.
-__device__ __forceinline__ bool position_keep(const CgDevParams& P, float x, float y, float z, float a) {
-    const double S = cg_sumsq_d(x, y, z);
-    const bool rm = (z < P.level_f) || (S >= P.s_far) || (S < P.s_near) || (a <= P.ang_lo) ||
-                    (a >= P.ang_hi);
-    return !rm;
+// filter_points_position (src/cone_detection.cpp:195-201), distance and level part:
+// true = removed. The float sum of squares decides unless it lies within 1e-6 (relative) of
+// a threshold; then the exact double S decides.
+__device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x, float y, float z) {
+    const float sf = (x * x + y * y) + z * z;
+    const bool far_c = sf > P.sfar_hi, nfar_c = sf < P.sfar_lo;
+    const bool near_c = sf < P.snear_lo, nnear_c = sf > P.snear_hi;
+    bool rm = (z < P.level_f) || far_c || near_c;
+    if (!(far_c || nfar_c) || !(near_c || nnear_c)) {
+        const double S = cg_sumsq_d(x, y, z);
+        rm = (z < P.level_f) || (S >= P.s_far) || (S < P.s_near);
+    }
+    return rm;
+}
+
+// Certified angle classification: sector (src/ground_removal.cpp:61-64) and the angle part of
+// filter_points_position (src/cone_detection.cpp:200-201) from a cheap atan2 approximation
+// (|error| < 1.5e-6 rad incl. glibc's own error; checked on device by cg_selftest_atan2f)
+// whenever the approximation lies more than CG_ANG_MARGIN from every sector boundary and both
+// angle thresholds. Otherwise the exact glibc restatement decides. Both decisions are
+// monotone step functions of the float angle, so equal classes at a - E and a + E certify.
+#define CG_ANG_MARGIN 8.0e-6f
+template <bool NEED_SECTOR, bool NEED_ANGLE>
+__device__ __forceinline__ void classify_angle(const CgDevParams& P, float x, float y, int& sector, bool& ang_rm) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float r = mn * __builtin_amdgcn_rcpf(mx);
+    const float q = r * r;
+    float p = 0.006811763625591993f;
+    p = p * q + -0.03360414505004883f;
+    p = p * q + 0.07962361723184586f;
+    p = p * q + -0.1323334127664566f;
+    p = p * q + 0.19807817041873932f;
+    p = p * q + -0.3331736922264099f;
+    p = p * q + 0.9999961256980896f;
+    float a = r * p;
+    if (ay > ax) a = 1.5707964f - a;
+    if (x < 0.f) a = 3.1415927f - a;
+    if (y < 0.f) a = -a;
+    // off-axis, not NaN (fmaxf/fminf drop NaN), and inside the range where v_rcp_f32(mx) is
+    // a normal number (mx < 2^126) and r does not underflow badly
+    bool ok = x == x && y == y && mn > 1.0e-30f && mx < 8.0e37f;
+    if (NEED_SECTOR) {
+        const float inv_sec = 1.0f / CG_SECTOR_ANGLE_RAD;
+        float wl = a - CG_ANG_MARGIN, wh = a + CG_ANG_MARGIN;
+        wl = wl < 0.f ? wl + 6.2831855f : wl;
+        wh = wh < 0.f ? wh + 6.2831855f : wh;
+        const int sl = (int)floorf(wl * inv_sec), sh = (int)floorf(wh * inv_sec);
+        ok = ok && sl == sh;
+        sector = sl > 16 ? 16 : sl;
+    }
+    if (NEED_ANGLE) {
+        ang_rm = (a <= P.ang_lo) || (a >= P.ang_hi);
+        ok = ok && fabsf(a - P.ang_lo) > CG_ANG_MARGIN && fabsf(a - P.ang_hi) > CG_ANG_MARGIN;
+    }
+    if (!ok) {
+        const float ae = cg_atan2f(y, x);
+        if (NEED_SECTOR) sector = cg_sector(ae);
+        if (NEED_ANGLE) ang_rm = (ae <= P.ang_lo) || (ae >= P.ang_hi);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -322,24 +417,30 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         const float mnb0 = (float)(int)fs->scal[S_MINB0], mnb1 = (float)(int)fs->scal[S_MINB1],
                     mnb2 = (float)(int)fs->scal[S_MINB2];
         const uint32_t mul1 = fs->scal[S_MUL1], mul2 = fs->scal[S_MUL2];
-        uint32_t n2 = 1;
-        while (n2 < M) n2 <<= 1;
-        for (uint32_t j = tid; j < n2; j += CG_BLOCK) {
-            uint64_t key = ~0ull;
-            if (j < M) {
-                const float4 p = W.P[j];
-                if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
-                    const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
-                    const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
-                    const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
-                    const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
-                    key = ((uint64_t)idx << 32) | j;
-                }
-            }
-            W.KEY[j] = key;
+        // keys (idx << 32 | position): unique, so any sort yields PCL's idx order with ties
+        // in point order. Non-finite points get idx 0xffffffff (beyond every real idx, which
+        // the overflow guard keeps below 2^31) and sort last.
+        auto voxel_key = [&](uint32_t j) -> uint64_t {
+            const float4 p = W.P[j];
+            if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return (0xffffffffull << 32) | j;
+            const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
+            const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
+            const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
+            const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
+            return ((uint64_t)idx << 32) | j;
+        };
+        if (M <= CG_RANK_SORT_MAX) {
+            uint64_t* tmp = (uint64_t*)W.VOX;      // VOX is free until the centroids
+            for (uint32_t j = tid; j < M; j += CG_BLOCK) tmp[j] = voxel_key(j);
+            __syncthreads();
+            rank_sort(tmp, W.KEY, M);
+        } else {
+            uint32_t n2 = 1;
+            while (n2 < M) n2 <<= 1;
+            for (uint32_t j = tid; j < n2; j += CG_BLOCK) W.KEY[j] = j < M ? voxel_key(j) : ~0ull;
+            __syncthreads();
+            bitonic_sort(W.KEY, n2);
         }
-        __syncthreads();
-        bitonic_sort(W.KEY, n2);
         const uint32_t Mf = fs->scal[S_MF];
         V = block_scan(
             Mf,
@@ -365,98 +466,120 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         }
         __syncthreads();
     }
+    STAMP(4);
     // ---- Euclidean clustering over the V voxel points ----
     uint32_t C = 0;
     if (V > 0) {
-        {   // neighbour-grid origin
-            float mn[3] = {INFINITY, INFINITY, INFINITY};
+        if (V <= CG_BRUTE_V) {
+            // all pairs (v < u), split over floor(1024 / V) lanes per voxel
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) { W.PAR[v] = v; W.CNT[v] = 0; }
+            __syncthreads();
+            const uint32_t nch = CG_BLOCK / V;
+            if (tid < V * nch) {
+                const uint32_t v = tid % V, c = tid / V;
+                const float4 q = W.VOX[v];
+                for (uint32_t u = v + 1 + c; u < V; u += nch) {
+                    const float4 p = W.VOX[u];
+                    const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+                    float acc = ddx * ddx;
+                    acc = acc + ddy * ddy;
+                    acc = acc + ddz * ddz;
+                    if (acc < P.r2) uf_union(W.PAR, v, u);
+                }
+            }
+            __syncthreads();
+        } else {
+            {   // neighbour-grid origin
+                float mn[3] = {INFINITY, INFINITY, INFINITY};
+                for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+                    const float4 p = W.VOX[v];
+                    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+                }
+#pragma unroll
+                for (int a = 0; a < 3; a++) mn[a] = wave_min(mn[a]);
+                if (l == 0) {
+#pragma unroll
+                    for (int a = 0; a < 3; a++) red[8 * w + a] = __float_as_uint(mn[a]);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    float o[3] = {INFINITY, INFINITY, INFINITY};
+                    for (int q = 0; q < WAVES; q++)
+#pragma unroll
+                        for (int a = 0; a < 3; a++) o[a] = fminf(o[a], __uint_as_float(red[8 * q + a]));
+#pragma unroll
+                    for (int a = 0; a < 3; a++) if (!isfinite(o[a])) o[a] = 0.f;
+                    fs->scal[S_ORGX] = __float_as_uint(o[0]);
+                    fs->scal[S_ORGY] = __float_as_uint(o[1]);
+                    fs->scal[S_ORGZ] = __float_as_uint(o[2]);
+                }
+                __syncthreads();
+            }
+            const float ox = __uint_as_float(fs->scal[S_ORGX]), oy = __uint_as_float(fs->scal[S_ORGY]),
+                        oz = __uint_as_float(fs->scal[S_ORGZ]);
+            auto cell = [&](float c, float o) -> uint32_t {
+                const float q = floorf((c - o) * P.cell_inv);
+                if (!(q >= 0.f)) return 0u;           // NaN or below origin
+                return q >= 1023.f ? 1023u : (uint32_t)q;
+            };
+            auto cell_key = [&](const float4& p) -> uint32_t {
+                return (cell(p.z, oz) << 20) | (cell(p.y, oy) << 10) | cell(p.x, ox);
+            };
+            uint32_t n2 = 1;
+            while (n2 < V) n2 <<= 1;
+            for (uint32_t j = tid; j < n2; j += CG_BLOCK)
+                W.KEY[j] = j < V ? (((uint64_t)cell_key(W.VOX[j]) << 16) | j) : ~0ull;
+            __syncthreads();
+            bitonic_sort(W.KEY, n2);
+            const uint32_t U = block_scan(
+                V,
+                [&](uint32_t j) -> uint32_t { return (j == 0 || (W.KEY[j] >> 16) != (W.KEY[j - 1] >> 16)) ? 1u : 0u; },
+                [&](uint32_t j, uint32_t e) {
+                    const uint64_t k = W.KEY[j];
+                    W.ORD[j] = (uint32_t)(k & 0xffffu);
+                    if (j == 0 || (k >> 16) != (W.KEY[j - 1] >> 16)) { W.UK[e] = (uint32_t)(k >> 16); W.A[e] = j; }
+                },
+                red);
+            if (tid == 0) W.A[U] = V;
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) { W.PAR[v] = v; W.CNT[v] = 0; }
+            __syncthreads();
+            // union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple)
             for (uint32_t v = tid; v < V; v += CG_BLOCK) {
-                const float4 p = W.VOX[v];
-                mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-            }
-#pragma unroll
-            for (int a = 0; a < 3; a++) mn[a] = wave_min(mn[a]);
-            if (l == 0) {
-#pragma unroll
-                for (int a = 0; a < 3; a++) red[8 * w + a] = __float_as_uint(mn[a]);
-            }
-            __syncthreads();
-            if (tid == 0) {
-                float o[3] = {INFINITY, INFINITY, INFINITY};
-                for (int q = 0; q < WAVES; q++)
-#pragma unroll
-                    for (int a = 0; a < 3; a++) o[a] = fminf(o[a], __uint_as_float(red[8 * q + a]));
-#pragma unroll
-                for (int a = 0; a < 3; a++) if (!isfinite(o[a])) o[a] = 0.f;
-                fs->scal[S_ORGX] = __float_as_uint(o[0]);
-                fs->scal[S_ORGY] = __float_as_uint(o[1]);
-                fs->scal[S_ORGZ] = __float_as_uint(o[2]);
-            }
-            __syncthreads();
-        }
-        const float ox = __uint_as_float(fs->scal[S_ORGX]), oy = __uint_as_float(fs->scal[S_ORGY]),
-                    oz = __uint_as_float(fs->scal[S_ORGZ]);
-        auto cell = [&](float c, float o) -> uint32_t {
-            const float q = floorf((c - o) * P.cell_inv);
-            if (!(q >= 0.f)) return 0u;           // NaN or below origin
-            return q >= 1023.f ? 1023u : (uint32_t)q;
-        };
-        auto cell_key = [&](const float4& p) -> uint32_t {
-            return (cell(p.z, oz) << 20) | (cell(p.y, oy) << 10) | cell(p.x, ox);
-        };
-        uint32_t n2 = 1;
-        while (n2 < V) n2 <<= 1;
-        for (uint32_t j = tid; j < n2; j += CG_BLOCK)
-            W.KEY[j] = j < V ? (((uint64_t)cell_key(W.VOX[j]) << 16) | j) : ~0ull;
-        __syncthreads();
-        bitonic_sort(W.KEY, n2);
-        const uint32_t U = block_scan(
-            V,
-            [&](uint32_t j) -> uint32_t { return (j == 0 || (W.KEY[j] >> 16) != (W.KEY[j - 1] >> 16)) ? 1u : 0u; },
-            [&](uint32_t j, uint32_t e) {
-                const uint64_t k = W.KEY[j];
-                W.ORD[j] = (uint32_t)(k & 0xffffu);
-                if (j == 0 || (k >> 16) != (W.KEY[j - 1] >> 16)) { W.UK[e] = (uint32_t)(k >> 16); W.A[e] = j; }
-            },
-            red);
-        if (tid == 0) W.A[U] = V;
-        for (uint32_t v = tid; v < V; v += CG_BLOCK) { W.PAR[v] = v; W.CNT[v] = 0; }
-        __syncthreads();
-        // union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple)
-        for (uint32_t v = tid; v < V; v += CG_BLOCK) {
-            const float4 q = W.VOX[v];
-            const uint32_t cx = cell(q.x, ox), cy = cell(q.y, oy), cz = cell(q.z, oz);
-            const uint32_t xlo = cx > 0 ? cx - 1 : 0, xhi = cx < 1023 ? cx + 1 : 1023;
-            for (int dz = -1; dz <= 1; dz++) {
-                const int zz = (int)cz + dz;
-                if (zz < 0 || zz > 1023) continue;
-                for (int dy = -1; dy <= 1; dy++) {
-                    const int yy = (int)cy + dy;
-                    if (yy < 0 || yy > 1023) continue;
-                    const uint32_t lo = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xlo;
-                    const uint32_t hi = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xhi;
-                    uint32_t a = 0, b = U;
-                    while (a < b) {
-                        const uint32_t m = (a + b) >> 1;
-                        if (W.UK[m] < lo) a = m + 1; else b = m;
-                    }
-                    for (uint32_t u = a; u < U && W.UK[u] <= hi; u++) {
-                        const uint32_t e = W.A[u + 1];
-                        for (uint32_t j = W.A[u]; j < e; j++) {
-                            const uint32_t o = W.ORD[j];
-                            if (o <= v) continue;
-                            const float4 p = W.VOX[o];
-                            const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
-                            float acc = ddx * ddx;
-                            acc = acc + ddy * ddy;
-                            acc = acc + ddz * ddz;
-                            if (acc < P.r2) uf_union(W.PAR, v, o);
+                const float4 q = W.VOX[v];
+                const uint32_t cx = cell(q.x, ox), cy = cell(q.y, oy), cz = cell(q.z, oz);
+                const uint32_t xlo = cx > 0 ? cx - 1 : 0, xhi = cx < 1023 ? cx + 1 : 1023;
+                for (int dz = -1; dz <= 1; dz++) {
+                    const int zz = (int)cz + dz;
+                    if (zz < 0 || zz > 1023) continue;
+                    for (int dy = -1; dy <= 1; dy++) {
+                        const int yy = (int)cy + dy;
+                        if (yy < 0 || yy > 1023) continue;
+                        const uint32_t lo = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xlo;
+                        const uint32_t hi = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xhi;
+                        uint32_t a = 0, b = U;
+                        while (a < b) {
+                            const uint32_t m = (a + b) >> 1;
+                            if (W.UK[m] < lo) a = m + 1; else b = m;
+                        }
+                        for (uint32_t u = a; u < U && W.UK[u] <= hi; u++) {
+                            const uint32_t e = W.A[u + 1];
+                            for (uint32_t j = W.A[u]; j < e; j++) {
+                                const uint32_t o = W.ORD[j];
+                                if (o <= v) continue;
+                                const float4 p = W.VOX[o];
+                                const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+                                float acc = ddx * ddx;
+                                acc = acc + ddy * ddy;
+                                acc = acc + ddz * ddz;
+                                if (acc < P.r2) uf_union(W.PAR, v, o);
+                            }
                         }
                     }
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
+        STAMP(5);
         for (uint32_t v = tid; v < V; v += CG_BLOCK) {
             W.LAB[v] = (int32_t)uf_find(W.PAR, v);
             W.ORD[v] = 0xffffffffu;   // becomes root -> output rank
@@ -578,82 +701,140 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = flags;
     }
+    STAMP(6);
 }
 
 // ------------------------------------------------------------------------------------------
-// Fused per-frame kernel. PPT points per lane (PPT_REG of their z in VGPRs, the rest in LDS).
+// Fused per-frame kernel. PPT points per lane; lane t owns points k*1024 + t.
+//
+// z of every point is kept on chip for the ground decision as the top 16 bits of its
+// order-preserving key (cg_zkey), 2 B per point in LDS (128 KiB at 64k points, overlaying the
+// backend arrays). Pass 2 decides `z < T[s]` from that prefix against the band
+// [min_s T[s], max_s T[s]] of the 17 sector thresholds, so it needs no per-point sector: a
+// prefix entirely below the band is ground in every sector, one entirely at or above it is
+// kept in every sector. Only points whose prefix overlaps the band re-read x, y, z from HBM
+// and recompute their sector (a few hundred of 65,536 on flat ground).
 template <int PPT, int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
-    constexpr int PPT_REG = PPT < 32 ? PPT : 32;
-    constexpr int NSW = (PPT + 5) / 6;
+    constexpr int G = 8;                          // points per load group (double-buffered)
+    constexpr int NG = PPT / G;
+    static_assert(PPT % G == 0, "PPT must be a multiple of the load group");
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
     constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
     FrontShared* fs = (FrontShared*)smem;
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
-    float* zl = (float*)bl;                       // z overlay for k >= PPT_REG
+    uint16_t* zq = (uint16_t*)bl;                 // z key prefixes, [k][lane-of-block]
 
     const uint32_t f = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
     const uint32_t N = L.n_points;
+    STAMP(0);
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
     if (tid < 64) fs->scal[tid] = 0;
     __syncthreads();
 
-    // ---- pass 1 ----
-    float zr[PPT_REG];
-    uint32_t sw[NSW];
+    // ---- pass 1: stream the frame ----
     uint64_t posm = 0;
-#pragma unroll
-    for (int q = 0; q < NSW; q++) sw[q] = 0;
     int cur_s = -1;
     float cur_m = 0.f;
+    uint32_t touched = 0;        // sector bins this lane saw (bit 17: NaN angle)
+    float3 cur[G], nxt[G];
 #pragma unroll
-    for (int k = 0; k < PPT; k++) {
-        const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
-        const bool valid = i < N;
-        float x = 0.f, y = 0.f, z = 0.f;
-        if (valid) load_xyz<LAYOUT>(fb, i, L, x, y, z);
-        const float a = cg_atan2f(y, x);
-        if (FILTER) posm |= (uint64_t)(valid && position_keep(P, x, y, z, a)) << k;
-        if (GROUND) {
-            const int s = cg_sector(a);
-            sw[k / 6] |= (uint32_t)s << (5 * (k % 6));
-            if (k < PPT_REG) zr[k < PPT_REG ? k : 0] = z;
-            else zl[(k - PPT_REG) * CG_BLOCK + tid] = z;
-            if (valid && s < CG_NUM_BINS && z == z) {
-                if (s != cur_s) {
-                    if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
-                    cur_s = s;
-                    cur_m = z;
-                } else {
-                    cur_m = fminf(cur_m, z);
+    for (int j = 0; j < G; j++) {
+        const uint32_t i = (uint32_t)j * CG_BLOCK + tid;
+        cur[j] = i < N ? load_xyz3<LAYOUT>(fb, i, L) : make_float3(0.f, 0.f, 0.f);
+    }
+#pragma unroll 1
+    for (int g = 0; g < NG; g++) {
+        if (g + 1 < NG) {
+#pragma unroll
+            for (int j = 0; j < G; j++) {
+                const uint32_t i = (uint32_t)((g + 1) * G + j) * CG_BLOCK + tid;
+                nxt[j] = i < N ? load_xyz3<LAYOUT>(fb, i, L) : make_float3(0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G; j++) {
+            const int k = g * G + j;
+            const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
+            const bool valid = i < N;
+            const float x = cur[j].x, y = cur[j].y, z = cur[j].z;
+            int s = 0;
+            bool ang_rm = false;
+            classify_angle<GROUND, FILTER>(P, x, y, s, ang_rm);
+            if (FILTER) posm |= (uint64_t)(valid && !ang_rm && !dist_level_remove(P, x, y, z)) << k;
+            if (GROUND) {
+                zq[k * CG_BLOCK + tid] = (uint16_t)(cg_zkey(z) >> 16);
+                if (valid && s < CG_NUM_BINS && z == z) {
+                    if (s != cur_s) {
+                        if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+                        touched |= 1u << s;
+                        cur_s = s;
+                        cur_m = z;
+                    } else {
+                        cur_m = fminf(cur_m, z);
+                    }
+                } else if (valid && s == CG_NAN_BIN) {
+                    touched |= 1u << CG_NAN_BIN;
                 }
             }
         }
+#pragma unroll
+        for (int j = 0; j < G; j++) cur[j] = nxt[j];
     }
-    if (GROUND && cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+    if (GROUND) {
+        if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) touched |= (uint32_t)__shfl_xor((int)touched, o, 64);
+        if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
+    }
     __syncthreads();
-    if (GROUND && tid < CG_NUM_BINS + 1) {
+    STAMP(1);
+    if (GROUND && tid < 64) {
         // (double)z < (double)low + 0.1  <=>  z < ceil_to_float(low + 0.1)  (ground_removal.cpp:75)
-        const float low = cg_fkey_inv(fs->sec_key[tid]);
-        fs->thr[tid] = cg_ceil_to_float((double)low + 0.1);
+        uint32_t tk = 0xffffffffu;
+        if (tid <= CG_NUM_BINS) {
+            const float low = cg_fkey_inv(fs->sec_key[tid]);
+            const float T = cg_ceil_to_float((double)low + 0.1);
+            fs->thr[tid] = T;
+            tk = T != T ? 0u : cg_zkey(T);          // NaN threshold: nothing is below it
+            fs->tkey[tid] = tk;
+        }
+        // band over the bins that hold points (an empty bin's threshold constrains nothing)
+        const bool used = tid <= CG_NUM_BINS && ((fs->scal[S_TOUCHED] >> tid) & 1u);
+        uint32_t mn = used ? tk : 0xffffffffu, mx = used ? tk : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        }
+        if (tid == 0) { fs->scal[S_TKMIN] = mn; fs->scal[S_TKMAX] = mx; }
     }
     __syncthreads();
 
     // ---- pass 2: keep bits and ballot counts ----
     uint64_t keepm = 0;
     uint32_t kground = 0;
-#pragma unroll
+    const uint32_t tkmin = fs->scal[S_TKMIN], tkmax = fs->scal[S_TKMAX];
+#pragma unroll 4
     for (int k = 0; k < PPT; k++) {
         const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
         const bool valid = i < N;
         bool keep_g = valid;
         if (GROUND) {
-            const float z = k < PPT_REG ? zr[k < PPT_REG ? k : 0] : zl[(k - PPT_REG) * CG_BLOCK + tid];
-            const uint32_t s = (sw[k / 6] >> (5 * (k % 6))) & 31u;
-            keep_g = valid && !(z < fs->thr[s]);
+            const uint32_t lo = (uint32_t)zq[k * CG_BLOCK + tid] << 16, hi = lo | 0xffffu;
+            bool below = hi < tkmin;               // below every sector's threshold
+            if (valid && !below && lo < tkmax) {   // inside the band: exact z and sector
+                float x, y, z;
+                load_xyz<LAYOUT>(fb, i, L, x, y, z);
+                int sx = 0;
+                bool unused = false;
+                classify_angle<true, false>(P, x, y, sx, unused);
+                below = cg_zkey(z) < fs->tkey[sx];
+            }
+            keep_g = valid && !below;
             kground += (uint32_t)__popcll(__ballot(keep_g));
         }
         const bool keep = FILTER ? (keep_g && ((posm >> k) & 1ull)) : keep_g;
@@ -668,11 +849,12 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
         PPT * WAVES, [&](uint32_t i) -> uint32_t { return fs->cnt[i]; },
         [&](uint32_t i, uint32_t e) { fs->cnt[i] = e; }, fs->red);
     const uint32_t K = GROUND ? fs->scal[S_K] : N;
+    STAMP(2);
 
     if (KMODE == CG_KMODE_GROUND) {
         // groundless cloud: K kept points in order, then N-K PointXYZI() (ground_removal.cpp:70-79)
         float4* out = (float4*)(L.ground + (uint64_t)f * N * 32);
-#pragma unroll
+#pragma unroll 4
         for (int k = 0; k < PPT; k++) {
             const uint64_t b = __ballot((keepm >> k) & 1ull);
             if ((keepm >> k) & 1ull) {
@@ -715,7 +897,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
         W = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
     }
     // ---- pass 3: gather survivors in point order ----
-#pragma unroll
+#pragma unroll 4
     for (int k = 0; k < PPT; k++) {
         const uint64_t b = __ballot((keepm >> k) & 1ull);
         if ((keepm >> k) & 1ull) {
@@ -726,6 +908,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     }
     for (uint32_t j = tid; j < npad; j += CG_BLOCK) W.P[Ms + j] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();
+    STAMP(3);
     if (use_lds) {
         Work WL;
         WL.P = bl->P; WL.KEY = bl->KEY; WL.VOX = bl->VOX; WL.A = bl->A; WL.PAR = bl->PAR; WL.CNT = bl->CNT;
@@ -774,7 +957,13 @@ __global__ void cg_selftest_atan2f_kernel(const float* y, const float* x, float*
     if (i < n) {
         const float a = cg_atan2f(y[i], x[i]);
         out[2 * i] = a;
-        out[2 * i + 1] = (float)cg_sector(a);
+        // sector through the certified fast path (must equal the exact one)
+        CgDevParams P{};
+        P.ang_lo = -4.0f; P.ang_hi = 4.0f;
+        int s = 0;
+        bool rm = false;
+        classify_angle<true, false>(P, x[i], y[i], s, rm);
+        out[2 * i + 1] = (float)s;
     }
 }
 __global__ void cg_selftest_sqrt_kernel(const double* in, double* out, uint32_t n) {

@@ -131,3 +131,31 @@ def test_batch_engine_matches_oracle(params):
         got = eng.fetch(f)
         ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE)
         assert_same_detection(got, ref, f"batch frame {f}")
+
+
+@pytest.mark.parametrize("clutter,cpr,frame", [(20, 8, 0), (20, 8, 1), (60, 10, 0), (200, 10, 0)])
+def test_dense_frames_match_oracle(params, pipe, clutter, cpr, frame):
+    """Cluttered scenes: M > 512 (bitonic voxel sort), V > 384 (neighbour-grid clustering),
+    C > 16 (PCL's introsort cluster order), M > 2048 (HBM-scratch backend)."""
+    raw = cp.synth_frames(1, first_frame=frame, rings=64, cols=1024, clutter=clutter, cones_per_row=cpr)
+    msg = cp.frame_cloud(raw[0])
+    got = pipe.cloud_handler(msg)
+    ref, hdr = O.run(params, msg, O.MODE_PIPELINE)
+    assert_same_detection(got, ref, f"clutter {clutter} f{frame}")
+    if int(hdr[2]) > 2048:
+        assert got.flags & cp.CG_F_GLOBAL_SCRATCH
+
+
+def test_dense_batch_mixed_paths(params):
+    """One batch mixing LDS-path and HBM-scratch-path frames."""
+    import torch
+    raws = [cp.synth_frames(1, first_frame=f, rings=64, cols=1024, clutter=c, cones_per_row=8)[0]
+            for f, c in ((0, 0), (1, 60), (2, 20), (3, 200), (4, 0))]
+    raw = np.stack(raws)
+    d = torch.from_numpy(raw).cuda()
+    eng = cp.BatchEngine(params)
+    eng.run(d.data_ptr(), raw.shape[0], 65536, 16, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for f in range(raw.shape[0]):
+        ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE)
+        assert_same_detection(eng.fetch(f), ref, f"mixed batch frame {f}")
