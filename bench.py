@@ -161,26 +161,39 @@ def fetch_headers(res, F):
     return out
 
 
+STAMP_NAMES = ["start", "pass1 stream", "thresholds", "pass2 keep bits", "compaction scan",
+               "pass3 gather", "voxel minmax", "voxel keys", "voxel sort", "voxel runs",
+               "voxel centroids", "cluster init", "cluster unions", "cluster roots", "cluster sizes",
+               "cluster keep scan", "cluster order", "csr offsets", "labels", "csr indices",
+               "centroids+header"]
+
+
 def phase_stamps(eng, step, F):
     """Diagnostic build of one batch: s_memrealtime stamps at phase boundaries (not timed)."""
-    import ctypes
     import numpy as np
     from cones_perception_amd import _abi
     lib = _abi.lib()
     _abi.check(lib.cg_debug_stamps(eng.handle, 1))
     step()
-    st = np.zeros((F, 16), np.uint64)
+    st = np.zeros((F, 32), np.uint64)
     _abi.check(lib.cg_debug_stamps_fetch(eng.handle, st.ctypes.data, F))
     _abi.check(lib.cg_debug_stamps(eng.handle, 0))
-    names = ["pass1 stream", "pass2+scan", "pass3 gather", "voxel", "cluster-union", "order+csr+centroid"]
-    t = st[:, :7].astype(np.int64)
-    t0 = t[:, 0].min()
-    out = {"wg_start_spread_us": float((t[:, 0].max() - t0) / 100.0),
-           "wg_end_spread_us": float((t[:, 6].max() - t[:, 6].min()) / 100.0),
-           "batch_span_us": float((t[:, 6].max() - t0) / 100.0)}
-    for i, n in enumerate(names):
-        d = (t[:, i + 1] - t[:, i]) / 100.0
-        out[n] = {"median_us": float(np.median(d)), "max_us": float(d.max())}
+    t = st.astype(np.int64)
+    out = {"batch_span_us": float((t[:, 20].max() - t[:, 0].min()) / 100.0),
+           "wg_end_spread_us": float((t[:, 20].max() - t[:, 20].min()) / 100.0)}
+    prev = t[:, 0].copy()
+    for i in range(1, 21):
+        have = t[:, i] > 0
+        if not have.any():
+            continue
+        d = np.where(have, t[:, i] - prev, 0) / 100.0
+        out[STAMP_NAMES[i]] = round(float(np.median(d[have])), 2)
+        prev = np.where(have, t[:, i], prev)
+    sub = t[:, 21] > 0
+    if sub.any():   # wave-0 progress marks inside pass 2 (no barrier): LDS loop, re-reads
+        out["pass2a lds loop (wave0)"] = round(float(np.median((t[sub, 21] - t[sub, 2]) / 100.0)), 2)
+        out["pass2b re-reads (wave0)"] = round(float(np.median((t[sub, 22] - t[sub, 21]) / 100.0)), 2)
+        out["pass2c ballots (wave0)"] = round(float(np.median((t[sub, 3] - t[sub, 22]) / 100.0)), 2)
     print("STAMPS " + json.dumps(out), flush=True)
 
 

@@ -254,13 +254,13 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
         if (h->stamps_frames < h->cap_frames) {
             hipFree(h->d_stamps);
             h->d_stamps = nullptr;
-            if (hipMalloc(&h->d_stamps, (size_t)h->cap_frames * 16 * 8) == hipSuccess)
+            if (hipMalloc(&h->d_stamps, (size_t)h->cap_frames * 32 * 8) == hipSuccess)
                 h->stamps_frames = h->cap_frames;
             else
                 h->stamps_frames = 0;
         }
         if (h->d_stamps) {
-            hipMemsetAsync(h->d_stamps, 0, (size_t)h->stamps_frames * 16 * 8, h->stream);
+            hipMemsetAsync(h->d_stamps, 0, (size_t)h->stamps_frames * 32 * 8, h->stream);
             hipStreamSynchronize(h->stream);
         }
         L.stamps = h->d_stamps;
@@ -502,7 +502,7 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames) {
     if (!h->d_stamps || n_frames > h->stamps_frames) return fail(CG_E_INVALID, "stamps not enabled");
     HIPCHK(hipSetDevice(h->device));
     if (h->last_stream) HIPCHK(hipStreamSynchronize(h->last_stream));
-    HIPCHK(hipMemcpy(out, h->d_stamps, (size_t)n_frames * 16 * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, h->d_stamps, (size_t)n_frames * 32 * 8, hipMemcpyDeviceToHost));
     return CG_OK;
 }
 

@@ -70,14 +70,15 @@ static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint16_t), "z-key overla
 enum {
     S_K = 0, S_MS, S_M, S_MF, S_V, S_C, S_U, S_FLAGS, S_PASS,
     S_MINB0, S_MINB1, S_MINB2, S_MUL1, S_MUL2,
-    S_ORGX, S_ORGY, S_ORGZ, S_TKMIN, S_TKMAX, S_TOUCHED, S_TMP
+    S_ORGX, S_ORGY, S_ORGZ, S_TKMIN, S_TKMAX, S_TOUCHED,
+    S_BMIN0, S_BMIN1, S_BMIN2, S_BMAX0, S_BMAX1, S_BMAX2, S_TMP
 };
 
 // Diagnostic phase stamps (s_memtime by lane 0 of each workgroup), only when L.stamps != 0.
 #define STAMP(ph)                                                                          \
     do {                                                                                   \
         if (L.stamps && threadIdx.x == 0)                                                  \
-            L.stamps[(uint64_t)blockIdx.x * 16 + (ph)] = __builtin_amdgcn_s_memrealtime();     \
+            L.stamps[(uint64_t)blockIdx.x * 32 + (ph)] = __builtin_amdgcn_s_memrealtime();     \
     } while (0)
 
 struct Work {
@@ -117,29 +118,56 @@ __device__ __forceinline__ uint32_t wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
+// Cross-lane steps use DPP (row_shr within 16-lane rows, row_bcast15/31 across rows), which
+// stay in the VALU; __shfl would go through ds_bpermute and pay an LDS round trip per step.
+template <int CTRL, int ROWS, int BANKS>
+__device__ __forceinline__ uint32_t dpp(uint32_t identity, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROWS, BANKS, false);
+}
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (l >= (uint32_t)o) x += y;
-    }
-    return x;
+    uint32_t v = x;
+    v += dpp<0x111, 0xf, 0xf>(0u, x);    // row_shr:1
+    v += dpp<0x112, 0xf, 0xf>(0u, x);    // row_shr:2
+    v += dpp<0x113, 0xf, 0xf>(0u, x);    // row_shr:3   -> sums of 4
+    v += dpp<0x114, 0xf, 0xe>(0u, v);    // row_shr:4, banks 1-3 -> 8
+    v += dpp<0x118, 0xf, 0xc>(0u, v);    // row_shr:8, banks 2-3 -> 16
+    v += dpp<0x142, 0xa, 0xf>(0u, v);    // row_bcast:15 into rows 1, 3
+    v += dpp<0x143, 0xc, 0xf>(0u, v);    // row_bcast:31 into rows 2, 3
+    return v;
+}
+// Reductions to lane 63 (Kogge-Stone in each row, then the two row broadcasts), read back
+// through an SGPR so every lane gets the result.
+template <class OP>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v, uint32_t id, OP op) {
+    v = op(v, dpp<0x111, 0xf, 0xf>(id, v));
+    v = op(v, dpp<0x112, 0xf, 0xf>(id, v));
+    v = op(v, dpp<0x114, 0xf, 0xf>(id, v));
+    v = op(v, dpp<0x118, 0xf, 0xf>(id, v));
+    v = op(v, dpp<0x142, 0xa, 0xf>(id, v));
+    v = op(v, dpp<0x143, 0xc, 0xf>(id, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-    return v;
+    return __uint_as_float(wave_reduce(__float_as_uint(v), __float_as_uint(INFINITY), [](uint32_t a, uint32_t b) {
+        return __float_as_uint(fminf(__uint_as_float(a), __uint_as_float(b)));
+    }));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    return __uint_as_float(wave_reduce(__float_as_uint(v), __float_as_uint(-INFINITY), [](uint32_t a, uint32_t b) {
+        return __float_as_uint(fmaxf(__uint_as_float(a), __uint_as_float(b)));
+    }));
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return wave_reduce(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    return wave_reduce(v, 0u, [](uint32_t a, uint32_t b) { return a | b; });
+}
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
+    return wave_reduce(v, 0xffffffffu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+}
+__device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
+    return wave_reduce(v, 0u, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
 }
 
 // Exclusive scan over i in [0, n) in chunks of 1024: val(i) -> emit(i, excl). Returns total.
@@ -187,15 +215,22 @@ __device__ __forceinline__ void bitonic_sort(uint64_t* S, uint32_t n2) {
 // sweep (every lane reads the same in[i]). Ends with a barrier.
 #define CG_RANK_SORT_MAX 512
 __device__ __forceinline__ void rank_sort(const uint64_t* in, uint64_t* out, uint32_t n) {
-    for (uint32_t j = threadIdx.x; j < n; j += CG_BLOCK) {
-        const uint64_t kj = in[j];
+    // g lanes (a power of two, consecutive in a wave) share one key's count
+    uint32_t g = 1;
+    while (g < 64 && (uint64_t)n * g * 2 <= CG_BLOCK) g <<= 1;
+    const uint32_t sub = threadIdx.x & (g - 1);
+    for (uint32_t base = 0; base < n * g; base += CG_BLOCK) {
+        const uint32_t t = base + threadIdx.x, j = t / g;
+        const uint64_t kj = j < n ? in[j] : 0ull;
         uint32_t r = 0;
-        uint32_t i = 0;
-        for (; i + 4 <= n; i += 4) {
-            r += (in[i] < kj) + (in[i + 1] < kj) + (in[i + 2] < kj) + (in[i + 3] < kj);
+        if (j < n) {
+            uint32_t i = sub;
+            for (; i + 3 * g < n; i += 4 * g)
+                r += (in[i] < kj) + (in[i + g] < kj) + (in[i + 2 * g] < kj) + (in[i + 3 * g] < kj);
+            for (; i < n; i += g) r += in[i] < kj;
         }
-        for (; i < n; i++) r += in[i] < kj;
-        out[r] = kj;
+        for (uint32_t o = 1; o < g; o <<= 1) r += (uint32_t)__shfl_xor((int)r, (int)o, 64);
+        if (j < n && sub == 0) out[r] = kj;
     }
     __syncthreads();
 }
@@ -297,19 +332,23 @@ __device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x,
 // angle thresholds. Otherwise the exact glibc restatement decides. Both decisions are
 // monotone step functions of the float angle, so equal classes at a - E and a + E certify.
 #define CG_ANG_MARGIN 8.0e-6f
+// The exact restatement is large and rarely executed: one out-of-line copy keeps it out of
+// the hot loops' instruction footprint.
+__device__ __noinline__ float cg_atan2f_cold(float y, float x) { return cg_atan2f(y, x); }
 template <bool NEED_SECTOR, bool NEED_ANGLE>
 __device__ __forceinline__ void classify_angle(const CgDevParams& P, float x, float y, int& sector, bool& ang_rm) {
     const float ax = fabsf(x), ay = fabsf(y);
     const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
     const float r = mn * __builtin_amdgcn_rcpf(mx);
     const float q = r * r;
+    // (explicit FMAs: this is our approximation, not a reference expression)
     float p = 0.006811763625591993f;
-    p = p * q + -0.03360414505004883f;
-    p = p * q + 0.07962361723184586f;
-    p = p * q + -0.1323334127664566f;
-    p = p * q + 0.19807817041873932f;
-    p = p * q + -0.3331736922264099f;
-    p = p * q + 0.9999961256980896f;
+    p = fmaf(p, q, -0.03360414505004883f);
+    p = fmaf(p, q, 0.07962361723184586f);
+    p = fmaf(p, q, -0.1323334127664566f);
+    p = fmaf(p, q, 0.19807817041873932f);
+    p = fmaf(p, q, -0.3331736922264099f);
+    p = fmaf(p, q, 0.9999961256980896f);
     float a = r * p;
     if (ay > ax) a = 1.5707964f - a;
     if (x < 0.f) a = 3.1415927f - a;
@@ -331,7 +370,7 @@ __device__ __forceinline__ void classify_angle(const CgDevParams& P, float x, fl
         ok = ok && fabsf(a - P.ang_lo) > CG_ANG_MARGIN && fabsf(a - P.ang_hi) > CG_ANG_MARGIN;
     }
     if (!ok) {
-        const float ae = cg_atan2f(y, x);
+        const float ae = cg_atan2f_cold(y, x);
         if (NEED_SECTOR) sector = cg_sector(ae);
         if (NEED_ANGLE) ang_rm = (ae <= P.ang_lo) || (ae >= P.ang_hi);
     }
@@ -343,73 +382,66 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
                                         const CgDevParams& P, uint32_t f, uint32_t flags) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     uint32_t* red = fs->red;
-    // ---- voxel grid: getMinMax3D over finite points ----
-    {
-        float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-        uint32_t nf = 0;
-        for (uint32_t j = tid; j < M; j += CG_BLOCK) {
-            const float4 p = W.P[j];
-            if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
-                mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-                mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-                nf++;
+    // ---- voxel grid: getMinMax3D (finite points; bounds gathered by the frontend) ----
+    if (w == 0) {
+        const uint32_t nfin = fs->scal[S_MF];
+        float bmn[3], bmx[3];
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            bmn[a] = cg_fkey_inv(fs->scal[S_BMIN0 + a]);
+            bmx[a] = cg_fkey_inv(fs->scal[S_BMAX0 + a]);
+        }
+        uint32_t pass = 0;
+        int min_b[3] = {0, 0, 0}, div_b[3] = {1, 1, 1};
+        if (nfin > 0) {
+            double prod = 1.0;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const float span = (bmx[a] - bmn[a]) * P.inv_leaf[a];
+                const double d = span >= 9.0e18f ? 9.0e18 : (double)((int64_t)span + 1);
+                prod *= d;
+            }
+            if (prod > 2147483647.0) pass = 1;
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                min_b[a] = (int)floorf(bmn[a] * P.inv_leaf[a]);
+                const int max_b = (int)floorf(bmx[a] * P.inv_leaf[a]);
+                div_b[a] = max_b - min_b[a] + 1;
             }
         }
-        float r[6];
-#pragma unroll
-        for (int a = 0; a < 3; a++) { r[a] = wave_min(mn[a]); r[3 + a] = wave_max(mx[a]); }
-        nf = wave_sum(nf);
         if (l == 0) {
-#pragma unroll
-            for (int a = 0; a < 6; a++) red[8 * w + a] = __float_as_uint(r[a]);
-            red[8 * w + 6] = nf;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-            uint32_t nfin = 0;
-            for (int q = 0; q < WAVES; q++) {
-#pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    bmn[a] = fminf(bmn[a], __uint_as_float(red[8 * q + a]));
-                    bmx[a] = fmaxf(bmx[a], __uint_as_float(red[8 * q + 3 + a]));
-                }
-                nfin += red[8 * q + 6];
-            }
-            uint32_t pass = 0;
-            int min_b[3] = {0, 0, 0}, div_b[3] = {1, 1, 1};
-            if (nfin > 0) {
-                double prod = 1.0;
-#pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    const float span = (bmx[a] - bmn[a]) * P.inv_leaf[a];
-                    const double d = span >= 9.0e18f ? 9.0e18 : (double)((int64_t)span + 1);
-                    prod *= d;
-                }
-                if (prod > 2147483647.0) pass = 1;
-#pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    min_b[a] = (int)floorf(bmn[a] * P.inv_leaf[a]);
-                    const int max_b = (int)floorf(bmx[a] * P.inv_leaf[a]);
-                    div_b[a] = max_b - min_b[a] + 1;
-                }
-            }
             fs->scal[S_PASS] = pass;
-            fs->scal[S_MF] = nfin;
             fs->scal[S_MINB0] = (uint32_t)min_b[0];
             fs->scal[S_MINB1] = (uint32_t)min_b[1];
             fs->scal[S_MINB2] = (uint32_t)min_b[2];
             fs->scal[S_MUL1] = (uint32_t)div_b[0];
             fs->scal[S_MUL2] = (uint32_t)div_b[0] * (uint32_t)div_b[1];
         }
-        __syncthreads();
     }
+    __syncthreads();
+    STAMP(6);
     const uint32_t pass = fs->scal[S_PASS];
     uint32_t V;
     float4* const vox_out = L.vox + (uint64_t)f * L.cap;
     if (pass) {
-        // overflow guard: output = *input_ (all M points, in order)
-        for (uint32_t j = tid; j < M; j += CG_BLOCK) { W.VOX[j] = W.P[j]; vox_out[j] = W.P[j]; }
+        // overflow guard: output = *input_ (all M points in point order)
+        uint64_t* tmp = (uint64_t*)W.VOX;
+        for (uint32_t j = tid; j < M; j += CG_BLOCK) tmp[j] = ((uint64_t)W.IDX[j] << 16) | j;
+        __syncthreads();
+        if (M <= CG_RANK_SORT_MAX) {
+            rank_sort(tmp, W.KEY, M);
+        } else {
+            uint32_t n2 = 1;
+            while (n2 < M) n2 <<= 1;
+            for (uint32_t j = tid; j < n2; j += CG_BLOCK) W.KEY[j] = j < M ? tmp[j] : ~0ull;
+            __syncthreads();
+            bitonic_sort(W.KEY, n2);
+        }
+        for (uint32_t r = tid; r < M; r += CG_BLOCK) {
+            const float4 pp = W.P[(uint32_t)(W.KEY[r] & 0xffffu)];
+            W.VOX[r] = pp;
+            vox_out[r] = pp;
+        }
         V = M;
         flags |= 0x1u;
         __syncthreads();
@@ -417,31 +449,35 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         const float mnb0 = (float)(int)fs->scal[S_MINB0], mnb1 = (float)(int)fs->scal[S_MINB1],
                     mnb2 = (float)(int)fs->scal[S_MINB2];
         const uint32_t mul1 = fs->scal[S_MUL1], mul2 = fs->scal[S_MUL2];
-        // keys (idx << 32 | position): unique, so any sort yields PCL's idx order with ties
-        // in point order. Non-finite points get idx 0xffffffff (beyond every real idx, which
-        // the overflow guard keeps below 2^31) and sort last.
+        // keys (idx << 32 | point index << 16 | slot): unique, so any sort yields PCL's idx
+        // order with ties in point order. Non-finite points get idx 0xffffffff (beyond every
+        // real idx, which the overflow guard keeps below 2^31) and sort last.
         auto voxel_key = [&](uint32_t j) -> uint64_t {
             const float4 p = W.P[j];
-            if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return (0xffffffffull << 32) | j;
+            const uint64_t lowbits = ((uint64_t)(W.IDX[j] & 0xffffu) << 16) | j;
+            if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return (0xffffffffull << 32) | lowbits;
             const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
             const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
             const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
             const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
-            return ((uint64_t)idx << 32) | j;
+            return ((uint64_t)idx << 32) | lowbits;
         };
         if (M <= CG_RANK_SORT_MAX) {
             uint64_t* tmp = (uint64_t*)W.VOX;      // VOX is free until the centroids
             for (uint32_t j = tid; j < M; j += CG_BLOCK) tmp[j] = voxel_key(j);
             __syncthreads();
+            STAMP(7);
             rank_sort(tmp, W.KEY, M);
         } else {
             uint32_t n2 = 1;
             while (n2 < M) n2 <<= 1;
             for (uint32_t j = tid; j < n2; j += CG_BLOCK) W.KEY[j] = j < M ? voxel_key(j) : ~0ull;
             __syncthreads();
+            STAMP(7);
             bitonic_sort(W.KEY, n2);
         }
         const uint32_t Mf = fs->scal[S_MF];
+        STAMP(8);
         V = block_scan(
             Mf,
             [&](uint32_t j) -> uint32_t { return (j == 0 || (W.KEY[j] >> 32) != (W.KEY[j - 1] >> 32)) ? 1u : 0u; },
@@ -451,12 +487,13 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             red);
         if (tid == 0) W.A[V] = Mf;
         __syncthreads();
+        STAMP(9);
         // CentroidPoint<PointXYZI>: float sums in ascending point position, / float(n)
         for (uint32_t v = tid; v < V; v += CG_BLOCK) {
             const uint32_t s = W.A[v], e = W.A[v + 1];
             float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
             for (uint32_t j = s; j < e; j++) {
-                const float4 p = W.P[(uint32_t)W.KEY[j]];
+                const float4 p = W.P[(uint32_t)(W.KEY[j] & 0xffffu)];
                 sx += p.x; sy += p.y; sz += p.z; si += p.w;
             }
             const float n = (float)(e - s);
@@ -466,26 +503,54 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         }
         __syncthreads();
     }
-    STAMP(4);
+    STAMP(10);
     // ---- Euclidean clustering over the V voxel points ----
     uint32_t C = 0;
     if (V > 0) {
         if (V <= CG_BRUTE_V) {
-            // all pairs (v < u), split over floor(1024 / V) lanes per voxel
+            // all pairs, split over nch = floor(1024 / V) lanes per voxel. (1) every voxel
+            // points at its smallest neighbour (or itself): a forest whose trees lie inside
+            // components; (2) pointer jumping flattens it; (3) the few edges between trees
+            // are united with the lock-free union. Roots stay each component's lowest index.
             for (uint32_t v = tid; v < V; v += CG_BLOCK) { W.PAR[v] = v; W.CNT[v] = 0; }
+            if (tid == 0) { fs->scal[S_TMP] = 0; fs->scal[S_TMP + 1] = 0; }
             __syncthreads();
+            STAMP(11);
             const uint32_t nch = CG_BLOCK / V;
-            if (tid < V * nch) {
-                const uint32_t v = tid % V, c = tid / V;
-                const float4 q = W.VOX[v];
-                for (uint32_t u = v + 1 + c; u < V; u += nch) {
-                    const float4 p = W.VOX[u];
-                    const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
-                    float acc = ddx * ddx;
-                    acc = acc + ddy * ddy;
-                    acc = acc + ddz * ddz;
-                    if (acc < P.r2) uf_union(W.PAR, v, u);
+            const bool act = tid < V * nch;
+            const uint32_t v = act ? tid % V : 0, c = act ? tid / V : 0;
+            const float4 q = W.VOX[v];
+            auto adj = [&](uint32_t u) -> bool {
+                const float4 p = W.VOX[u];
+                const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+                float acc = ddx * ddx;
+                acc = acc + ddy * ddy;
+                acc = acc + ddz * ddz;
+                return acc < P.r2;
+            };
+            if (act) {
+                for (uint32_t u = c; u < v; u += nch)
+                    if (adj(u)) { atomicMin(&W.PAR[v], u); break; }
+            }
+            __syncthreads();
+            // flatten: per-iteration "changed" flags alternate between two words; the word
+            // for the next iteration is cleared before the barrier that ends this one
+            for (uint32_t iter = 0;; iter++) {
+                bool changed = false;
+                for (uint32_t x = tid; x < V; x += CG_BLOCK) {
+                    const uint32_t p = W.PAR[x], pp = W.PAR[p];
+                    if (pp != p) { W.PAR[x] = pp; changed = true; }
                 }
+                if (__ballot(changed) && l == 0) atomicOr(&fs->scal[S_TMP + (iter & 1)], 1u);
+                __syncthreads();
+                const bool again = fs->scal[S_TMP + (iter & 1)] != 0;
+                if (tid == 0) fs->scal[S_TMP + ((iter + 1) & 1)] = 0;
+                __syncthreads();
+                if (!again) break;
+            }
+            if (act) {
+                for (uint32_t u = v + 1 + c; u < V; u += nch)
+                    if (adj(u) && ld_rlx(W.PAR + v) != ld_rlx(W.PAR + u)) uf_union(W.PAR, v, u);
             }
             __syncthreads();
         } else {
@@ -579,14 +644,16 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             }
             __syncthreads();
         }
-        STAMP(5);
+        STAMP(12);
         for (uint32_t v = tid; v < V; v += CG_BLOCK) {
             W.LAB[v] = (int32_t)uf_find(W.PAR, v);
             W.ORD[v] = 0xffffffffu;   // becomes root -> output rank
         }
         __syncthreads();
+        STAMP(13);
         for (uint32_t v = tid; v < V; v += CG_BLOCK) atomicAdd(&W.CNT[W.LAB[v]], 1u);
         __syncthreads();
+        STAMP(14);
         // kept components in discovery (seed) order; DROOT/DSZ/RANK/FIN overlay W.P (dead)
         uint32_t* const DROOT = (uint32_t*)W.P;
         uint32_t* const DSZ = DROOT + V;
@@ -603,6 +670,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
                 if ((uint32_t)W.LAB[v] == v && c >= P.min_cl && c <= P.max_cl) { DROOT[d] = v; DSZ[d] = c; }
             },
             red);
+        STAMP(15);
         // cluster order: PCL sorts the reversed discovery list ascending by size with std::sort
         if (C > CG_SORT_THRESHOLD) {
             if (tid == 0) {
@@ -632,6 +700,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             }
         }
         __syncthreads();
+        STAMP(16);
         const uint32_t tot = block_scan(
             C, [&](uint32_t k) -> uint32_t { return DSZ[FIN[k]]; },
             [&](uint32_t k, uint32_t e) { W.OFF[k] = e; }, red);
@@ -639,6 +708,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         for (uint32_t d = tid; d < C; d += CG_BLOCK) W.ORD[DROOT[d]] = RANK[d];
         for (uint32_t k = tid; k < C; k += CG_BLOCK) W.CNT[k] = 0;   // CSR cursors
         __syncthreads();
+        STAMP(17);
         int32_t* const lab_out = L.lab + (uint64_t)f * L.cap;
         for (uint32_t v = tid; v < V; v += CG_BLOCK) {
             const int32_t lb = (int32_t)W.ORD[(uint32_t)W.LAB[v]];
@@ -646,9 +716,33 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             lab_out[v] = lb;
         }
         __syncthreads();
-        // stable counting sort of voxel indices by cluster rank (one wave, ascending v)
+        STAMP(18);
+        // CSR indices, ascending voxel index inside each cluster
         int32_t* const idx_out = L.idx + (uint64_t)f * L.cap;
-        if (w == 0) {
+        if (V <= CG_BRUTE_V) {
+            // rank inside the cluster = popcount of the cluster's membership bits below v;
+            // the bitmasks overlay A | PAR | CNT (dead here), 6 words per cluster
+            constexpr uint32_t MW = (CG_BRUTE_V + 63) / 64;
+            unsigned long long* mask = (unsigned long long*)W.A;
+            for (uint32_t x = tid; x < C * MW; x += CG_BLOCK) mask[x] = 0ull;
+            __syncthreads();
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+                const int32_t k = W.LAB[v];
+                if (k >= 0) atomicOr(&mask[(uint32_t)k * MW + (v >> 6)], 1ull << (v & 63));
+            }
+            __syncthreads();
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+                const int32_t k = W.LAB[v];
+                if (k < 0) continue;
+                const unsigned long long* mk = mask + (uint32_t)k * MW;
+                uint32_t r = (uint32_t)__popcll(mk[v >> 6] & ((1ull << (v & 63)) - 1ull));
+                for (uint32_t q = 0; q < (v >> 6); q++) r += (uint32_t)__popcll(mk[q]);
+                const uint32_t pos = W.OFF[k] + r;
+                W.IDX[pos] = v;
+                idx_out[pos] = (int32_t)v;
+            }
+        } else if (w == 0) {
+            // stable counting sort by cluster rank (one wave, ascending v)
             for (uint32_t base = 0; base < V; base += 64) {
                 const uint32_t v = base + l;
                 const int32_t k = v < V ? W.LAB[v] : -1;
@@ -677,6 +771,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         for (uint32_t k = tid; k < C; k += CG_BLOCK) {
             const uint32_t s = W.OFF[k], e = W.OFF[k + 1];
             float x = 0.0f, y = 0.0f;
+#pragma unroll 4
             for (uint32_t i = s; i < e; i++) {
                 const float4 p = W.VOX[W.IDX[i]];
                 x += p.x;
@@ -701,7 +796,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = flags;
     }
-    STAMP(6);
+    STAMP(20);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -724,7 +819,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
     FrontShared* fs = (FrontShared*)smem;
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
-    uint16_t* zq = (uint16_t*)bl;                 // z key prefixes, [k][lane-of-block]
+    uint16_t* zq = (uint16_t*)bl;                 // z key prefixes, [k/4][lane][k%4]
 
     const uint32_t f = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
@@ -732,7 +827,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     STAMP(0);
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
-    if (tid < 64) fs->scal[tid] = 0;
+    if (tid < 64) fs->scal[tid] = (tid >= S_BMIN0 && tid <= S_BMIN2) ? 0xffffffffu : 0u;
     __syncthreads();
 
     // ---- pass 1: stream the frame ----
@@ -766,7 +861,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
             classify_angle<GROUND, FILTER>(P, x, y, s, ang_rm);
             if (FILTER) posm |= (uint64_t)(valid && !ang_rm && !dist_level_remove(P, x, y, z)) << k;
             if (GROUND) {
-                zq[k * CG_BLOCK + tid] = (uint16_t)(cg_zkey(z) >> 16);
+                zq[((k >> 2) * CG_BLOCK + tid) * 4 + (k & 3)] = (uint16_t)(cg_zkey(z) >> 16);
                 if (valid && s < CG_NUM_BINS && z == z) {
                     if (s != cur_s) {
                         if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
@@ -786,8 +881,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     }
     if (GROUND) {
         if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) touched |= (uint32_t)__shfl_xor((int)touched, o, 64);
+        touched = wave_or(touched);
         if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
     }
     __syncthreads();
@@ -804,91 +898,127 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
         }
         // band over the bins that hold points (an empty bin's threshold constrains nothing)
         const bool used = tid <= CG_NUM_BINS && ((fs->scal[S_TOUCHED] >> tid) & 1u);
-        uint32_t mn = used ? tk : 0xffffffffu, mx = used ? tk : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-            mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-        }
+        const uint32_t mn = wave_umin(used ? tk : 0xffffffffu), mx = wave_umax(used ? tk : 0u);
         if (tid == 0) { fs->scal[S_TKMIN] = mn; fs->scal[S_TKMAX] = mx; }
     }
     __syncthreads();
-
-    // ---- pass 2: keep bits and ballot counts ----
-    uint64_t keepm = 0;
-    uint32_t kground = 0;
-    const uint32_t tkmin = fs->scal[S_TKMIN], tkmax = fs->scal[S_TKMAX];
-#pragma unroll 4
-    for (int k = 0; k < PPT; k++) {
-        const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
-        const bool valid = i < N;
-        bool keep_g = valid;
-        if (GROUND) {
-            const uint32_t lo = (uint32_t)zq[k * CG_BLOCK + tid] << 16, hi = lo | 0xffffu;
-            bool below = hi < tkmin;               // below every sector's threshold
-            if (valid && !below && lo < tkmax) {   // inside the band: exact z and sector
-                float x, y, z;
-                load_xyz<LAYOUT>(fb, i, L, x, y, z);
-                int sx = 0;
-                bool unused = false;
-                classify_angle<true, false>(P, x, y, sx, unused);
-                below = cg_zkey(z) < fs->tkey[sx];
-            }
-            keep_g = valid && !below;
-            kground += (uint32_t)__popcll(__ballot(keep_g));
-        }
-        const bool keep = FILTER ? (keep_g && ((posm >> k) & 1ull)) : keep_g;
-        keepm |= (uint64_t)keep << k;
-        const uint64_t b = __ballot(keep);
-        if (l == 0) fs->cnt[k * WAVES + w] = (uint32_t)__popcll(b);
-    }
-    if (GROUND && l == 0) atomicAdd(&fs->scal[S_K], kground);
-    __syncthreads();
-    // stable compaction offsets over (k, wave) in point order
-    const uint32_t Ms = block_scan(
-        PPT * WAVES, [&](uint32_t i) -> uint32_t { return fs->cnt[i]; },
-        [&](uint32_t i, uint32_t e) { fs->cnt[i] = e; }, fs->red);
-    const uint32_t K = GROUND ? fs->scal[S_K] : N;
     STAMP(2);
 
+    // ---- pass 2: ground decisions from the LDS prefixes ----
+    // A prefix p (top 16 bits of the z key) is below every used sector's threshold iff
+    // p < tkmin >> 16, and at or above all of them iff (p << 16) >= tkmax; prefixes in
+    // between are ambiguous and resolve from HBM (all of a lane's re-reads issued together).
+    uint64_t keepgm = 0, ambm = 0;
+    if (GROUND) {
+        const uint32_t tkmin = fs->scal[S_TKMIN], tkmax = fs->scal[S_TKMAX];
+        const uint32_t pb = tkmin >> 16, pa = (tkmax >> 16) + ((tkmax & 0xffffu) ? 1u : 0u);
+        const uint2* zq4 = (const uint2*)zq;
+#pragma unroll 4
+        for (int k4 = 0; k4 < PPT / 4; k4++) {
+            const uint2 wv = zq4[k4 * CG_BLOCK + tid];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = 4 * k4 + j;
+                const uint32_t pref = ((j < 2 ? wv.x : wv.y) >> (16 * (j & 1))) & 0xffffu;
+                const bool valid = (uint32_t)k * CG_BLOCK + tid < N;
+                const bool below = pref < pb, amb = !below && pref < pa;
+                keepgm |= (uint64_t)(valid && !below && !amb) << k;
+                ambm |= (uint64_t)(valid && amb) << k;
+            }
+        }
+        STAMP(21);
+        while (ambm) {
+            int ks[4];
+            float3 pt[4];
+            uint64_t m = ambm;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ks[q] = m ? __builtin_ctzll(m) : -1;
+                if (m) m &= m - 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (ks[q] >= 0) pt[q] = load_xyz3<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (ks[q] < 0) continue;
+                int sx = 0;
+                bool unused = false;
+                classify_angle<true, false>(P, pt[q].x, pt[q].y, sx, unused);
+                if (!(cg_zkey(pt[q].z) < fs->tkey[sx])) keepgm |= 1ull << ks[q];
+            }
+            ambm = m;
+        }
+        const uint32_t kc = wave_sum((uint32_t)__popcll(keepgm));
+        if (l == 0) atomicAdd(&fs->scal[S_K], kc);
+    } else {
+#pragma unroll 8
+        for (int k = 0; k < PPT; k++) keepgm |= (uint64_t)((uint32_t)k * CG_BLOCK + tid < N) << k;
+    }
+    STAMP(22);
+
     if (KMODE == CG_KMODE_GROUND) {
-        // groundless cloud: K kept points in order, then N-K PointXYZI() (ground_removal.cpp:70-79)
+        // groundless cloud: K kept points in point order, then N-K PointXYZI()
+        // (ground_removal.cpp:70-79); stable order comes from per-(k, wave) ballot counts
+#pragma unroll 8
+        for (int k = 0; k < PPT; k++) {
+            const uint64_t bb = __ballot((keepgm >> k) & 1ull);
+            if (l == 0) fs->cnt[k * WAVES + w] = (uint32_t)__popcll(bb);
+        }
+        __syncthreads();
+        STAMP(3);
+        const uint32_t Kc = block_scan(
+            PPT * WAVES, [&](uint32_t i) -> uint32_t { return fs->cnt[i]; },
+            [&](uint32_t i, uint32_t e) { fs->cnt[i] = e; }, fs->red);
+        STAMP(4);
         float4* out = (float4*)(L.ground + (uint64_t)f * N * 32);
 #pragma unroll 4
         for (int k = 0; k < PPT; k++) {
-            const uint64_t b = __ballot((keepm >> k) & 1ull);
-            if ((keepm >> k) & 1ull) {
+            const uint64_t bb = __ballot((keepgm >> k) & 1ull);
+            if ((keepgm >> k) & 1ull) {
                 const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
-                const uint32_t dst = fs->cnt[k * WAVES + w] + (uint32_t)__popcll(b & ((1ull << l) - 1ull));
-                const float4 p = load_xyzi<LAYOUT>(fb, i, L);
-                out[2 * dst] = make_float4(p.x, p.y, p.z, 1.0f);
-                out[2 * dst + 1] = make_float4(p.w, 0.f, 0.f, 0.f);
+                const uint32_t dst = fs->cnt[k * WAVES + w] + (uint32_t)__popcll(bb & ((1ull << l) - 1ull));
+                const float4 pp = load_xyzi<LAYOUT>(fb, i, L);
+                out[2 * dst] = make_float4(pp.x, pp.y, pp.z, 1.0f);
+                out[2 * dst + 1] = make_float4(pp.w, 0.f, 0.f, 0.f);
             }
         }
-        for (uint32_t j = Ms + tid; j < N; j += CG_BLOCK) {
+        for (uint32_t j = Kc + tid; j < N; j += CG_BLOCK) {
             out[2 * j] = make_float4(0.f, 0.f, 0.f, 1.0f);
             out[2 * j + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         if (tid == 0) {
             uint32_t* h = L.hdr + (uint64_t)f * 8;
-            h[0] = N; h[1] = K; h[2] = N; h[3] = 0; h[4] = 0; h[5] = 0;
+            h[0] = N; h[1] = Kc; h[2] = N; h[3] = 0; h[4] = 0; h[5] = 0;
         }
         return;
     }
 
+    // ---- compaction: per-wave atomic append; each survivor carries its point index, and
+    // the voxel sort orders by (voxel idx, point index), so append order does not matter ----
+    const uint64_t keepm = FILTER ? (keepgm & posm) : keepgm;
+    const uint32_t nsv = (uint32_t)__popcll(keepm);
+    const uint32_t incl = wave_incl_scan(nsv);
+    uint32_t wbase = 0;
+    if (l == 63) wbase = atomicAdd(&fs->scal[S_MS], incl);
+    wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
+    uint32_t pos = wbase + incl - nsv;
+    __syncthreads();   // counts complete; z-prefix overlay in LDS is dead from here on
+    STAMP(3);
+    const uint32_t Ms = fs->scal[S_MS];
+    const uint32_t K = GROUND ? fs->scal[S_K] : N;
     // pipeline: the detector input is the groundless cloud, whose N-K trailing
     // PointXYZI() points survive the filter iff P.zero_pass (src/cone_detection.cpp:195-201)
     const uint32_t npad = (KMODE == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
     const uint32_t M = Ms + npad;
     const bool use_lds = M <= CG_MMAX;
-    uint32_t flags = use_lds ? 0u : 0x2u;
+    const uint32_t flags = use_lds ? 0u : 0x2u;
     if (tid == 0) {
         uint32_t* h = L.hdr + (uint64_t)f * 8;
         h[0] = N;
         h[1] = K;
     }
-    __syncthreads();   // z overlay in LDS is dead from here on
-
+    STAMP(4);
     Work W;
     if (use_lds) {
         W.P = bl->P; W.KEY = bl->KEY; W.VOX = bl->VOX; W.A = bl->A; W.PAR = bl->PAR; W.CNT = bl->CNT;
@@ -896,19 +1026,61 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     } else {
         W = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
     }
-    // ---- pass 3: gather survivors in point order ----
-#pragma unroll 4
-    for (int k = 0; k < PPT; k++) {
-        const uint64_t b = __ballot((keepm >> k) & 1ull);
-        if ((keepm >> k) & 1ull) {
-            const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
-            const uint32_t dst = fs->cnt[k * WAVES + w] + (uint32_t)__popcll(b & ((1ull << l) - 1ull));
-            W.P[dst] = load_xyzi<LAYOUT>(fb, i, L);
+    // ---- gather survivors (4 loads in flight per lane) and the VoxelGrid bounds ----
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t nfin = 0;
+    auto bound = [&](const float4& p) {
+        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+            nfin++;
+        }
+    };
+    {
+        uint64_t m = keepm;
+        while (m) {
+            int ks[4];
+            float4 pt[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ks[q] = m ? __builtin_ctzll(m) : -1;
+                if (m) m &= m - 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (ks[q] >= 0) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (ks[q] < 0) continue;
+                W.P[pos] = pt[q];
+                W.IDX[pos] = (uint32_t)ks[q] * CG_BLOCK + tid;   // point index
+                bound(pt[q]);
+                pos++;
+            }
         }
     }
-    for (uint32_t j = tid; j < npad; j += CG_BLOCK) W.P[Ms + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (uint32_t j = tid; j < npad; j += CG_BLOCK) {
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        W.P[Ms + j] = z4;
+        W.IDX[Ms + j] = 0xffffu;   // after every kept point; exact-zero terms are order-free
+        bound(z4);
+    }
+    {
+        float r[6];
+#pragma unroll
+        for (int a = 0; a < 3; a++) { r[a] = wave_min(mn[a]); r[3 + a] = wave_max(mx[a]); }
+        const uint32_t nf = wave_sum(nfin);
+        if (l == 0 && nf) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                atomicMin(&fs->scal[S_BMIN0 + a], cg_fkey(r[a]));
+                atomicMax(&fs->scal[S_BMAX0 + a], cg_fkey(r[3 + a]));
+            }
+            atomicAdd(&fs->scal[S_MF], nf);
+        }
+    }
     __syncthreads();
-    STAMP(3);
+    STAMP(5);
     if (use_lds) {
         Work WL;
         WL.P = bl->P; WL.KEY = bl->KEY; WL.VOX = bl->VOX; WL.A = bl->A; WL.PAR = bl->PAR; WL.CNT = bl->CNT;

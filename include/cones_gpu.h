@@ -168,7 +168,7 @@ int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out);
 int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out, uint32_t n);
 int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
 
-/* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz; 16 slots per frame) for the
+/* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz; 32 slots per frame) for the
  * next batch calls; enable = 0 frees the buffer. Fetch synchronises the batch stream. */
 int cg_debug_stamps(cg_handle* h, int enable);
 int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
