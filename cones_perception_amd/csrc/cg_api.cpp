@@ -94,6 +94,11 @@ int prepare(const cg_params& p, CgDevParams& d) {
     d.sfar_hi = cg_ceil_to_float(d.s_far * (1.0 + 1e-6));
     d.snear_lo = cg_floor_to_float(d.s_near * (1.0 - 1e-6));
     d.snear_hi = cg_ceil_to_float(d.s_near * (1.0 + 1e-6));
+    // z-code window: every sector threshold is ceil(low + 0.1) with low <= default_lowest_point,
+    // so thresholds lie at or below T_max; codes resolve 1/64 m over ~4 m below it
+    const float tmax = cg_ceil_to_float((double)p.default_lowest_point + 0.1);
+    d.zq_scale = 64.0f;
+    d.zq_z0 = (tmax == tmax && std::isfinite(tmax)) ? tmax - 254.0f / 64.0f : 0.0f;
     // does PointXYZI() (0,0,0) survive filter_points_position?
     const float a0 = cg_atan2f(0.0f, 0.0f);
     const double S0 = 0.0;
@@ -143,6 +148,14 @@ struct cg_handle {
 };
 
 namespace {
+
+// The handle's private stream, created lazily: batch calls that pass their own stream never
+// need one, and every stream costs one of the process's few hardware queues.
+int own_stream(cg_handle* h) {
+    if (h->stream) return CG_OK;
+    HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    return CG_OK;
+}
 
 void free_batch(cg_handle* h) {
     hipFree(h->d_hdr); hipFree(h->d_vox); hipFree(h->d_lab); hipFree(h->d_offs);
@@ -259,10 +272,7 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
             else
                 h->stamps_frames = 0;
         }
-        if (h->d_stamps) {
-            hipMemsetAsync(h->d_stamps, 0, (size_t)h->stamps_frames * 32 * 8, h->stream);
-            hipStreamSynchronize(h->stream);
-        }
+        if (h->d_stamps) hipMemset(h->d_stamps, 0, (size_t)h->stamps_frames * 32 * 8);
         L.stamps = h->d_stamps;
     }
 }
@@ -313,6 +323,8 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     int rc = check_view(in);
     if (rc) return rc;
     HIPCHK(hipSetDevice(h->device));
+    rc = own_stream(h);
+    if (rc) return rc;
     const uint32_t n = in->width * in->height;
     rc = ensure_batch(h, 1, n, kmode == CG_KMODE_GROUND);
     if (rc) return rc;
@@ -388,11 +400,7 @@ int cg_create(const cg_params* params, int device, cg_handle** out) {
     h->device = device;
     h->params = p;
     h->dp = dp;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete h;
-        return fail(CG_E_DEVICE, "hipStreamCreate failed");
-    }
-    *out = h;
+    *out = h;   // the handle's own stream is created on first use (see own_stream)
     return CG_OK;
 }
 
@@ -459,6 +467,10 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     L.off_x = b->off_x; L.off_y = b->off_y; L.off_z = b->off_z; L.off_i = b->off_intensity;
     L.is_dense = b->is_dense;
     fill_launch_outputs(h, L);
+    if (!hip_stream) {
+        rc = own_stream(h);
+        if (rc) return rc;
+    }
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     HIPCHK((hipError_t)cg_launch_batch(L, h->dp, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s));
     h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
@@ -510,6 +522,8 @@ int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out,
     if (!h || (n && (!y || !x || !out))) return fail(CG_E_INVALID, "null argument");
     if (!n) return CG_OK;
     HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
     float *dy = nullptr, *dx = nullptr, *dout = nullptr;
     HIPCHK(hipMalloc(&dy, (size_t)n * 4));
     HIPCHK(hipMalloc(&dx, (size_t)n * 4));
@@ -527,6 +541,8 @@ int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n) {
     if (!h || (n && (!s || !out))) return fail(CG_E_INVALID, "null argument");
     if (!n) return CG_OK;
     HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
     double *din = nullptr, *dout = nullptr;
     HIPCHK(hipMalloc(&din, (size_t)n * 8));
     HIPCHK(hipMalloc(&dout, (size_t)n * 8));

@@ -22,7 +22,8 @@ struct CgDevParams {
     // fast-path certificates (float bounds around the exact double thresholds): a float
     // sum of squares below *_lo / above *_hi decides the compare without the double path
     float sfar_lo, sfar_hi, snear_lo, snear_hi;
-    int32_t pad_;
+    // 8-bit z code window for the on-chip ground decision: q(z) = floor((z - zq_z0) * zq_scale)
+    float zq_z0, zq_scale;
 };
 
 // One batch launch: uniform frames, device-resident input and outputs.
@@ -48,9 +49,9 @@ struct CgLaunch {
     uint64_t* stamps;
 };
 
-#define CG_BLOCK 1024          // one workgroup (16 waves) per frame
-#define CG_MMAX 2048           // LDS-path capacity (points surviving the filter)
-#define CG_MAX_POINTS 65536    // 64 points per lane
+#define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
+#define CG_MMAX 1024           // LDS-path capacity (points surviving the filter)
+#define CG_MAX_POINTS 65536    // 128 points per lane
 
 enum { CG_LAYOUT_GENERIC = 0, CG_LAYOUT_XYZI16 = 1, CG_LAYOUT_PCL32 = 2 };
 enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };

@@ -33,7 +33,7 @@
 #include "cg_sort.h"
 
 #define WAVES (CG_BLOCK / 64)
-#define CG_BRUTE_V 384        // voxel count up to which clustering tests all pairs
+#define CG_BRUTE_V 256        // voxel count up to which clustering tests all pairs
 
 // ------------------------------------------------------------------------------------------
 // LDS map. The frontend's 16-bit z-key prefixes (zq) overlay the backend arrays, which are
@@ -42,7 +42,7 @@ struct FrontShared {
     uint32_t sec_key[CG_NUM_BINS + 1];
     float thr[CG_NUM_BINS + 1];
     uint32_t tkey[CG_NUM_BINS + 1];
-    uint32_t cnt[CG_BLOCK];        // survivors per (k, wave), then exclusive offsets
+    uint32_t cnt[CG_MAX_POINTS / 64];  // ground-only mode: kept per (k, wave), then offsets
     uint32_t red[8 * WAVES];       // wave partials
     uint32_t scal[64];             // broadcast scalars
     int32_t stk[3 * CG_SORT_STACK];// introsort stack (cluster order)
@@ -64,7 +64,7 @@ struct BackLds {
 };
 #define SMEM_BYTES (FRONT_BYTES + sizeof(BackLds))
 static_assert(SMEM_BYTES <= 163840, "LDS budget");
-static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint16_t), "z-key overlay must fit");
+static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overlay must fit");
 
 // Scalar slots in FrontShared::scal
 enum {
@@ -800,26 +800,68 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
 }
 
 // ------------------------------------------------------------------------------------------
-// Fused per-frame kernel. PPT points per lane; lane t owns points k*1024 + t.
+// Per-lane bit sets over the PPT points of a lane (NW 64-bit words; word index may be a
+// run-time value, resolved with selects so the words stay in VGPRs).
+template <int NW>
+struct LaneBits {
+    uint64_t w[NW];
+    __device__ __forceinline__ void clear() {
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = 0;
+    }
+    __device__ __forceinline__ void set_byte(int byte_idx, uint32_t v8) {   // 8 bits at 8*byte_idx
+        const int wi = byte_idx >> 3, sh = (byte_idx & 7) * 8;
+#pragma unroll
+        for (int i = 0; i < NW; i++)
+            if (i == wi) w[i] |= (uint64_t)v8 << sh;
+    }
+    __device__ __forceinline__ bool get(int k) const {
+        uint64_t x = w[0];
+#pragma unroll
+        for (int i = 1; i < NW; i++)
+            if ((k >> 6) == i) x = w[i];
+        return (x >> (k & 63)) & 1ull;
+    }
+    __device__ __forceinline__ uint32_t count() const {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) c += (uint32_t)__popcll(w[i]);
+        return c;
+    }
+};
+
+// 8-bit monotone z code: q(z) = clamp(floor((z - z0) * 64), 0, 255), NaN -> 255. For any T,
+// q(z) < q(T) implies z < T and q(z) > q(T) implies z > T; equal codes are ambiguous.
+__device__ __forceinline__ uint32_t zcode(float z, const CgDevParams& P) {
+    if (z != z) return 255u;
+    const float q = floorf((z - P.zq_z0) * P.zq_scale);
+    return (uint32_t)fminf(fmaxf(q, 0.f), 255.f);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused per-frame kernel: one 512-lane workgroup per frame, two workgroups per CU (launch
+// bounds: 4 waves per SIMD, so <= 128 VGPRs) so that one
+// frame's latency-bound backend overlaps another frame's HBM streaming. PPT points per lane;
+// lane t owns points k*512 + t.
 //
-// z of every point is kept on chip for the ground decision as the top 16 bits of its
-// order-preserving key (cg_zkey), 2 B per point in LDS (128 KiB at 64k points, overlaying the
-// backend arrays). Pass 2 decides `z < T[s]` from that prefix against the band
-// [min_s T[s], max_s T[s]] of the 17 sector thresholds, so it needs no per-point sector: a
-// prefix entirely below the band is ground in every sector, one entirely at or above it is
-// kept in every sector. Only points whose prefix overlaps the band re-read x, y, z from HBM
-// and recompute their sector (a few hundred of 65,536 on flat ground).
+// z of every point stays on chip for the ground decision as an 8-bit monotone code (64 KiB at
+// 64k points, overlaying the backend arrays). Pass 2 decides `z < T[s]` against the band
+// [min_s T[s], max_s T[s]] of the used sector thresholds, so it needs no per-point sector:
+// a code below q(min T) is ground in every sector, one above q(max T) is kept in every sector.
+// Only points whose code equals a band code re-read x, y, z from HBM and recompute their
+// sector (tens of points per frame on flat ground: the code step is 1/64 m).
 template <int PPT, int LAYOUT, int KMODE>
-__global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
+__global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
     constexpr int G = 8;                          // points per load group (double-buffered)
     constexpr int NG = PPT / G;
-    static_assert(PPT % G == 0, "PPT must be a multiple of the load group");
+    constexpr int NW = (PPT + 63) / 64;
+    static_assert(PPT % G == 0 && PPT % 8 == 0, "PPT must be a multiple of the load group");
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
     constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
     FrontShared* fs = (FrontShared*)smem;
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
-    uint16_t* zq = (uint16_t*)bl;                 // z key prefixes, [k/4][lane][k%4]
+    uint8_t* zq = (uint8_t*)bl;                   // z codes, [k/8][lane][k%8]
 
     const uint32_t f = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
@@ -831,7 +873,8 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     __syncthreads();
 
     // ---- pass 1: stream the frame ----
-    uint64_t posm = 0;
+    LaneBits<NW> posm;
+    posm.clear();
     int cur_s = -1;
     float cur_m = 0.f;
     uint32_t touched = 0;        // sector bins this lane saw (bit 17: NaN angle)
@@ -850,6 +893,8 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
                 nxt[j] = i < N ? load_xyz3<LAYOUT>(fb, i, L) : make_float3(0.f, 0.f, 0.f);
             }
         }
+        uint32_t gpos = 0;
+        uint64_t codes = 0;
 #pragma unroll
         for (int j = 0; j < G; j++) {
             const int k = g * G + j;
@@ -859,9 +904,9 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
             int s = 0;
             bool ang_rm = false;
             classify_angle<GROUND, FILTER>(P, x, y, s, ang_rm);
-            if (FILTER) posm |= (uint64_t)(valid && !ang_rm && !dist_level_remove(P, x, y, z)) << k;
+            if (FILTER) gpos |= (uint32_t)(valid && !ang_rm && !dist_level_remove(P, x, y, z)) << j;
             if (GROUND) {
-                zq[((k >> 2) * CG_BLOCK + tid) * 4 + (k & 3)] = (uint16_t)(cg_zkey(z) >> 16);
+                codes |= (uint64_t)zcode(z, P) << (8 * j);
                 if (valid && s < CG_NUM_BINS && z == z) {
                     if (s != cur_s) {
                         if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
@@ -876,6 +921,8 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
                 }
             }
         }
+        if (FILTER) posm.set_byte(g, gpos);
+        if (GROUND) ((uint64_t*)zq)[g * CG_BLOCK + tid] = codes;   // one ds_write_b64 per group
 #pragma unroll
         for (int j = 0; j < G; j++) cur[j] = nxt[j];
     }
@@ -888,72 +935,76 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
     STAMP(1);
     if (GROUND && tid < 64) {
         // (double)z < (double)low + 0.1  <=>  z < ceil_to_float(low + 0.1)  (ground_removal.cpp:75)
-        uint32_t tk = 0xffffffffu;
+        uint32_t tk = 0xffffffffu, tq = 0xffffffffu, tqmax = 0u;
+        const bool used = tid <= CG_NUM_BINS && ((fs->scal[S_TOUCHED] >> tid) & 1u);
         if (tid <= CG_NUM_BINS) {
             const float low = cg_fkey_inv(fs->sec_key[tid]);
             const float T = cg_ceil_to_float((double)low + 0.1);
             fs->thr[tid] = T;
             tk = T != T ? 0u : cg_zkey(T);          // NaN threshold: nothing is below it
             fs->tkey[tid] = tk;
+            if (used) { tq = T != T ? 0u : zcode(T, P); tqmax = T != T ? 0u : tq; }
         }
         // band over the bins that hold points (an empty bin's threshold constrains nothing)
-        const bool used = tid <= CG_NUM_BINS && ((fs->scal[S_TOUCHED] >> tid) & 1u);
-        const uint32_t mn = wave_umin(used ? tk : 0xffffffffu), mx = wave_umax(used ? tk : 0u);
-        if (tid == 0) { fs->scal[S_TKMIN] = mn; fs->scal[S_TKMAX] = mx; }
+        const uint32_t qlo = wave_umin(tq), qhi = wave_umax(tqmax);
+        if (tid == 0) { fs->scal[S_TKMIN] = qlo; fs->scal[S_TKMAX] = qhi; }
     }
     __syncthreads();
     STAMP(2);
 
-    // ---- pass 2: ground decisions from the LDS prefixes ----
-    // A prefix p (top 16 bits of the z key) is below every used sector's threshold iff
-    // p < tkmin >> 16, and at or above all of them iff (p << 16) >= tkmax; prefixes in
-    // between are ambiguous and resolve from HBM (all of a lane's re-reads issued together).
-    uint64_t keepgm = 0, ambm = 0;
+    // ---- pass 2: ground decisions from the LDS codes ----
+    LaneBits<NW> keepgm, ambm;
+    keepgm.clear();
+    ambm.clear();
     if (GROUND) {
-        const uint32_t tkmin = fs->scal[S_TKMIN], tkmax = fs->scal[S_TKMAX];
-        const uint32_t pb = tkmin >> 16, pa = (tkmax >> 16) + ((tkmax & 0xffffu) ? 1u : 0u);
-        const uint2* zq4 = (const uint2*)zq;
-#pragma unroll 4
-        for (int k4 = 0; k4 < PPT / 4; k4++) {
-            const uint2 wv = zq4[k4 * CG_BLOCK + tid];
+        const uint32_t qlo = fs->scal[S_TKMIN], qhi = fs->scal[S_TKMAX];
+#pragma unroll 2
+        for (int g = 0; g < NG; g++) {
+            const uint64_t codes = ((const uint64_t*)zq)[g * CG_BLOCK + tid];
+            uint32_t kb = 0, ab = 0;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int k = 4 * k4 + j;
-                const uint32_t pref = ((j < 2 ? wv.x : wv.y) >> (16 * (j & 1))) & 0xffffu;
-                const bool valid = (uint32_t)k * CG_BLOCK + tid < N;
-                const bool below = pref < pb, amb = !below && pref < pa;
-                keepgm |= (uint64_t)(valid && !below && !amb) << k;
-                ambm |= (uint64_t)(valid && amb) << k;
+            for (int j = 0; j < 8; j++) {
+                const uint32_t c = (uint32_t)(codes >> (8 * j)) & 0xffu;
+                const bool valid = (uint32_t)(g * 8 + j) * CG_BLOCK + tid < N;
+                const bool below = c < qlo, above = c > qhi;
+                kb |= (uint32_t)(valid && above) << j;
+                ab |= (uint32_t)(valid && !below && !above) << j;
             }
+            keepgm.set_byte(g, kb);
+            ambm.set_byte(g, ab);
         }
         STAMP(21);
-        while (ambm) {
-            int ks[4];
-            float3 pt[4];
-            uint64_t m = ambm;
+        // ambiguous: exact z and sector from HBM, four re-reads in flight per lane
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                ks[q] = m ? __builtin_ctzll(m) : -1;
-                if (m) m &= m - 1;
+        for (int wi = 0; wi < NW; wi++) {
+            uint64_t m = ambm.w[wi];
+            while (m) {
+                int ks[4];
+                float3 pt[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    ks[q] = m ? __builtin_ctzll(m) : -1;
+                    if (m) m &= m - 1;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (ks[q] >= 0) pt[q] = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid, L);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (ks[q] < 0) continue;
+                    int sx = 0;
+                    bool unused = false;
+                    classify_angle<true, false>(P, pt[q].x, pt[q].y, sx, unused);
+                    if (!(cg_zkey(pt[q].z) < fs->tkey[sx])) keepgm.w[wi] |= 1ull << ks[q];
+                }
             }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (ks[q] >= 0) pt[q] = load_xyz3<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ks[q] < 0) continue;
-                int sx = 0;
-                bool unused = false;
-                classify_angle<true, false>(P, pt[q].x, pt[q].y, sx, unused);
-                if (!(cg_zkey(pt[q].z) < fs->tkey[sx])) keepgm |= 1ull << ks[q];
-            }
-            ambm = m;
         }
-        const uint32_t kc = wave_sum((uint32_t)__popcll(keepgm));
+        const uint32_t kc = wave_sum(keepgm.count());
         if (l == 0) atomicAdd(&fs->scal[S_K], kc);
     } else {
-#pragma unroll 8
-        for (int k = 0; k < PPT; k++) keepgm |= (uint64_t)((uint32_t)k * CG_BLOCK + tid < N) << k;
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if ((uint32_t)k * CG_BLOCK + tid < N) keepgm.w[k >> 6] |= 1ull << (k & 63);
     }
     STAMP(22);
 
@@ -962,7 +1013,7 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
         // (ground_removal.cpp:70-79); stable order comes from per-(k, wave) ballot counts
 #pragma unroll 8
         for (int k = 0; k < PPT; k++) {
-            const uint64_t bb = __ballot((keepgm >> k) & 1ull);
+            const uint64_t bb = __ballot(keepgm.get(k));
             if (l == 0) fs->cnt[k * WAVES + w] = (uint32_t)__popcll(bb);
         }
         __syncthreads();
@@ -974,8 +1025,9 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
         float4* out = (float4*)(L.ground + (uint64_t)f * N * 32);
 #pragma unroll 4
         for (int k = 0; k < PPT; k++) {
-            const uint64_t bb = __ballot((keepgm >> k) & 1ull);
-            if ((keepgm >> k) & 1ull) {
+            const bool kp = keepgm.get(k);
+            const uint64_t bb = __ballot(kp);
+            if (kp) {
                 const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
                 const uint32_t dst = fs->cnt[k * WAVES + w] + (uint32_t)__popcll(bb & ((1ull << l) - 1ull));
                 const float4 pp = load_xyzi<LAYOUT>(fb, i, L);
@@ -996,14 +1048,16 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
 
     // ---- compaction: per-wave atomic append; each survivor carries its point index, and
     // the voxel sort orders by (voxel idx, point index), so append order does not matter ----
-    const uint64_t keepm = FILTER ? (keepgm & posm) : keepgm;
-    const uint32_t nsv = (uint32_t)__popcll(keepm);
+    LaneBits<NW> keepm;
+#pragma unroll
+    for (int i = 0; i < NW; i++) keepm.w[i] = FILTER ? (keepgm.w[i] & posm.w[i]) : keepgm.w[i];
+    const uint32_t nsv = keepm.count();
     const uint32_t incl = wave_incl_scan(nsv);
     uint32_t wbase = 0;
     if (l == 63) wbase = atomicAdd(&fs->scal[S_MS], incl);
     wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
     uint32_t pos = wbase + incl - nsv;
-    __syncthreads();   // counts complete; z-prefix overlay in LDS is dead from here on
+    __syncthreads();   // counts complete; z-code overlay in LDS is dead from here on
     STAMP(3);
     const uint32_t Ms = fs->scal[S_MS];
     const uint32_t K = GROUND ? fs->scal[S_K] : N;
@@ -1036,8 +1090,9 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
             nfin++;
         }
     };
-    {
-        uint64_t m = keepm;
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) {
+        uint64_t m = keepm.w[wi];
         while (m) {
             int ks[4];
             float4 pt[4];
@@ -1048,12 +1103,12 @@ __global__ __launch_bounds__(CG_BLOCK, 1) void cg_frame_kernel(CgLaunch L, CgDev
             }
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (ks[q] >= 0) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
+                if (ks[q] >= 0) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid, L);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (ks[q] < 0) continue;
                 W.P[pos] = pt[q];
-                W.IDX[pos] = (uint32_t)ks[q] * CG_BLOCK + tid;   // point index
+                W.IDX[pos] = (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid;   // point index
                 bound(pt[q]);
                 pos++;
             }
@@ -1114,12 +1169,12 @@ int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
     if (L.n_frames == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 &&
                         L.off_i == 12;
-    if (L.n_points <= 16 * CG_BLOCK) {
-        return xyzi16 ? launch3<16, CG_LAYOUT_XYZI16>(L, P, kmode, s)
-                      : launch3<16, CG_LAYOUT_GENERIC>(L, P, kmode, s);
+    if (L.n_points <= 32 * CG_BLOCK) {
+        return xyzi16 ? launch3<32, CG_LAYOUT_XYZI16>(L, P, kmode, s)
+                      : launch3<32, CG_LAYOUT_GENERIC>(L, P, kmode, s);
     }
-    return xyzi16 ? launch3<64, CG_LAYOUT_XYZI16>(L, P, kmode, s)
-                  : launch3<64, CG_LAYOUT_GENERIC>(L, P, kmode, s);
+    return xyzi16 ? launch3<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_XYZI16>(L, P, kmode, s)
+                  : launch3<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_GENERIC>(L, P, kmode, s);
 }
 
 // ------------------------------------------------------------------------------------------
