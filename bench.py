@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--single-frame", action="store_true", help="also time C2 single-frame latency")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: per-phase in-kernel timing")
+    ap.add_argument("--scatter", action="store_true",
+                    help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
+                         "scatter to ranks, process, gather per-frame headers (reported separately)")
     ap.add_argument("--streams", type=int, default=3,
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
@@ -108,16 +111,18 @@ def main():
     bytes_per_launch = float((16.0 * N + 20.0 * V + 8.0 * Cn + 64.0).sum())
     achieved_gbs = bytes_per_launch / (avg_kernel_ms * 1e-3) / 1e9
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    from cones_perception_amd import dist as cd
+    elapsed = cd.max_over_ranks(elapsed, dev)
     total_frames = F * args.steps * world
     fps = total_frames / elapsed
 
     if args.stamps and rank == 0:
         torch.cuda.synchronize(dev)
         phase_stamps(engines[0], lambda: step(0), F)
+
+    scatter = None
+    if args.scatter and world > 1:
+        scatter = scatter_composition(cp, cd, engines[0], streams[0], raw, F, N, dev, rank, world, args.steps)
 
     single = None
     if args.single_frame and rank == 0:
@@ -153,6 +158,8 @@ def main():
         }
         if single is not None:
             line["single_frame"] = single
+        if scatter is not None:
+            line["c4_scatter_gather"] = scatter
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -206,6 +213,44 @@ def phase_stamps(eng, step, F):
         out["pass2b re-reads (wave0)"] = round(float(np.median((t[sub, 22] - t[sub, 21]) / 100.0)), 2)
         out["pass2c ballots (wave0)"] = round(float(np.median((t[sub, 3] - t[sub, 22]) / 100.0)), 2)
     print("STAMPS " + json.dumps(out), flush=True)
+
+
+def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps):
+    """C4 as composed in SURVEY.md §8e: rank 0 holds all world*F frames in HBM; each step
+    scatters F frames to every rank over RCCL, runs the batch, and gathers the per-frame
+    result headers back to rank 0. Timed like the main loop (barrier + sync, max over ranks)."""
+    import torch
+    import torch.distributed as dist
+    allf = None
+    if rank == 0:
+        allf = torch.from_numpy(cp.synth_frames(F * world, first_frame=0, rings=64, cols=N // 64)).to(dev)
+    hdr = torch.empty((F, 8), dtype=torch.int32, device=dev)
+
+    def one():
+        mine = cd.scatter_frames(allf, F, raw.shape[1], dev)
+        with torch.cuda.stream(stream):
+            stream.wait_stream(torch.cuda.current_stream(dev))
+            eng.run(mine.data_ptr(), F, N, 16, stream=stream.cuda_stream)
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        # header words: copy out of the engine's device buffer (int32 view)
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpyDtoDAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        hip.hipMemcpyDtoDAsync(hdr.data_ptr(), eng.results().d_header, F * 32,
+                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        return cd.gather_headers(hdr)
+
+    one()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    el = cd.max_over_ranks(time.perf_counter() - t0, dev)
+    return {"frames_per_s": F * world * steps / el, "ms_per_step": el / steps * 1e3,
+            "includes": "RCCL scatter of the batch from rank 0, processing, gather of headers"}
 
 
 def single_frame_latency(cp, params, raw, device, reps=200):

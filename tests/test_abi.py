@@ -1,0 +1,118 @@
+"""The C-ABI boundary on CPU: the library loads, exports every symbol include/cones_gpu.h
+declares, parameter defaults/profiles mirror the reference, error behaviour without a device,
+and the synthetic-frame generator is deterministic. No GPU compute is called here."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import cones_perception_amd as cp
+from cones_perception_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cones_gpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(cg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    names = declared_functions()
+    assert "cg_pipeline" in names and "cg_run_batch" in names and len(names) >= 18
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (cg_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+
+
+def test_header_compiles_as_c_and_cpp(tmp_path):
+    src = tmp_path / "h.c"
+    src.write_text('#include "cones_gpu.h"\nint main(void){cg_params p; cg_params_init(&p); return 0;}\n')
+    for cc in (["gcc", "-std=c99"], ["g++", "-x", "c++"]):
+        r = subprocess.run(cc + ["-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_ctypes_struct_sizes_match_c(tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "cones_gpu.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
+                   'sizeof(cg_params), sizeof(cg_cloud_view), sizeof(cg_ground_result), sizeof(cg_detect_result),'
+                   'sizeof(cg_batch), sizeof(cg_batch_results), sizeof(cg_synth_cfg)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [C.sizeof(t) for t in (_abi.cg_params, _abi.cg_cloud_view, _abi.cg_ground_result,
+                                  _abi.cg_detect_result, _abi.cg_batch, _abi.cg_batch_results, _abi.cg_synth_cfg)]
+    assert got == want
+
+
+def test_params_defaults_mirror_reference():
+    p = _abi.cg_params()
+    _abi.lib().cg_params_init(C.byref(p))
+    # src/ground_removal.cpp:18-19, src/cone_detection.cpp:27-43
+    assert (p.num_of_sectors, p.default_lowest_point) == (16, np.float32(-0.1))
+    assert (p.distance_treshold_max, p.distance_treshold_min, p.level_threshold, p.angle_threshold) == \
+        (7.0, 0.7, -0.5, 90.0)
+    assert (p.min_cluster_size, p.max_cluster_size) == (3, 50)
+    assert p.cone_position_extension_length == 0.05 and p.voxel_filter_leaf_size_x == 0.04
+
+
+def test_profiles_and_yaml(tmp_path):
+    sim = cp.load_params("simulation")
+    assert (sim.distance_treshold_max, sim.min_cluster_size, sim.max_cluster_size) == (10.0, 2, 500)
+    y = tmp_path / "p.yaml"
+    y.write_text("distance_treshold_max: 6.0\nlevel_threshold: -0.09\nunknown_key: 3\n")
+    p = cp.load_params("simulation", str(y))
+    assert p.distance_treshold_max == 6.0 and p.level_threshold == -0.09 and p.max_cluster_size == 500
+
+
+def test_null_arguments_fail_loudly():
+    lib = _abi.lib()
+    r = _abi.cg_detect_result()
+    v = _abi.cg_cloud_view()
+    assert lib.cg_pipeline(None, C.byref(v), C.byref(r)) == _abi.CG_E_INVALID
+    assert lib.cg_last_error()
+    assert lib.cg_run_batch(None, None, 0, None) == _abi.CG_E_INVALID
+
+
+def test_create_without_device_reports_device_error():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    h = C.c_void_p()
+    rc = _abi.lib().cg_create(None, 0, C.byref(h))
+    assert rc == _abi.CG_E_DEVICE and h.value is None
+    assert b"device" in _abi.lib().cg_last_error().lower()
+    with pytest.raises(cp.CgError):
+        cp.ConePipeline()
+
+
+def test_synth_deterministic_and_thread_invariant():
+    a = cp.synth_frames(3, first_frame=7, rings=16, cols=256, threads=1)
+    b = cp.synth_frames(3, first_frame=7, rings=16, cols=256, threads=3)
+    c = cp.synth_frames(1, first_frame=8, rings=16, cols=256, threads=1)
+    assert np.array_equal(a, b) and np.array_equal(a[1], c[0])
+    p16 = cp.frame_cloud(a[0], 16).xyzi()
+    raw32 = cp.synth_frames(1, first_frame=7, rings=16, cols=256, point_step=32)
+    p32 = cp.frame_cloud(raw32[0], 32).xyzi()
+    assert np.array_equal(p16.view(np.uint32), p32.view(np.uint32))
+    assert np.isfinite(p16).all() and len(p16) == 16 * 256
+
+
+def test_pointcloud2_roundtrip_and_layouts():
+    rng = np.random.default_rng(0)
+    pts = rng.standard_normal((100, 4)).astype(np.float32)
+    for layout in (16, 32):
+        msg = cp.PointCloud2.from_xyzi(pts, layout=layout)
+        assert np.array_equal(msg.xyzi(), pts)
+        v = msg.view()
+        assert v.point_step == layout and v.off_intensity == (12 if layout == 16 else 16)
+    msg = cp.PointCloud2.from_xyzi(pts, intensity=False)
+    assert msg.view().off_intensity == -1

@@ -1,0 +1,74 @@
+"""World-size-2 gloo runs of the multi-GPU plumbing (cones_perception_amd/dist.py) on CPU:
+frame ownership, max-over-ranks timing, root scatter of frames and gather of per-frame result
+headers. Per-frame results come from the CPU restatement (the GPU path needs a device), so
+this checks that sharded processing + gather equals processing the whole batch in one rank."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+F, RINGS, COLS = 3, 16, 256
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _headers(frames):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cones_perception_amd as cp
+    import oracle_py as O
+    params = cp.load_params("simulation")
+    out = np.zeros((frames.shape[0], 8), np.int32)
+    for i in range(frames.shape[0]):
+        det, hdr = O.run(params, cp.frame_cloud(frames[i]), O.MODE_PIPELINE)
+        out[i, :5] = hdr[:5].astype(np.int32)
+        out[i, 5] = int(np.abs(det.centroids).sum() * 1000) if len(det.centroids) else 0
+    return out
+
+
+def _worker(rank, ws, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    import cones_perception_amd as cp
+    from cones_perception_amd import dist as cd
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    dev = torch.device("cpu")
+    # (1) weak-scaling ownership: each rank synthesises its own frames
+    mine = list(cd.frame_range(rank, F))
+    own = cp.synth_frames(F, first_frame=mine[0], rings=RINGS, cols=COLS)
+    # (2) C4 composition: root scatters the whole batch; must equal the owned frames
+    allf = torch.from_numpy(cp.synth_frames(F * ws, first_frame=0, rings=RINGS, cols=COLS)) if rank == 0 else None
+    got = cd.scatter_frames(allf, F, own.shape[1], dev)
+    assert np.array_equal(got.numpy(), own)
+    hdr = torch.from_numpy(_headers(own))
+    gathered = cd.gather_headers(hdr)
+    t = cd.max_over_ranks(float(rank + 1), dev)
+    if rank == 0:
+        np.save(result_path, np.concatenate([gathered.numpy().reshape(-1), [int(t)]]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_batch_equals_single_rank(tmp_path):
+    ws = 2
+    out = str(tmp_path / "res.npy")
+    mp.spawn(_worker, args=(ws, _free_port(), out), nprocs=ws, join=True)
+    res = np.load(out)
+    gathered, tmax = res[:-1].reshape(ws * F, 8), int(res[-1])
+    sys.path.insert(0, ROOT)
+    import cones_perception_amd as cp
+    single = _headers(cp.synth_frames(ws * F, first_frame=0, rings=RINGS, cols=COLS))
+    assert np.array_equal(gathered, single)
+    assert tmax == ws

@@ -159,3 +159,42 @@ def test_dense_batch_mixed_paths(params):
     for f in range(raw.shape[0]):
         ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE)
         assert_same_detection(eng.fetch(f), ref, f"mixed batch frame {f}")
+
+
+import kat_clouds as KC  # noqa: E402
+
+_KATS = KC.all_kats()
+
+
+@pytest.mark.parametrize("kat", _KATS, ids=[k[0] for k in _KATS])
+@pytest.mark.parametrize("mode", ["pipeline", "detect", "ground"])
+def test_kat_gpu_matches_oracle(kat, mode):
+    """Known-answer edge clouds through the C-ABI single-frame calls vs the CPU restatement."""
+    name, pts, over, _ = kat
+    params = cp.load_params("simulation", over)
+    msg = cp.PointCloud2.from_xyzi(pts)
+    if mode == "ground":
+        out = cp.GroundRemover(params).cloud_handler(msg)
+        ref, hdr = O.run(params, msg, O.MODE_GROUND)
+        assert out.n_kept == int(hdr[1]), name
+        g = out.data.view(np.float32).reshape(-1, 8)
+        r = ref.view(np.float32).reshape(-1, 8)
+        assert np.array_equal(g[:, :5].view(np.uint32), r[:, :5].view(np.uint32)), name
+        return
+    eng = cp.ConePipeline(params) if mode == "pipeline" else cp.ConeDetector(params)
+    got = eng.cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_PIPELINE if mode == "pipeline" else O.MODE_DETECT)
+    assert_same_detection(got, ref, f"{name}/{mode}")
+
+
+def test_detector_missing_intensity_quirk(params):
+    """src/cone_detection.cpp:142-151: a detector input without an intensity field gets a
+    fake FLOAT32 field at offset 0, so intensity reads x."""
+    raw = cp.synth_frames(1, first_frame=3, rings=16, cols=1024)
+    msg = cp.frame_cloud(raw[0])
+    msg.fields = [f for f in msg.fields if f.name != "intensity"]
+    det = cp.ConeDetector(params)
+    got = det.cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_DETECT, intensity_offset=0)
+    assert_same_detection(got, ref, "no-intensity detector")
+    assert np.array_equal(got.voxels[:, 3].view(np.uint32), ref.voxels[:, 3].view(np.uint32))
