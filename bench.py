@@ -151,9 +151,13 @@ def main():
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),
                          "kernel": "cg_frame_kernel", "avg_kernel_ms": avg_kernel_ms,
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         # launches on S streams overlap, so per-launch duration counts shared
+                         # time S-fold; the aggregate rate is bytes of all launches / wall time
+                         "aggregate_achieved": bytes_per_launch * args.steps * world / elapsed / 1e9 / world,
+                         "aggregate_frac": bytes_per_launch * args.steps / elapsed / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
         }
         if single is not None:
@@ -163,6 +167,17 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def traffic_per_launch(F):
+    """HBM bytes per launch from the committed PMC summary (profiles/r1_traffic.json:
+    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction), scaled to this launch's frames."""
+    p = os.path.join(ROOT, "profiles", "r1_traffic.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        t = json.load(fh)
+    return t["hbm_bytes_per_frame"] * F
 
 
 def fetch_headers(res, F):
