@@ -59,6 +59,18 @@ def build(verbose=False, force=False):
     return LIB
 
 
+def build_host_demo(verbose=False):
+    """g++ build of the C++ node mirror demo (host/nodes_demo.cpp) against libcones_gpu.so."""
+    lib = build(verbose)
+    out = os.path.join(PKG, "lib", "nodes_demo")
+    src = os.path.join(PKG, "host", "nodes_demo.cpp")
+    if _stale(out, [src, os.path.join(PKG, "host", "cones_nodes.hpp"), lib]):
+        _run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(PKG, "host"),
+              src, "-o", out, "-L", os.path.dirname(lib), "-lcones_gpu",
+              "-Wl,-rpath,$ORIGIN"], verbose)
+    return out
+
+
 def build_oracle(verbose=False):
     """Compile the CPU restatement (test infrastructure, oracle/)."""
     _run(["make", "-C", os.path.join(ROOT, "oracle")], verbose)
@@ -68,3 +80,4 @@ def build_oracle(verbose=False):
 if __name__ == "__main__":
     print(build(verbose=True, force="--force" in sys.argv))
     print(build_oracle(verbose=True))
+    print(build_host_demo(verbose=True))

@@ -1,0 +1,68 @@
+// nodes_demo.cpp — runs the two-node composition of launch/cones_perception.launch
+// (GroundRemover -> groundless_cloud -> ConeDetector) through the C++ mirror and checks that
+// it equals the fused cg_pipeline on the same frames, bit for bit. Exit 0 on success.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "cones_nodes.hpp"
+
+using namespace cones_gpu;
+
+static PointCloud2 synth_cloud(uint64_t frame) {
+    cg_synth_cfg cfg;
+    cg_synth_default(&cfg);
+    PointCloud2 msg;
+    msg.width = cfg.rings * cfg.cols;
+    msg.fields = {{"x", 0}, {"y", 4}, {"z", 8}, {"intensity", 12}};
+    msg.point_step = 16;
+    msg.row_step = 16 * msg.width;
+    msg.data.resize((size_t)msg.row_step);
+    check(cg_synth_frames(&cfg, frame, 1, msg.data.data(), msg.row_step, 1));
+    return msg;
+}
+
+static bool same(const std::vector<float>& a, const std::vector<float>& b) {
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); i++) {
+        if (std::isnan(a[i]) && std::isnan(b[i])) continue;
+        uint32_t x, y;
+        std::memcpy(&x, &a[i], 4);
+        std::memcpy(&y, &b[i], 4);
+        if (x != y) return false;
+    }
+    return true;
+}
+
+int main(int argc, char** argv) {
+    const int frames = argc > 1 ? std::atoi(argv[1]) : 4;
+    cg_params p;
+    cg_params_init(&p);   // reference defaults, then the simulation profile
+    p.distance_treshold_max = 10.0; p.distance_treshold_min = 1.0; p.level_threshold = -5.0;
+    p.angle_threshold = 160.0; p.min_cluster_size = 2; p.max_cluster_size = 500;
+    try {
+        GroundRemover ground(p);
+        ConeDetector detector(p);
+        ConePipeline fused(p);
+        for (int f = 0; f < frames; f++) {
+            const PointCloud2 msg = synth_cloud((uint64_t)f);
+            const PointCloud2 groundless = ground.cloud_handler(msg);
+            const Detection a = detector.cloud_handler(groundless);
+            const Detection b = fused.cloud_handler(msg);
+            const bool ok = a.n_filtered == b.n_filtered && ground.n_kept == b.n_kept &&
+                            same(a.voxels, b.voxels) && a.clusters == b.clusters &&
+                            same(a.centroids, b.centroids);
+            std::printf("frame %d: N=%u K=%u M=%u V=%zu C=%zu %s\n", f, msg.width, b.n_kept, b.n_filtered,
+                        b.voxels.size() / 4, b.clusters.size(), ok ? "two-node == fused" : "MISMATCH");
+            for (size_t c = 0; c < b.clusters.size(); c++)
+                std::printf("  cone %zu: %zu voxels at (%.3f, %.3f)\n", c, b.clusters[c].size(),
+                            b.centroids[2 * c], b.centroids[2 * c + 1]);
+            if (!ok) return 1;
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        return 2;
+    }
+    return 0;
+}

@@ -198,3 +198,14 @@ def test_detector_missing_intensity_quirk(params):
     ref, _ = O.run(params, msg, O.MODE_DETECT, intensity_offset=0)
     assert_same_detection(got, ref, "no-intensity detector")
     assert np.array_equal(got.voxels[:, 3].view(np.uint32), ref.voxels[:, 3].view(np.uint32))
+
+
+def test_cpp_node_mirror_two_node_equals_fused():
+    """The C++ mirror of the reference nodes (host/cones_nodes.hpp): GroundRemover ->
+    groundless_cloud (PCL PointXYZI layout) -> ConeDetector equals the fused pipeline."""
+    import subprocess
+    from cones_perception_amd import build as B
+    exe = B.build_host_demo()
+    r = subprocess.run([exe, "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("two-node == fused") == 3
