@@ -119,6 +119,9 @@ def main():
     if args.stamps and rank == 0:
         torch.cuda.synchronize(dev)
         phase_stamps(engines[0], lambda: step(0), F)
+        if S > 1:   # the same batch with the other streams' batches in flight beside it
+            phase_stamps(engines[0], lambda: step(0), F,
+                         around=lambda: [step(i) for i in range(1, S)], tag="loaded")
 
     scatter = None
     if args.scatter and world > 1:
@@ -201,18 +204,23 @@ STAMP_NAMES = ["start", "pass1 stream", "thresholds", "pass2 keep bits", "compac
                "centroids+header"]
 
 
-def phase_stamps(eng, step, F):
-    """Diagnostic build of one batch: s_memrealtime stamps at phase boundaries (not timed)."""
+def phase_stamps(eng, step, F, around=None, tag="alone"):
+    """Diagnostic build of one batch: s_memrealtime stamps at phase boundaries (not timed).
+    With `around`, other batches are enqueued on the other streams before and after it."""
     import numpy as np
     from cones_perception_amd import _abi
     lib = _abi.lib()
     _abi.check(lib.cg_debug_stamps(eng.handle, 1))
+    if around:
+        around()
     step()
+    if around:
+        around()
     st = np.zeros((F, 32), np.uint64)
     _abi.check(lib.cg_debug_stamps_fetch(eng.handle, st.ctypes.data, F))
     _abi.check(lib.cg_debug_stamps(eng.handle, 0))
     t = st.astype(np.int64)
-    out = {"batch_span_us": float((t[:, 20].max() - t[:, 0].min()) / 100.0),
+    out = {"tag": tag, "batch_span_us": float((t[:, 20].max() - t[:, 0].min()) / 100.0),
            "wg_end_spread_us": float((t[:, 20].max() - t[:, 20].min()) / 100.0)}
     prev = t[:, 0].copy()
     for i in range(1, 21):
@@ -227,6 +235,8 @@ def phase_stamps(eng, step, F):
         out["pass2a lds loop (wave0)"] = round(float(np.median((t[sub, 21] - t[sub, 2]) / 100.0)), 2)
         out["pass2b re-reads (wave0)"] = round(float(np.median((t[sub, 22] - t[sub, 21]) / 100.0)), 2)
         out["pass2c ballots (wave0)"] = round(float(np.median((t[sub, 3] - t[sub, 22]) / 100.0)), 2)
+    life = (t[:, 20] - t[:, 0]) / 100.0
+    out["wg_lifetime_us_p10_p50_p90"] = [round(float(np.percentile(life, q)), 1) for q in (10, 50, 90)]
     print("STAMPS " + json.dumps(out), flush=True)
 
 

@@ -313,12 +313,18 @@ __device__ __forceinline__ float4 load_xyzi(const uint8_t* fb, uint32_t i, const
 // filter_points_position (src/cone_detection.cpp:195-201), distance and level part:
 // true = removed. The float sum of squares decides unless it lies within 1e-6 (relative) of
 // a threshold; then the exact double S decides.
-__device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x, float y, float z) {
+// Fast form: decides from the float sum alone; returns false (uncertain) when only the
+// exact double S can decide.
+__device__ __forceinline__ bool dist_level_fast(const CgDevParams& P, float x, float y, float z, bool& rm) {
     const float sf = (x * x + y * y) + z * z;
     const bool far_c = sf > P.sfar_hi, nfar_c = sf < P.sfar_lo;
     const bool near_c = sf < P.snear_lo, nnear_c = sf > P.snear_hi;
-    bool rm = (z < P.level_f) || far_c || near_c;
-    if (!(far_c || nfar_c) || !(near_c || nnear_c)) {
+    rm = (z < P.level_f) | far_c | near_c;
+    return (far_c | nfar_c) & (near_c | nnear_c);
+}
+__device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x, float y, float z) {
+    bool rm;
+    if (!dist_level_fast(P, x, y, z, rm)) {
         const double S = cg_sumsq_d(x, y, z);
         rm = (z < P.level_f) || (S >= P.s_far) || (S < P.s_near);
     }
@@ -335,8 +341,10 @@ __device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x,
 // The exact restatement is large and rarely executed: one out-of-line copy keeps it out of
 // the hot loops' instruction footprint.
 __device__ __noinline__ float cg_atan2f_cold(float y, float x) { return cg_atan2f(y, x); }
+// Fast form: returns false (uncertain) where only the exact restatement can decide.
 template <bool NEED_SECTOR, bool NEED_ANGLE>
-__device__ __forceinline__ void classify_angle(const CgDevParams& P, float x, float y, int& sector, bool& ang_rm) {
+__device__ __forceinline__ bool classify_angle_fast(const CgDevParams& P, float x, float y, int& sector,
+                                                    bool& ang_rm) {
     const float ax = fabsf(x), ay = fabsf(y);
     const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
     const float r = mn * __builtin_amdgcn_rcpf(mx);
@@ -355,21 +363,25 @@ __device__ __forceinline__ void classify_angle(const CgDevParams& P, float x, fl
     if (y < 0.f) a = -a;
     // off-axis, not NaN (fmaxf/fminf drop NaN), and inside the range where v_rcp_f32(mx) is
     // a normal number (mx < 2^126) and r does not underflow badly
-    bool ok = x == x && y == y && mn > 1.0e-30f && mx < 8.0e37f;
+    bool ok = (x == x) & (y == y) & (mn > 1.0e-30f) & (mx < 8.0e37f);
     if (NEED_SECTOR) {
         const float inv_sec = 1.0f / CG_SECTOR_ANGLE_RAD;
         float wl = a - CG_ANG_MARGIN, wh = a + CG_ANG_MARGIN;
         wl = wl < 0.f ? wl + 6.2831855f : wl;
         wh = wh < 0.f ? wh + 6.2831855f : wh;
         const int sl = (int)floorf(wl * inv_sec), sh = (int)floorf(wh * inv_sec);
-        ok = ok && sl == sh;
+        ok = ok & (sl == sh);
         sector = sl > 16 ? 16 : sl;
     }
     if (NEED_ANGLE) {
-        ang_rm = (a <= P.ang_lo) || (a >= P.ang_hi);
-        ok = ok && fabsf(a - P.ang_lo) > CG_ANG_MARGIN && fabsf(a - P.ang_hi) > CG_ANG_MARGIN;
+        ang_rm = (a <= P.ang_lo) | (a >= P.ang_hi);
+        ok = ok & (fabsf(a - P.ang_lo) > CG_ANG_MARGIN) & (fabsf(a - P.ang_hi) > CG_ANG_MARGIN);
     }
-    if (!ok) {
+    return ok;
+}
+template <bool NEED_SECTOR, bool NEED_ANGLE>
+__device__ __forceinline__ void classify_angle(const CgDevParams& P, float x, float y, int& sector, bool& ang_rm) {
+    if (!classify_angle_fast<NEED_SECTOR, NEED_ANGLE>(P, x, y, sector, ang_rm)) {
         const float ae = cg_atan2f_cold(y, x);
         if (NEED_SECTOR) sector = cg_sector(ae);
         if (NEED_ANGLE) ang_rm = (ae <= P.ang_lo) || (ae >= P.ang_hi);
@@ -855,7 +867,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     constexpr int G = 8;                          // points per load group (double-buffered)
     constexpr int NG = PPT / G;
     constexpr int NW = (PPT + 63) / 64;
-    static_assert(PPT % G == 0 && PPT % 8 == 0, "PPT must be a multiple of the load group");
+    static_assert(PPT % (2 * G) == 0, "PPT must be a multiple of two load groups");
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
     constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
@@ -873,61 +885,98 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     __syncthreads();
 
     // ---- pass 1: stream the frame ----
-    LaneBits<NW> posm;
+    // Two explicit load buffers (A, B), the loop unrolled by two: group g+1 is in flight while
+    // group g is classified, with no register copies between iterations (a copy of a buffer
+    // whose loads are outstanding would force a full vmcnt drain). Loads are branch-free: an
+    // index past the frame reads point N-1 again, which can only repeat that point's own
+    // sector-min contribution; its filter and uncertainty bits are masked. Points the
+    // certified fast classification cannot decide are redone exactly after the loop.
+    LaneBits<NW> posm, uncm;
     posm.clear();
+    uncm.clear();
     int cur_s = -1;
     float cur_m = 0.f;
     uint32_t touched = 0;        // sector bins this lane saw (bit 17: NaN angle)
-    float3 cur[G], nxt[G];
+    const uint32_t nlast = N ? N - 1 : 0u;
+    auto load_group = [&](float3* buf, int g) {
 #pragma unroll
-    for (int j = 0; j < G; j++) {
-        const uint32_t i = (uint32_t)j * CG_BLOCK + tid;
-        cur[j] = i < N ? load_xyz3<LAYOUT>(fb, i, L) : make_float3(0.f, 0.f, 0.f);
-    }
-#pragma unroll 1
-    for (int g = 0; g < NG; g++) {
-        if (g + 1 < NG) {
-#pragma unroll
-            for (int j = 0; j < G; j++) {
-                const uint32_t i = (uint32_t)((g + 1) * G + j) * CG_BLOCK + tid;
-                nxt[j] = i < N ? load_xyz3<LAYOUT>(fb, i, L) : make_float3(0.f, 0.f, 0.f);
-            }
-        }
-        uint32_t gpos = 0;
+        for (int j = 0; j < G; j++)
+            buf[j] = load_xyz3<LAYOUT>(fb, min((uint32_t)(g * G + j) * CG_BLOCK + tid, nlast), L);
+    };
+    auto run_group = [&](const float3* buf, int g) {
+        uint32_t gpos = 0, gunc = 0;
         uint64_t codes = 0;
 #pragma unroll
         for (int j = 0; j < G; j++) {
-            const int k = g * G + j;
-            const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
-            const bool valid = i < N;
-            const float x = cur[j].x, y = cur[j].y, z = cur[j].z;
+            const float x = buf[j].x, y = buf[j].y, z = buf[j].z;
             int s = 0;
-            bool ang_rm = false;
-            classify_angle<GROUND, FILTER>(P, x, y, s, ang_rm);
-            if (FILTER) gpos |= (uint32_t)(valid && !ang_rm && !dist_level_remove(P, x, y, z)) << j;
+            bool ang_rm = false, drm = false;
+            bool ok = classify_angle_fast<GROUND, FILTER>(P, x, y, s, ang_rm);
+            if (FILTER) {
+                ok = dist_level_fast(P, x, y, z, drm) & ok;
+                gpos |= (uint32_t)(ok & !ang_rm & !drm) << j;
+            }
+            gunc |= (uint32_t)!ok << j;
             if (GROUND) {
                 codes |= (uint64_t)zcode(z, P) << (8 * j);
-                if (valid && s < CG_NUM_BINS && z == z) {
-                    if (s != cur_s) {
-                        if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
-                        touched |= 1u << s;
-                        cur_s = s;
-                        cur_m = z;
-                    } else {
-                        cur_m = fminf(cur_m, z);
-                    }
-                } else if (valid && s == CG_NAN_BIN) {
-                    touched |= 1u << CG_NAN_BIN;
-                }
+                // run-length sector minimum: flush the lane's run when the sector changes
+                const bool upd = ok & (z == z);
+                const bool flush = upd & (s != cur_s);
+                if (flush & (cur_s >= 0)) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+                touched |= flush ? 1u << s : 0u;
+                cur_m = flush ? z : (upd ? fminf(cur_m, z) : cur_m);
+                cur_s = flush ? s : cur_s;
             }
         }
         if (FILTER) posm.set_byte(g, gpos);
+        uncm.set_byte(g, gunc);
         if (GROUND) ((uint64_t*)zq)[g * CG_BLOCK + tid] = codes;   // one ds_write_b64 per group
+    };
+    if (N) {
+        float3 A[G], B[G];
+        load_group(A, 0);
+#pragma unroll 1
+        for (int g = 0; g < NG; g += 2) {
+            load_group(B, g + 1);
+            run_group(A, g);
+            load_group(A, g + 2);   // past the frame on the last trip: every lane reads point N-1
+            run_group(B, g + 1);
+        }
+    }
+    {   // points k*512 + tid >= N do not exist: drop their bits
+        const uint32_t nv = tid < N ? (N - tid + CG_BLOCK - 1) / CG_BLOCK : 0u;
 #pragma unroll
-        for (int j = 0; j < G; j++) cur[j] = nxt[j];
+        for (int wi = 0; wi < NW; wi++) {
+            const int c = (int)nv - 64 * wi;
+            const uint64_t vm = c >= 64 ? ~0ull : (c <= 0 ? 0ull : (1ull << c) - 1ull);
+            posm.w[wi] &= vm;
+            uncm.w[wi] &= vm;
+        }
+    }
+    if (GROUND && cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+    // uncertain points: exact angle (glibc restatement) and exact double distance
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) {
+        uint64_t m = uncm.w[wi];
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            const float3 p = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + k) * CG_BLOCK + tid, L);
+            const float ae = cg_atan2f_cold(p.y, p.x);
+            if (GROUND) {
+                const int s = cg_sector(ae);
+                if (s < CG_NUM_BINS && p.z == p.z) {
+                    atomicMin(&fs->sec_key[s], cg_fkey(p.z));
+                    touched |= 1u << s;
+                } else if (s == CG_NAN_BIN) {
+                    touched |= 1u << CG_NAN_BIN;
+                }
+            }
+            if (FILTER && !((ae <= P.ang_lo) || (ae >= P.ang_hi)) && !dist_level_remove(P, p.x, p.y, p.z))
+                posm.w[wi] |= 1ull << k;
+        }
     }
     if (GROUND) {
-        if (cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
         touched = wave_or(touched);
         if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
     }
