@@ -99,6 +99,7 @@ int prepare(const cg_params& p, CgDevParams& d) {
     const float tmax = cg_ceil_to_float((double)p.default_lowest_point + 0.1);
     d.zq_scale = 64.0f;
     d.zq_z0 = (tmax == tmax && std::isfinite(tmax)) ? tmax - 254.0f / 64.0f : 0.0f;
+    d.zq_bias = -d.zq_z0 * d.zq_scale;
     // does PointXYZI() (0,0,0) survive filter_points_position?
     const float a0 = cg_atan2f(0.0f, 0.0f);
     const double S0 = 0.0;

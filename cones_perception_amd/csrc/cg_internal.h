@@ -22,8 +22,9 @@ struct CgDevParams {
     // fast-path certificates (float bounds around the exact double thresholds): a float
     // sum of squares below *_lo / above *_hi decides the compare without the double path
     float sfar_lo, sfar_hi, snear_lo, snear_hi;
-    // 8-bit z code window for the on-chip ground decision: q(z) = floor((z - zq_z0) * zq_scale)
-    float zq_z0, zq_scale;
+    // 8-bit z code window for the on-chip ground decision:
+    // q(z) = trunc(clamp(fl(z * zq_scale + zq_bias), 0, 255)), zq_bias = -zq_z0 * zq_scale
+    float zq_z0, zq_scale, zq_bias;
 };
 
 // One batch launch: uniform frames, device-resident input and outputs.

@@ -338,6 +338,7 @@ __device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x,
 // angle thresholds. Otherwise the exact glibc restatement decides. Both decisions are
 // monotone step functions of the float angle, so equal classes at a - E and a + E certify.
 #define CG_ANG_MARGIN 8.0e-6f
+#define CG_SEC_MARGIN_T 2.0e-5f
 // The exact restatement is large and rarely executed: one out-of-line copy keeps it out of
 // the hot loops' instruction footprint.
 __device__ __noinline__ float cg_atan2f_cold(float y, float x) { return cg_atan2f(y, x); }
@@ -345,8 +346,11 @@ __device__ __noinline__ float cg_atan2f_cold(float y, float x) { return cg_atan2
 template <bool NEED_SECTOR, bool NEED_ANGLE>
 __device__ __forceinline__ bool classify_angle_fast(const CgDevParams& P, float x, float y, int& sector,
                                                     bool& ang_rm) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    // |x|, |y| ordered as unsigned bit patterns (monotone for non-NaN; a NaN fails `ok`):
+    // no IEEE canonicalisation as fmaxf / fminf would need
+    const uint32_t bx = __float_as_uint(x) & 0x7fffffffu, by = __float_as_uint(y) & 0x7fffffffu;
+    const float ax = __uint_as_float(bx), ay = __uint_as_float(by);
+    const float mx = __uint_as_float(max(bx, by)), mn = __uint_as_float(min(bx, by));
     const float r = mn * __builtin_amdgcn_rcpf(mx);
     const float q = r * r;
     // (explicit FMAs: this is our approximation, not a reference expression)
@@ -358,24 +362,29 @@ __device__ __forceinline__ bool classify_angle_fast(const CgDevParams& P, float 
     p = fmaf(p, q, -0.3331736922264099f);
     p = fmaf(p, q, 0.9999961256980896f);
     float a = r * p;
-    if (ay > ax) a = 1.5707964f - a;
+    if (by > bx) a = 1.5707964f - a;
     if (x < 0.f) a = 3.1415927f - a;
     if (y < 0.f) a = -a;
     // off-axis, not NaN (fmaxf/fminf drop NaN), and inside the range where v_rcp_f32(mx) is
     // a normal number (mx < 2^126) and r does not underflow badly
     bool ok = (x == x) & (y == y) & (mn > 1.0e-30f) & (mx < 8.0e37f);
     if (NEED_SECTOR) {
-        const float inv_sec = 1.0f / CG_SECTOR_ANGLE_RAD;
-        float wl = a - CG_ANG_MARGIN, wh = a + CG_ANG_MARGIN;
-        wl = wl < 0.f ? wl + 6.2831855f : wl;
-        wh = wh < 0.f ? wh + 6.2831855f : wh;
-        const int sl = (int)floorf(wl * inv_sec), sh = (int)floorf(wh * inv_sec);
-        ok = ok & (sl == sh);
-        sector = sl > 16 ? 16 : sl;
+        // t ~ wrap(a) / sector: the reference floors fl(fl(wrap(ae)) / SEC) (cg_sector). With
+        // |a - ae| <= 1.5e-6 rad, |t - wrap(ae)/SEC| <= 7.9e-6 (3.9e-6 from the angle, the rest
+        // from the roundings of both wraps, 1/SEC, 2pi/SEC, this fma and the reference's
+        // division), so a fractional part farther than CG_SEC_MARGIN_T from an integer certifies
+        // the bin. Near a = 0 the two wraps may disagree: |a| > CG_ANG_MARGIN certifies the sign.
+        const float t = fmaf(a, 1.0f / CG_SECTOR_ANGLE_RAD, a < 0.f ? 6.2831855f / CG_SECTOR_ANGLE_RAD : 0.f);
+        const float fl = floorf(t);
+        ok = ok & (fabsf((t - fl) - 0.5f) < 0.5f - CG_SEC_MARGIN_T) & (fabsf(a) > CG_ANG_MARGIN);
+        sector = (int)fl;   // <= 16: t <= 2pi / SEC + rounding = 16.37
     }
     if (NEED_ANGLE) {
-        ang_rm = (a <= P.ang_lo) | (a >= P.ang_hi);
-        ok = ok & (fabsf(a - P.ang_lo) > CG_ANG_MARGIN) & (fabsf(a - P.ang_hi) > CG_ANG_MARGIN);
+        // ang_lo == -ang_hi exactly (cg_api.cpp prepare), so a <= ang_lo || a >= ang_hi is
+        // |a| >= ang_hi (NaN thresholds: false either way)
+        const float aa = fabsf(a);
+        ang_rm = aa >= P.ang_hi;
+        ok = ok & (fabsf(aa - P.ang_hi) > CG_ANG_MARGIN);
     }
     return ok;
 }
@@ -842,12 +851,12 @@ struct LaneBits {
     }
 };
 
-// 8-bit monotone z code: q(z) = clamp(floor((z - z0) * 64), 0, 255), NaN -> 255. For any T,
-// q(z) < q(T) implies z < T and q(z) > q(T) implies z > T; equal codes are ambiguous.
+// 8-bit monotone z code: q(z) = trunc(clamp(fl(z * 64 + b), 0, 255)), NaN -> 255, b = -64 z0.
+// Any monotone non-decreasing q serves: for any T, q(z) < q(T) implies z < T and q(z) > q(T)
+// implies z > T; equal codes are ambiguous. Thresholds are coded by this same function.
 __device__ __forceinline__ uint32_t zcode(float z, const CgDevParams& P) {
-    if (z != z) return 255u;
-    const float q = floorf((z - P.zq_z0) * P.zq_scale);
-    return (uint32_t)fminf(fmaxf(q, 0.f), 255.f);
+    const float q = __builtin_amdgcn_fmed3f(fmaf(z, P.zq_scale, P.zq_bias), 0.f, 255.f);
+    return z == z ? (uint32_t)q : 255u;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -894,8 +903,8 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     LaneBits<NW> posm, uncm;
     posm.clear();
     uncm.clear();
-    int cur_s = -1;
-    float cur_m = 0.f;
+    int cur_s = 0;
+    float cur_m = INFINITY;      // minimum z of the lane's current run of sector cur_s
     uint32_t touched = 0;        // sector bins this lane saw (bit 17: NaN angle)
     const uint32_t nlast = N ? N - 1 : 0u;
     auto load_group = [&](float3* buf, int g) {
@@ -904,8 +913,9 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             buf[j] = load_xyz3<LAYOUT>(fb, min((uint32_t)(g * G + j) * CG_BLOCK + tid, nlast), L);
     };
     auto run_group = [&](const float3* buf, int g) {
-        uint32_t gpos = 0, gunc = 0;
-        uint64_t codes = 0;
+        // per-point bits are accumulated as v = 2v + bit (one add-with-carry from the compare
+        // mask), i.e. point j lands in bit G-1-j; a bit reverse per group restores the order
+        uint32_t rpos = 0, runc = 0, clo = 0, chi = 0;
 #pragma unroll
         for (int j = 0; j < G; j++) {
             const float x = buf[j].x, y = buf[j].y, z = buf[j].z;
@@ -914,23 +924,32 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             bool ok = classify_angle_fast<GROUND, FILTER>(P, x, y, s, ang_rm);
             if (FILTER) {
                 ok = dist_level_fast(P, x, y, z, drm) & ok;
-                gpos |= (uint32_t)(ok & !ang_rm & !drm) << j;
+                rpos = rpos + rpos + (uint32_t)(ok & !ang_rm & !drm);
             }
-            gunc |= (uint32_t)!ok << j;
+            runc = runc + runc + (uint32_t)!ok;
             if (GROUND) {
-                codes |= (uint64_t)zcode(z, P) << (8 * j);
-                // run-length sector minimum: flush the lane's run when the sector changes
-                const bool upd = ok & (z == z);
-                const bool flush = upd & (s != cur_s);
-                if (flush & (cur_s >= 0)) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
-                touched |= flush ? 1u << s : 0u;
-                cur_m = flush ? z : (upd ? fminf(cur_m, z) : cur_m);
-                cur_s = flush ? s : cur_s;
+                if (j < 4) clo |= zcode(z, P) << (8 * j);
+                else chi |= zcode(z, P) << (8 * (j - 4));
+                // run-length sector minimum: an uncertain point or a NaN z continues the run
+                // with +inf; a sector change flushes the run (rare: a lane's consecutive points
+                // are 512 apart, a few degrees of azimuth on a spinning sensor)
+                const bool good = ok & (z == z);
+                const int ss = good ? s : cur_s;
+                const float zz = good ? z : INFINITY;
+                if (ss != cur_s) {
+                    if (cur_m != INFINITY) {
+                        atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+                        touched |= 1u << cur_s;
+                    }
+                    cur_m = INFINITY;
+                }
+                cur_m = zz < cur_m ? zz : cur_m;   // never NaN
+                cur_s = ss;
             }
         }
-        if (FILTER) posm.set_byte(g, gpos);
-        uncm.set_byte(g, gunc);
-        if (GROUND) ((uint64_t*)zq)[g * CG_BLOCK + tid] = codes;   // one ds_write_b64 per group
+        if (FILTER) posm.set_byte(g, __builtin_bitreverse32(rpos) >> (32 - G));
+        uncm.set_byte(g, __builtin_bitreverse32(runc) >> (32 - G));
+        if (GROUND) ((uint2*)zq)[g * CG_BLOCK + tid] = make_uint2(clo, chi);   // one ds_write_b64
     };
     if (N) {
         float3 A[G], B[G];
@@ -953,7 +972,10 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             uncm.w[wi] &= vm;
         }
     }
-    if (GROUND && cur_s >= 0) atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+    if (GROUND && cur_m != INFINITY) {
+        atomicMin(&fs->sec_key[cur_s], cg_fkey(cur_m));
+        touched |= 1u << cur_s;
+    }
     // uncertain points: exact angle (glibc restatement) and exact double distance
 #pragma unroll
     for (int wi = 0; wi < NW; wi++) {
