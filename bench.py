@@ -63,10 +63,12 @@ def main():
     # each rank owns frames [rank*F, (rank+1)*F): distinct synthetic scenes per rank
     raw = cp.synth_frames(F, first_frame=rank * F, rings=args.rings, cols=args.cols,
                           threads=min(16, os.cpu_count() or 1))
-    d_in = torch.from_numpy(raw).to(dev)
+    # one resident copy of the batch per stream: consecutive in-flight steps read distinct
+    # buffers (together larger than the 256 MB Infinity Cache), as a live sensor stream would
+    S = max(1, args.streams)
+    d_ins = [torch.from_numpy(raw).to(dev) for _ in range(S)]
     # one engine (own output buffers) per stream; dedicated streams: the default stream's
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
-    S = max(1, args.streams)
     engines = [cp.BatchEngine(params, device=local) for _ in range(S)]
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
     assert all(st.cuda_stream != 0 for st in streams)
@@ -77,7 +79,7 @@ def main():
         i = counter[0] if idx is None else idx
         counter[0] += 1
         e, st = engines[i % S], streams[i % S]
-        e.run(d_in.data_ptr(), F, N, 16, stream=st.cuda_stream)
+        e.run(d_ins[i % S].data_ptr(), F, N, 16, stream=st.cuda_stream)
         return st
 
     torch.cuda.synchronize(dev)
@@ -199,7 +201,7 @@ def fetch_headers(res, F):
 
 STAMP_NAMES = ["start", "pass1 stream", "thresholds", "pass2 keep bits", "compaction scan",
                "pass3 gather", "voxel minmax", "voxel keys", "voxel sort", "voxel runs",
-               "voxel centroids", "cluster init", "cluster unions", "cluster roots", "cluster sizes",
+               "voxel centroids", "cluster adjacency", "cluster forest", "cluster roots", "cluster sizes",
                "cluster keep scan", "cluster order", "csr offsets", "labels", "csr indices",
                "centroids+header"]
 
@@ -235,6 +237,12 @@ def phase_stamps(eng, step, F, around=None, tag="alone"):
         out["pass2a lds loop (wave0)"] = round(float(np.median((t[sub, 21] - t[sub, 2]) / 100.0)), 2)
         out["pass2b re-reads (wave0)"] = round(float(np.median((t[sub, 22] - t[sub, 21]) / 100.0)), 2)
         out["pass2c ballots (wave0)"] = round(float(np.median((t[sub, 3] - t[sub, 22]) / 100.0)), 2)
+    sub = (t[:, 23] > 0) & (t[:, 24] > 0)
+    if sub.any():   # brute-force clustering: adjacency, parents, flatten, cross-tree unions
+        out["clusterA adjacency"] = round(float(np.median((t[sub, 11] - t[sub, 10]) / 100.0)), 2)
+        out["clusterB parents"] = round(float(np.median((t[sub, 23] - t[sub, 11]) / 100.0)), 2)
+        out["clusterC flatten"] = round(float(np.median((t[sub, 24] - t[sub, 23]) / 100.0)), 2)
+        out["clusterD cross unions"] = round(float(np.median((t[sub, 12] - t[sub, 24]) / 100.0)), 2)
     life = (t[:, 20] - t[:, 0]) / 100.0
     out["wg_lifetime_us_p10_p50_p90"] = [round(float(np.percentile(life, q)), 1) for q in (10, 50, 90)]
     print("STAMPS " + json.dumps(out), flush=True)

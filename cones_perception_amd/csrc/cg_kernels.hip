@@ -215,19 +215,26 @@ __device__ __forceinline__ void bitonic_sort(uint64_t* S, uint32_t n2) {
 // sweep (every lane reads the same in[i]). Ends with a barrier.
 #define CG_RANK_SORT_MAX 512
 __device__ __forceinline__ void rank_sort(const uint64_t* in, uint64_t* out, uint32_t n) {
-    // g lanes (a power of two, consecutive in a wave) share one key's count
+    // g lanes (a power of two, consecutive in a wave) share one key's count, each over a
+    // contiguous slice read as 16-byte pairs, eight keys in flight
     uint32_t g = 1;
     while (g < 64 && (uint64_t)n * g * 2 <= CG_BLOCK) g <<= 1;
     const uint32_t sub = threadIdx.x & (g - 1);
+    const uint32_t per = ((n + g - 1) / g + 1) & ~1u;   // even: slices start 16-byte aligned
+    const ulonglong2* in2 = (const ulonglong2*)in;
     for (uint32_t base = 0; base < n * g; base += CG_BLOCK) {
         const uint32_t t = base + threadIdx.x, j = t / g;
         const uint64_t kj = j < n ? in[j] : 0ull;
         uint32_t r = 0;
         if (j < n) {
-            uint32_t i = sub;
-            for (; i + 3 * g < n; i += 4 * g)
-                r += (in[i] < kj) + (in[i + g] < kj) + (in[i + 2 * g] < kj) + (in[i + 3 * g] < kj);
-            for (; i < n; i += g) r += in[i] < kj;
+            const uint32_t lo = min(n, sub * per), hi = min(n, lo + per);
+            uint32_t i = lo;
+            for (; i + 8 <= hi; i += 8) {
+                const ulonglong2 a = in2[i / 2], b = in2[i / 2 + 1], c = in2[i / 2 + 2], d = in2[i / 2 + 3];
+                r += (a.x < kj) + (a.y < kj) + (b.x < kj) + (b.y < kj) + (c.x < kj) + (c.y < kj) +
+                     (d.x < kj) + (d.y < kj);
+            }
+            for (; i < hi; i++) r += in[i] < kj;
         }
         for (uint32_t o = 1; o < g; o <<= 1) r += (uint32_t)__shfl_xor((int)r, (int)o, 64);
         if (j < n && sub == 0) out[r] = kj;
@@ -529,49 +536,83 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
     uint32_t C = 0;
     if (V > 0) {
         if (V <= CG_BRUTE_V) {
-            // all pairs, split over nch = floor(1024 / V) lanes per voxel. (1) every voxel
-            // points at its smallest neighbour (or itself): a forest whose trees lie inside
-            // components; (2) pointer jumping flattens it; (3) the few edges between trees
-            // are united with the lock-free union. Roots stay each component's lowest index.
-            for (uint32_t v = tid; v < V; v += CG_BLOCK) { W.PAR[v] = v; W.CNT[v] = 0; }
-            if (tid == 0) { fs->scal[S_TMP] = 0; fs->scal[S_TMP + 1] = 0; }
+            // (1) adjacency bitmasks: row v, 16-column chunk c is one task; lanes of a wave share
+            // c, so the column voxels are LDS broadcasts. A voxel is its own neighbour (distance
+            // 0 < r2) unless it is not finite (passthrough clouds), then it is isolated.
+            // (2) every voxel points at its lowest neighbour (<= itself): a forest whose trees
+            // lie inside components; (3) pointer jumping flattens it; (4) only edges leaving a
+            // tree (row & ~members(tree)) are united. Roots stay each component's lowest index.
+            uint16_t* const adj = (uint16_t*)W.KEY;                // [V][16] chunks, 32 B rows
+            unsigned long long* const tm = (unsigned long long*)W.P;   // [V][4] tree members
+            const uint32_t nc = (V + 15) >> 4, nw = (V + 63) >> 6;
+            for (uint32_t t = tid; t < V * nc; t += CG_BLOCK) {
+                const uint32_t c = t / V, v = t - c * V;
+                const float4 q = W.VOX[v];
+                uint32_t bits = 0;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    float4 pc[8];
+#pragma unroll
+                    for (int b = 0; b < 8; b++) pc[b] = W.VOX[min(16 * c + 8 * h + b, V - 1)];
+#pragma unroll
+                    for (int b = 0; b < 8; b++) {
+                        const float ddx = q.x - pc[b].x, ddy = q.y - pc[b].y, ddz = q.z - pc[b].z;
+                        float acc = ddx * ddx;
+                        acc = acc + ddy * ddy;
+                        acc = acc + ddz * ddz;
+                        bits |= (uint32_t)(acc < P.r2 && 16 * c + 8 * h + b < V) << (8 * h + b);
+                    }
+                }
+                adj[v * 16 + c] = (uint16_t)bits;
+            }
+            for (uint32_t t = tid; t < V * 4; t += CG_BLOCK) tm[t] = 0ull;
+            if (tid == 0) { fs->scal[S_TMP] = 0; fs->scal[S_TMP + 1] = 0; fs->scal[S_TMP + 2] = 0; }
             __syncthreads();
             STAMP(11);
-            const uint32_t nch = CG_BLOCK / V;
-            const bool act = tid < V * nch;
-            const uint32_t v = act ? tid % V : 0, c = act ? tid / V : 0;
-            const float4 q = W.VOX[v];
-            auto adj = [&](uint32_t u) -> bool {
-                const float4 p = W.VOX[u];
-                const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
-                float acc = ddx * ddx;
-                acc = acc + ddy * ddy;
-                acc = acc + ddz * ddz;
-                return acc < P.r2;
+            auto row = [&](uint32_t v, uint32_t i) -> unsigned long long {
+                const unsigned long long x = ((const unsigned long long*)(adj + v * 16))[i];
+                const uint32_t hi = V - 64 * i;   // columns >= V were never written
+                return hi >= 64 ? x : x & ((1ull << hi) - 1ull);
             };
-            if (act) {
-                for (uint32_t u = c; u < v; u += nch)
-                    if (adj(u)) { atomicMin(&W.PAR[v], u); break; }
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+                uint32_t p = v;
+                for (uint32_t i = 0; i < nw; i++) {
+                    const unsigned long long x = row(v, i);
+                    if (x) { p = min(v, 64 * i + (uint32_t)__builtin_ctzll(x)); break; }
+                }
+                W.PAR[v] = p;
+                W.CNT[v] = 0;
             }
             __syncthreads();
-            // flatten: per-iteration "changed" flags alternate between two words; the word
-            // for the next iteration is cleared before the barrier that ends this one
-            for (uint32_t iter = 0;; iter++) {
+            STAMP(23);
+            // flatten: one barrier per round; round r sets flag r%3 and clears flag (r+1)%3,
+            // which every thread last read before the barrier ending round r-1
+            for (uint32_t r = 0;; r++) {
                 bool changed = false;
                 for (uint32_t x = tid; x < V; x += CG_BLOCK) {
                     const uint32_t p = W.PAR[x], pp = W.PAR[p];
                     if (pp != p) { W.PAR[x] = pp; changed = true; }
                 }
-                if (__ballot(changed) && l == 0) atomicOr(&fs->scal[S_TMP + (iter & 1)], 1u);
+                if (__ballot(changed) && l == 0) atomicOr(&fs->scal[S_TMP + r % 3], 1u);
+                if (tid == 0) fs->scal[S_TMP + (r + 1) % 3] = 0;
                 __syncthreads();
-                const bool again = fs->scal[S_TMP + (iter & 1)] != 0;
-                if (tid == 0) fs->scal[S_TMP + ((iter + 1) & 1)] = 0;
-                __syncthreads();
-                if (!again) break;
+                if (!fs->scal[S_TMP + r % 3]) break;
             }
-            if (act) {
-                for (uint32_t u = v + 1 + c; u < V; u += nch)
-                    if (adj(u) && ld_rlx(W.PAR + v) != ld_rlx(W.PAR + u)) uf_union(W.PAR, v, u);
+            for (uint32_t v = tid; v < V; v += CG_BLOCK)
+                atomicOr(&tm[W.PAR[v] * 4 + (v >> 6)], 1ull << (v & 63));
+            __syncthreads();
+            STAMP(24);
+            for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+                const uint32_t rv = W.PAR[v];
+                for (uint32_t i = v >> 6; i < nw; i++) {
+                    unsigned long long x = row(v, i) & ~tm[rv * 4 + i];
+                    if (i == (v >> 6)) x &= ~((2ull << (v & 63)) - 1ull);   // u > v only
+                    while (x) {
+                        const uint32_t u = 64 * i + (uint32_t)__builtin_ctzll(x);
+                        x &= x - 1;
+                        uf_union(W.PAR, v, u);
+                    }
+                }
             }
             __syncthreads();
         } else {
@@ -792,8 +833,18 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         for (uint32_t k = tid; k < C; k += CG_BLOCK) {
             const uint32_t s = W.OFF[k], e = W.OFF[k + 1];
             float x = 0.0f, y = 0.0f;
-#pragma unroll 4
-            for (uint32_t i = s; i < e; i++) {
+            uint32_t i = s;
+            for (; i + 8 <= e; i += 8) {   // members fetched eight at a time, summed in order
+                uint32_t id[8];
+                float2 pv[8];
+#pragma unroll
+                for (int b = 0; b < 8; b++) id[b] = W.IDX[i + b];
+#pragma unroll
+                for (int b = 0; b < 8; b++) { const float4 p = W.VOX[id[b]]; pv[b] = make_float2(p.x, p.y); }
+#pragma unroll
+                for (int b = 0; b < 8; b++) { x += pv[b].x; y += pv[b].y; }
+            }
+            for (; i < e; i++) {
                 const float4 p = W.VOX[W.IDX[i]];
                 x += p.x;
                 y += p.y;
@@ -830,12 +881,14 @@ struct LaneBits {
 #pragma unroll
         for (int i = 0; i < NW; i++) w[i] = 0;
     }
-    __device__ __forceinline__ void set_byte(int byte_idx, uint32_t v8) {   // 8 bits at 8*byte_idx
-        const int wi = byte_idx >> 3, sh = (byte_idx & 7) * 8;
+    template <int WIDTH>
+    __device__ __forceinline__ void set_bits(int grp, uint32_t v) {   // WIDTH bits at WIDTH*grp
+        const int wi = grp / (64 / WIDTH), sh = (grp % (64 / WIDTH)) * WIDTH;
 #pragma unroll
         for (int i = 0; i < NW; i++)
-            if (i == wi) w[i] |= (uint64_t)v8 << sh;
+            if (i == wi) w[i] |= (uint64_t)v << sh;
     }
+    __device__ __forceinline__ void set_byte(int byte_idx, uint32_t v8) { set_bits<8>(byte_idx, v8); }
     __device__ __forceinline__ bool get(int k) const {
         uint64_t x = w[0];
 #pragma unroll
@@ -947,8 +1000,8 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
                 cur_s = ss;
             }
         }
-        if (FILTER) posm.set_byte(g, __builtin_bitreverse32(rpos) >> (32 - G));
-        uncm.set_byte(g, __builtin_bitreverse32(runc) >> (32 - G));
+        if (FILTER) posm.template set_bits<G>(g, __builtin_bitreverse32(rpos) >> (32 - G));
+        uncm.template set_bits<G>(g, __builtin_bitreverse32(runc) >> (32 - G));
         if (GROUND) ((uint2*)zq)[g * CG_BLOCK + tid] = make_uint2(clo, chi);   // one ds_write_b64
     };
     if (N) {
