@@ -243,6 +243,11 @@ def phase_stamps(eng, step, F, around=None, tag="alone"):
         out["clusterB parents"] = round(float(np.median((t[sub, 23] - t[sub, 11]) / 100.0)), 2)
         out["clusterC flatten"] = round(float(np.median((t[sub, 24] - t[sub, 23]) / 100.0)), 2)
         out["clusterD cross unions"] = round(float(np.median((t[sub, 12] - t[sub, 24]) / 100.0)), 2)
+    sub = (t[:, 25] > 0) & (t[:, 26] > 0)
+    if sub.any():   # gather (wave 0): survivor loads, pads + bounds, barrier wait
+        out["gatherA loads (wave0)"] = round(float(np.median((t[sub, 25] - t[sub, 4]) / 100.0)), 2)
+        out["gatherB bounds (wave0)"] = round(float(np.median((t[sub, 26] - t[sub, 25]) / 100.0)), 2)
+        out["gatherC barrier (wave0)"] = round(float(np.median((t[sub, 5] - t[sub, 26]) / 100.0)), 2)
     life = (t[:, 20] - t[:, 0]) / 100.0
     out["wg_lifetime_us_p10_p50_p90"] = [round(float(np.percentile(life, q)), 1) for q in (10, 50, 90)]
     print("STAMPS " + json.dumps(out), flush=True)

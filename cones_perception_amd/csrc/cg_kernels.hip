@@ -120,6 +120,16 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
 }
 // Cross-lane steps use DPP (row_shr within 16-lane rows, row_bcast15/31 across rows), which
 // stay in the VALU; __shfl would go through ds_bpermute and pay an LDS round trip per step.
+// v = 2v + (this lane's bit of the wave mask m): one v_addc_co_u32 with the compare mask as
+// carry-in. Used to pack per-point decisions into per-lane bit strings (first point in the
+// highest bit); the compiler otherwise spends a select, a shift and an or per bit.
+__device__ __forceinline__ uint32_t shl1_add(uint32_t v, uint64_t m) {
+    uint32_t r;
+    asm volatile("v_addc_co_u32 %0, vcc, %1, %1, %2" : "=v"(r) : "v"(v), "s"(m) : "vcc");
+    return r;
+}
+__device__ __forceinline__ uint32_t shl1_add_if(uint32_t v, bool b) { return shl1_add(v, __builtin_amdgcn_ballot_w64(b)); }
+
 template <int CTRL, int ROWS, int BANKS>
 __device__ __forceinline__ uint32_t dpp(uint32_t identity, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROWS, BANKS, false);
@@ -889,6 +899,11 @@ struct LaneBits {
             if (i == wi) w[i] |= (uint64_t)v << sh;
     }
     __device__ __forceinline__ void set_byte(int byte_idx, uint32_t v8) { set_bits<8>(byte_idx, v8); }
+    __device__ __forceinline__ void clear_bit(int k) {
+#pragma unroll
+        for (int i = 0; i < NW; i++)
+            if ((k >> 6) == i) w[i] &= ~(1ull << (k & 63));
+    }
     __device__ __forceinline__ bool get(int k) const {
         uint64_t x = w[0];
 #pragma unroll
@@ -977,9 +992,9 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             bool ok = classify_angle_fast<GROUND, FILTER>(P, x, y, s, ang_rm);
             if (FILTER) {
                 ok = dist_level_fast(P, x, y, z, drm) & ok;
-                rpos = rpos + rpos + (uint32_t)(ok & !ang_rm & !drm);
+                rpos = shl1_add_if(rpos, ok & !ang_rm & !drm);
             }
-            runc = runc + runc + (uint32_t)!ok;
+            runc = shl1_add_if(runc, !ok);
             if (GROUND) {
                 if (j < 4) clo |= zcode(z, P) << (8 * j);
                 else chi |= zcode(z, P) << (8 * (j - 4));
@@ -1055,6 +1070,22 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
         touched = wave_or(touched);
         if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
     }
+    // the lane's first two filter survivors are the likely first gather loads: issue them now,
+    // they land while the thresholds and pass 2 run (a survivor that turns out to be ground
+    // costs one wasted load)
+    int pk[2] = {-1, -1};
+    float4 pv[2];
+    if (FILTER) {
+#pragma unroll
+        for (int wi = 0; wi < NW; wi++) {
+            uint64_t m = posm.w[wi];
+            if (pk[0] < 0 && m) { pk[0] = 64 * wi + __builtin_ctzll(m); m &= m - 1; }
+            if (pk[1] < 0 && m) pk[1] = 64 * wi + __builtin_ctzll(m);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            pv[q] = load_xyzi<LAYOUT>(fb, min((uint32_t)(pk[q] < 0 ? 0 : pk[q]) * CG_BLOCK + tid, nlast), L);
+    }
     __syncthreads();
     STAMP(1);
     if (GROUND && tid < 64) {
@@ -1082,20 +1113,34 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     ambm.clear();
     if (GROUND) {
         const uint32_t qlo = fs->scal[S_TKMIN], qhi = fs->scal[S_TKMAX];
-#pragma unroll 2
+        // all of the lane's code words first (the pass-1 load buffers are dead), then two
+        // compares per code: c > qhi keeps, qlo <= c <= qhi is ambiguous, c < qlo is ground.
+        // Bits accumulate as v = 2v + bit and are bit-reversed per group, as in pass 1.
+        uint2 cw[NG];
+#pragma unroll
+        for (int g = 0; g < NG; g++) cw[g] = ((const uint2*)zq)[g * CG_BLOCK + tid];
+#pragma unroll
         for (int g = 0; g < NG; g++) {
-            const uint64_t codes = ((const uint64_t*)zq)[g * CG_BLOCK + tid];
-            uint32_t kb = 0, ab = 0;
+            uint32_t kr = 0, ar = 0;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const uint32_t c = (uint32_t)(codes >> (8 * j)) & 0xffu;
-                const bool valid = (uint32_t)(g * 8 + j) * CG_BLOCK + tid < N;
-                const bool below = c < qlo, above = c > qhi;
-                kb |= (uint32_t)(valid && above) << j;
-                ab |= (uint32_t)(valid && !below && !above) << j;
+                const uint32_t c = ((j < 4 ? cw[g].x : cw[g].y) >> (8 * (j & 3))) & 0xffu;
+                const bool kp = c > qhi, nb = c >= qlo;
+                kr = shl1_add_if(kr, kp);
+                ar = shl1_add_if(ar, nb & !kp);
             }
-            keepgm.set_byte(g, kb);
-            ambm.set_byte(g, ab);
+            keepgm.set_byte(g, __builtin_bitreverse32(kr) >> 24);
+            ambm.set_byte(g, __builtin_bitreverse32(ar) >> 24);
+        }
+        {   // points k*512 + tid >= N do not exist
+            const uint32_t nv = tid < N ? (N - tid + CG_BLOCK - 1) / CG_BLOCK : 0u;
+#pragma unroll
+            for (int wi = 0; wi < NW; wi++) {
+                const int c = (int)nv - 64 * wi;
+                const uint64_t vm = c >= 64 ? ~0ull : (c <= 0 ? 0ull : (1ull << c) - 1ull);
+                keepgm.w[wi] &= vm;
+                ambm.w[wi] &= vm;
+            }
         }
         STAMP(21);
         // ambiguous: exact z and sector from HBM, four re-reads in flight per lane
@@ -1215,6 +1260,16 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
         }
     };
 #pragma unroll
+    for (int q = 0; q < 2; q++) {
+        if (pk[q] >= 0 && keepm.get(pk[q])) {
+            keepm.clear_bit(pk[q]);
+            W.P[pos] = pv[q];
+            W.IDX[pos] = (uint32_t)pk[q] * CG_BLOCK + tid;
+            bound(pv[q]);
+            pos++;
+        }
+    }
+#pragma unroll
     for (int wi = 0; wi < NW; wi++) {
         uint64_t m = keepm.w[wi];
         while (m) {
@@ -1238,6 +1293,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             }
         }
     }
+    STAMP(25);
     for (uint32_t j = tid; j < npad; j += CG_BLOCK) {
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         W.P[Ms + j] = z4;
@@ -1258,6 +1314,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             atomicAdd(&fs->scal[S_MF], nf);
         }
     }
+    STAMP(26);
     __syncthreads();
     STAMP(5);
     if (use_lds) {
