@@ -1317,6 +1317,11 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     STAMP(26);
     __syncthreads();
     STAMP(5);
+#ifdef CG_EXPERIMENT_FRONT_ONLY
+    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[2] = M; h[3] = 0; h[4] = 0; h[5] = 0; }
+    STAMP(20);
+    return;
+#endif
     if (use_lds) {
         Work WL;
         WL.P = bl->P; WL.KEY = bl->KEY; WL.VOX = bl->VOX; WL.A = bl->A; WL.PAR = bl->PAR; WL.CNT = bl->CNT;
