@@ -212,6 +212,12 @@ class _Handle:
     def handle(self):
         return self._h
 
+    def debug_route(self, route: int):
+        """Diagnostics: 1 = every frame through the large-frame path, 2 = also its global
+        backend, 0 = automatic (frames of > 65,536 points take the large path)."""
+        check(lib().cg_debug_route(self._h, route))
+        return self
+
 
 class GroundRemover(_Handle):
     """GroundRemover::cloud_handler (src/ground_removal.cpp:50-89) on the GPU."""

@@ -18,7 +18,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
-HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h")] + \
+HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h", "cg_device.h")] + \
           [os.path.join(ROOT, "include", "cones_gpu.h")]
 
 
@@ -48,7 +48,7 @@ def build(verbose=False, force=False):
     if force or _stale(o, [src] + HEADERS):
         _run(["gcc", "-O2", "-fPIC", "-ffp-contract=off", "-std=c11", "-Wall", "-c", src, "-o", o], verbose)
     objs.append(o)
-    for name in ("cg_kernels.hip", "cg_api.cpp"):
+    for name in ("cg_kernels.hip", "cg_large.hip", "cg_api.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(OBJ, name.rsplit(".", 1)[0] + ".o")
         if force or _stale(o, [src] + HEADERS):

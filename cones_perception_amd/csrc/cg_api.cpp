@@ -142,6 +142,11 @@ struct cg_handle {
     std::vector<int32_t> h_lab, h_offs, h_idx;
     uint8_t* h_ground = nullptr;  // pinned
     size_t h_ground_bytes = 0;
+    // frames of more than CG_MAX_POINTS points (cg_large.hip): scratch for one frame
+    uint8_t* d_large = nullptr;
+    uint32_t large_points = 0;
+    LgScratch lg{};
+    int route = 0;                // cg_debug_route
     // diagnostics
     bool stamps_on = false;
     uint64_t* d_stamps = nullptr;
@@ -159,8 +164,8 @@ int own_stream(cg_handle* h) {
 }
 
 void free_batch(cg_handle* h) {
-    hipFree(h->d_hdr); hipFree(h->d_vox); hipFree(h->d_lab); hipFree(h->d_offs);
-    hipFree(h->d_idx); hipFree(h->d_cen); hipFree(h->d_ground); hipFree(h->d_scratch);
+    (void)hipFree(h->d_hdr); (void)hipFree(h->d_vox); (void)hipFree(h->d_lab); (void)hipFree(h->d_offs);
+    (void)hipFree(h->d_idx); (void)hipFree(h->d_cen); (void)hipFree(h->d_ground); (void)hipFree(h->d_scratch);
     h->d_hdr = nullptr; h->d_vox = nullptr; h->d_lab = nullptr; h->d_offs = nullptr;
     h->d_idx = nullptr; h->d_cen = nullptr; h->d_ground = nullptr; h->d_scratch = nullptr;
     h->cap_frames = h->cap_points = 0;
@@ -180,7 +185,8 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     HIPCHK(hipMalloc(&h->d_offs, F * (C + 1) * 4));
     HIPCHK(hipMalloc(&h->d_idx, F * C * 4));
     HIPCHK(hipMalloc(&h->d_cen, F * C * 8));
-    h->scratch_stride = (cg_scratch_bytes(np) + 255) & ~255ull;
+    // the frame kernel's HBM fallback (M > CG_MMAX) serves frames of <= CG_MAX_POINTS points
+    h->scratch_stride = (cg_scratch_bytes(std::min<uint32_t>(np, CG_MAX_POINTS)) + 255) & ~255ull;
     HIPCHK(hipMalloc(&h->d_scratch, F * h->scratch_stride));
     if (had_ground) HIPCHK(hipMalloc(&h->d_ground, F * C * 32));
     h->cap_frames = nf;
@@ -191,9 +197,9 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
 int check_view(const cg_cloud_view* v) {
     if (!v) return fail(CG_E_INVALID, "null cloud view");
     const uint64_t n = (uint64_t)v->width * v->height;
-    if (n > CG_MAX_POINTS)
-        return fail(CG_E_CAPACITY, "cloud has %llu points; the frame engine supports <= %d",
-                    (unsigned long long)n, CG_MAX_POINTS);
+    if (n > CG_MAX_FRAME_POINTS)
+        return fail(CG_E_CAPACITY, "cloud has %llu points; the engine supports <= %u",
+                    (unsigned long long)n, (unsigned)CG_MAX_FRAME_POINTS);
     if (n == 0) return CG_OK;
     if (!v->data) return fail(CG_E_INVALID, "null cloud data");
     if (v->point_step == 0) return fail(CG_E_INVALID, "point_step is 0");
@@ -219,13 +225,13 @@ int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L) {
     const uint32_t step = verbatim ? v->point_step : 16;
     const size_t bytes = std::max<size_t>((size_t)n * step, 16);
     if (bytes > h->h_stage_bytes) {
-        if (h->h_stage) hipHostFree(h->h_stage);
+        if (h->h_stage) (void)hipHostFree(h->h_stage);
         h->h_stage = nullptr;
         HIPCHK(hipHostMalloc(&h->h_stage, bytes, hipHostMallocDefault));
         h->h_stage_bytes = bytes;
     }
     if (bytes > h->d_in_bytes) {
-        if (h->d_in) hipFree(h->d_in);
+        if (h->d_in) (void)hipFree(h->d_in);
         h->d_in = nullptr;
         HIPCHK(hipMalloc(&h->d_in, bytes));
         h->d_in_bytes = bytes;
@@ -266,16 +272,43 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
     L.stamps = nullptr;
     if (h->stamps_on) {
         if (h->stamps_frames < h->cap_frames) {
-            hipFree(h->d_stamps);
+            (void)hipFree(h->d_stamps);
             h->d_stamps = nullptr;
             if (hipMalloc(&h->d_stamps, (size_t)h->cap_frames * 32 * 8) == hipSuccess)
                 h->stamps_frames = h->cap_frames;
             else
                 h->stamps_frames = 0;
         }
-        if (h->d_stamps) hipMemset(h->d_stamps, 0, (size_t)h->stamps_frames * 32 * 8);
+        if (h->d_stamps) (void)hipMemset(h->d_stamps, 0, (size_t)h->stamps_frames * 32 * 8);
         L.stamps = h->d_stamps;
     }
+}
+
+int ensure_large(cg_handle* h, uint32_t n) {
+    if (n <= h->large_points && h->d_large) return CG_OK;
+    if (h->d_large) (void)hipFree(h->d_large);
+    h->d_large = nullptr;
+    h->large_points = 0;
+    HIPCHK(hipMalloc(&h->d_large, cg_large_bytes(n)));
+    cg_large_layout(h->d_large, n, h->lg);
+    h->large_points = n;
+    return CG_OK;
+}
+
+// Frames of <= CG_MAX_POINTS points run as one batch launch of the frame kernel; larger
+// frames (or every frame, under cg_debug_route) go through the multi-workgroup large path.
+int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
+    const bool large = L.n_points > CG_MAX_POINTS || (h->route != 0 && L.n_points > 0);
+    if (!large) {
+        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s));
+        return CG_OK;
+    }
+    int rc = ensure_large(h, L.n_points);
+    if (rc) return rc;
+    h->lg.force_global = h->route == 2 ? 1u : 0u;
+    L.stamps = nullptr;
+    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, h->lg, s));
+    return CG_OK;
 }
 
 int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
@@ -333,12 +366,13 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     rc = stage_frame(h, in, L);
     if (rc) return rc;
     fill_launch_outputs(h, L);
-    HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, h->stream));
+    rc = launch_frames(h, L, kmode, h->stream);
+    if (rc) return rc;
     h->last_frames = 1; h->last_points = n; h->last_mode = kmode; h->last_stream = h->stream;
     if (kmode == CG_KMODE_GROUND) {
         const size_t bytes = std::max<size_t>((size_t)n * 32, 32);
         if (bytes > h->h_ground_bytes) {
-            if (h->h_ground) hipHostFree(h->h_ground);
+            if (h->h_ground) (void)hipHostFree(h->h_ground);
             h->h_ground = nullptr;
             HIPCHK(hipHostMalloc(&h->h_ground, bytes, hipHostMallocDefault));
             h->h_ground_bytes = bytes;
@@ -407,14 +441,15 @@ int cg_create(const cg_params* params, int device, cg_handle** out) {
 
 int cg_destroy(cg_handle* h) {
     if (!h) return CG_OK;
-    hipSetDevice(h->device);
-    if (h->stream) hipStreamSynchronize(h->stream);
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_batch(h);
-    if (h->d_stamps) hipFree(h->d_stamps);
-    if (h->d_in) hipFree(h->d_in);
-    if (h->h_stage) hipHostFree(h->h_stage);
-    if (h->h_ground) hipHostFree(h->h_ground);
-    if (h->stream) hipStreamDestroy(h->stream);
+    if (h->d_stamps) (void)hipFree(h->d_stamps);
+    if (h->d_in) (void)hipFree(h->d_in);
+    if (h->d_large) (void)hipFree(h->d_large);
+    if (h->h_stage) (void)hipHostFree(h->h_stage);
+    if (h->h_ground) (void)hipHostFree(h->h_ground);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return CG_OK;
 }
@@ -445,9 +480,9 @@ int cg_pipeline(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out) {
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     if (!h || !b) return fail(CG_E_INVALID, "null argument");
     if (mode != CG_MODE_PIPELINE && mode != CG_MODE_DETECT) return fail(CG_E_INVALID, "bad mode %d", mode);
-    if (b->n_points > CG_MAX_POINTS)
-        return fail(CG_E_CAPACITY, "frames of %u points; the frame engine supports <= %d", b->n_points,
-                    CG_MAX_POINTS);
+    if (b->n_points > CG_MAX_FRAME_POINTS)
+        return fail(CG_E_CAPACITY, "frames of %u points; the engine supports <= %u", b->n_points,
+                    (unsigned)CG_MAX_FRAME_POINTS);
     if (b->n_frames && b->n_points && !b->d_data) return fail(CG_E_INVALID, "null batch data");
     if (b->point_step == 0 || b->point_step % 4 || b->frame_stride % 4 ||
         b->frame_stride < (uint64_t)b->n_points * b->point_step)
@@ -473,7 +508,8 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
         if (rc) return rc;
     }
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
-    HIPCHK((hipError_t)cg_launch_batch(L, h->dp, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s));
+    rc = launch_frames(h, L, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s);
+    if (rc) return rc;
     h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
     return CG_OK;
 }
@@ -498,12 +534,28 @@ int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out) {
     return fetch_frame(h, h->last_stream, frame, out);
 }
 
+int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words) {
+    if (!h || !out) return fail(CG_E_INVALID, "null argument");
+    if (!h->d_large) return fail(CG_E_INVALID, "no large frame has run on this handle");
+    const uint32_t n = std::min<uint32_t>(n_words, LG_META_WORDS);
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, h->lg.meta, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return CG_OK;
+}
+
+int cg_debug_route(cg_handle* h, int route) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    if (route < 0 || route > 2) return fail(CG_E_INVALID, "bad route %d", route);
+    h->route = route;
+    return CG_OK;
+}
+
 int cg_debug_stamps(cg_handle* h, int enable) {
     if (!h) return fail(CG_E_INVALID, "null handle");
     HIPCHK(hipSetDevice(h->device));
     h->stamps_on = enable != 0;
     if (!h->stamps_on && h->d_stamps) {
-        hipFree(h->d_stamps);
+        (void)hipFree(h->d_stamps);
         h->d_stamps = nullptr;
         h->stamps_frames = 0;
     }
@@ -534,7 +586,7 @@ int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out,
     HIPCHK((hipError_t)cg_launch_selftest_atan2f(dy, dx, dout, n, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
-    hipFree(dy); hipFree(dx); hipFree(dout);
+    (void)hipFree(dy); (void)hipFree(dx); (void)hipFree(dout);
     return CG_OK;
 }
 
@@ -551,7 +603,7 @@ int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n) {
     HIPCHK((hipError_t)cg_launch_selftest_sqrt(din, dout, n, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
-    hipFree(din); hipFree(dout);
+    (void)hipFree(din); (void)hipFree(dout);
     return CG_OK;
 }
 

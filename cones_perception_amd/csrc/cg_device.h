@@ -24,15 +24,13 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
 }
 // Cross-lane steps use DPP (row_shr within 16-lane rows, row_bcast15/31 across rows), which
 // stay in the VALU; __shfl would go through ds_bpermute and pay an LDS round trip per step.
-// v = 2v + (this lane's bit of the wave mask m): one v_addc_co_u32 with the compare mask as
-// carry-in. Used to pack per-point decisions into per-lane bit strings (first point in the
-// highest bit); the compiler otherwise spends a select, a shift and an or per bit.
-__device__ __forceinline__ uint32_t shl1_add(uint32_t v, uint64_t m) {
-    uint32_t r;
-    asm volatile("v_addc_co_u32 %0, vcc, %1, %1, %2" : "=v"(r) : "v"(v), "s"(m) : "vcc");
-    return r;
-}
-__device__ __forceinline__ uint32_t shl1_add_if(uint32_t v, bool b) { return shl1_add(v, __builtin_amdgcn_ballot_w64(b)); }
+// v = 2v + bit: per-point decisions packed into per-lane bit strings, first point in the
+// highest bit (bit-reversed once per group by the callers). Plain C on purpose: a hand-written
+// v_addc_co_u32 taking the compare mask as carry-in was faster, but gfx950 needs wait states
+// between a VALU write of a lane mask and a VALU read of it (the compiler pads its own code
+// with s_nop), and inline assembly is invisible to the hazard recognizer, so it read stale
+// masks under some schedules.
+__device__ __forceinline__ uint32_t shl1_add_if(uint32_t v, bool b) { return v + v + (uint32_t)b; }
 
 template <int CTRL, int ROWS, int BANKS>
 __device__ __forceinline__ uint32_t dpp(uint32_t identity, uint32_t v) {
@@ -554,29 +552,43 @@ __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const 
             amb.w[wi] &= vm;
         }
     }
-    // ambiguous: exact z and sector from HBM, four re-reads in flight per lane
+    // ambiguous: exact z and sector from HBM, one point at a time (rare: tens per frame)
 #pragma unroll
     for (int wi = 0; wi < NW; wi++) {
         uint64_t m = amb.w[wi];
         while (m) {
-            int ks[4];
-            float3 pt[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                ks[q] = m ? __builtin_ctzll(m) : -1;
-                if (m) m &= m - 1;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (ks[q] >= 0) pt[q] = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid, L);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ks[q] < 0) continue;
-                int sx = 0;
-                bool unused = false;
-                classify_angle<true, false>(P, pt[q].x, pt[q].y, sx, unused);
-                if (!(cg_zkey(pt[q].z) < tkey[sx])) keep.w[wi] |= 1ull << ks[q];
-            }
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            const float3 p = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + k) * CG_BLOCK + tid, L);
+            int sx = 0;
+            bool unused = false;
+            classify_angle<true, false>(P, p.x, p.y, sx, unused);
+            if (!(cg_zkey(p.z) < tkey[sx])) keep.w[wi] |= 1ull << k;
         }
+    }
+}
+
+// pcl::VoxelGrid::applyFilter setup (PCL 1.10, src/cone_detection.cpp:240-249) from the
+// getMinMax3D bounds of the nfin finite points: the int64 overflow guard (pass = 1: output the
+// input unchanged) and min_b / div_b of the idx computation.
+__device__ __forceinline__ void voxel_grid_setup(uint32_t nfin, const float* bmn, const float* bmx,
+                                                 const CgDevParams& P, uint32_t& pass, int* min_b,
+                                                 int* div_b) {
+    pass = 0;
+    for (int a = 0; a < 3; a++) { min_b[a] = 0; div_b[a] = 1; }
+    if (nfin == 0) return;
+    double prod = 1.0;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float span = (bmx[a] - bmn[a]) * P.inv_leaf[a];
+        const double d = span >= 9.0e18f ? 9.0e18 : (double)((int64_t)span + 1);
+        prod *= d;
+    }
+    if (prod > 2147483647.0) pass = 1;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        min_b[a] = (int)floorf(bmn[a] * P.inv_leaf[a]);
+        const int max_b = (int)floorf(bmx[a] * P.inv_leaf[a]);
+        div_b[a] = max_b - min_b[a] + 1;
     }
 }

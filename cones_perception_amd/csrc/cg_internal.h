@@ -52,10 +52,46 @@ struct CgLaunch {
 
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
 #define CG_MMAX 1024           // LDS-path capacity (points surviving the filter)
-#define CG_MAX_POINTS 65536    // 128 points per lane
+#define CG_MAX_POINTS 65536    // frame kernel: 128 points per lane; larger frames: cg_large.hip
+#define CG_MAX_FRAME_POINTS (1u << 28)
 
 enum { CG_LAYOUT_GENERIC = 0, CG_LAYOUT_XYZI16 = 1, CG_LAYOUT_PCL32 = 2 };
 enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };
+
+// ---- frames of more than CG_MAX_POINTS points (cg_large.hip) ----
+#define LG_CHUNK 65536         // points per front workgroup
+// per-frame meta words in HBM
+enum {
+    LG_SECKEY = 0,             // 18 words: sector minima (order-preserving keys)
+    LG_TOUCHED = 18, LG_K, LG_MC, LG_MS, LG_NFIN,
+    LG_BMIN, LG_BMAX = LG_BMIN + 3, LG_V = LG_BMAX + 3, LG_C, LG_U, LG_PASS,
+    LG_MINB, LG_MUL1 = LG_MINB + 3, LG_MUL2, LG_ORG, LG_NFIN_ALL = LG_ORG + 3, LG_SCAN_N,
+    LG_META_WORDS = 64
+};
+struct LgScratch {
+    uint32_t* meta;
+    uint64_t* codes;          // z codes, [chunk][group][lane] words of 8
+    uint64_t* keep;           // ground-only mode: kept bits, [chunk][lane][2]
+    uint32_t* chunk_cnt;      // ground-only mode: kept points per chunk
+    float4* cand_p; uint32_t* cand_i;   // filter candidates (pipeline) and their frame index
+    float4* surv_p; uint32_t* surv_i;   // survivors (detector input points)
+    uint64_t* key0; uint64_t* key1;     // radix sort ping-pong
+    uint32_t* val0; uint32_t* val1;
+    uint32_t* hist;           // 256 x tiles + 1
+    uint32_t* tsum;           // tiles + 2
+    float4* vox;              // voxel points
+    uint32_t* run;            // voxel run starts
+    uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
+    uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
+};
+// Bytes of the large-frame scratch for frames of n points, and its layout at base.
+uint64_t cg_large_bytes(uint32_t n_points);
+void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
+// Run n_frames frames of more than CG_MAX_POINTS points, one at a time (synchronises s).
+int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s);
+// The LDS backend of the frame kernel on a large frame's survivors (M <= CG_MMAX).
+int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
+                            uint32_t npad, uint32_t K, hipStream_t s);
 
 // Bytes of HBM scratch one frame of n points needs for the global (non-LDS) path.
 uint64_t cg_scratch_bytes(uint32_t n_points);

@@ -121,23 +121,8 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             bmx[a] = cg_fkey_inv(fs->scal[S_BMAX0 + a]);
         }
         uint32_t pass = 0;
-        int min_b[3] = {0, 0, 0}, div_b[3] = {1, 1, 1};
-        if (nfin > 0) {
-            double prod = 1.0;
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                const float span = (bmx[a] - bmn[a]) * P.inv_leaf[a];
-                const double d = span >= 9.0e18f ? 9.0e18 : (double)((int64_t)span + 1);
-                prod *= d;
-            }
-            if (prod > 2147483647.0) pass = 1;
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                min_b[a] = (int)floorf(bmn[a] * P.inv_leaf[a]);
-                const int max_b = (int)floorf(bmx[a] * P.inv_leaf[a]);
-                div_b[a] = max_b - min_b[a] + 1;
-            }
-        }
+        int min_b[3], div_b[3];
+        voxel_grid_setup(nfin, bmn, bmx, P, pass, min_b, div_b);
         if (l == 0) {
             fs->scal[S_PASS] = pass;
             fs->scal[S_MINB0] = (uint32_t)min_b[0];
@@ -807,6 +792,64 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     } else {
         backend(W, M, fs, L, P, f, flags);
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Large frames whose detector input fits the LDS path (M <= CG_MMAX): the survivors come from
+// HBM in append order; sorted by frame index they get ranks as point indices, so the voxel
+// keys order ties exactly as the frame kernel does. npad PointXYZI() pads follow.
+__global__ __launch_bounds__(CG_BLOCK, 2) void cg_lg_back_small(CgLaunch L, CgDevParams P, LgScratch S,
+                                                                uint32_t f, uint32_t npad, uint32_t K) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+    FrontShared* fs = (FrontShared*)smem;
+    BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t Ms = S.meta[LG_MS], M = Ms + npad;
+    if (tid < 64) fs->scal[tid] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t zk = cg_fkey(0.0f);
+        for (int a = 0; a < 3; a++) {
+            uint32_t lo = S.meta[LG_BMIN + a], hi = S.meta[LG_BMAX + a];
+            if (npad) { lo = min(lo, zk); hi = max(hi, zk); }
+            fs->scal[S_BMIN0 + a] = lo;
+            fs->scal[S_BMAX0 + a] = hi;
+        }
+        fs->scal[S_MF] = S.meta[LG_NFIN] + npad;
+        uint32_t* h = L.hdr + (uint64_t)f * 8;
+        h[0] = L.n_points;
+        h[1] = K;
+    }
+    uint64_t* tmp = (uint64_t*)bl->VOX;
+    for (uint32_t j = tid; j < Ms; j += CG_BLOCK) tmp[j] = ((uint64_t)S.surv_i[j] << 16) | j;
+    __syncthreads();
+    if (Ms <= CG_RANK_SORT_MAX) {
+        rank_sort(tmp, bl->KEY, Ms);
+    } else {
+        uint32_t n2 = 1;
+        while (n2 < Ms) n2 <<= 1;
+        for (uint32_t j = tid; j < n2; j += CG_BLOCK) bl->KEY[j] = j < Ms ? tmp[j] : ~0ull;
+        __syncthreads();
+        bitonic_sort(bl->KEY, n2);
+    }
+    for (uint32_t r = tid; r < Ms; r += CG_BLOCK) {
+        bl->P[r] = S.surv_p[(uint32_t)(bl->KEY[r] & 0xffffu)];
+        bl->IDX[r] = r;
+    }
+    for (uint32_t j = tid; j < npad; j += CG_BLOCK) {
+        bl->P[Ms + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        bl->IDX[Ms + j] = 0xffffu;   // after every kept point
+    }
+    __syncthreads();
+    Work W;
+    W.P = bl->P; W.KEY = bl->KEY; W.VOX = bl->VOX; W.A = bl->A; W.PAR = bl->PAR; W.CNT = bl->CNT;
+    W.UK = bl->UK; W.LAB = bl->LAB; W.ORD = bl->ORD; W.IDX = bl->IDX; W.OFF = bl->OFF;
+    backend(W, M, fs, L, P, f, 0u);
+}
+int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
+                            uint32_t npad, uint32_t K, hipStream_t s) {
+    hipLaunchKernelGGL(cg_lg_back_small, dim3(1), dim3(CG_BLOCK), 0, s, L, P, S, f, npad, K);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------

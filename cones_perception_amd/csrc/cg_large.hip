@@ -1,0 +1,812 @@
+// cg_large.hip — frames of more than 65,536 points (C5's 1M-point dense frame,
+// and any LiDAR with more than 64 x 1024 returns). Same semantics as the frame kernel
+// (cg_kernels.hip), spread over many workgroups per frame and HBM scratch:
+//
+//   lg_front    one 512-lane workgroup per 65,536-point chunk: pass 1 (stream_pass1), z codes
+//               to HBM, per-chunk sector minima merged with global atomicMin, filter
+//               candidates appended with their frame index (detector mode: survivors + bounds)
+//   lg_decide   per chunk: thresholds, pass 2 over the chunk's codes (kept count K); the
+//               candidates of the chunk's share decided by their code (exactly when ambiguous),
+//               survivors appended, VoxelGrid bounds merged
+//   lg_ground_* ground-only mode: stable per-chunk output offsets, kept points then zero pads
+//   backend     M <= CG_MMAX: one workgroup from LDS (cg_kernels.hip, cg_launch_lg_back_small);
+//               otherwise the global backend below: voxel keys (PCL idx, frame index) sorted by
+//               a stable LSD radix sort, voxel runs + centroids in frame-index order, a
+//               neighbour grid (cells >= tolerance) sorted the same way, union-find with
+//               global atomics (roots = lowest voxel index = PCL's seed), size filter, PCL's
+//               cluster order, CSR by a (rank, voxel) sort, per-cluster centroids.
+//
+// Every sum keeps the reference's order (PCL sorts by idx; ties in point order here, as in
+// the frame kernel), so results are bit-identical to the frame kernel's on the same input.
+#include <hip/hip_runtime.h>
+#include "cg_internal.h"
+#include "../../include/cones_gpu.h"
+#include "cg_math.h"
+#include "cg_sort.h"
+#include "cg_device.h"
+
+#define LG_TILE 4096   // elements per scan / sort workgroup (512 threads x 8)
+
+// ------------------------------------------------------------------------------------------
+// Meta words (initialised by lg_init).
+__global__ void lg_init(LgScratch S, CgDevParams P) {
+    const uint32_t t = threadIdx.x;
+    if (t < LG_META_WORDS) {
+        uint32_t v = 0;
+        if (t <= CG_NUM_BINS) v = cg_fkey(P.default_low);
+        if (t >= LG_BMIN && t < LG_BMIN + 3) v = 0xffffffffu;
+        S.meta[t] = v;
+    }
+}
+
+// Bounds of finite points, merged into the frame's meta words (order-preserving keys).
+struct Bounds {
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t n = 0;
+    __device__ __forceinline__ void add(const float4& p) {
+        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+            n++;
+        }
+    }
+    __device__ __forceinline__ void merge(uint32_t* meta) {   // every lane of the wave calls
+        float r[6];
+#pragma unroll
+        for (int a = 0; a < 3; a++) { r[a] = wave_min(mn[a]); r[3 + a] = wave_max(mx[a]); }
+        const uint32_t nf = wave_sum(n);
+        if (lane_id() == 0 && nf) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                atomicMin(&meta[LG_BMIN + a], cg_fkey(r[a]));
+                atomicMax(&meta[LG_BMAX + a], cg_fkey(r[3 + a]));
+            }
+            atomicAdd(&meta[LG_NFIN], nf);
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// Front: pass 1 per chunk.
+template <int LAYOUT, int KMODE>
+__global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+    constexpr int PPT = LG_CHUNK / CG_BLOCK;
+    constexpr int NW = (PPT + 63) / 64;
+    constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
+    constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
+    __shared__ uint32_t sec_key[CG_NUM_BINS + 1];
+    const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id();
+    const uint64_t base = (uint64_t)c * LG_CHUNK;
+    const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
+    const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
+    if (tid <= CG_NUM_BINS) sec_key[tid] = cg_fkey(P.default_low);
+    __syncthreads();
+    LaneBits<NW> posm;
+    uint32_t touched = 0;
+    uint2* codes = (uint2*)S.codes + (uint64_t)c * (LG_CHUNK / 8);
+    stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, Nc, L, P, sec_key, posm, touched,
+                                             [&](int g, uint2 cw) { codes[g * CG_BLOCK + tid] = cw; });
+    if (GROUND) {
+        touched = wave_or(touched);
+        if (l == 0 && touched) atomicOr(&S.meta[LG_TOUCHED], touched);
+    }
+    __syncthreads();
+    if (GROUND && tid <= CG_NUM_BINS) atomicMin(&S.meta[LG_SECKEY + tid], sec_key[tid]);
+    if (!FILTER) return;
+    // pipeline: filter candidates (ground decided later); detector: the survivors themselves
+    const uint32_t n = posm.count();
+    const uint32_t incl = wave_incl_scan(n);
+    uint32_t wbase = 0;
+    if (l == 63 && incl) wbase = atomicAdd(&S.meta[GROUND ? LG_MC : LG_MS], incl);
+    wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
+    uint32_t pos = wbase + incl - n;
+    float4* const op = GROUND ? S.cand_p : S.surv_p;
+    uint32_t* const oi = GROUND ? S.cand_i : S.surv_i;
+    Bounds bd;
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) {
+        uint64_t m = posm.w[wi];
+        while (m) {
+            const uint32_t k = 64 * wi + __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t i = k * CG_BLOCK + tid;
+            const float4 p = load_xyzi<LAYOUT>(fb, i, L);
+            op[pos] = p;
+            oi[pos] = (uint32_t)base + i;
+            pos++;
+            if (!GROUND) bd.add(p);
+        }
+    }
+    if (!GROUND) bd.merge(S.meta);
+}
+
+// Decide: thresholds, pass 2 per chunk, candidates -> survivors.
+template <int LAYOUT, int KMODE>
+__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+    constexpr int PPT = LG_CHUNK / CG_BLOCK;
+    constexpr int NW = (PPT + 63) / 64;
+    __shared__ float thr[CG_NUM_BINS + 1];
+    __shared__ uint32_t tkey[CG_NUM_BINS + 1], band[2], kcount;
+    const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id();
+    const uint64_t base = (uint64_t)c * LG_CHUNK;
+    const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
+    const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
+    if (tid < 64) sector_thresholds(S.meta + LG_SECKEY, S.meta[LG_TOUCHED], P, thr, tkey, &band[0], &band[1]);
+    if (tid == 0) kcount = 0;
+    __syncthreads();
+    const uint32_t qlo = band[0], qhi = band[1];
+    const uint2* codes = (const uint2*)S.codes + (uint64_t)c * (LG_CHUNK / 8);
+    LaneBits<NW> keep;
+    pass2_keep<PPT, LAYOUT>(fb, Nc, L, P, qlo, qhi, tkey, [&](int g) { return codes[g * CG_BLOCK + tid]; }, keep);
+    const uint32_t kc = wave_sum(keep.count());
+    if (l == 0) atomicAdd(&kcount, kc);
+    if (KMODE == CG_KMODE_GROUND) {
+#pragma unroll
+        for (int wi = 0; wi < NW; wi++) S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi] = keep.w[wi];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        atomicAdd(&S.meta[LG_K], kcount);
+        if (KMODE == CG_KMODE_GROUND) S.chunk_cnt[c] = kcount;
+    }
+    if (KMODE == CG_KMODE_GROUND) return;
+    // this chunk's share of the candidates (written by lg_front, complete at kernel entry)
+    const uint32_t Mc = S.meta[LG_MC];
+    const uint32_t per = (Mc + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = min(Mc, c * per), hi = min(Mc, lo + per);
+    const uint8_t* cb = (const uint8_t*)S.codes;
+    Bounds bd;
+    for (uint32_t i0 = lo; i0 < hi; i0 += CG_BLOCK) {   // uniform trip count
+        const uint32_t i = i0 + tid;
+        bool kp = false;
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t pidx = 0;
+        if (i < hi) {
+            pidx = S.cand_i[i];
+            p = S.cand_p[i];
+            const uint32_t cc = pidx / LG_CHUNK, r = pidx % LG_CHUNK, k = r / CG_BLOCK, ln = r % CG_BLOCK;
+            const uint32_t code = cb[(uint64_t)cc * LG_CHUNK + ((k >> 3) * CG_BLOCK + ln) * 8 + (k & 7)];
+            if (code > qhi) {
+                kp = true;
+            } else if (code >= qlo) {   // ambiguous: exact sector and threshold
+                int sx = 0;
+                bool unused = false;
+                classify_angle<true, false>(P, p.x, p.y, sx, unused);
+                kp = !(cg_zkey(p.z) < tkey[sx]);
+            }
+        }
+        const uint64_t bal = __ballot(kp);
+        uint32_t wb = 0;
+        if (l == 0 && bal) wb = atomicAdd(&S.meta[LG_MS], (uint32_t)__popcll(bal));
+        wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, 0);
+        if (kp) {
+            const uint32_t pos = wb + mbcnt(bal);
+            S.surv_p[pos] = p;
+            S.surv_i[pos] = pidx;
+            bd.add(p);
+        }
+    }
+    bd.merge(S.meta);
+}
+
+// Ground-only output: each chunk's kept points at its stable offset, then the zero pads.
+template <int LAYOUT>
+__global__ __launch_bounds__(CG_BLOCK, 2) void lg_ground_out(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+    constexpr int PPT = LG_CHUNK / CG_BLOCK;
+    constexpr int NW = (PPT + 63) / 64;
+    __shared__ uint32_t cnt[PPT * WAVES];
+    __shared__ uint32_t red[8 * WAVES];
+    __shared__ uint32_t chunk_off;
+    const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint64_t base = (uint64_t)c * LG_CHUNK;
+    const uint32_t N = L.n_points;
+    const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
+    LaneBits<NW> keep;
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) keep.w[wi] = S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi];
+    if (tid == 0) {
+        uint32_t o = 0;
+        for (uint32_t q = 0; q < c; q++) o += S.chunk_cnt[q];
+        chunk_off = o;
+    }
+#pragma unroll 8
+    for (int k = 0; k < PPT; k++) {
+        const uint64_t bb = __ballot(keep.get(k));
+        if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(bb);
+    }
+    __syncthreads();
+    block_scan(PPT * WAVES, [&](uint32_t i) -> uint32_t { return cnt[i]; },
+               [&](uint32_t i, uint32_t e) { cnt[i] = e; }, red);
+    const uint32_t off = chunk_off;
+    float4* out = (float4*)(L.ground + (uint64_t)f * N * 32);
+#pragma unroll 4
+    for (int k = 0; k < PPT; k++) {
+        const bool kp = keep.get(k);
+        const uint64_t bb = __ballot(kp);
+        if (kp) {
+            const uint32_t i = (uint32_t)k * CG_BLOCK + tid;
+            const uint32_t dst = off + cnt[k * WAVES + w] + (uint32_t)__popcll(bb & ((1ull << l) - 1ull));
+            const float4 pp = load_xyzi<LAYOUT>(fb, i, L);
+            out[2 * dst] = make_float4(pp.x, pp.y, pp.z, 1.0f);
+            out[2 * dst + 1] = make_float4(pp.w, 0.f, 0.f, 0.f);
+        }
+    }
+    // zero pads (src/ground_removal.cpp:79): PointXYZI() after the K kept points
+    const uint32_t K = S.meta[LG_K];
+    for (uint64_t j = (uint64_t)K + (uint64_t)c * CG_BLOCK + tid; j < N; j += (uint64_t)gridDim.x * CG_BLOCK) {
+        out[2 * j] = make_float4(0.f, 0.f, 0.f, 1.0f);
+        out[2 * j + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (c == 0 && tid == 0) {
+        uint32_t* h = L.hdr + (uint64_t)f * 8;
+        h[0] = N; h[1] = K; h[2] = 0; h[3] = 0; h[4] = 0; h[5] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Device-wide exclusive scan of flag(i) over i < n (count from meta[n_word] when n_word >= 0),
+// calling emit(i, position) for every flagged i; the total goes to meta[total_word].
+// Three launches: per-tile counts, one-block scan of the tile counts, emit.
+template <class FLAG>
+__global__ __launch_bounds__(CG_BLOCK) void lg_scan_count(uint32_t n, int n_word, const uint32_t* meta, FLAG flag,
+                                                          uint32_t* tsum) {
+    __shared__ uint32_t red[WAVES];
+    if (n_word >= 0) n = meta[n_word];
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
+    uint32_t c = 0;
+    for (int q = 0; q < 8; q++) c += (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u;
+    c = wave_sum(c);
+    if (lane_id() == 0) red[wave_id()] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < WAVES; w++) t += red[w];
+        tsum[blockIdx.x] = t;
+    }
+}
+// In-place exclusive scan of a[0, n) by one workgroup; a[n] = total, also to *total if set.
+__global__ __launch_bounds__(CG_BLOCK) void lg_scan_tiles(uint32_t* a, uint32_t n, uint32_t* total) {
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t t = block_scan(n, [&](uint32_t i) -> uint32_t { return a[i]; },
+                                  [&](uint32_t i, uint32_t e) { a[i] = e; }, red);
+    if (threadIdx.x == 0) {
+        a[n] = t;
+        if (total) *total = t;
+    }
+}
+template <class FLAG, class EMIT>
+__global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, const uint32_t* meta, FLAG flag,
+                                                         EMIT emit, const uint32_t* tsum) {
+    __shared__ uint32_t red[WAVES];
+    if (n_word >= 0) n = meta[n_word];
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
+    uint32_t fl[8], c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) { fl[q] = (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u; c += fl[q]; }
+    const uint32_t inc = wave_incl_scan(c);
+    if (lane_id() == 63) red[wave_id()] = inc;
+    __syncthreads();
+    uint32_t wo = 0;
+    for (uint32_t w = 0; w < wave_id(); w++) wo += red[w];
+    uint32_t pos = tsum[blockIdx.x] + wo + inc - c;
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if (fl[q]) emit((uint32_t)(b0 + q), pos++);
+}
+
+// ------------------------------------------------------------------------------------------
+// Stable LSD radix sort of (64-bit key, 32-bit value) pairs, 8 bits per pass.
+__global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint32_t n, uint32_t shift,
+                                                       uint32_t* hist) {
+    __shared__ uint32_t h[256];
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE;
+    for (int q = 0; q < 8; q++) {
+        const uint64_t i = b0 + (uint64_t)q * CG_BLOCK + threadIdx.x;
+        if (i < n) atomicAdd(&h[(key[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+}
+// hist (scanned, digit-major) gives each (digit, tile) its output base. Within a tile the
+// elements go in 8 rounds of 512 in index order; a round ranks equal digits per wave with
+// eight ballots (the wave's lanes whose digit matches bit for bit) and offsets waves by the
+// per-wave digit counts of the round, so equal keys keep their input order (stable).
+__global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                                          uint32_t* vout, uint32_t n, uint32_t shift,
+                                                          const uint32_t* hist) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wcnt[WAVES][256];
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    if (tid < 256) run[tid] = hist[tid * gridDim.x + blockIdx.x];
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE;
+    const uint64_t lt = (1ull << l) - 1ull;
+    for (int q = 0; q < 8; q++) {
+        for (uint32_t x = tid; x < WAVES * 256; x += CG_BLOCK) (&wcnt[0][0])[x] = 0;
+        __syncthreads();
+        const uint64_t i = b0 + (uint64_t)q * CG_BLOCK + tid;
+        const bool valid = i < n;
+        uint64_t k = 0;
+        uint32_t v = 0, d = 0;
+        if (valid) { k = kin[i]; v = vin[i]; d = (uint32_t)(k >> shift) & 255u; }
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            m &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(m & lt);
+        if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = run[d] + rank;
+            for (uint32_t u = 0; u < w; u++) pos += wcnt[u][d];
+            kout[pos] = k;
+            vout[pos] = v;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t t = 0;
+            for (int u = 0; u < WAVES; u++) t += wcnt[u][tid];
+            run[tid] += t;
+        }
+        __syncthreads();
+    }
+}
+
+namespace {
+
+uint32_t tiles_of(uint64_t n) { return (uint32_t)((n + LG_TILE - 1) / LG_TILE); }
+uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + CG_BLOCK - 1) / CG_BLOCK); }
+uint32_t bits_of(uint64_t v) { uint32_t b = 0; while (b < 64 && (1ull << b) <= v) b++; return b ? b : 1; }
+
+// Sort n pairs in (k[0], v[0]); returns the buffer index (0 or 1) that holds the result.
+int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s) {
+    uint64_t* k[2] = {S.key0, S.key1};
+    uint32_t* v[2] = {S.val0, S.val1};
+    int cur = 0;
+    if (n <= 1) return cur;
+    const uint32_t nt = tiles_of(n);
+    for (uint32_t shift = 0; shift < bits; shift += 8) {
+        hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist);
+        hipLaunchKernelGGL(lg_scan_tiles, dim3(1), dim3(CG_BLOCK), 0, s, S.hist, 256 * nt, (uint32_t*)nullptr);
+        hipLaunchKernelGGL(lg_rs_scatter, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
+                           shift, S.hist);
+        cur ^= 1;
+    }
+    return cur;
+}
+
+template <class FLAG, class EMIT>
+void scan_emit(LgScratch& S, uint32_t n_max, int n_word, FLAG flag, EMIT emit, int total_word, hipStream_t s) {
+    const uint32_t nt = std::max<uint32_t>(1, tiles_of(n_max));
+    hipLaunchKernelGGL((lg_scan_count<FLAG>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, S.tsum);
+    hipLaunchKernelGGL(lg_scan_tiles, dim3(1), dim3(CG_BLOCK), 0, s, S.tsum, nt, S.meta + total_word);
+    hipLaunchKernelGGL((lg_scan_emit<FLAG, EMIT>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, emit,
+                       S.tsum);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Global backend (M > CG_MMAX). The detector's input is the M = Ms + npad points: survivors
+// (surv_p / surv_i, any order; frame index pidx) and npad PointXYZI() pads after every kept
+// point (pidx = N + j). PB bits hold a pidx.
+__device__ __forceinline__ float4 lg_point(const LgScratch& S, uint32_t j, uint32_t Ms) {
+    return j < Ms ? S.surv_p[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// pcl::VoxelGrid setup from the bounds (getMinMax3D + the int64 overflow guard)
+__global__ void lg_grid_setup(LgScratch S, CgDevParams P, uint32_t npad, uint32_t Mtot) {
+    if (threadIdx.x != 0) return;
+    uint32_t* m = S.meta;
+    float bmn[3], bmx[3];
+    uint32_t nfin = m[LG_NFIN];
+    for (int a = 0; a < 3; a++) {
+        bmn[a] = nfin ? cg_fkey_inv(m[LG_BMIN + a]) : INFINITY;
+        bmx[a] = nfin ? cg_fkey_inv(m[LG_BMAX + a]) : -INFINITY;
+        if (npad) { bmn[a] = fminf(bmn[a], 0.f); bmx[a] = fmaxf(bmx[a], 0.f); }
+    }
+    nfin += npad;
+    uint32_t pass = 0;
+    int min_b[3] = {0, 0, 0}, div_b[3] = {1, 1, 1};
+    voxel_grid_setup(nfin, bmn, bmx, P, pass, min_b, div_b);
+    m[LG_NFIN_ALL] = nfin;
+    m[LG_PASS] = pass;
+    m[LG_SCAN_N] = pass ? Mtot : nfin;   // runs over the finite points, or every point
+    for (int a = 0; a < 3; a++) m[LG_MINB + a] = (uint32_t)min_b[a];
+    m[LG_MUL1] = (uint32_t)div_b[0];
+    m[LG_MUL2] = (uint32_t)div_b[0] * (uint32_t)div_b[1];
+    m[LG_ORG + 0] = __float_as_uint(nfin ? bmn[0] : 0.f);
+    m[LG_ORG + 1] = __float_as_uint(nfin ? bmn[1] : 0.f);
+    m[LG_ORG + 2] = __float_as_uint(nfin ? bmn[2] : 0.f);
+}
+
+// keys: passthrough -> pidx; else (PCL idx << PB | pidx), non-finite idx = 0xffffffff (last)
+__global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevParams P, uint32_t Mtot, uint32_t N,
+                                                          uint32_t PB) {
+    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (j >= Mtot) return;
+    const uint32_t* m = S.meta;
+    const uint32_t Ms = m[LG_MS];
+    const float4 p = lg_point(S, j, Ms);
+    const uint64_t pidx = j < Ms ? S.surv_i[j] : (uint64_t)N + (j - Ms);
+    uint64_t key;
+    if (m[LG_PASS]) {
+        key = pidx;
+    } else if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
+        key = (0xffffffffull << PB) | pidx;
+    } else {
+        const float mnb0 = (float)(int)m[LG_MINB], mnb1 = (float)(int)m[LG_MINB + 1], mnb2 = (float)(int)m[LG_MINB + 2];
+        const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
+        const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
+        const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
+        const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * m[LG_MUL1] + (uint32_t)i2 * m[LG_MUL2];
+        key = ((uint64_t)idx << PB) | pidx;
+    }
+    S.key0[j] = key;
+    S.val0[j] = j;
+}
+
+struct VoxelHead {   // start of a voxel run among the finite points (every point if passthrough)
+    const uint64_t* key; const uint32_t* meta; uint32_t PB;
+    __device__ uint32_t operator()(uint32_t r) const {
+        if (meta[LG_PASS]) return 1u;
+        return (r == 0 || (key[r] >> PB) != (key[r - 1] >> PB)) ? 1u : 0u;
+    }
+};
+struct VoxelEmit {
+    uint32_t* run;
+    __device__ void operator()(uint32_t r, uint32_t v) const { run[v] = r; }
+};
+
+// CentroidPoint: float sums in ascending frame index / float(n); passthrough copies the point
+__global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScratch S, uint32_t f, uint32_t Mtot,
+                                                               int buf) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint32_t* m = S.meta;
+    const uint32_t V = m[LG_V], Ms = m[LG_MS];
+    if (v >= V) return;
+    const uint32_t* val = buf ? S.val1 : S.val0;
+    float4* vox_out = L.vox + (uint64_t)f * L.cap;
+    S.par[v] = v;
+    S.cnt[v] = 0;
+    S.rk[v] = 0xffffffffu;
+    if (m[LG_PASS]) {
+        const float4 p = lg_point(S, val[v], Ms);
+        S.vox[v] = p;
+        vox_out[v] = p;
+        return;
+    }
+    const uint32_t s = S.run[v], e = v + 1 < V ? S.run[v + 1] : m[LG_NFIN_ALL];
+    float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
+    for (uint32_t r = s; r < e; r++) {
+        const float4 p = lg_point(S, val[r], Ms);
+        sx += p.x; sy += p.y; sz += p.z; si += p.w;
+    }
+    const float n = (float)(e - s);
+    const float4 c = make_float4(sx / n, sy / n, sz / n, si / n);
+    S.vox[v] = c;
+    vox_out[v] = c;
+}
+
+// neighbour grid: cells of edge >= tolerance, so an edge joins voxels in adjacent cells
+__device__ __forceinline__ uint32_t lg_cell(float c, float o, float inv) {
+    const float q = floorf((c - o) * inv);
+    if (!(q >= 0.f)) return 0u;
+    return q >= 1023.f ? 1023u : (uint32_t)q;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_cell_keys(LgScratch S, CgDevParams P, uint32_t V, uint32_t VB) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const float ox = __uint_as_float(S.meta[LG_ORG]), oy = __uint_as_float(S.meta[LG_ORG + 1]),
+                oz = __uint_as_float(S.meta[LG_ORG + 2]);
+    const float4 q = S.vox[v];
+    const uint32_t ck = (lg_cell(q.z, oz, P.cell_inv) << 20) | (lg_cell(q.y, oy, P.cell_inv) << 10) |
+                        lg_cell(q.x, ox, P.cell_inv);
+    S.key0[v] = ((uint64_t)ck << VB) | v;
+    S.val0[v] = v;
+}
+struct CellHead {
+    const uint64_t* key; uint32_t VB;
+    __device__ uint32_t operator()(uint32_t r) const {
+        return (r == 0 || (key[r] >> VB) != (key[r - 1] >> VB)) ? 1u : 0u;
+    }
+};
+struct CellEmit {
+    const uint64_t* key; uint32_t VB; uint32_t* uk; uint32_t* ca;
+    __device__ void operator()(uint32_t r, uint32_t u) const { uk[u] = (uint32_t)(key[r] >> VB); ca[u] = r; }
+};
+__global__ __launch_bounds__(CG_BLOCK) void lg_cell_order(LgScratch S, uint32_t V, uint32_t VB, int buf) {
+    const uint32_t r = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint64_t* key = buf ? S.key1 : S.key0;
+    if (r < V) S.ord[r] = (uint32_t)(key[r] & ((1ull << VB) - 1ull));
+    if (r == 0) S.ca[S.meta[LG_U]] = V;
+}
+
+// union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple)
+__global__ __launch_bounds__(CG_BLOCK) void lg_union(LgScratch S, CgDevParams P, uint32_t V) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const uint32_t U = S.meta[LG_U];
+    const float ox = __uint_as_float(S.meta[LG_ORG]), oy = __uint_as_float(S.meta[LG_ORG + 1]),
+                oz = __uint_as_float(S.meta[LG_ORG + 2]);
+    const float4 q = S.vox[v];
+    const uint32_t cx = lg_cell(q.x, ox, P.cell_inv), cy = lg_cell(q.y, oy, P.cell_inv), cz = lg_cell(q.z, oz, P.cell_inv);
+    const uint32_t xlo = cx > 0 ? cx - 1 : 0, xhi = cx < 1023 ? cx + 1 : 1023;
+    for (int dz = -1; dz <= 1; dz++) {
+        const int zz = (int)cz + dz;
+        if (zz < 0 || zz > 1023) continue;
+        for (int dy = -1; dy <= 1; dy++) {
+            const int yy = (int)cy + dy;
+            if (yy < 0 || yy > 1023) continue;
+            const uint32_t lo = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xlo;
+            const uint32_t hi = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xhi;
+            uint32_t a = 0, b = U;
+            while (a < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (S.uk[mid] < lo) a = mid + 1; else b = mid;
+            }
+            for (uint32_t u = a; u < U && S.uk[u] <= hi; u++) {
+                const uint32_t e = S.ca[u + 1];
+                for (uint32_t j = S.ca[u]; j < e; j++) {
+                    const uint32_t o = S.ord[j];
+                    if (o <= v) continue;
+                    const float4 p = S.vox[o];
+                    const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+                    float acc = ddx * ddx;
+                    acc = acc + ddy * ddy;
+                    acc = acc + ddz * ddz;
+                    if (acc < P.r2) uf_union(S.par, v, o);
+                }
+            }
+        }
+    }
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_find(LgScratch S, uint32_t V) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const uint32_t r = uf_find(S.par, v);
+    S.lab[v] = r;
+    atomicAdd(&S.cnt[r], 1u);
+}
+struct KeepRoot {   // component seeds whose size passes min <= size <= max, in seed order
+    const uint32_t* lab; const uint32_t* cnt; uint32_t lo, hi;
+    __device__ uint32_t operator()(uint32_t v) const {
+        const uint32_t c = cnt[v];
+        return (lab[v] == v && c >= lo && c <= hi) ? 1u : 0u;
+    }
+};
+struct KeepEmit {
+    const uint32_t* cnt; uint32_t* droot; uint32_t* dsz;
+    __device__ void operator()(uint32_t v, uint32_t d) const { droot[d] = v; dsz[d] = cnt[v]; }
+};
+
+// cluster order: PCL sorts the reversed discovery list ascending by size with std::sort
+// (restated, cg_sort.h); <= 16 clusters is an insertion sort: (size desc, seed asc)
+__global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
+    __shared__ int32_t stk[3 * CG_SORT_STACK];
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t C = S.meta[LG_C];
+    if (C > CG_SORT_THRESHOLD) {
+        if (tid == 0) {
+            uint64_t* rec = S.key0;
+            for (uint32_t i = 0; i < C; i++) {
+                const uint32_t d = C - 1 - i;
+                rec[i] = ((uint64_t)S.dsz[d] << 32) | d;
+            }
+            cg_std_sort(rec, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, stk);
+            for (uint32_t k = 0; k < C; k++) {
+                const uint32_t d = (uint32_t)rec[C - 1 - k];
+                S.fin[k] = d;
+                S.rank[d] = k;
+            }
+        }
+    } else {
+        for (uint32_t d = tid; d < C; d += CG_BLOCK) {
+            const uint32_t sd = S.dsz[d];
+            uint32_t r = 0;
+            for (uint32_t e = 0; e < C; e++) {
+                const uint32_t se = S.dsz[e];
+                r += (se > sd) || (se == sd && e < d);
+            }
+            S.rank[d] = r;
+            S.fin[r] = d;
+        }
+    }
+    __syncthreads();
+    const uint32_t tot = block_scan(C, [&](uint32_t k) -> uint32_t { return S.dsz[S.fin[k]]; },
+                                    [&](uint32_t k, uint32_t e) { S.off[k] = e; }, red);
+    if (tid == 0) S.off[C] = tot;
+    for (uint32_t d = tid; d < C; d += CG_BLOCK) S.rk[S.droot[d]] = S.rank[d];
+}
+// labels (cluster rank or -1) and the (rank, voxel) keys of the CSR sort
+__global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, uint32_t f, uint32_t V, uint32_t VB) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const uint32_t rk = S.rk[S.lab[v]];
+    (L.lab + (uint64_t)f * L.cap)[v] = rk == 0xffffffffu ? -1 : (int32_t)rk;
+    S.key0[v] = rk == 0xffffffffu ? ~0ull : (((uint64_t)rk << VB) | v);
+    S.val0[v] = v;
+}
+// CSR indices (ascending voxel index inside each cluster), per-cluster centroid + radial push
+// (src/cone_detection.cpp:261-279), offsets and the frame header
+__global__ __launch_bounds__(CG_BLOCK) void lg_csr(CgLaunch L, LgScratch S, uint32_t f, uint32_t VB, int buf,
+                                                   uint32_t Mtot, uint32_t K) {
+    const uint32_t i = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint32_t* m = S.meta;
+    const uint32_t C = m[LG_C], tot = C ? S.off[C] : 0u;
+    const uint64_t* key = buf ? S.key1 : S.key0;
+    if (i < tot) (L.idx + (uint64_t)f * L.cap)[i] = (int32_t)(key[i] & ((1ull << VB) - 1ull));
+    if (i <= C) (L.offs + (uint64_t)f * (L.cap + 1))[i] = C ? (int32_t)S.off[i] : 0;
+    if (i == 0) {
+        uint32_t* h = L.hdr + (uint64_t)f * 8;
+        h[CG_HDR_N] = L.n_points;
+        h[CG_HDR_K] = K;
+        h[CG_HDR_M] = Mtot;
+        h[CG_HDR_V] = m[LG_V];
+        h[CG_HDR_C] = C;
+        h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u);
+    }
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+    const uint32_t k = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint32_t C = S.meta[LG_C];
+    if (k >= C) return;
+    const int32_t* idx = L.idx + (uint64_t)f * L.cap;
+    const uint32_t s = S.off[k], e = S.off[k + 1];
+    float x = 0.0f, y = 0.0f;
+    uint32_t i = s;
+    for (; i + 8 <= e; i += 8) {   // members fetched eight at a time, summed in order
+        float2 pv[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) { const float4 p = S.vox[idx[i + b]]; pv[b] = make_float2(p.x, p.y); }
+#pragma unroll
+        for (int b = 0; b < 8; b++) { x += pv[b].x; y += pv[b].y; }
+    }
+    for (; i < e; i++) {
+        const float4 p = S.vox[idx[i]];
+        x += p.x;
+        y += p.y;
+    }
+    const int j = (int)(e - s);
+    const float px = x / (float)j, py = y / (float)j;
+    const double Sq = ((double)px * (double)px + (double)py * (double)py) + 0.0;
+    const float len = (float)__builtin_sqrt(Sq);
+    const float qx = (float)((double)px + (double)(px / len) * P.ext);
+    const float qy = (float)((double)py + (double)(py / len) * P.ext);
+    (L.cen + (uint64_t)f * L.cap)[k] = make_float2(qx, qy);
+}
+
+// ------------------------------------------------------------------------------------------
+// Host driver: one frame at a time on stream s. Synchronises twice per frame (survivor count
+// and voxel count size the backend launches).
+int cg_run_large(const CgLaunch& L0, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s) {
+    const uint32_t N = L0.n_points;
+    const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
+    const bool xyzi16 = L0.point_step == 16 && L0.off_x == 0 && L0.off_y == 4 && L0.off_z == 8 && L0.off_i == 12;
+    hipError_t e;
+    uint32_t hm[LG_META_WORDS];
+    for (uint32_t f = 0; f < L0.n_frames; f++) {
+        const CgLaunch& L = L0;
+        hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
+#define LG_FRONT(LAY, KM) hipLaunchKernelGGL((lg_front<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
+#define LG_DECIDE(LAY, KM) hipLaunchKernelGGL((lg_decide<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
+        if (xyzi16) {
+            if (kmode == CG_KMODE_PIPELINE) { LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE); LG_DECIDE(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE); }
+            else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_DETECT);
+            else {
+                LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_GROUND); LG_DECIDE(CG_LAYOUT_XYZI16, CG_KMODE_GROUND);
+                hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_XYZI16>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+            }
+        } else {
+            if (kmode == CG_KMODE_PIPELINE) { LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE); LG_DECIDE(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE); }
+            else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_DETECT);
+            else {
+                LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_GROUND); LG_DECIDE(CG_LAYOUT_GENERIC, CG_KMODE_GROUND);
+                hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_GENERIC>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+            }
+        }
+#undef LG_FRONT
+#undef LG_DECIDE
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (kmode == CG_KMODE_GROUND) continue;
+        if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        const uint32_t K = kmode == CG_KMODE_PIPELINE ? hm[LG_K] : N;
+        const uint32_t Ms = hm[LG_MS];
+        const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
+        const uint32_t Mtot = Ms + npad;
+        if (Mtot <= CG_MMAX && !S.force_global) {
+            if ((e = (hipError_t)cg_launch_lg_back_small(L, P, S, f, npad, K, s)) != hipSuccess) return e;
+            continue;
+        }
+        // ---- global backend ----
+        const uint32_t PB = bits_of((uint64_t)N + npad);
+        const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
+        hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad, Mtot);
+        hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
+        int buf = radix_sort(S, Mtot, 32 + PB, s);
+        const uint64_t* vkey = buf ? S.key1 : S.key0;
+        // runs over the finite points (non-finite keys sort last); passthrough: every point
+        scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
+        hipLaunchKernelGGL(lg_voxel_centroids, dim3(mb), dim3(CG_BLOCK), 0, s, L, S, f, Mtot, buf);
+        if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        const uint32_t V = hm[LG_V];
+        const uint32_t VB = bits_of(V);
+        const uint32_t vb = std::max<uint32_t>(1, blocks_of(V));
+        if (V > 0) {
+            hipLaunchKernelGGL(lg_cell_keys, dim3(vb), dim3(CG_BLOCK), 0, s, S, P, V, VB);
+            const int cb = radix_sort(S, V, 30 + VB, s);
+            const uint64_t* ckey = cb ? S.key1 : S.key0;
+            scan_emit(S, V, -1, CellHead{ckey, VB}, CellEmit{ckey, VB, S.uk, S.ca}, LG_U, s);
+            hipLaunchKernelGGL(lg_cell_order, dim3(vb), dim3(CG_BLOCK), 0, s, S, V, VB, cb);
+            hipLaunchKernelGGL(lg_union, dim3(vb), dim3(CG_BLOCK), 0, s, S, P, V);
+            hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
+            scan_emit(S, V, -1, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
+            hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
+            hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, L, S, f, V, VB);
+            const int kb = radix_sort(S, V, 2 * VB, s);
+            hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)V + 1)), dim3(CG_BLOCK), 0, s, L, S, f, VB, kb, Mtot, K);
+            hipLaunchKernelGGL(lg_centroids, dim3(vb), dim3(CG_BLOCK), 0, s, L, P, S, f);
+        } else {
+            hipLaunchKernelGGL(lg_csr, dim3(1), dim3(CG_BLOCK), 0, s, L, S, f, VB, 0, Mtot, K);
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+// ------------------------------------------------------------------------------------------
+// Scratch layout (one frame at a time).
+namespace {
+template <class F>
+uint64_t lg_walk(uint32_t n, F place) {
+    const uint64_t N = std::max<uint32_t>(n, 1), nch = (N + LG_CHUNK - 1) / LG_CHUNK, nt = tiles_of(N);
+    uint64_t off = 0;
+    auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~255ull; return o; };
+    place(0, take(LG_META_WORDS * 4));
+    place(1, take(nch * LG_CHUNK));
+    place(2, take(nch * CG_BLOCK * 2 * 8));
+    place(3, take(nch * 4 + 4));
+    place(4, take(N * 16)); place(5, take(N * 4));
+    place(6, take(N * 16)); place(7, take(N * 4));
+    place(8, take(N * 8)); place(9, take(N * 8));
+    place(10, take(N * 4)); place(11, take(N * 4));
+    place(12, take((256 * nt + 2) * 4));
+    place(13, take((nt + 2) * 4));
+    place(14, take(N * 16));
+    place(15, take((N + 2) * 4));
+    for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));
+    return off;
+}
+}  // namespace
+uint64_t cg_large_bytes(uint32_t n) { return lg_walk(n, [](int, uint64_t) {}); }
+void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
+    uint32_t** arr[12] = {&S.par, &S.cnt, &S.lab, &S.uk, &S.ca, &S.ord, &S.droot, &S.dsz, &S.rank, &S.fin, &S.off, &S.rk};
+    lg_walk(n, [&](int k, uint64_t o) {
+        uint8_t* p = base + o;
+        switch (k) {
+            case 0: S.meta = (uint32_t*)p; break;
+            case 1: S.codes = (uint64_t*)p; break;
+            case 2: S.keep = (uint64_t*)p; break;
+            case 3: S.chunk_cnt = (uint32_t*)p; break;
+            case 4: S.cand_p = (float4*)p; break;
+            case 5: S.cand_i = (uint32_t*)p; break;
+            case 6: S.surv_p = (float4*)p; break;
+            case 7: S.surv_i = (uint32_t*)p; break;
+            case 8: S.key0 = (uint64_t*)p; break;
+            case 9: S.key1 = (uint64_t*)p; break;
+            case 10: S.val0 = (uint32_t*)p; break;
+            case 11: S.val1 = (uint32_t*)p; break;
+            case 12: S.hist = (uint32_t*)p; break;
+            case 13: S.tsum = (uint32_t*)p; break;
+            case 14: S.vox = (float4*)p; break;
+            case 15: S.run = (uint32_t*)p; break;
+            default: *arr[k - 16] = (uint32_t*)p; break;
+        }
+    });
+}

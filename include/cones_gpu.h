@@ -29,16 +29,16 @@ extern "C" {
 #define CG_E_INVALID   1   /* bad argument / unsupported cloud layout */
 #define CG_E_DEVICE    2   /* HIP runtime error or no gfx950 device */
 #define CG_E_OOM       3   /* device or pinned host allocation failed */
-#define CG_E_CAPACITY  4   /* frame larger than the batch engine supports (N > 65536) */
+#define CG_E_CAPACITY  4   /* frame larger than the engine supports (N > 2^28 points) */
 
 /* result flags (cg_detect_result.flags, batch header word CG_HDR_FLAGS) */
 #define CG_F_VOXEL_PASSTHROUGH 0x1u  /* PCL VoxelGrid overflow guard hit: voxel cloud = input */
-#define CG_F_GLOBAL_SCRATCH    0x2u  /* frame too large for the LDS path; ran from HBM scratch */
+#define CG_F_GLOBAL_SCRATCH    0x2u  /* detector input too large for the LDS backend; ran from HBM */
 #define CG_F_ORDER_CANONICAL   0x4u  /* >16 clusters: order is (size desc, seed asc); PCL's
                                         std::sort may order equal-size clusters differently */
 
 /* ---- parameters --------------------------------------------------------------------- */
-/* Field names are the YAML keys, misspellings kept (config/*.yaml). */
+/* Field names are the YAML keys, misspellings kept (config/ *.yaml). */
 typedef struct cg_params {
     /* config/ground_removal_params.yaml; defaults src/ground_removal.cpp:18-19 */
     int32_t num_of_sectors;          /* read but inert: sector width is fixed at 22 deg (G1) */
@@ -136,7 +136,9 @@ typedef struct cg_batch {
 #define CG_MODE_DETECT   1   /* detector only (cg_detect semantics) */
 
 /* Enqueue one pass of the hot path over the batch on `hip_stream` (hipStream_t; NULL = the
- * handle's own stream). Results stay on the device until the next batch call. */
+ * handle's own stream). Results stay on the device until the next batch call. Frames of more
+ * than 65,536 points run through the multi-workgroup large-frame path one frame at a time,
+ * and the call synchronises the stream (it sizes each frame's backend from its counts). */
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream);
 
 /* Per-frame header words in the device result buffer. */
@@ -172,6 +174,13 @@ int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
  * next batch calls; enable = 0 frees the buffer. Fetch synchronises the batch stream. */
 int cg_debug_stamps(cg_handle* h, int enable);
 int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
+
+/* Diagnostics: route every frame through the large-frame path (1), and also through its
+ * global HBM backend even when the detector input fits the LDS backend (2); 0 = automatic. */
+int cg_debug_route(cg_handle* h, int route);
+/* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
+ * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */
+int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words);
 
 /* Exported library version string. */
 const char* cg_version(void);
