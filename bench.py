@@ -39,6 +39,9 @@ def main():
                     help="threads of the frame-parallel CPU leg (the box's CPU share is 16)")
     ap.add_argument("--single-frame", action="store_true", help="also time C2 single-frame latency")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: per-phase in-kernel timing")
+    ap.add_argument("--c5", action="store_true",
+                    help="also time C5's frame shape on this GPU: one 1,048,576-point dense frame "
+                         "(128 rings x 8192 columns + clutter) through the large-frame path")
     ap.add_argument("--scatter", action="store_true",
                     help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
                          "scatter to ranks, process, gather per-frame headers (reported separately)")
@@ -131,6 +134,10 @@ def main():
     if args.scatter and world > 1:
         scatter = scatter_composition(cp, cd, engines[0], streams[0], raw, F, N, dev, rank, world, args.steps)
 
+    c5 = None
+    if args.c5 and rank == 0:
+        c5 = c5_single_gpu(cp, params, local)
+
     single = None
     if args.single_frame and rank == 0:
         single = single_frame_latency(cp, params, raw, local)
@@ -169,6 +176,8 @@ def main():
         }
         if single is not None:
             line["single_frame"] = single
+        if c5 is not None:
+            line["c5_single_gpu"] = c5
         if scatter is not None:
             line["c4_scatter_gather"] = scatter
         print(json.dumps(line), flush=True)
@@ -291,6 +300,29 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
     el = cd.max_over_ranks(time.perf_counter() - t0, dev)
     return {"frames_per_s": F * world * steps / el, "ms_per_step": el / steps * 1e3,
             "includes": "RCCL scatter of the batch from rank 0, processing, gather of headers"}
+
+
+def c5_single_gpu(cp, params, device, reps=20):
+    """C5's frame shape on one GPU, device-resident: one 1M-point dense frame per call of the
+    batch engine (large-frame path; the call synchronises once the frame is done)."""
+    import torch
+    raw = cp.synth_frames(1, first_frame=0, rings=128, cols=8192, clutter=60, cones_per_row=12)
+    d = torch.from_numpy(raw).to(torch.device("cuda", device))
+    eng = cp.BatchEngine(params, device=device)
+    st = torch.cuda.Stream(torch.device("cuda", device))
+    n = raw.shape[1] // 16
+    for _ in range(3):
+        eng.run(d.data_ptr(), 1, n, 16, stream=st.cuda_stream)
+    st.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.run(d.data_ptr(), 1, n, 16, stream=st.cuda_stream)
+    st.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    r = eng.fetch(0)
+    return {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt, "points": n, "K": r.n_kept,
+            "M": r.n_filtered, "V": int(r.voxels.shape[0]), "C": int(r.centroids.shape[0]),
+            "includes": "device-resident input; two host syncs per frame (large-frame path)"}
 
 
 def single_frame_latency(cp, params, raw, device, reps=200):

@@ -111,6 +111,7 @@ _SIGS = {
     "cg_debug_stamps": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_debug_route": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_debug_large_meta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "cg_debug_large_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "cg_debug_stamps_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_synth_default": (None, [C.POINTER(cg_synth_cfg)]),
     "cg_synth_frames": (C.c_int, [C.POINTER(cg_synth_cfg), C.c_uint64, C.c_uint32, C.c_void_p,

@@ -258,9 +258,12 @@ __device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x,
 // monotone step functions of the float angle, so equal classes at a - E and a + E certify.
 #define CG_ANG_MARGIN 8.0e-6f
 #define CG_SEC_MARGIN_T 2.0e-5f
-// The exact restatement is large and rarely executed: one out-of-line copy keeps it out of
-// the hot loops' instruction footprint.
-__device__ __noinline__ float cg_atan2f_cold(float y, float x) { return cg_atan2f(y, x); }
+// The exact restatement, for the rare points the fast classification cannot certify. Inlined
+// into those (cold) branches: an out-of-line call from inside divergent loops corrupted the
+// caller's per-lane state under some schedules (lanes that took the call lost their keep bits
+// in lg_decide; no scratch or register overlap explained it), and the call-free form is
+// deterministic.
+__device__ __forceinline__ float cg_atan2f_cold(float y, float x) { return cg_atan2f(y, x); }
 // Fast form: returns false (uncertain) where only the exact restatement can decide.
 template <bool NEED_SECTOR, bool NEED_ANGLE>
 __device__ __forceinline__ bool classify_angle_fast(const CgDevParams& P, float x, float y, int& sector,

@@ -59,7 +59,7 @@ enum { CG_LAYOUT_GENERIC = 0, CG_LAYOUT_XYZI16 = 1, CG_LAYOUT_PCL32 = 2 };
 enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };
 
 // ---- frames of more than CG_MAX_POINTS points (cg_large.hip) ----
-#define LG_CHUNK 65536         // points per front workgroup
+#define LG_CHUNK 8192          // points per front workgroup (16 per lane): a 1M frame fills 128
 // per-frame meta words in HBM
 enum {
     LG_SECKEY = 0,             // 18 words: sector minima (order-preserving keys)

@@ -2,7 +2,7 @@
 // and any LiDAR with more than 64 x 1024 returns). Same semantics as the frame kernel
 // (cg_kernels.hip), spread over many workgroups per frame and HBM scratch:
 //
-//   lg_front    one 512-lane workgroup per 65,536-point chunk: pass 1 (stream_pass1), z codes
+//   lg_front    one 512-lane workgroup per 8,192-point chunk: pass 1 (stream_pass1), z codes
 //               to HBM, per-chunk sector minima merged with global atomicMin, filter
 //               candidates appended with their frame index (detector mode: survivors + bounds)
 //   lg_decide   per chunk: thresholds, pass 2 over the chunk's codes (kept count K); the
@@ -204,10 +204,11 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void lg_ground_out(CgLaunch L, CgDevPa
     LaneBits<NW> keep;
 #pragma unroll
     for (int wi = 0; wi < NW; wi++) keep.w[wi] = S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi];
-    if (tid == 0) {
+    if (w == 0) {   // kept points of the chunks before this one
         uint32_t o = 0;
-        for (uint32_t q = 0; q < c; q++) o += S.chunk_cnt[q];
-        chunk_off = o;
+        for (uint32_t q = l; q < c; q += 64) o += S.chunk_cnt[q];
+        o = wave_sum(o);
+        if (l == 0) chunk_off = o;
     }
 #pragma unroll 8
     for (int k = 0; k < PPT; k++) {
@@ -525,9 +526,12 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_cell_order(LgScratch S, uint32_t 
     if (r == 0) S.ca[S.meta[LG_U]] = V;
 }
 
-// union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple)
+// union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple). One
+// wave per voxel: for each of the 9 (z, y) rows of neighbour cells, the cells x-1..x+1 are
+// consecutive in the cell-sorted order, so their voxels form one contiguous range of ord[]
+// that the 64 lanes stride over.
 __global__ __launch_bounds__(CG_BLOCK) void lg_union(LgScratch S, CgDevParams P, uint32_t V) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint32_t v = blockIdx.x * WAVES + wave_id(), l = lane_id();
     if (v >= V) return;
     const uint32_t U = S.meta[LG_U];
     const float ox = __uint_as_float(S.meta[LG_ORG]), oy = __uint_as_float(S.meta[LG_ORG + 1]),
@@ -543,23 +547,26 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_union(LgScratch S, CgDevParams P,
             if (yy < 0 || yy > 1023) continue;
             const uint32_t lo = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xlo;
             const uint32_t hi = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xhi;
-            uint32_t a = 0, b = U;
+            uint32_t a = 0, b = U;       // first cell >= lo
             while (a < b) {
                 const uint32_t mid = (a + b) >> 1;
                 if (S.uk[mid] < lo) a = mid + 1; else b = mid;
             }
-            for (uint32_t u = a; u < U && S.uk[u] <= hi; u++) {
-                const uint32_t e = S.ca[u + 1];
-                for (uint32_t j = S.ca[u]; j < e; j++) {
-                    const uint32_t o = S.ord[j];
-                    if (o <= v) continue;
-                    const float4 p = S.vox[o];
-                    const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
-                    float acc = ddx * ddx;
-                    acc = acc + ddy * ddy;
-                    acc = acc + ddz * ddz;
-                    if (acc < P.r2) uf_union(S.par, v, o);
-                }
+            uint32_t e = a, b2 = U;      // first cell > hi
+            while (e < b2) {
+                const uint32_t mid = (e + b2) >> 1;
+                if (S.uk[mid] <= hi) e = mid + 1; else b2 = mid;
+            }
+            const uint32_t j1 = S.ca[e];
+            for (uint32_t j = S.ca[a] + l; j < j1; j += 64) {
+                const uint32_t o = S.ord[j];
+                if (o <= v) continue;
+                const float4 p = S.vox[o];
+                const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+                float acc = ddx * ddx;
+                acc = acc + ddy * ddy;
+                acc = acc + ddz * ddz;
+                if (acc < P.r2) uf_union(S.par, v, o);
             }
         }
     }
@@ -744,7 +751,7 @@ int cg_run_large(const CgLaunch& L0, const CgDevParams& P, int kmode, LgScratch 
             const uint64_t* ckey = cb ? S.key1 : S.key0;
             scan_emit(S, V, -1, CellHead{ckey, VB}, CellEmit{ckey, VB, S.uk, S.ca}, LG_U, s);
             hipLaunchKernelGGL(lg_cell_order, dim3(vb), dim3(CG_BLOCK), 0, s, S, V, VB, cb);
-            hipLaunchKernelGGL(lg_union, dim3(vb), dim3(CG_BLOCK), 0, s, S, P, V);
+            hipLaunchKernelGGL(lg_union, dim3((V + WAVES - 1) / WAVES), dim3(CG_BLOCK), 0, s, S, P, V);
             hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
             scan_emit(S, V, -1, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
             hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);

@@ -181,6 +181,9 @@ int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */
 int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words);
+/* Diagnostics: raw large-frame scratch of the last frame: 0 = meta words, 1 = z codes
+ * ([chunk][group][lane] words of 8 codes), 2 = ground-mode kept bits. */
+int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes);
 
 /* Exported library version string. */
 const char* cg_version(void);

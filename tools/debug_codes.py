@@ -1,0 +1,36 @@
+"""Diagnostic: large-path z codes across repeated runs and against host-computed codes."""
+import os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import cones_perception_amd as cp
+from cones_perception_amd import _abi
+params = cp.load_params("simulation")
+raw = cp.synth_frames(1, first_frame=0, rings=128, cols=8192, clutter=60, cones_per_row=12)
+msg = cp.frame_cloud(raw[0])
+N = raw.shape[1] // 16
+CH = 8192
+z = raw[0].view(np.float32).reshape(-1, 4)[:, 2]
+tmax = np.float32(np.float64(np.float32(-0.1)) + 0.1)   # cg_ceil_to_float, close enough here
+z0 = np.float32(tmax - np.float32(254.0 / 64.0))
+bias = np.float32(-z0 * np.float32(64.0))
+q = np.float32(z * np.float32(64.0)) + bias
+exp = np.where(np.isnan(z), 255, np.clip(q, 0, 255).astype(np.uint32)).astype(np.uint8)
+# device layout: [chunk][g][lane][j], point = chunk*CH + (g*8+j)*512 + lane
+i = np.arange(N)
+c, r = i // CH, i % CH
+k, ln = r // 512, r % 512
+pos = c * CH + ((k >> 3) * 512 + ln) * 8 + (k & 7)
+for name, obj in (("ground", cp.GroundRemover(params)), ("pipeline", cp.ConePipeline(params))):
+    runs = []
+    for rep in range(6):
+        obj.cloud_handler(msg)
+        buf = np.zeros(N, np.uint8)
+        _abi.check(_abi.lib().cg_debug_large_buffer(obj.handle, 1, buf.ctypes.data, N))
+        runs.append(buf[pos])
+    runs = np.array(runs)
+    var = (runs != runs[0]).any(0)
+    bad = (runs != exp[None, :]).any(0)
+    print(name, "codes varying across runs:", int(var.sum()), "codes != host:", int(bad.sum()))
+    for p in np.where(bad)[0][:8]:
+        print("   point", p, "z", z[p], "host", exp[p], "gpu runs", runs[:, p].tolist())
