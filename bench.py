@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--c5", action="store_true",
                     help="also time C5's frame shape on this GPU: one 1,048,576-point dense frame "
                          "(128 rings x 8192 columns + clutter) through the large-frame path")
+    ap.add_argument("--c5-tiled", action="store_true",
+                    help="also time C5 tiled over the ranks: each rank holds a contiguous tile of "
+                         "the 1M-point frame; sector keys / counts merged, survivors gathered to rank 0")
     ap.add_argument("--scatter", action="store_true",
                     help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
                          "scatter to ranks, process, gather per-frame headers (reported separately)")
@@ -138,6 +141,10 @@ def main():
     if args.c5 and rank == 0:
         c5 = c5_single_gpu(cp, params, local)
 
+    c5t = None
+    if args.c5_tiled:
+        c5t = c5_tiled(cp, cd, params, local, rank, world)
+
     single = None
     if args.single_frame and rank == 0:
         single = single_frame_latency(cp, params, raw, local)
@@ -178,6 +185,8 @@ def main():
             line["single_frame"] = single
         if c5 is not None:
             line["c5_single_gpu"] = c5
+        if c5t is not None:
+            line["c5_tiled"] = c5t
         if scatter is not None:
             line["c4_scatter_gather"] = scatter
         print(json.dumps(line), flush=True)
@@ -323,6 +332,49 @@ def c5_single_gpu(cp, params, device, reps=20):
     return {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt, "points": n, "K": r.n_kept,
             "M": r.n_filtered, "V": int(r.voxels.shape[0]), "C": int(r.centroids.shape[0]),
             "includes": "device-resident input; two host syncs per frame (large-frame path)"}
+
+
+def c5_tiled(cp, cd, params, device, rank, world, reps=20):
+    """C5 tiled over the ranks (one GPU each): rank r holds points tile_range(r) of the
+    1M-point frame in its HBM. Per frame: pass 1 on the tile, one MIN all-reduce of the sector
+    keys, the keep decision, one all-gather of count words, one all-gather of survivors to
+    rank 0, backend on rank 0. Time = max over ranks; rank 0 checks the tiled result against
+    the single-GPU large path on the whole frame."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", device)
+    raw = cp.synth_frames(1, first_frame=0, rings=128, cols=8192, clutter=60, cones_per_row=12)
+    n_total = raw.shape[1] // 16
+    lo, hi = cd.tile_range(n_total, rank, world)
+    tile = torch.from_numpy(np.ascontiguousarray(raw[0, lo * 16: hi * 16])).to(dev)
+    eng = cp.BatchEngine(params, device=device)
+    run = lambda: cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        det = run()
+    torch.cuda.synchronize(dev)
+    el = cd.max_over_ranks(time.perf_counter() - t0, dev)
+    out = {"ms_per_frame": el / reps * 1e3, "frames_per_s": reps / el, "ranks": world,
+           "points": n_total, "tile_points": hi - lo,
+           "includes": "device-resident tiles; 3 collectives + host syncs per frame; backend on rank 0"}
+    if rank == 0:
+        full = torch.from_numpy(raw).to(dev)
+        ref_eng = cp.BatchEngine(params, device=device)
+        ref_eng.run(full.data_ptr(), 1, n_total, 16)
+        ref = ref_eng.fetch(0)
+        out["identical_to_single_gpu"] = bool(
+            det.n_kept == ref.n_kept and det.n_filtered == ref.n_filtered
+            and np.array_equal(det.voxels.view(np.uint32), ref.voxels.view(np.uint32))
+            and np.array_equal(det.labels, ref.labels)
+            and np.array_equal(det.centroids.view(np.uint32), ref.centroids.view(np.uint32)))
+        out["C"] = int(det.centroids.shape[0])
+    return out
 
 
 def single_frame_latency(cp, params, raw, device, reps=200):

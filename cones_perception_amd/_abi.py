@@ -82,6 +82,15 @@ class cg_batch_results(C.Structure):
     ]
 
 
+class cg_tile(C.Structure):
+    _fields_ = [("d_data", C.c_void_p), ("first", C.c_uint32), ("n", C.c_uint32), ("n_total", C.c_uint32),
+                ("point_step", C.c_uint32), ("off_x", C.c_int32), ("off_y", C.c_int32), ("off_z", C.c_int32),
+                ("off_intensity", C.c_int32)]
+
+
+CG_TILE_KEYS, CG_TILE_COUNTS = 19, 9
+
+
 class cg_synth_cfg(C.Structure):
     _fields_ = [
         ("rings", C.c_uint32), ("cols", C.c_uint32),
@@ -104,6 +113,10 @@ _SIGS = {
     "cg_detect": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_detect_result)]),
     "cg_pipeline": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_detect_result)]),
     "cg_run_batch": (C.c_int, [C.c_void_p, C.POINTER(cg_batch), C.c_int, C.c_void_p]),
+    "cg_tile_front": (C.c_int, [C.c_void_p, C.POINTER(cg_tile), C.c_void_p]),
+    "cg_tile_decide": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cg_tile_survivors": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "cg_tile_backend": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     "cg_batch_results_get": (C.c_int, [C.c_void_p, C.POINTER(cg_batch_results)]),
     "cg_batch_fetch": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(cg_detect_result)]),
     "cg_selftest_atan2f": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),

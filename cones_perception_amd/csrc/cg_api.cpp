@@ -147,6 +147,8 @@ struct cg_handle {
     uint32_t large_points = 0;
     LgScratch lg{};
     int route = 0;                // cg_debug_route
+    cg_tile tile{};               // the rank's tile (cg_tile_front .. cg_tile_decide)
+    bool tile_ready = false;
     // diagnostics
     bool stamps_on = false;
     uint64_t* d_stamps = nullptr;
@@ -532,6 +534,112 @@ int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out) {
     if (frame >= h->last_frames) return fail(CG_E_INVALID, "frame %u >= %u", frame, h->last_frames);
     HIPCHK(hipSetDevice(h->device));
     return fetch_frame(h, h->last_stream, frame, out);
+}
+
+// ---- tiled frames (C5) ----------------------------------------------------------------------
+namespace {
+CgLaunch tile_launch(const cg_tile& t) {
+    CgLaunch L{};
+    L.in = (const uint8_t*)t.d_data;
+    L.n_frames = 1;
+    L.n_points = t.n;
+    L.frame_stride = (uint64_t)t.n * t.point_step;
+    L.point_step = t.point_step;
+    L.off_x = t.off_x; L.off_y = t.off_y; L.off_z = t.off_z; L.off_i = t.off_intensity;
+    L.is_dense = 0;
+    return L;
+}
+}  // namespace
+
+int cg_tile_front(cg_handle* h, const cg_tile* t, uint32_t* keys) {
+    if (!h || !t || !keys) return fail(CG_E_INVALID, "null argument");
+    if (t->n && !t->d_data) return fail(CG_E_INVALID, "null tile data");
+    if (t->n_total > CG_MAX_FRAME_POINTS || (uint64_t)t->first + t->n > t->n_total)
+        return fail(CG_E_INVALID, "tile [%u, %u + %u) outside a frame of %u points", t->first, t->first, t->n, t->n_total);
+    if (t->point_step == 0 || t->point_step % 4) return fail(CG_E_INVALID, "bad point_step");
+    const int32_t offs[4] = {t->off_x, t->off_y, t->off_z, t->off_intensity};
+    for (int32_t o : offs)
+        if (o >= 0 && (o % 4 || (uint32_t)o + 4 > t->point_step)) return fail(CG_E_INVALID, "bad field offset %d", o);
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
+    rc = ensure_large(h, std::max<uint32_t>(t->n, 1));
+    if (rc) return rc;
+    h->tile = *t;
+    CgLaunch L = tile_launch(*t);
+    LgScratch S = h->lg;
+    S.pidx_base = t->first;
+    HIPCHK((hipError_t)cg_large_front(L, h->dp, CG_KMODE_PIPELINE, S, h->stream, 0, true));
+    HIPCHK(hipMemcpyAsync(keys, S.meta + LG_SECKEY, CG_TILE_KEYS * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->tile_ready = true;
+    return CG_OK;
+}
+
+int cg_tile_decide(cg_handle* h, const uint32_t* merged_keys, uint32_t* counts) {
+    if (!h || !merged_keys || !counts) return fail(CG_E_INVALID, "null argument");
+    if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_decide before cg_tile_front");
+    HIPCHK(hipSetDevice(h->device));
+    LgScratch S = h->lg;
+    S.pidx_base = h->tile.first;
+    HIPCHK(hipMemcpyAsync(S.meta + LG_SECKEY, merged_keys, CG_TILE_KEYS * 4, hipMemcpyHostToDevice, h->stream));
+    CgLaunch L = tile_launch(h->tile);
+    HIPCHK((hipError_t)cg_large_decide(L, h->dp, S, h->stream, 0));
+    uint32_t m[LG_META_WORDS];
+    HIPCHK(hipMemcpyAsync(m, S.meta, sizeof(m), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    counts[0] = m[LG_K];
+    counts[1] = m[LG_MS];
+    counts[2] = m[LG_NFIN];
+    for (int a = 0; a < 3; a++) { counts[3 + a] = m[LG_BMIN + a]; counts[6 + a] = m[LG_BMAX + a]; }
+    return CG_OK;
+}
+
+int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t capacity) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_survivors before cg_tile_front");
+    HIPCHK(hipSetDevice(h->device));
+    uint32_t n = 0;
+    HIPCHK(hipMemcpyAsync(&n, h->lg.meta + LG_MS, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (n > capacity) return fail(CG_E_INVALID, "%u survivors do not fit %u", n, capacity);
+    if (n && (!d_points || !d_index)) return fail(CG_E_INVALID, "null output buffers");
+    if (n) {
+        HIPCHK(hipMemcpyAsync(d_points, h->lg.surv_p, (size_t)n * 16, hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(hipMemcpyAsync(d_index, h->lg.surv_i, (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CG_OK;
+}
+
+int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index, uint32_t n_survivors,
+                    const uint32_t* merged_counts, uint32_t n_total) {
+    if (!h || !merged_counts) return fail(CG_E_INVALID, "null argument");
+    if (n_survivors && (!d_points || !d_index)) return fail(CG_E_INVALID, "null survivors");
+    if (n_total == 0 || n_total > CG_MAX_FRAME_POINTS || n_survivors > n_total || merged_counts[0] > n_total ||
+        merged_counts[1] != n_survivors)
+        return fail(CG_E_INVALID, "inconsistent tile counts (%u survivors, K %u, N %u)", n_survivors,
+                    merged_counts[0], n_total);
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
+    rc = ensure_large(h, n_total);
+    if (rc) return rc;
+    rc = ensure_batch(h, 1, n_total, false);
+    if (rc) return rc;
+    LgScratch S = h->lg;
+    S.pidx_base = 0;
+    S.force_global = h->route == 2 ? 1u : 0u;
+    HIPCHK((hipError_t)cg_large_set_survivors(S, h->dp, d_points, d_index, n_survivors, merged_counts, h->stream));
+    CgLaunch L{};
+    L.n_frames = 1;
+    L.n_points = n_total;
+    fill_launch_outputs(h, L);
+    L.stamps = nullptr;
+    HIPCHK((hipError_t)cg_large_backend(L, h->dp, CG_KMODE_PIPELINE, S, h->stream, 0, n_total, merged_counts[0]));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
+    return CG_OK;
 }
 
 int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words) {

@@ -83,12 +83,25 @@ struct LgScratch {
     uint32_t* run;            // voxel run starts
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
+    uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };
 // Bytes of the large-frame scratch for frames of n points, and its layout at base.
 uint64_t cg_large_bytes(uint32_t n_points);
 void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
 // Run n_frames frames of more than CG_MAX_POINTS points, one at a time (synchronises s).
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s);
+// The phases of cg_run_large for one frame f (also the tiles of cg_tile_*):
+//   front: meta init + pass 1 (ground-only mode: the whole ground output);
+//   decide: thresholds from meta, pass 2, candidates -> survivors (pipeline mode);
+//   backend: detector backend over meta[LG_MS] survivors + npad pads, header N = n_total, K.
+int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
+                   bool init);
+int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f);
+int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
+                     uint32_t n_total, uint32_t K);
+// A tiled frame's gathered survivors and merged counts (K, Ms, nfin, bounds keys) into S.
+int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_points, const uint32_t* d_index,
+                           uint32_t n, const uint32_t* counts, hipStream_t s);
 // The LDS backend of the frame kernel on a large frame's survivors (M <= CG_MMAX).
 int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
                             uint32_t npad, uint32_t K, hipStream_t s);

@@ -112,7 +112,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
             const uint32_t i = k * CG_BLOCK + tid;
             const float4 p = load_xyzi<LAYOUT>(fb, i, L);
             op[pos] = p;
-            oi[pos] = (uint32_t)base + i;
+            oi[pos] = S.pidx_base + (uint32_t)base + i;
             pos++;
             if (!GROUND) bd.add(p);
         }
@@ -164,7 +164,8 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
         if (i < hi) {
             pidx = S.cand_i[i];
             p = S.cand_p[i];
-            const uint32_t cc = pidx / LG_CHUNK, r = pidx % LG_CHUNK, k = r / CG_BLOCK, ln = r % CG_BLOCK;
+            const uint32_t lp = pidx - S.pidx_base;   // index within this launch's points
+            const uint32_t cc = lp / LG_CHUNK, r = lp % LG_CHUNK, k = r / CG_BLOCK, ln = r % CG_BLOCK;
             const uint32_t code = cb[(uint64_t)cc * LG_CHUNK + ((k >> 3) * CG_BLOCK + ln) * 8 + (k & 7)];
             if (code > qhi) {
                 kp = true;
@@ -687,82 +688,135 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams
     (L.cen + (uint64_t)f * L.cap)[k] = make_float2(qx, qy);
 }
 
+// Gathered survivors of a tiled frame (cg_tile_backend): meta reset, survivors copied into
+// scratch, the merged counts written where the backend reads them.
+__global__ void lg_set_counts(LgScratch S, uint32_t K, uint32_t Ms, uint32_t nfin, uint32_t b0, uint32_t b1,
+                              uint32_t b2, uint32_t b3, uint32_t b4, uint32_t b5) {
+    if (threadIdx.x != 0) return;
+    uint32_t* m = S.meta;
+    m[LG_K] = K; m[LG_MS] = Ms; m[LG_NFIN] = nfin;
+    m[LG_BMIN] = b0; m[LG_BMIN + 1] = b1; m[LG_BMIN + 2] = b2;
+    m[LG_BMAX] = b3; m[LG_BMAX + 1] = b4; m[LG_BMAX + 2] = b5;
+}
+int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_points, const uint32_t* d_index,
+                           uint32_t n, const uint32_t* c, hipStream_t s) {
+    hipError_t e;
+    hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
+    if (n) {
+        if ((e = hipMemcpyAsync(S.surv_p, d_points, (size_t)n * 16, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(S.surv_i, d_index, (size_t)n * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(lg_set_counts, dim3(1), dim3(64), 0, s, S, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Host phases (cg_run_large below, and the tiles of cg_tile_*): front, decide, backend.
+int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
+                   bool init) {
+    const uint32_t N = L.n_points;
+    const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
+    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
+    if (init) hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
+    if (nch == 0) return hipGetLastError();
+#define LG_FRONT(LAY, KM) hipLaunchKernelGGL((lg_front<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
+    if (xyzi16) {
+        if (kmode == CG_KMODE_PIPELINE) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE);
+        else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_DETECT);
+        else {
+            LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_GROUND);
+            hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_GROUND>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+            hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_XYZI16>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+        }
+    } else {
+        if (kmode == CG_KMODE_PIPELINE) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE);
+        else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_DETECT);
+        else {
+            LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_GROUND);
+            hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_GROUND>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+            hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_GENERIC>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+        }
+    }
+#undef LG_FRONT
+    return hipGetLastError();
+}
+
+int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f) {
+    const uint32_t nch = (uint32_t)(((uint64_t)L.n_points + LG_CHUNK - 1) / LG_CHUNK);
+    if (nch == 0) return hipSuccess;
+    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
+    if (xyzi16)
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+    else
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+    return hipGetLastError();
+}
+
+// Detector backend over meta[LG_MS] survivors (surv_p / surv_i, frame indices < n_total) and,
+// in pipeline mode with zero_pass, the n_total - K pads; results in frame slot f.
+int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
+                     uint32_t N, uint32_t K) {
+    hipError_t e;
+    uint32_t hm[LG_META_WORDS];
+    if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint32_t Ms = hm[LG_MS];
+    const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
+    const uint32_t Mtot = Ms + npad;
+    CgLaunch Lh = L;
+    Lh.n_points = N;   // the header's N is the whole frame's
+    if (Mtot <= CG_MMAX && !S.force_global) return cg_launch_lg_back_small(Lh, P, S, f, npad, K, s);
+    const uint32_t PB = bits_of((uint64_t)N + npad);
+    const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
+    hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad, Mtot);
+    hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
+    int buf = radix_sort(S, Mtot, 32 + PB, s);
+    const uint64_t* vkey = buf ? S.key1 : S.key0;
+    // runs over the finite points (non-finite keys sort last); passthrough: every point
+    scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
+    hipLaunchKernelGGL(lg_voxel_centroids, dim3(mb), dim3(CG_BLOCK), 0, s, Lh, S, f, Mtot, buf);
+    if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint32_t V = hm[LG_V];
+    const uint32_t VB = bits_of(V);
+    const uint32_t vb = std::max<uint32_t>(1, blocks_of(V));
+    if (V > 0) {
+        hipLaunchKernelGGL(lg_cell_keys, dim3(vb), dim3(CG_BLOCK), 0, s, S, P, V, VB);
+        const int cb = radix_sort(S, V, 30 + VB, s);
+        const uint64_t* ckey = cb ? S.key1 : S.key0;
+        scan_emit(S, V, -1, CellHead{ckey, VB}, CellEmit{ckey, VB, S.uk, S.ca}, LG_U, s);
+        hipLaunchKernelGGL(lg_cell_order, dim3(vb), dim3(CG_BLOCK), 0, s, S, V, VB, cb);
+        hipLaunchKernelGGL(lg_union, dim3((V + WAVES - 1) / WAVES), dim3(CG_BLOCK), 0, s, S, P, V);
+        hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
+        scan_emit(S, V, -1, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
+        hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
+        hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, S, f, V, VB);
+        const int kb = radix_sort(S, V, 2 * VB, s);
+        hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)V + 1)), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, kb, Mtot, K);
+        hipLaunchKernelGGL(lg_centroids, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
+    } else {
+        hipLaunchKernelGGL(lg_csr, dim3(1), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, 0, Mtot, K);
+    }
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // Host driver: one frame at a time on stream s. Synchronises twice per frame (survivor count
 // and voxel count size the backend launches).
-int cg_run_large(const CgLaunch& L0, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s) {
-    const uint32_t N = L0.n_points;
-    const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
-    const bool xyzi16 = L0.point_step == 16 && L0.off_x == 0 && L0.off_y == 4 && L0.off_z == 8 && L0.off_i == 12;
+int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s) {
+    const uint32_t N = L.n_points;
     hipError_t e;
-    uint32_t hm[LG_META_WORDS];
-    for (uint32_t f = 0; f < L0.n_frames; f++) {
-        const CgLaunch& L = L0;
-        hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
-#define LG_FRONT(LAY, KM) hipLaunchKernelGGL((lg_front<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
-#define LG_DECIDE(LAY, KM) hipLaunchKernelGGL((lg_decide<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
-        if (xyzi16) {
-            if (kmode == CG_KMODE_PIPELINE) { LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE); LG_DECIDE(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE); }
-            else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_DETECT);
-            else {
-                LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_GROUND); LG_DECIDE(CG_LAYOUT_XYZI16, CG_KMODE_GROUND);
-                hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_XYZI16>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-            }
-        } else {
-            if (kmode == CG_KMODE_PIPELINE) { LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE); LG_DECIDE(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE); }
-            else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_DETECT);
-            else {
-                LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_GROUND); LG_DECIDE(CG_LAYOUT_GENERIC, CG_KMODE_GROUND);
-                hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_GENERIC>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-            }
-        }
-#undef LG_FRONT
-#undef LG_DECIDE
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+    S.pidx_base = 0;
+    for (uint32_t f = 0; f < L.n_frames; f++) {
+        if ((e = (hipError_t)cg_large_front(L, P, kmode, S, s, f, true)) != hipSuccess) return e;
         if (kmode == CG_KMODE_GROUND) continue;
-        if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        const uint32_t K = kmode == CG_KMODE_PIPELINE ? hm[LG_K] : N;
-        const uint32_t Ms = hm[LG_MS];
-        const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
-        const uint32_t Mtot = Ms + npad;
-        if (Mtot <= CG_MMAX && !S.force_global) {
-            if ((e = (hipError_t)cg_launch_lg_back_small(L, P, S, f, npad, K, s)) != hipSuccess) return e;
-            continue;
+        if (kmode == CG_KMODE_PIPELINE && (e = (hipError_t)cg_large_decide(L, P, S, s, f)) != hipSuccess) return e;
+        uint32_t K = N;
+        if (kmode == CG_KMODE_PIPELINE) {
+            if ((e = hipMemcpyAsync(&K, S.meta + LG_K, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         }
-        // ---- global backend ----
-        const uint32_t PB = bits_of((uint64_t)N + npad);
-        const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
-        hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad, Mtot);
-        hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
-        int buf = radix_sort(S, Mtot, 32 + PB, s);
-        const uint64_t* vkey = buf ? S.key1 : S.key0;
-        // runs over the finite points (non-finite keys sort last); passthrough: every point
-        scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
-        hipLaunchKernelGGL(lg_voxel_centroids, dim3(mb), dim3(CG_BLOCK), 0, s, L, S, f, Mtot, buf);
-        if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        const uint32_t V = hm[LG_V];
-        const uint32_t VB = bits_of(V);
-        const uint32_t vb = std::max<uint32_t>(1, blocks_of(V));
-        if (V > 0) {
-            hipLaunchKernelGGL(lg_cell_keys, dim3(vb), dim3(CG_BLOCK), 0, s, S, P, V, VB);
-            const int cb = radix_sort(S, V, 30 + VB, s);
-            const uint64_t* ckey = cb ? S.key1 : S.key0;
-            scan_emit(S, V, -1, CellHead{ckey, VB}, CellEmit{ckey, VB, S.uk, S.ca}, LG_U, s);
-            hipLaunchKernelGGL(lg_cell_order, dim3(vb), dim3(CG_BLOCK), 0, s, S, V, VB, cb);
-            hipLaunchKernelGGL(lg_union, dim3((V + WAVES - 1) / WAVES), dim3(CG_BLOCK), 0, s, S, P, V);
-            hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
-            scan_emit(S, V, -1, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
-            hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
-            hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, L, S, f, V, VB);
-            const int kb = radix_sort(S, V, 2 * VB, s);
-            hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)V + 1)), dim3(CG_BLOCK), 0, s, L, S, f, VB, kb, Mtot, K);
-            hipLaunchKernelGGL(lg_centroids, dim3(vb), dim3(CG_BLOCK), 0, s, L, P, S, f);
-        } else {
-            hipLaunchKernelGGL(lg_csr, dim3(1), dim3(CG_BLOCK), 0, s, L, S, f, VB, 0, Mtot, K);
-        }
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = (hipError_t)cg_large_backend(L, P, kmode, S, s, f, N, K)) != hipSuccess) return e;
     }
     return hipSuccess;
 }

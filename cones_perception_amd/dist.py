@@ -46,3 +46,118 @@ def gather_headers(headers, dst: int = 0):
     bufs = [torch.empty_like(headers) for _ in range(ws)] if dist.get_rank() == dst else None
     dist.gather(headers, bufs, dst=dst)
     return torch.cat(bufs, 0) if bufs is not None else None
+
+
+# ---------------------------------------------------------------------------------------------
+# C5: one large frame tiled across ranks (include/cones_gpu.h, cg_tile_*). Tiles are contiguous
+# point-index ranges; for a column-major spinning LiDAR (point = column * rings + ring) a range
+# is an azimuth wedge, i.e. a spatial tile. The exchange steps are two small all-reduces (the
+# 18 sector-minimum keys with the used-bin mask, then counts and VoxelGrid bounds) and one
+# gather of the survivors (a few percent of the points) to the rank that runs the backend.
+
+def tile_range(n_total: int, rank: int, world_size: int):
+    """Points [lo, hi) of rank's tile."""
+    per = (n_total + world_size - 1) // world_size
+    lo = min(n_total, rank * per)
+    return lo, min(n_total, lo + per)
+
+
+def _distributed() -> bool:
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _coll_device(device):
+    """Collectives run on the GPU under RCCL ("nccl") and on the host under gloo."""
+    return device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def merge_tile_keys(keys, device):
+    """keys: uint32[19] of this rank -> merged uint32[19]: words 0-17 MIN (order-preserving
+    sector-minimum keys), word 18 bitwise OR of the used-bin masks. One MIN all-reduce: RCCL
+    has no bitwise reduction, and OR over ranks of a bit is -MIN(-bit)."""
+    import numpy as np
+    if not _distributed():
+        return np.asarray(keys, np.uint32).copy()
+    cd = _coll_device(device)
+    v = np.empty(18 + 32, np.int64)
+    v[:18] = np.asarray(keys[:18], np.int64)
+    v[18:] = -((int(keys[18]) >> np.arange(32)) & 1)
+    t = torch.from_numpy(v).to(cd)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    r = t.cpu().numpy()
+    out = np.zeros(19, np.uint32)
+    out[:18] = r[:18].astype(np.uint32)
+    out[18] = int(sum(1 << b for b in range(32) if r[18 + b] < 0))
+    return out
+
+
+def merge_tile_counts(counts, device, per_rank: bool = False):
+    """counts: uint32[9] (K, survivors, finite survivors, bounds-min keys x3, bounds-max keys x3)
+    -> merged: SUM, SUM, SUM, MIN x3, MAX x3. One all-gather, reduced on the host; with
+    per_rank, also every rank's survivor count (the sizes gather_survivors needs)."""
+    import numpy as np
+    if not _distributed():
+        out = np.asarray(counts, np.uint32).copy()
+        return (out, [int(out[1])]) if per_rank else out
+    cd = _coll_device(device)
+    ws = dist.get_world_size()
+    t = torch.from_numpy(np.asarray(counts, np.int64).copy()).to(cd)
+    parts = [torch.empty_like(t) for _ in range(ws)]
+    dist.all_gather(parts, t)
+    c = torch.stack(parts).cpu().numpy()
+    out = np.concatenate([c[:, :3].sum(0), c[:, 3:6].min(0), c[:, 6:9].max(0)]).astype(np.uint32)
+    return (out, [int(x) for x in c[:, 1]]) if per_rank else out
+
+
+def gather_survivors(points, index, device, dst: int = 0, sizes=None):
+    """Gather every rank's survivors ((n, 4) float32 and (n,) int32, any n) to dst as one
+    concatenation in rank order (the backend does not depend on the order). Others get None.
+    The index rides as a fifth float32 column (bit-cast), so it is one all-gather when `sizes`
+    (every rank's n, from merge_tile_counts(per_rank=True)) is known, two otherwise."""
+    if not _distributed():
+        return points.to(device).contiguous(), index.to(device).contiguous()
+    cd = _coll_device(device)
+    ws = dist.get_world_size()
+    if sizes is None:
+        n = torch.tensor([points.shape[0]], dtype=torch.int64, device=cd)
+        parts = [torch.zeros_like(n) for _ in range(ws)]
+        dist.all_gather(parts, n)
+        sizes = [int(x.item()) for x in parts]
+    m = max(1, max(sizes))
+    rows = torch.zeros((m, 5), dtype=torch.float32, device=cd)
+    k = points.shape[0]
+    rows[:k, :4] = points.to(cd)
+    rows[:k, 4] = index.to(cd).view(torch.float32)
+    parts = [torch.empty_like(rows) for _ in range(ws)]
+    dist.all_gather(parts, rows)
+    if dist.get_rank() != dst:
+        return None, None
+    allr = torch.cat([parts[r][: sizes[r]] for r in range(ws)], 0).to(device)
+    return allr[:, :4].contiguous(), allr[:, 4].contiguous().view(torch.int32)
+
+
+def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, device, point_step: int = 16,
+                    offsets=(0, 4, 8, 12), dst: int = 0):
+    """Pipeline one frame of n_total points whose points [first, first + n) are at d_tile_ptr
+    on this rank's GPU. `engine` is a cones_perception_amd.BatchEngine (the handle). Returns the
+    frame's Detection on dst (bit-identical to the single-GPU call on the whole frame)."""
+    import ctypes as C
+    import numpy as np
+    from . import _abi
+    lib, h = _abi.lib(), engine.handle
+    t = _abi.cg_tile(d_tile_ptr, first, n, n_total, point_step, *offsets)
+    keys = np.zeros(_abi.CG_TILE_KEYS, np.uint32)
+    _abi.check(lib.cg_tile_front(h, C.byref(t), keys.ctypes.data))
+    merged = merge_tile_keys(keys, device)
+    counts = np.zeros(_abi.CG_TILE_COUNTS, np.uint32)
+    _abi.check(lib.cg_tile_decide(h, merged.ctypes.data, counts.ctypes.data))
+    ns = int(counts[1])
+    sp = torch.empty((max(ns, 1), 4), dtype=torch.float32, device=device)
+    si = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
+    _abi.check(lib.cg_tile_survivors(h, sp.data_ptr(), si.data_ptr(), sp.shape[0]))
+    total, sizes = merge_tile_counts(counts, device, per_rank=True)
+    gp, gi = gather_survivors(sp[:ns], si[:ns], device, dst, sizes=sizes)
+    if _distributed() and dist.get_rank() != dst:
+        return None
+    _abi.check(lib.cg_tile_backend(h, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]), total.ctypes.data, n_total))
+    return engine.fetch(0)

@@ -164,6 +164,32 @@ int cg_batch_results_get(cg_handle* h, cg_batch_results* out);
 /* Synchronise the batch stream and copy one frame's results to handle-owned host buffers. */
 int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out);
 
+/* ---- one large frame tiled across ranks (C5; one process per GPU) ----------------------- */
+/* A rank's tile: points [first, first + n) of a frame of n_total points, in device memory
+ * (d_data = the tile's first point). Pipeline semantics (ground removal + detector), results
+ * bit-identical to the single-GPU call on the whole frame. Protocol per frame:
+ *   1. cg_tile_front on every rank -> keys; merge across ranks: words 0-17 MIN (sector-minimum
+ *      keys, order-preserving), word 18 bitwise OR (sector bins holding points);
+ *   2. cg_tile_decide with the merged keys -> counts; merge: K, survivors, finite survivors SUM,
+ *      words 3-5 MIN (bounds minimum keys), words 6-8 MAX (bounds maximum keys);
+ *   3. cg_tile_survivors copies the rank's survivors (x,y,z,i float4 + frame index) out; the
+ *      survivors of all ranks are gathered (any order) on one rank, which runs
+ *   4. cg_tile_backend with the merged counts; results as frame 0 of cg_batch_results_get /
+ *      cg_batch_fetch. Calls synchronise the handle's stream. */
+typedef struct cg_tile {
+    const void* d_data;
+    uint32_t first, n, n_total;
+    uint32_t point_step;
+    int32_t  off_x, off_y, off_z, off_intensity;
+} cg_tile;
+#define CG_TILE_KEYS   19
+#define CG_TILE_COUNTS 9
+int cg_tile_front(cg_handle* h, const cg_tile* t, uint32_t* keys);
+int cg_tile_decide(cg_handle* h, const uint32_t* merged_keys, uint32_t* counts);
+int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t capacity);
+int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index, uint32_t n_survivors,
+                    const uint32_t* merged_counts, uint32_t n_total);
+
 /* ---- device self-checks (tests) ------------------------------------------------------ */
 /* Evaluate the device atan2f / sector / sqrt restatements on n host inputs (device round
  * trip), for comparison with the host libm in tests. */
