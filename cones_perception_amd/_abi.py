@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libcones_gpu.so")
+# CONES_GPU_LIB: an alternative build of the same library (tools/build_variant.sh experiments)
+LIB_PATH = os.environ.get("CONES_GPU_LIB") or os.path.join(_HERE, "lib", "libcones_gpu.so")
 
 CG_OK, CG_E_INVALID, CG_E_DEVICE, CG_E_OOM, CG_E_CAPACITY = 0, 1, 2, 3, 4
 CG_F_VOXEL_PASSTHROUGH, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL = 0x1, 0x2, 0x4

@@ -76,6 +76,8 @@ int prepare(const cg_params& p, CgDevParams& d) {
     const double ntheta = -p.angle_threshold * M_PI / 180;
     d.ang_lo = cg_floor_to_float(ntheta);
     d.ang_hi = cg_ceil_to_float(theta);
+    d.ang_cert_hi = cg_ceil_to_float((double)d.ang_hi + (double)CG_ANG_MARGIN);
+    d.ang_cert_lo = cg_floor_to_float((double)d.ang_hi - (double)CG_ANG_MARGIN);
     // pcl::VoxelGrid::setLeafSize(float, float, float): inverse = 1.0f / leaf
     d.inv_leaf[0] = 1.0f / (float)p.voxel_filter_leaf_size_x;
     d.inv_leaf[1] = 1.0f / (float)p.voxel_filter_leaf_size_y;
@@ -89,7 +91,8 @@ int prepare(const cg_params& p, CgDevParams& d) {
     d.min_cl = (uint32_t)p.min_cluster_size;
     d.max_cl = (uint32_t)p.max_cluster_size;
     d.ext = p.cone_position_extension_length;
-    // float certificates for the distance compares: |fl((x^2+y^2)+z^2) - S| <= 4 ulp(S)
+    // float certificates for the distance compares: the device's fma(x,x,fma(y,y,z*z)) is
+    // within 3 roundings (2e-7 relative) of S, far inside the 1e-6 slack
     d.sfar_lo = cg_floor_to_float(d.s_far * (1.0 - 1e-6));
     d.sfar_hi = cg_ceil_to_float(d.s_far * (1.0 + 1e-6));
     d.snear_lo = cg_floor_to_float(d.s_near * (1.0 - 1e-6));
@@ -97,9 +100,9 @@ int prepare(const cg_params& p, CgDevParams& d) {
     // z-code window: every sector threshold is ceil(low + 0.1) with low <= default_lowest_point,
     // so thresholds lie at or below T_max; codes resolve 1/64 m over ~4 m below it
     const float tmax = cg_ceil_to_float((double)p.default_lowest_point + 0.1);
-    d.zq_scale = 64.0f;
-    d.zq_z0 = (tmax == tmax && std::isfinite(tmax)) ? tmax - 254.0f / 64.0f : 0.0f;
-    d.zq_bias = -d.zq_z0 * d.zq_scale;
+    // (descending code: T_max codes 1, so a NaN z, coded 0, is below qlo whenever it can be)
+    d.zq_z0 = (tmax == tmax && std::isfinite(tmax)) ? tmax : 0.0f;
+    d.zq_bias = 64.0f * d.zq_z0 + 1.0f;
     // does PointXYZI() (0,0,0) survive filter_points_position?
     const float a0 = cg_atan2f(0.0f, 0.0f);
     const double S0 = 0.0;

@@ -235,7 +235,7 @@ __device__ __forceinline__ float4 load_xyzi(const uint8_t* fb, uint32_t i, const
 // Fast form: decides from the float sum alone; returns false (uncertain) when only the
 // exact double S can decide.
 __device__ __forceinline__ bool dist_level_fast(const CgDevParams& P, float x, float y, float z, bool& rm) {
-    const float sf = (x * x + y * y) + z * z;
+    const float sf = fmaf(x, x, fmaf(y, y, z * z));   // a certificate only: 3 roundings
     const bool far_c = sf > P.sfar_hi, nfar_c = sf < P.sfar_lo;
     const bool near_c = sf < P.snear_lo, nnear_c = sf > P.snear_hi;
     rm = (z < P.level_f) | far_c | near_c;
@@ -252,12 +252,10 @@ __device__ __forceinline__ bool dist_level_remove(const CgDevParams& P, float x,
 
 // Certified angle classification: sector (src/ground_removal.cpp:61-64) and the angle part of
 // filter_points_position (src/cone_detection.cpp:200-201) from a cheap atan2 approximation
-// (|error| < 1.5e-6 rad incl. glibc's own error; checked on device by cg_selftest_atan2f)
+// (|error| < 2.3e-6 rad incl. glibc's own error; checked on device by cg_selftest_atan2f)
 // whenever the approximation lies more than CG_ANG_MARGIN from every sector boundary and both
 // angle thresholds. Otherwise the exact glibc restatement decides. Both decisions are
 // monotone step functions of the float angle, so equal classes at a - E and a + E certify.
-#define CG_ANG_MARGIN 8.0e-6f
-#define CG_SEC_MARGIN_T 2.0e-5f
 // The exact restatement, for the rare points the fast classification cannot certify. Inlined
 // into those (cold) branches: an out-of-line call from inside divergent loops corrupted the
 // caller's per-lane state under some schedules (lanes that took the call lost their keep bits
@@ -276,37 +274,40 @@ __device__ __forceinline__ bool classify_angle_fast(const CgDevParams& P, float 
     const float r = mn * __builtin_amdgcn_rcpf(mx);
     const float q = r * r;
     // (explicit FMAs: this is our approximation, not a reference expression)
-    float p = 0.006811763625591993f;
-    p = fmaf(p, q, -0.03360414505004883f);
-    p = fmaf(p, q, 0.07962361723184586f);
-    p = fmaf(p, q, -0.1323334127664566f);
-    p = fmaf(p, q, 0.19807817041873932f);
-    p = fmaf(p, q, -0.3331736922264099f);
-    p = fmaf(p, q, 0.9999961256980896f);
-    float a = r * p;
-    if (by > bx) a = 1.5707964f - a;
-    if (x < 0.f) a = 3.1415927f - a;
-    if (y < 0.f) a = -a;
-    // off-axis, not NaN (fmaxf/fminf drop NaN), and inside the range where v_rcp_f32(mx) is
-    // a normal number (mx < 2^126) and r does not underflow badly
-    bool ok = (x == x) & (y == y) & (mn > 1.0e-30f) & (mx < 8.0e37f);
+    // (6-term fit of atan(r)/r in r^2 on [0, 1]: 1.7e-6 rad; tools/ has no generator, the
+    // bound is checked on device by cg_selftest_atan2f across every decision boundary)
+    float p = -0.011719568632543087f;
+    p = fmaf(p, q, 0.05264842137694359f);
+    p = fmaf(p, q, -0.11642742902040482f);
+    p = fmaf(p, q, 0.19354073703289032f);
+    p = fmaf(p, q, -0.3326228857040405f);
+    p = fmaf(p, q, 0.9999772310256958f);
+    float aa = r * p;                        // |a|
+    if (by > bx) aa = 1.5707964f - aa;
+    if (x < 0.f) aa = 3.1415927f - aa;
+    const bool yneg = y < 0.f;               // a = yneg ? -aa : aa
+    // off-axis, not NaN, and inside the range where v_rcp_f32(mx) is a normal number
+    // (mx < 2^126) and r does not underflow badly. A NaN x or y has the largest magnitude bit
+    // pattern, so mx is NaN and fails mx < 8e37.
+    bool ok = (mn > 1.0e-30f) & (mx < 8.0e37f);
     if (NEED_SECTOR) {
         // t ~ wrap(a) / sector: the reference floors fl(fl(wrap(ae)) / SEC) (cg_sector). With
-        // |a - ae| <= 1.5e-6 rad, |t - wrap(ae)/SEC| <= 7.9e-6 (3.9e-6 from the angle, the rest
+        // |a - ae| <= 2.3e-6 rad, |t - wrap(ae)/SEC| <= 1.0e-5 (6.0e-6 from the angle, the rest
         // from the roundings of both wraps, 1/SEC, 2pi/SEC, this fma and the reference's
         // division), so a fractional part farther than CG_SEC_MARGIN_T from an integer certifies
         // the bin. Near a = 0 the two wraps may disagree: |a| > CG_ANG_MARGIN certifies the sign.
-        const float t = fmaf(a, 1.0f / CG_SECTOR_ANGLE_RAD, a < 0.f ? 6.2831855f / CG_SECTOR_ANGLE_RAD : 0.f);
-        const float fl = floorf(t);
-        ok = ok & (fabsf((t - fl) - 0.5f) < 0.5f - CG_SEC_MARGIN_T) & (fabsf(a) > CG_ANG_MARGIN);
-        sector = (int)fl;   // <= 16: t <= 2pi / SEC + rounding = 16.37
+        // fma(-aa, 1/SEC, c) == fma(aa, -1/SEC, c) exactly; t >= 0, so trunc is floor and
+        // v_fract_f32 is t - floor(t) exactly.
+        const float t = fmaf(aa, yneg ? -1.0f / CG_SECTOR_ANGLE_RAD : 1.0f / CG_SECTOR_ANGLE_RAD,
+                             yneg ? 6.2831855f / CG_SECTOR_ANGLE_RAD : 0.f);
+        ok = ok & (fabsf(__builtin_amdgcn_fractf(t) - 0.5f) < 0.5f - CG_SEC_MARGIN_T) & (aa > CG_ANG_MARGIN);
+        sector = (int)t;   // <= 16: t <= 2pi / SEC + rounding = 16.37
     }
     if (NEED_ANGLE) {
         // ang_lo == -ang_hi exactly (cg_api.cpp prepare), so a <= ang_lo || a >= ang_hi is
         // |a| >= ang_hi (NaN thresholds: false either way)
-        const float aa = fabsf(a);
-        ang_rm = aa >= P.ang_hi;
-        ok = ok & (fabsf(aa - P.ang_hi) > CG_ANG_MARGIN);
+        ang_rm = aa >= P.ang_cert_hi;
+        ok = ok & (ang_rm | (aa < P.ang_cert_lo));
     }
     return ok;
 }
@@ -357,13 +358,23 @@ struct LaneBits {
     }
 };
 
-// 8-bit monotone z code: q(z) = trunc(clamp(fl(z * 64 + b), 0, 255)), NaN -> 255, b = -64 z0.
-// Any monotone non-decreasing q serves: for any T, q(z) < q(T) implies z < T and q(z) > q(T)
-// implies z > T; equal codes are ambiguous. Thresholds are coded by this same function.
-__device__ __forceinline__ uint32_t zcode(float z, const CgDevParams& P) {
-    const float q = __builtin_amdgcn_fmed3f(fmaf(z, P.zq_scale, P.zq_bias), 0.f, 255.f);
-    return z == z ? (uint32_t)q : 255u;
+// 8-bit z code, monotone NON-INCREASING in z: d(z) = sat_u8(rne(fl(zq_bias - 64 z))), one
+// v_cvt_pk_u8_f32 (round to nearest even, saturating to [0, 255], NaN -> 0; measured by
+// tools/isa_probe.hip) that also packs the byte into its code word. For any threshold T:
+// d(z) > d(T) implies z < T, and d(z) < d(T) implies !(z < T); equal codes are ambiguous.
+// A NaN z codes 0, the "above every threshold" end, where z < T is false too. Thresholds are
+// coded by this same function, so the rounding and the window (zq_bias) only decide how many
+// points are ambiguous, never a result.
+#define CG_ZQ_SCALE (-64.0f)
+__device__ __forceinline__ uint32_t zcode_into(float z, float zq_bias, uint32_t byte, uint32_t word) {
+    return __builtin_amdgcn_cvt_pk_u8_f32(fmaf(z, CG_ZQ_SCALE, zq_bias), byte, word);
 }
+__device__ __forceinline__ uint32_t zcode(float z, const CgDevParams& P) { return zcode_into(z, P.zq_bias, 0u, 0u); }
+// Pass-2 classes of a point's code c against the band [qlo, qhi] = [min, max] of the used
+// sectors' threshold codes: kept in every sector if c < qlo, ground in every sector if c > qhi,
+// otherwise ambiguous (exact re-read).
+__device__ __forceinline__ bool zc_kept(uint32_t c, uint32_t qlo) { return c < qlo; }
+__device__ __forceinline__ bool zc_not_ground(uint32_t c, uint32_t qhi) { return c <= qhi; }
 
 
 // ------------------------------------------------------------------------------------------
@@ -397,6 +408,10 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
     float cur_m = INFINITY;      // minimum z of the lane's current run of sector cur_s
     touched = 0;                 // sector bins this lane saw (bit 17: NaN angle)
     const uint32_t nlast = N ? N - 1 : 0u;
+    // the z-code bias as a loop-invariant VGPR (v_fmamk takes it from a VGPR only; left to
+    // itself the compiler re-materialises it from its SGPR once per point)
+    float zbias = P.zq_bias;
+    asm volatile("" : "+v"(zbias));
     auto load_group = [&](float3* buf, int g) {
 #pragma unroll
         for (int j = 0; j < G; j++)
@@ -418,14 +433,18 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
             }
             runc = shl1_add_if(runc, !ok);
             if (GROUND) {
-                if (j < 4) clo |= zcode(z, P) << (8 * j);
-                else chi |= zcode(z, P) << (8 * (j - 4));
-                // run-length sector minimum: an uncertain point or a NaN z continues the run
-                // with +inf; a sector change flushes the run (rare: a lane's consecutive points
+                if (j < 4) clo = zcode_into(z, zbias, j, clo);
+                else chi = zcode_into(z, zbias, j - 4, chi);
+                // materialise this point's bits now: left alone, the compiler sinks the packing
+                // below the run-flush branches and keeps every point's compare masks alive in
+                // SGPRs across them (spilled to VGPR lanes: +6 VALU per point, -6% throughput).
+                // An empty asm emits no instruction, so it hides nothing from the hazard
+                // recognizer.
+                asm volatile("" : "+v"(rpos), "+v"(runc), "+v"(clo), "+v"(chi));
+                // run-length sector minimum: an uncertain point continues the run without
+                // contributing, a NaN z never lowers it; a sector change flushes the run (rare: a lane's consecutive points
                 // are 512 apart, a few degrees of azimuth on a spinning sensor)
-                const bool good = ok & (z == z);
-                const int ss = good ? s : cur_s;
-                const float zz = good ? z : INFINITY;
+                const int ss = ok ? s : cur_s;
                 if (ss != cur_s) {
                     if (cur_m != INFINITY) {
                         atomicMin(&sec_key[cur_s], cg_fkey(cur_m));
@@ -433,7 +452,7 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
                     }
                     cur_m = INFINITY;
                 }
-                cur_m = zz < cur_m ? zz : cur_m;   // never NaN
+                if (ok & (z < cur_m)) cur_m = z;   // a NaN z never lowers it
                 cur_s = ss;
             }
         }
@@ -506,15 +525,17 @@ __device__ __forceinline__ void sector_thresholds(const uint32_t* sec_key, uint3
         const float T = cg_ceil_to_float((double)low + 0.1);
         thr[tid] = T;
         tkey[tid] = T != T ? 0u : cg_zkey(T);          // NaN threshold: nothing is below it
-        if (used) { tq = T != T ? 0u : zcode(T, P); tqmax = T != T ? 0u : tq; }
+        // a NaN threshold keeps every point (z < NaN is false): it must not make the band
+        // declare any point ground (qhi = 255) and constrains nothing on the kept side
+        if (used) { tq = T != T ? 0xffffffffu : zcode(T, P); tqmax = T != T ? 255u : tq; }
     }
     const uint32_t qlo = wave_umin(tq), qhi = wave_umax(tqmax);
     if (tid == 0) { *qlo_out = qlo; *qhi_out = qhi; }
 }
 
 // Pass 2 over the lane's PPT points: codes(g) returns the lane's code word of group g (8
-// points). Two compares per code: c > qhi keeps, qlo <= c <= qhi is ambiguous, c < qlo is
-// ground. Ambiguous points re-read x, y, z and compare exactly against their own sector's
+// points). Two compares per code (zc_kept, zc_not_ground): c < qlo keeps, qlo <= c <= qhi is
+// ambiguous, c > qhi is ground. Ambiguous points re-read x, y, z and compare exactly against their own sector's
 // threshold key. keep returns the lane's kept points (points past N excluded).
 template <int PPT, int LAYOUT, class CODES>
 __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const CgLaunch& L,
@@ -538,7 +559,7 @@ __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const 
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const uint32_t c = ((j < 4 ? cw[g].x : cw[g].y) >> (8 * (j & 3))) & 0xffu;
-            const bool kp = c > qhi, nb = c >= qlo;
+            const bool kp = zc_kept(c, qlo), nb = zc_not_ground(c, qhi);
             kr = shl1_add_if(kr, kp);
             ar = shl1_add_if(ar, nb & !kp);
         }

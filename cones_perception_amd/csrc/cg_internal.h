@@ -22,10 +22,20 @@ struct CgDevParams {
     // fast-path certificates (float bounds around the exact double thresholds): a float
     // sum of squares below *_lo / above *_hi decides the compare without the double path
     float sfar_lo, sfar_hi, snear_lo, snear_hi;
-    // 8-bit z code window for the on-chip ground decision:
-    // q(z) = trunc(clamp(fl(z * zq_scale + zq_bias), 0, 255)), zq_bias = -zq_z0 * zq_scale
-    float zq_z0, zq_scale, zq_bias;
+    // 8-bit z code window for the on-chip ground decision (cg_device.h zcode):
+    // d(z) = sat_u8(rne(fl(zq_bias - 64 z))), d(zq_z0) = 1 for the highest possible threshold
+    float zq_z0, zq_bias;
+    // angle-filter certificates: |a| >= ang_cert_hi removes and |a| < ang_cert_lo keeps for
+    // every exact angle within CG_ANG_MARGIN of the fast approximation a
+    float ang_cert_lo, ang_cert_hi;
 };
+
+// Certified fast angle classification (cg_device.h classify_angle_fast): the approximation's
+// error bound is 2.3e-6 rad (polynomial, v_rcp_f32 and roundings 2.0e-6 against the true
+// atan2, glibc's own rounding 2.4e-7); decisions are certified only farther than these
+// margins from a boundary (radians / sector units), everything else takes the exact path.
+#define CG_ANG_MARGIN 8.0e-6f
+#define CG_SEC_MARGIN_T 2.5e-5f
 
 // One batch launch: uniform frames, device-resident input and outputs.
 struct CgLaunch {
@@ -50,7 +60,9 @@ struct CgLaunch {
     uint64_t* stamps;
 };
 
+#ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
+#endif
 #define CG_MMAX 1024           // LDS-path capacity (points surviving the filter)
 #define CG_MAX_POINTS 65536    // frame kernel: 128 points per lane; larger frames: cg_large.hip
 #define CG_MAX_FRAME_POINTS (1u << 28)

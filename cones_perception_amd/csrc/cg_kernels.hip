@@ -890,13 +890,16 @@ __global__ void cg_selftest_atan2f_kernel(const float* y, const float* x, float*
     if (i < n) {
         const float a = cg_atan2f(y[i], x[i]);
         out[2 * i] = a;
-        // sector through the certified fast path (must equal the exact one)
+        // sector and angle-filter decision (|a| >= 1.3) through the certified fast path (must
+        // equal the exact ones): sector + 32 * removed
         CgDevParams P{};
-        P.ang_lo = -4.0f; P.ang_hi = 4.0f;
+        P.ang_lo = -1.3f; P.ang_hi = 1.3f;
+        P.ang_cert_lo = 1.3f - 2.0f * CG_ANG_MARGIN;   // (the host derives these in prepare)
+        P.ang_cert_hi = 1.3f + 2.0f * CG_ANG_MARGIN;
         int s = 0;
         bool rm = false;
-        classify_angle<true, false>(P, x[i], y[i], s, rm);
-        out[2 * i + 1] = (float)s;
+        classify_angle<true, true>(P, x[i], y[i], s, rm);
+        out[2 * i + 1] = (float)(s + (rm ? 32 : 0));
     }
 }
 __global__ void cg_selftest_sqrt_kernel(const double* in, double* out, uint32_t n) {

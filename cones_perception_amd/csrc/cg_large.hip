@@ -167,9 +167,9 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
             const uint32_t lp = pidx - S.pidx_base;   // index within this launch's points
             const uint32_t cc = lp / LG_CHUNK, r = lp % LG_CHUNK, k = r / CG_BLOCK, ln = r % CG_BLOCK;
             const uint32_t code = cb[(uint64_t)cc * LG_CHUNK + ((k >> 3) * CG_BLOCK + ln) * 8 + (k & 7)];
-            if (code > qhi) {
+            if (zc_kept(code, qlo)) {
                 kp = true;
-            } else if (code >= qlo) {   // ambiguous: exact sector and threshold
+            } else if (zc_not_ground(code, qhi)) {   // ambiguous: exact sector and threshold
                 int sx = 0;
                 bool unused = false;
                 classify_angle<true, false>(P, p.x, p.y, sx, unused);

@@ -192,7 +192,9 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
 
 /* ---- device self-checks (tests) ------------------------------------------------------ */
 /* Evaluate the device atan2f / sector / sqrt restatements on n host inputs (device round
- * trip), for comparison with the host libm in tests. */
+ * trip), for comparison with the host libm in tests. atan2f: out[2i] = the exact restatement,
+ * out[2i+1] = sector + 32 * (angle filter at ang_hi = 1.3 removes it), both through the
+ * certified fast classification. */
 int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out, uint32_t n);
 int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
 

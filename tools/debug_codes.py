@@ -12,10 +12,9 @@ N = raw.shape[1] // 16
 CH = 8192
 z = raw[0].view(np.float32).reshape(-1, 4)[:, 2]
 tmax = np.float32(np.float64(np.float32(-0.1)) + 0.1)   # cg_ceil_to_float, close enough here
-z0 = np.float32(tmax - np.float32(254.0 / 64.0))
-bias = np.float32(-z0 * np.float32(64.0))
-q = np.float32(z * np.float32(64.0)) + bias
-exp = np.where(np.isnan(z), 255, np.clip(q, 0, 255).astype(np.uint32)).astype(np.uint8)
+bias = np.float32(np.float32(64.0) * tmax + np.float32(1.0))
+q = bias - np.float32(64.0) * z              # descending code (cg_device.h zcode)
+exp = np.where(np.isnan(z), 0, np.clip(np.rint(q), 0, 255)).astype(np.uint8)
 # device layout: [chunk][g][lane][j], point = chunk*CH + (g*8+j)*512 + lane
 i = np.arange(N)
 c, r = i // CH, i % CH
