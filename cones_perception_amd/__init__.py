@@ -219,8 +219,20 @@ class _Handle:
         return self
 
 
+def pcl_header(header: dict) -> dict:
+    """The header after pcl::fromROSMsg then pcl::toROSMsg (pcl_conversions, PCL 1.10): the
+    stamp is carried as microseconds (toNSec() / 1000, then * 1000), so nanoseconds truncate.
+    Header dicts use the keys seq, stamp_sec, stamp_nsec, frame_id."""
+    out = dict(header)
+    if "stamp_nsec" in out:
+        out["stamp_nsec"] = int(out["stamp_nsec"]) // 1000 * 1000
+    return out
+
+
 class GroundRemover(_Handle):
-    """GroundRemover::cloud_handler (src/ground_removal.cpp:50-89) on the GPU."""
+    """GroundRemover::cloud_handler (src/ground_removal.cpp:50-89) on the GPU. The published
+    message takes toROSMsg's fields and header (set before toROSMsg, lines 83-86, and then
+    overwritten by it): PointXYZI's fields, the PCL round trip of the input header."""
 
     def cloud_handler(self, msg: PointCloud2) -> PointCloud2:
         v = msg.view(intensity_offset=msg.offset_of("intensity"))
@@ -231,7 +243,7 @@ class GroundRemover(_Handle):
         out = PointCloud2(r.width, r.height,
                           [PointField("x", 0), PointField("y", 4), PointField("z", 8),
                            PointField("intensity", 16)], 32, 32 * r.width, data, msg.is_dense,
-                          dict(msg.header))
+                          pcl_header(msg.header))
         out.n_kept = r.n_kept
         return out
 
@@ -250,6 +262,11 @@ class ConeDetector(_Handle):
         self.intensity_in_cloud_checked = False
         self.intensity_in_cloud = True
 
+    def recrop(self, centers) -> List[np.ndarray]:
+        """get_reconstructed_cone (src/cone_detection.cpp:222-238) around each (x, y) centre,
+        over the last cloud_handler call's whole cloud: one (n, 4) x,y,z,intensity array each."""
+        return _recrop(self._h, centers)
+
     def cloud_handler(self, msg: PointCloud2) -> Detection:
         if not self.intensity_in_cloud_checked:
             if not msg.has_field("intensity"):
@@ -263,6 +280,17 @@ class ConeDetector(_Handle):
         return _detection(r)
 
 
+def _recrop(h, centers) -> List[np.ndarray]:
+    cen = np.ascontiguousarray(np.asarray(centers, np.float32).reshape(-1, 2))
+    r = _abi.cg_crop_result()
+    check(lib().cg_recrop(h, cen.ctypes.data if cen.size else None, cen.shape[0], C.byref(r)))
+    n = r.n_centers
+    offs = np.ctypeslib.as_array(r.offsets, (n + 1,)).copy()
+    tot = int(offs[-1])
+    pts = np.ctypeslib.as_array(r.points, (tot * 4,)).reshape(tot, 4).copy() if tot else np.zeros((0, 4), np.float32)
+    return [pts[offs[i]:offs[i + 1]] for i in range(n)]
+
+
 class ConePipeline(ConeDetector):
     """ground_removal -> cone_detection (launch/cones_perception.launch:17-37), fused."""
     _mode = "pipeline"
@@ -273,6 +301,125 @@ class ConePipeline(ConeDetector):
         r = _abi.cg_detect_result()
         check(lib().cg_pipeline(self._h, C.byref(v), C.byref(r)))
         return _detection(r)
+
+
+# ---------------------------------------------------------------------------------------
+# The detector node after the hot path: tracking, re-crop, colour service, publication
+# (src/cone_detection.cpp:171-186, 222-363).
+UNKNOWN, YELLOW, BLUE, ORANGE = range(4)         # perception_handling::Color (color.hpp)
+CONES_TOPICS = ("cones_cloud_unknowns", "cones_cloud_yellows", "cones_cloud_blues", "cones_cloud_oranges")
+POINTXYZI_FIELDS = (("x", 0), ("y", 4), ("z", 8), ("intensity", 16))
+
+
+def to_ros_msg(xyzi: np.ndarray, header: Optional[dict] = None) -> PointCloud2:
+    """pcl::toROSMsg of a pcl::PointCloud<PointXYZI> filled by push_back (PCL 1.10): height 1,
+    width n (an empty cloud: width 0, height 1), PointXYZI's fields, point_step 32, is_dense.
+    Point bytes: x, y, z, data[3] = 1.0f, intensity, then 12 padding bytes (written as zeros;
+    the reference's are uninitialised, so only declared fields are comparable)."""
+    pts = np.asarray(xyzi, np.float32).reshape(-1, 4)
+    n = pts.shape[0]
+    buf = np.zeros((n, 8), np.float32)
+    buf[:, 0:3] = pts[:, 0:3]
+    buf[:, 3] = 1.0
+    buf[:, 4] = pts[:, 3]
+    return PointCloud2(n, 1, [PointField(a, o) for a, o in POINTXYZI_FIELDS], 32, 32 * n,
+                       buf.view(np.uint8).reshape(-1), True, dict(header or {}))
+
+
+class ConeTracker:
+    """get_centroid_clouds' frame-to-frame matching (src/cone_detection.cpp:251-339) through the
+    C-ABI tracker: match() -> statuses (colour 0..3, CG_TRACK_DROPPED, CG_TRACK_NEED_COLOR),
+    commit(colours of the NEED_COLOR centroids, or None when the service call failed),
+    clouds() -> the four colour clouds as (k, 2) x, y arrays."""
+
+    def __init__(self, classify_colors: bool = True, use_points_buffer: bool = False,
+                 cones_matching_dist_theshold: float = 0.5):
+        p = _abi.cg_track_params()
+        lib().cg_track_params_init(C.byref(p))
+        p.classify_colors = 1 if classify_colors else 0
+        p.use_points_buffer = 1 if use_points_buffer else 0
+        p.cones_matching_dist_theshold = cones_matching_dist_theshold
+        self.params = p
+        t = C.c_void_p()
+        check(lib().cg_tracker_create(C.byref(p), C.byref(t)))
+        self._t = t
+
+    def close(self):
+        if getattr(self, "_t", None):
+            lib().cg_tracker_destroy(self._t)
+            self._t = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def match(self, centroids):
+        cen = np.ascontiguousarray(np.asarray(centroids, np.float32).reshape(-1, 2))
+        st = np.zeros(max(cen.shape[0], 1), np.int32)
+        need = C.c_uint32()
+        check(lib().cg_tracker_match(self._t, cen.ctypes.data if cen.size else None, cen.shape[0],
+                                     st.ctypes.data, C.byref(need)))
+        return st[: cen.shape[0]], need.value
+
+    def commit(self, colors=None):
+        if colors is None:
+            check(lib().cg_tracker_commit(self._t, None, 0))
+        else:
+            c = np.ascontiguousarray(np.asarray(colors, np.int32).reshape(-1))
+            check(lib().cg_tracker_commit(self._t, c.ctypes.data if c.size else None, c.size))
+
+    def clouds(self) -> List[np.ndarray]:
+        out = []
+        for i in range(_abi.CG_NUM_COLORS):
+            xy = C.POINTER(C.c_float)()
+            n = C.c_uint32()
+            check(lib().cg_tracker_cloud(self._t, i, C.byref(xy), C.byref(n)))
+            out.append(np.ctypeslib.as_array(xy, (n.value * 2,)).reshape(-1, 2).copy() if n.value
+                       else np.zeros((0, 2), np.float32))
+        return out
+
+
+class ConeDetectorNode:
+    """The whole ConeDetector::cloud_handler (src/cone_detection.cpp:130-187): the hot path on the
+    GPU (cg_detect, or cg_pipeline when it stands in for the ground_removal:=true composition),
+    tracking, the re-crop of cones that need a colour, the colour service and the four published
+    clouds. `classifier(crop_msgs) -> colours or None` stands in for the ClassifyColorSrv call
+    (src/cone_detection.cpp:342-363): it receives one PointXYZI message per cone with
+    header.frame_id = cones_frame_id; None (or no classifier) is a failed call. cloud_handler
+    returns the four messages published on CONES_TOPICS, index = colour."""
+
+    def __init__(self, params=None, device: int = 0, classify_colors: bool = True, use_points_buffer: bool = False,
+                 classifier=None, cones_frame_id: str = "cloud", fused_ground_removal: bool = False):
+        self.params = params if params is not None else load_params()
+        self.detector = (ConePipeline if fused_ground_removal else ConeDetector)(self.params, device)
+        self.tracker = ConeTracker(classify_colors, use_points_buffer, self.params.cones_matching_dist_theshold)
+        self.classifier = classifier
+        self.cones_frame_id = cones_frame_id
+        self.last_detection: Optional[Detection] = None
+
+    def cloud_handler(self, msg: PointCloud2) -> List[PointCloud2]:
+        det = self.detector.cloud_handler(msg)
+        self.last_detection = det
+        status, n_need = self.tracker.match(det.centroids)
+        colors = None
+        if n_need:
+            need = det.centroids[status == _abi.CG_TRACK_NEED_COLOR]
+            crops = [to_ros_msg(c, {"frame_id": self.cones_frame_id}) for c in self.detector.recrop(need)]
+            colors = self.classifier(crops) if self.classifier is not None else None
+            if colors is not None and len(colors) != n_need:
+                colors = None
+        self.tracker.commit(colors)
+        out = []
+        for xy in self.tracker.clouds():
+            pts = np.zeros((xy.shape[0], 4), np.float32)
+            pts[:, 0:2] = xy
+            m = to_ros_msg(pts)
+            m.header = dict(msg.header)                            # line 182
+            m.fields = [PointField(f.name, f.offset, f.datatype, f.count) for f in msg.fields]   # 183
+            out.append(m)
+        return out
 
 
 class BatchEngine(_Handle):

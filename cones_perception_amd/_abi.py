@@ -92,6 +92,18 @@ class cg_tile(C.Structure):
 CG_TILE_KEYS, CG_TILE_COUNTS = 19, 9
 
 
+class cg_crop_result(C.Structure):
+    _fields_ = [("n_centers", C.c_uint32), ("offsets", C.POINTER(C.c_uint32)), ("points", C.POINTER(C.c_float))]
+
+
+class cg_track_params(C.Structure):
+    _fields_ = [("classify_colors", C.c_uint8), ("use_points_buffer", C.c_uint8),
+                ("cones_matching_dist_theshold", C.c_double)]
+
+
+CG_NUM_COLORS, CG_TRACK_DROPPED, CG_TRACK_NEED_COLOR = 4, -1, -2
+
+
 class cg_synth_cfg(C.Structure):
     _fields_ = [
         ("rings", C.c_uint32), ("cols", C.c_uint32),
@@ -127,6 +139,15 @@ _SIGS = {
     "cg_debug_large_meta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_debug_large_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "cg_debug_stamps_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "cg_recrop": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(cg_crop_result)]),
+    "cg_track_params_init": (None, [C.POINTER(cg_track_params)]),
+    "cg_tracker_create": (C.c_int, [C.POINTER(cg_track_params), C.POINTER(C.c_void_p)]),
+    "cg_tracker_destroy": (C.c_int, [C.c_void_p]),
+    "cg_tracker_set_params": (C.c_int, [C.c_void_p, C.POINTER(cg_track_params)]),
+    "cg_tracker_match": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.POINTER(C.c_uint32)]),
+    "cg_tracker_commit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "cg_tracker_cloud": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.POINTER(C.c_float)),
+                                   C.POINTER(C.c_uint32)]),
     "cg_synth_default": (None, [C.POINTER(cg_synth_cfg)]),
     "cg_synth_frames": (C.c_int, [C.POINTER(cg_synth_cfg), C.c_uint64, C.c_uint32, C.c_void_p,
                                   C.c_uint64, C.c_uint32]),

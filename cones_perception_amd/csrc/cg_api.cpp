@@ -29,6 +29,13 @@ int fail(int code, const char* fmt, ...) {
     g_err = buf;
     return code;
 }
+}  // namespace
+
+// shared with the host-only translation units (cg_track.cpp)
+int cg_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+namespace {
+
 #define HIPCHK(expr)                                                                     \
     do {                                                                                 \
         hipError_t e_ = (expr);                                                          \
@@ -152,6 +159,18 @@ struct cg_handle {
     int route = 0;                // cg_debug_route
     cg_tile tile{};               // the rank's tile (cg_tile_front .. cg_tile_decide)
     bool tile_ready = false;
+    // the last single-frame call, for cg_recrop
+    bool last_single = false;
+    CgLaunch last_in{};
+    uint32_t last_k = 0;
+    uint32_t* d_seckeys = nullptr;   // 18 words per frame inside d_hdr (not owned)
+    RcBox* d_boxes = nullptr;
+    uint32_t* d_rc_cnt = nullptr;    // boxes x blocks, twice (counts, offsets)
+    size_t rc_cnt_cap = 0;
+    float4* d_rc_out = nullptr;
+    size_t rc_out_cap = 0;
+    std::vector<uint32_t> h_rc_cnt, h_rc_off;
+    std::vector<float> h_rc_pts, h_rc_dev;
     // diagnostics
     bool stamps_on = false;
     uint64_t* d_stamps = nullptr;
@@ -173,6 +192,7 @@ void free_batch(cg_handle* h) {
     (void)hipFree(h->d_idx); (void)hipFree(h->d_cen); (void)hipFree(h->d_ground); (void)hipFree(h->d_scratch);
     h->d_hdr = nullptr; h->d_vox = nullptr; h->d_lab = nullptr; h->d_offs = nullptr;
     h->d_idx = nullptr; h->d_cen = nullptr; h->d_ground = nullptr; h->d_scratch = nullptr;
+    h->d_seckeys = nullptr;
     h->cap_frames = h->cap_points = 0;
 }
 
@@ -184,7 +204,9 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     const bool had_ground = h->d_ground != nullptr || ground;
     free_batch(h);
     const uint64_t F = nf, C = np;
-    HIPCHK(hipMalloc(&h->d_hdr, F * CG_HDR_WORDS * 4));
+    // headers, then each frame's 18 final sector-minimum keys (cg_recrop of a pipeline frame)
+    HIPCHK(hipMalloc(&h->d_hdr, F * (CG_HDR_WORDS + CG_NUM_BINS + 1) * 4));
+    h->d_seckeys = h->d_hdr + F * CG_HDR_WORDS;
     HIPCHK(hipMalloc(&h->d_vox, F * C * 16));
     HIPCHK(hipMalloc(&h->d_lab, F * C * 4));
     HIPCHK(hipMalloc(&h->d_offs, F * (C + 1) * 4));
@@ -371,9 +393,14 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     rc = stage_frame(h, in, L);
     if (rc) return rc;
     fill_launch_outputs(h, L);
+    h->last_single = false;
+    if (kmode == CG_KMODE_PIPELINE) {
+        L.seckeys = h->d_seckeys;
+    }
     rc = launch_frames(h, L, kmode, h->stream);
     if (rc) return rc;
     h->last_frames = 1; h->last_points = n; h->last_mode = kmode; h->last_stream = h->stream;
+    h->last_in = L;
     if (kmode == CG_KMODE_GROUND) {
         const size_t bytes = std::max<size_t>((size_t)n * 32, 32);
         if (bytes > h->h_ground_bytes) {
@@ -392,7 +419,23 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         gres->data = h->h_ground;
         return CG_OK;
     }
-    return fetch_frame(h, h->stream, 0, dres);
+    rc = fetch_frame(h, h->stream, 0, dres);
+    if (rc) return rc;
+    h->last_k = h->h_hdr[CG_HDR_K];
+    h->last_single = true;
+    return CG_OK;
+}
+
+// get_reconstructed_cone's box (src/cone_detection.cpp:228-229) as exact float bounds:
+// (double)x <= (double)cx + (double)0.228f / 1.5  <=>  x <= floor_to_float(that double sum)
+RcBox crop_box(float cx, float cy) {
+    const double w = (double)0.228f / 1.5;   // CONE_WIDTH is a const float (line 22)
+    RcBox b;
+    b.lox = cg_ceil_to_float((double)cx - w);
+    b.hix = cg_floor_to_float((double)cx + w);
+    b.loy = cg_ceil_to_float((double)cy - w);
+    b.hiy = cg_floor_to_float((double)cy + w);
+    return b;
 }
 
 }  // namespace
@@ -452,6 +495,9 @@ int cg_destroy(cg_handle* h) {
     if (h->d_stamps) (void)hipFree(h->d_stamps);
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->d_large) (void)hipFree(h->d_large);
+    if (h->d_boxes) (void)hipFree(h->d_boxes);
+    if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);
+    if (h->d_rc_out) (void)hipFree(h->d_rc_out);
     if (h->h_stage) (void)hipHostFree(h->h_stage);
     if (h->h_ground) (void)hipHostFree(h->h_ground);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -480,6 +526,79 @@ int cg_detect(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out) {
 int cg_pipeline(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out) {
     if (!out) return fail(CG_E_INVALID, "null result");
     return run_single(h, in, CG_KMODE_PIPELINE, out, nullptr);
+}
+
+int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop_result* out) {
+    if (!h || !out || (n_centers && !centers_xy)) return fail(CG_E_INVALID, "null argument");
+    if (!h->last_single || (h->last_mode != CG_KMODE_DETECT && h->last_mode != CG_KMODE_PIPELINE))
+        return fail(CG_E_INVALID, "cg_recrop needs a preceding cg_detect or cg_pipeline call on the handle");
+    HIPCHK(hipSetDevice(h->device));
+    const bool pipe = h->last_mode == CG_KMODE_PIPELINE;
+    const CgLaunch& L = h->last_in;
+    const uint32_t N = L.n_points, nblk = cg_recrop_blocks(N);
+    const uint32_t npad = pipe ? N - h->last_k : 0u;   // the groundless cloud's PointXYZI() tail
+    h->h_rc_off.assign((size_t)n_centers + 1, 0u);
+    h->h_rc_pts.clear();
+    std::vector<RcBox> boxes(std::min<uint32_t>(n_centers, CG_RECROP_MAX_BOXES));
+    if (!h->d_boxes && n_centers) HIPCHK(hipMalloc(&h->d_boxes, CG_RECROP_MAX_BOXES * sizeof(RcBox)));
+    for (uint32_t c0 = 0; c0 < n_centers; c0 += CG_RECROP_MAX_BOXES) {
+        const uint32_t nb = std::min<uint32_t>(CG_RECROP_MAX_BOXES, n_centers - c0);
+        for (uint32_t b = 0; b < nb; b++) boxes[b] = crop_box(centers_xy[2 * (c0 + b)], centers_xy[2 * (c0 + b) + 1]);
+        const size_t ncnt = (size_t)nb * nblk;
+        if (2 * ncnt > h->rc_cnt_cap) {
+            (void)hipFree(h->d_rc_cnt);
+            h->d_rc_cnt = nullptr;
+            h->rc_cnt_cap = 0;
+            HIPCHK(hipMalloc(&h->d_rc_cnt, 2 * ncnt * 4));
+            h->rc_cnt_cap = 2 * ncnt;
+        }
+        HIPCHK(hipMemcpyAsync(h->d_boxes, boxes.data(), nb * sizeof(RcBox), hipMemcpyHostToDevice, h->stream));
+        h->h_rc_cnt.assign(ncnt, 0u);
+        if (ncnt) {
+            HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, h->d_seckeys, h->d_boxes, nb, h->d_rc_cnt, nullptr,
+                                                nullptr, false, h->stream));
+            HIPCHK(hipMemcpyAsync(h->h_rc_cnt.data(), h->d_rc_cnt, ncnt * 4, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+        }
+        // device slots: box-major, blocks in order
+        std::vector<uint32_t> off(ncnt), box_lo(nb), box_n(nb, 0u);
+        uint64_t total = 0;
+        for (size_t q = 0; q < ncnt; q++) {
+            if (q % nblk == 0) box_lo[q / nblk] = (uint32_t)total;
+            off[q] = (uint32_t)total;
+            total += h->h_rc_cnt[q];
+            box_n[q / nblk] += h->h_rc_cnt[q];
+        }
+        if (total > 0xffffffffull) return fail(CG_E_CAPACITY, "re-crop output exceeds 2^32 points");
+        h->h_rc_dev.assign((size_t)total * 4, 0.f);
+        if (total) {
+            if (total > h->rc_out_cap) {
+                (void)hipFree(h->d_rc_out);
+                h->d_rc_out = nullptr;
+                h->rc_out_cap = 0;
+                HIPCHK(hipMalloc(&h->d_rc_out, total * 16));
+                h->rc_out_cap = total;
+            }
+            HIPCHK(hipMemcpyAsync(h->d_rc_cnt + ncnt, off.data(), ncnt * 4, hipMemcpyHostToDevice, h->stream));
+            HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, h->d_seckeys, h->d_boxes, nb, nullptr,
+                                                h->d_rc_cnt + ncnt, h->d_rc_out, true, h->stream));
+            HIPCHK(hipMemcpyAsync(h->h_rc_dev.data(), h->d_rc_out, total * 16, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+        }
+        // each box: its device points in cloud order, then the zero pads if the box holds the origin
+        for (uint32_t b = 0; b < nb; b++) {
+            const size_t lo = box_lo[b], hi = lo + box_n[b];
+            h->h_rc_pts.insert(h->h_rc_pts.end(), h->h_rc_dev.begin() + 4 * lo, h->h_rc_dev.begin() + 4 * hi);
+            const RcBox& x = boxes[b];
+            if (npad && 0.f >= x.lox && 0.f <= x.hix && 0.f >= x.loy && 0.f <= x.hiy)
+                h->h_rc_pts.insert(h->h_rc_pts.end(), (size_t)npad * 4, 0.f);
+            h->h_rc_off[c0 + b + 1] = (uint32_t)(h->h_rc_pts.size() / 4);
+        }
+    }
+    out->n_centers = n_centers;
+    out->offsets = h->h_rc_off.data();
+    out->points = h->h_rc_pts.empty() ? nullptr : h->h_rc_pts.data();
+    return CG_OK;
 }
 
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
@@ -516,6 +635,7 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     rc = launch_frames(h, L, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s);
     if (rc) return rc;
     h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
+    h->last_single = false;
     return CG_OK;
 }
 
@@ -642,6 +762,7 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
     HIPCHK((hipError_t)cg_large_backend(L, h->dp, CG_KMODE_PIPELINE, S, h->stream, 0, n_total, merged_counts[0]));
     HIPCHK(hipStreamSynchronize(h->stream));
     h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
+    h->last_single = false;
     return CG_OK;
 }
 

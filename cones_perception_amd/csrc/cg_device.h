@@ -269,7 +269,6 @@ __device__ __forceinline__ bool classify_angle_fast(const CgDevParams& P, float 
     // |x|, |y| ordered as unsigned bit patterns (monotone for non-NaN; a NaN fails `ok`):
     // no IEEE canonicalisation as fmaxf / fminf would need
     const uint32_t bx = __float_as_uint(x) & 0x7fffffffu, by = __float_as_uint(y) & 0x7fffffffu;
-    const float ax = __uint_as_float(bx), ay = __uint_as_float(by);
     const float mx = __uint_as_float(max(bx, by)), mn = __uint_as_float(min(bx, by));
     const float r = mn * __builtin_amdgcn_rcpf(mx);
     const float q = r * r;

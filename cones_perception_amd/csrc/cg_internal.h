@@ -30,6 +30,9 @@ struct CgDevParams {
     float ang_cert_lo, ang_cert_hi;
 };
 
+// Sets the thread-local message cg_last_error returns; returns code.
+int cg_set_error(int code, const char* msg);
+
 // Certified fast angle classification (cg_device.h classify_angle_fast): the approximation's
 // error bound is 2.3e-6 rad (polynomial, v_rcp_f32 and roundings 2.0e-6 against the true
 // atan2, glibc's own rounding 2.4e-7); decisions are certified only farther than these
@@ -58,6 +61,8 @@ struct CgLaunch {
     uint64_t scratch_stride;
     // diagnostics: per-workgroup phase timestamps (16 slots per frame) or null
     uint64_t* stamps;
+    // per-frame final sector-minimum keys (18 words) for cg_recrop, or null (ground modes)
+    uint32_t* seckeys;
 };
 
 #ifndef CG_BLOCK
@@ -122,5 +127,16 @@ int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScr
 uint64_t cg_scratch_bytes(uint32_t n_points);
 // Enqueue the batch kernel. Returns a hipError_t.
 int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
+// Cone re-crop (cg_recrop.hip): exact float form of the reference's double box compares.
+struct RcBox { float lox, hix, loy, hiy; };
+#define CG_RECROP_MAX_BOXES 256   // boxes per launch (more: several launches)
+uint32_t cg_recrop_blocks(uint32_t n_points);
+// write = false: cnt[b * blocks + blk] = points of block blk in box b; write = true: out at
+// off[b * blocks + blk] + in-block rank. pipeline: only groundless-cloud points (d_seckeys =
+// the frame's 18 sector-minimum keys).
+int cg_launch_recrop(const CgLaunch& L, const CgDevParams& P, bool pipeline, const uint32_t* d_seckeys,
+                     const RcBox* d_boxes, uint32_t nb, uint32_t* d_cnt, const uint32_t* d_off, float4* d_out,
+                     bool write, hipStream_t s);
+
 int cg_launch_selftest_atan2f(const float* y, const float* x, float* out, uint32_t n, hipStream_t s);
 int cg_launch_selftest_sqrt(const double* in, double* out, uint32_t n, hipStream_t s);

@@ -572,7 +572,6 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
 template <int PPT, int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
     constexpr int G = 8;                          // points per load group (double-buffered)
-    constexpr int NG = PPT / G;
     constexpr int NW = (PPT + 63) / 64;
     static_assert(PPT % (2 * G) == 0, "PPT must be a multiple of two load groups");
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
@@ -619,8 +618,10 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     }
     __syncthreads();
     STAMP(1);
-    if (GROUND && tid < 64)
+    if (GROUND && tid < 64) {
         sector_thresholds(fs->sec_key, fs->scal[S_TOUCHED], P, fs->thr, fs->tkey, &fs->scal[S_TKMIN], &fs->scal[S_TKMAX]);
+        if (L.seckeys && tid <= CG_NUM_BINS) L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = fs->sec_key[tid];
+    }
     __syncthreads();
     STAMP(2);
 

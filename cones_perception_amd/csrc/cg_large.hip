@@ -810,6 +810,10 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
     for (uint32_t f = 0; f < L.n_frames; f++) {
         if ((e = (hipError_t)cg_large_front(L, P, kmode, S, s, f, true)) != hipSuccess) return e;
         if (kmode == CG_KMODE_GROUND) continue;
+        if (kmode == CG_KMODE_PIPELINE && L.seckeys &&
+            (e = hipMemcpyAsync(L.seckeys + (uint64_t)f * (CG_NUM_BINS + 1), S.meta + LG_SECKEY,
+                                (CG_NUM_BINS + 1) * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return e;
         if (kmode == CG_KMODE_PIPELINE && (e = (hipError_t)cg_large_decide(L, P, S, s, f)) != hipSuccess) return e;
         uint32_t K = N;
         if (kmode == CG_KMODE_PIPELINE) {

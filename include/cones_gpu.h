@@ -190,6 +190,52 @@ int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t
 int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index, uint32_t n_survivors,
                     const uint32_t* merged_counts, uint32_t n_total);
 
+/* ---- detector node after the hot path (src/cone_detection.cpp:171-186, 222-339) -------- */
+/* Cone re-crop, ConeDetector::get_reconstructed_cone (src/cone_detection.cpp:222-238): for each
+ * cone centre (x, y), every point of the last single-frame call's detector input (the "whole
+ * cloud" get_centroid_clouds receives: the cg_detect input after decoding, or the groundless
+ * cloud of a cg_pipeline call, zero pads included) with
+ *     cx - 0.228f/1.5 <= x <= cx + 0.228f/1.5  and the same in y   (double compares),
+ * in cloud order, as x, y, z, intensity. This is what the colour classifier receives.
+ * Arrays are library-owned, valid until the next call on the handle. */
+typedef struct cg_crop_result {
+    uint32_t n_centers;
+    const uint32_t* offsets;  /* n_centers + 1 */
+    const float*    points;   /* offsets[n_centers] x 4 */
+} cg_crop_result;
+int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop_result* out);
+
+/* Tracking and the four colour clouds, ConeDetector::get_centroid_clouds
+ * (src/cone_detection.cpp:251-339). Host code; no device. One frame is two calls, split where
+ * the reference calls the colour service (src/cone_detection.cpp:320-327):
+ *   cg_tracker_match  with the frame's centroids in cluster order (cg_detect_result.centroids):
+ *                     status[c] = CG_TRACK_DROPPED (not published: no previous frame, or no
+ *                     previous cone within cones_matching_dist_theshold while
+ *                     use_points_buffer), a colour 0..3 (published in that cloud: colour known
+ *                     from the previous frame, or 0 = unknown when classify_colors is off), or
+ *                     CG_TRACK_NEED_COLOR (re-crop with cg_recrop and classify);
+ *   cg_tracker_commit with the classifier's colours for the CG_TRACK_NEED_COLOR centroids in
+ *                     order (NULL: the service call failed, all unknown); builds the clouds in
+ *                     the reference's push order and rolls the previous-frame state.
+ * cg_tracker_cloud then returns colour cloud `color` as (x, y) pairs (z = 0, intensity = 0):
+ * the points the node publishes on cones_topics[color] (src/cone_detection.cpp:46-49). */
+#define CG_NUM_COLORS        4     /* perception_handling::Color: unknown, yellow, blue, orange */
+#define CG_TRACK_DROPPED    (-1)
+#define CG_TRACK_NEED_COLOR (-2)
+typedef struct cg_track_params {
+    uint8_t classify_colors;              /* ~classify_colors: node default 1, launch files 0 */
+    uint8_t use_points_buffer;            /* ~use_points_buffer: node default 0, launch files 1 */
+    double  cones_matching_dist_theshold; /* default 0.5 */
+} cg_track_params;
+typedef struct cg_tracker cg_tracker;
+void cg_track_params_init(cg_track_params* p);   /* the node's class-member defaults */
+int  cg_tracker_create(const cg_track_params* p, cg_tracker** out);
+int  cg_tracker_destroy(cg_tracker* t);
+int  cg_tracker_set_params(cg_tracker* t, const cg_track_params* p);
+int  cg_tracker_match(cg_tracker* t, const float* centroids_xy, uint32_t n, int32_t* status, uint32_t* n_need);
+int  cg_tracker_commit(cg_tracker* t, const int32_t* colors, uint32_t n_colors);
+int  cg_tracker_cloud(const cg_tracker* t, int color, const float** xy, uint32_t* n);
+
 /* ---- device self-checks (tests) ------------------------------------------------------ */
 /* Evaluate the device atan2f / sector / sqrt restatements on n host inputs (device round
  * trip), for comparison with the host libm in tests. atan2f: out[2i] = the exact restatement,

@@ -16,6 +16,9 @@
 //   clustering        pcl::extractEuclideanClusters + KdTreeFLANN     called src/cone_detection.cpp:206-220
 //   cluster order     std::sort(clusters.rbegin(), rend(), size<)     (EuclideanClusterExtraction::extract)
 //   centroid          ConeDetector::get_centroid_clouds (centroid)    src/cone_detection.cpp:261-279
+//   re-crop           ConeDetector::get_reconstructed_cone            src/cone_detection.cpp:222-238
+//   tracking          ConeDetector::get_centroid_clouds (matching)    src/cone_detection.cpp:251-339
+//                     with the colour service as a callback           src/cone_detection.cpp:342-363
 // libm calls (atan2f, sqrt, pow, floorf) go to the host glibc, as in the reference build.
 // Compiled with -O2 -ffp-contract=off and no -march flags (a stock x86-64 Noetic build has no
 // FMA). Defined divergences from the reference's undefined behaviour:
@@ -30,6 +33,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <vector>
 
 namespace {
@@ -374,9 +378,154 @@ void detect(std::vector<Pt>& cloud, bool is_dense, const Params& prm, int order,
     o.offsets[clusters.size()] = off;
 }
 
+// ---------------- detector node after the hot path ----------------
+// ConeDetector::get_reconstructed_cone (src/cone_detection.cpp:222-238): the whole cloud's
+// points within CONE_WIDTH / 1.5 of the centre in x and in y, double compares, in cloud order.
+const float kConeWidth = 0.228;   // src/cone_detection.cpp:22
+
+std::vector<Pt> reconstructed_cone(const Pt& centre, const std::vector<Pt>& whole) {
+    const double half = kConeWidth / 1.5;
+    std::vector<Pt> crop;
+    for (const Pt& q : whole) {
+        const bool in_x = centre.x + half >= q.x && centre.x - half <= q.x;
+        const bool in_y = centre.y + half >= q.y && centre.y - half <= q.y;
+        if (!(in_x && in_y)) continue;
+        Pt r;   // a fresh PointXYZI with the four fields copied
+        r.x = q.x; r.y = q.y; r.z = q.z; r.intensity = q.intensity;
+        crop.push_back(r);
+    }
+    return crop;
+}
+
+// The whole cloud get_centroid_clouds receives (input_cloud_copy, src/cone_detection.cpp:158):
+// the decoded detector input; for the fused pipeline, the ground node's output.
+std::vector<Pt> whole_cloud(const View& v, int mode, const Params& prm) {
+    std::vector<Pt> cloud = decode(v);
+    if (mode == 0) ground_remove(cloud, prm);
+    return cloud;
+}
+
+// One colour per crop from the test's stand-in for the colour service; a negative answer
+// fails the whole (single) service call, leaving every colour unknown (lines 321, 359).
+typedef int (*ClassifyFn)(void* ctx, const float* xyzi, uint32_t n);
+
+// ConeDetector's tracking state (src/cone_detection.cpp:60-63): null until the first frame.
+struct Node {
+    bool classify_colors = true, use_points_buffer = false;
+    double matching = 0.5;
+    std::unique_ptr<std::vector<Pt>> prev_detected;
+    std::unique_ptr<std::vector<Pt>> prev_clouds[4];
+};
+
+bool matches(const Node& nd, const Pt& a, const Pt& b) {
+    return euclidan_dist(a.x, a.y, a.z, b.x, b.y, b.z) < nd.matching;
+}
+
+// get_centroid_clouds (src/cone_detection.cpp:251-339) after the centroid arithmetic: the
+// centroids arrive in cluster order; clouds[i] receives what cones_pubs[i] publishes.
+void centroid_clouds(Node& nd, const std::vector<Pt>& whole, const float* cen, uint32_t n, ClassifyFn classify,
+                     void* ctx, std::vector<Pt> clouds[4]) {
+    auto current = std::make_unique<std::vector<Pt>>();
+    std::vector<std::vector<Pt>> to_classify;
+    std::vector<Pt> to_classify_centroids;
+    for (uint32_t c = 0; c < n; c++) {
+        Pt p;
+        p.x = cen[2 * c]; p.y = cen[2 * c + 1]; p.z = 0.0f;
+        current->push_back(p);
+        if (!nd.prev_detected) continue;
+        for (const Pt& prev : *nd.prev_detected) {
+            if (nd.use_points_buffer && !matches(nd, p, prev)) continue;
+            if (!nd.classify_colors) {
+                clouds[0].push_back(p);
+                break;
+            }
+            int known = -1;
+            for (int i = 1; i < 4 && known < 0; i++) {
+                if (!nd.prev_clouds[i]) continue;
+                for (const Pt& q : *nd.prev_clouds[i])
+                    if (matches(nd, p, q)) { known = i; break; }
+            }
+            if (known >= 0) {
+                clouds[known].push_back(p);
+            } else {
+                to_classify.push_back(reconstructed_cone(p, whole));
+                to_classify_centroids.push_back(p);
+            }
+            break;
+        }
+    }
+    if (nd.classify_colors) {
+        std::vector<int> colours(to_classify.size(), 0);
+        bool ok = true;
+        std::vector<int> answer(to_classify.size(), 0);
+        for (size_t k = 0; k < to_classify.size(); k++) {
+            std::vector<float> xyzi;
+            for (const Pt& q : to_classify[k]) xyzi.insert(xyzi.end(), {q.x, q.y, q.z, q.intensity});
+            answer[k] = classify ? classify(ctx, xyzi.data(), (uint32_t)to_classify[k].size()) : -1;
+            ok = ok && answer[k] >= 0 && answer[k] < 4;
+        }
+        if (ok) colours = answer;
+        for (size_t k = 0; k < to_classify.size(); k++) clouds[colours[k]].push_back(to_classify_centroids[k]);
+    }
+    for (int i = 0; i < 4; i++) nd.prev_clouds[i] = std::make_unique<std::vector<Pt>>(clouds[i]);
+    nd.prev_detected = std::move(current);
+}
+
 }  // namespace
 
 extern "C" {
+
+// get_reconstructed_cone for n centres over the whole cloud of `view` (mode 0: the groundless
+// cloud of the pipeline, 1: the detector input). offsets: n + 1; points: cap x 4 floats.
+// Returns the total point count (which may exceed cap; then points holds the first cap).
+uint32_t oracle_recrop(const void* params, const void* view, int mode, const float* centres, uint32_t n,
+                       uint32_t* offsets, float* points, uint32_t cap) {
+    const Params& prm = *(const Params*)params;
+    const std::vector<Pt> whole = whole_cloud(*(const View*)view, mode, prm);
+    uint32_t total = 0;
+    offsets[0] = 0;
+    for (uint32_t c = 0; c < n; c++) {
+        Pt ctr;
+        ctr.x = centres[2 * c]; ctr.y = centres[2 * c + 1]; ctr.z = 0.0f;
+        for (const Pt& q : reconstructed_cone(ctr, whole)) {
+            if (total < cap) {
+                float* o = points + 4 * (size_t)total;
+                o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.intensity;
+            }
+            total++;
+        }
+        offsets[c + 1] = total;
+    }
+    return total;
+}
+
+void* oracle_node_create(int classify_colors, int use_points_buffer, double matching) {
+    Node* nd = new Node;
+    nd->classify_colors = classify_colors != 0;
+    nd->use_points_buffer = use_points_buffer != 0;
+    nd->matching = matching;
+    return nd;
+}
+void oracle_node_destroy(void* node) { delete (Node*)node; }
+
+// One frame of the node after the hot path: centroids (n x 2, cluster order) and the frame's
+// whole cloud (view, mode as oracle_recrop). counts[4] = points per colour cloud; xy holds
+// colour i's points at xy + i * cap * 2.
+int oracle_node_step(void* node, const void* params, const void* view, int mode, const float* centroids,
+                     uint32_t n, ClassifyFn classify, void* ctx, uint32_t* counts, float* xy, uint32_t cap) {
+    const Params& prm = *(const Params*)params;
+    const std::vector<Pt> whole = whole_cloud(*(const View*)view, mode, prm);
+    std::vector<Pt> clouds[4];
+    centroid_clouds(*(Node*)node, whole, centroids, n, classify, ctx, clouds);
+    for (int i = 0; i < 4; i++) {
+        counts[i] = (uint32_t)clouds[i].size();
+        for (size_t k = 0; k < clouds[i].size() && k < cap; k++) {
+            xy[((size_t)i * cap + k) * 2] = clouds[i][k].x;
+            xy[((size_t)i * cap + k) * 2 + 1] = clouds[i][k].y;
+        }
+    }
+    return 0;
+}
 
 // mode: 0 = pipeline (ground removal then detector), 1 = detector only, 2 = ground only.
 // order: 0 = stable voxel sums (device order), 1 = PCL std::sort order.

@@ -26,7 +26,69 @@ def lib():
         _lib.oracle_atan2f.argtypes = [C.c_float, C.c_float]
         _lib.oracle_sector.restype = C.c_int
         _lib.oracle_sector.argtypes = [C.c_float, C.c_float]
+        _lib.oracle_recrop.restype = C.c_uint32
+        _lib.oracle_recrop.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_void_p,
+                                       C.c_void_p, C.c_uint32]
+        _lib.oracle_node_create.restype = C.c_void_p
+        _lib.oracle_node_create.argtypes = [C.c_int, C.c_int, C.c_double]
+        _lib.oracle_node_destroy.restype = None
+        _lib.oracle_node_destroy.argtypes = [C.c_void_p]
+        _lib.oracle_node_step.restype = C.c_int
+        _lib.oracle_node_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_uint32,
+                                          CLASSIFY_FN, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     return _lib
+
+
+CLASSIFY_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_uint32)
+
+
+def recrop(params, msg: PointCloud2, mode, centres, intensity_offset=None):
+    """get_reconstructed_cone over the whole cloud of msg (mode: MODE_PIPELINE = the groundless
+    cloud, MODE_DETECT = the detector input): one (n, 4) array per centre."""
+    v = msg.view(intensity_offset=intensity_offset)
+    cen = np.ascontiguousarray(np.asarray(centres, np.float32).reshape(-1, 2))
+    n = cen.shape[0]
+    offs = np.zeros(n + 1, np.uint32)
+    cap = 1 << 16
+    while True:
+        pts = np.zeros((cap, 4), np.float32)
+        tot = lib().oracle_recrop(C.addressof(params), C.addressof(v), mode, cen.ctypes.data, n,
+                                  offs.ctypes.data, pts.ctypes.data, cap)
+        if tot <= cap:
+            break
+        cap = int(tot)
+    return [pts[offs[i]:offs[i + 1]].copy() for i in range(n)]
+
+
+class Node:
+    """The restated node state after the hot path (tracking + colour clouds)."""
+
+    def __init__(self, classify_colors=True, use_points_buffer=False, matching=0.5):
+        self._n = lib().oracle_node_create(int(classify_colors), int(use_points_buffer), matching)
+
+    def __del__(self):
+        if getattr(self, "_n", None):
+            lib().oracle_node_destroy(self._n)
+            self._n = None
+
+    def step(self, params, msg: PointCloud2, mode, centroids, classify, intensity_offset=None):
+        """classify(xyzi (n, 4) array) -> colour 0..3, or -1 to fail the frame's service call.
+        Returns the four colour clouds as (k, 2) arrays."""
+        v = msg.view(intensity_offset=intensity_offset)
+        cen = np.ascontiguousarray(np.asarray(centroids, np.float32).reshape(-1, 2))
+
+        def cb(_ctx, ptr, n):
+            a = np.ctypeslib.as_array(ptr, (n * 4,)).reshape(n, 4).copy() if n else np.zeros((0, 4), np.float32)
+            return int(classify(a))
+
+        fn = CLASSIFY_FN(cb)
+        cap = max(cen.shape[0], 1)
+        counts = np.zeros(4, np.uint32)
+        xy = np.zeros((4, cap, 2), np.float32)
+        lib().oracle_node_step(self._n, C.addressof(params), C.addressof(v), mode,
+                               cen.ctypes.data if cen.size else None, cen.shape[0], fn, None,
+                               counts.ctypes.data, xy.ctypes.data, cap)
+        return [xy[i, : counts[i]].copy() for i in range(4)]
 
 
 def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_STABLE, intensity_offset=None):

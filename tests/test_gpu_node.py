@@ -1,0 +1,179 @@
+"""GPU parity of the detector node after the hot path: the cone re-crop (cg_recrop,
+get_reconstructed_cone, src/cone_detection.cpp:222-238) and the whole ConeDetector::cloud_handler
+(src/cone_detection.cpp:130-187: hot path, tracking, re-crop, colour service, the four published
+clouds) against the CPU restatement, bit for bit.
+
+The colour service is a stand-in that depends on the exact crop (point count and intensity
+sum), so a crop that differs in any point usually changes a colour and the published clouds."""
+import numpy as np
+import pytest
+
+import cones_perception_amd as cp
+import oracle_py as O
+from cones_perception_amd import _abi
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame(rings=64, cols=1024, frame=0, clutter=20, cpr=6, step=16):
+    raw = cp.synth_frames(1, first_frame=frame, rings=rings, cols=cols, clutter=clutter, cones_per_row=cpr,
+                          point_step=step)
+    return cp.frame_cloud(raw[0], point_step=step)
+
+
+def _same_crops(got, ref, ctx):
+    assert len(got) == len(ref), ctx
+    for c, (g, r) in enumerate(zip(got, ref)):
+        assert g.shape == r.shape, (ctx, c, g.shape, r.shape)
+        assert np.array_equal(g.view(np.uint32), r.view(np.uint32)), (ctx, c)
+
+
+def _centres(det, rng, extra=12):
+    """The detection's centroids, centres scattered over the cloud, one at the origin (the
+    pipeline's zero pads), a NaN and one far away."""
+    pts = [det.centroids.reshape(-1, 2), rng.uniform(-9, 9, (extra, 2)),
+           [[0.0, 0.0], [np.nan, 1.0], [500.0, 500.0], [0.1, -0.05]]]
+    return np.concatenate([np.asarray(p, np.float32).reshape(-1, 2) for p in pts]).astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def params():
+    return cp.load_params("simulation")
+
+
+@pytest.mark.parametrize("rings,cols", [(64, 1024), (128, 1024)])   # 128 x 1024: the large-frame path
+def test_recrop_pipeline_matches_oracle(params, rings, cols):
+    msg = _frame(rings, cols, frame=2)
+    pipe = cp.ConePipeline(params)
+    det = pipe.cloud_handler(msg)
+    cen = _centres(det, np.random.default_rng(rings))
+    got = pipe.recrop(cen)
+    ref = O.recrop(params, msg, O.MODE_PIPELINE, cen)
+    _same_crops(got, ref, f"pipeline {rings}x{cols}")
+    assert sum(len(c) for c in got) > 0
+    assert len(got[-4]) >= det.n_points - det.n_kept   # the origin box holds every zero pad
+
+
+def test_recrop_detect_matches_oracle(params):
+    msg = _frame(frame=3)
+    d = cp.ConeDetector(params)
+    det = d.cloud_handler(msg)
+    cen = _centres(det, np.random.default_rng(5))
+    _same_crops(d.recrop(cen), O.recrop(params, msg, O.MODE_DETECT, cen), "detect")
+
+
+def test_recrop_without_intensity_field_reads_x(params):
+    """src/cone_detection.cpp:142-151: no intensity field -> intensity aliases x (offset 0)."""
+    msg = _frame(frame=4)
+    msg.fields = [f for f in msg.fields if f.name != "intensity"]
+    d = cp.ConeDetector(params)
+    det = d.cloud_handler(msg)
+    cen = _centres(det, np.random.default_rng(6))
+    got = d.recrop(cen)
+    _same_crops(got, O.recrop(params, msg, O.MODE_DETECT, cen, intensity_offset=0), "no intensity")
+    for c in got:
+        assert np.array_equal(c[:, 3].view(np.uint32), c[:, 0].view(np.uint32))
+
+
+def test_recrop_many_centres_and_edges(params):
+    """More centres than one launch takes (256), duplicates, and boxes whose edges sit exactly
+    on points (the double compares are inclusive)."""
+    msg = _frame(frame=5)
+    pipe = cp.ConePipeline(params)
+    pipe.cloud_handler(msg)
+    xyz = msg.xyzi()
+    rng = np.random.default_rng(9)
+    pick = xyz[rng.integers(0, len(xyz), 300)]
+    half = np.float64(np.float32(0.228)) / 1.5
+    cen = np.concatenate([pick[:, :2],
+                          (pick[:40, :2].astype(np.float64) - half).astype(np.float32),   # edge on a point
+                          pick[:10, :2]]).astype(np.float32)
+    _same_crops(pipe.recrop(cen), O.recrop(params, msg, O.MODE_PIPELINE, cen), "many")
+    assert pipe.recrop(np.zeros((0, 2), np.float32)) == []
+
+
+def test_recrop_requires_a_detector_call(params):
+    h = cp.ConePipeline(params)
+    with pytest.raises(_abi.CgError):
+        h.recrop([[1.0, 2.0]])
+
+
+def _service(crop_xyzi):
+    return (len(crop_xyzi) + int(np.floor(crop_xyzi[:, 3].astype(np.float64).sum()))) % 4 if len(crop_xyzi) else 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("classify,buffer", [(True, False), (True, True), (False, True)])
+def test_node_matches_oracle_over_frames(params, fused, classify, buffer):
+    """Eight consecutive frames through ConeDetectorNode (GPU) and the restated node fed with the
+    restated detections: the published clouds, headers and field lists. The service call fails
+    on frames 3 and 6 (every colour then stays unknown)."""
+    state = {"frame": 0, "asked": 0}
+    failing = {3, 6}
+
+    def classifier(msgs):
+        state["asked"] += len(msgs)
+        assert all(m.header.get("frame_id") == "cloud" and m.point_step == 32 for m in msgs)
+        if state["frame"] in failing:
+            return None
+        return [_service(m.xyzi()) for m in msgs]
+
+    node = cp.ConeDetectorNode(params, classify_colors=classify, use_points_buffer=buffer, classifier=classifier,
+                               fused_ground_removal=fused)
+    ref_node = O.Node(classify, buffer, params.cones_matching_dist_theshold)
+    mode = O.MODE_PIPELINE if fused else O.MODE_DETECT
+    published = 0
+    base = _frame(frame=10).xyzi()
+    rng = np.random.default_rng(11)
+    for f in range(8):
+        state["frame"] = f
+        # one scene seen from a vehicle creeping forward: consecutive frames track
+        pts = base.copy()
+        pts[:, 0] -= np.float32(0.07 * f)
+        pts[:, :3] += rng.normal(0, 0.01, (len(pts), 3)).astype(np.float32)
+        msg = cp.PointCloud2.from_xyzi(pts, layout=16)
+        msg.header = {"seq": f, "stamp_sec": 100 + f, "stamp_nsec": 123456789, "frame_id": "lidar"}
+        outs = node.cloud_handler(msg)
+        det, _ = O.run(params, msg, mode)
+        ref = ref_node.step(params, msg, mode, det.centroids, lambda c: -1 if f in failing else _service(c))
+        assert len(outs) == 4
+        for i, m in enumerate(outs):
+            assert m.header == msg.header                                          # line 182
+            assert [(q.name, q.offset) for q in m.fields] == [(q.name, q.offset) for q in msg.fields]   # 183
+            assert m.point_step == 32 and m.height == 1 and m.width == len(ref[i])
+            recs = m.data.view(np.float32).reshape(-1, 8)
+            assert np.array_equal(recs[:, 0:2].view(np.uint32), ref[i].view(np.uint32)), (f, i)
+            assert np.all(recs[:, 2] == 0) and np.all(recs[:, 3] == 1.0) and np.all(recs[:, 4] == 0)
+            published += m.width
+    assert published > 0
+    assert (state["asked"] > 0) == classify
+
+
+def test_ground_node_message_header_and_fields(params):
+    """src/ground_removal.cpp:81-86: header and fields are set before toROSMsg, which replaces
+    them: PointXYZI's fields and the input header after PCL's microsecond stamp."""
+    msg = _frame(frame=6)
+    msg.header = {"seq": 7, "stamp_sec": 1700000000, "stamp_nsec": 987654321, "frame_id": "velodyne"}
+    out = cp.GroundRemover(params).cloud_handler(msg)
+    assert out.header == {"seq": 7, "stamp_sec": 1700000000, "stamp_nsec": 987654000, "frame_id": "velodyne"}
+    assert [(f.name, f.offset) for f in out.fields] == [("x", 0), ("y", 4), ("z", 8), ("intensity", 16)]
+    assert (out.point_step, out.width * out.height) == (32, msg.width * msg.height)
+
+
+def test_handles_leave_no_sticky_hip_error(params):
+    """Every handle kind, on a fused-path and a large-path frame, with a re-crop where it applies,
+    then closed: the runtime's last-error state stays clean (a stale error would surface in the
+    next handle's first launch check)."""
+    import ctypes
+    cp.lib()
+    hip = ctypes.CDLL("libamdhip64.so.7")        # the runtime already loaded (same soname)
+    hip.hipGetLastError.restype = ctypes.c_int
+    assert hip.hipGetLastError() == 0
+    for cls in (cp.ConePipeline, cp.ConeDetector, cp.GroundRemover):
+        for rings in (64, 128):
+            h = cls(params)
+            h.cloud_handler(_frame(rings, 1024, frame=7))
+            if cls is not cp.GroundRemover:
+                h.recrop([[2.0, 1.0], [0.0, 0.0]])
+            h.close()
+            assert hip.hipGetLastError() == 0, (cls.__name__, rings)
