@@ -9,8 +9,10 @@
 // calls include/cones_gpu.h for every per-point operation. INTEGRATION.md shows the same
 // calls inside the real nodes.
 #pragma once
+#include <array>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -26,9 +28,24 @@ struct PointField {           // sensor_msgs/PointField
     uint32_t count = 1;
 };
 
-struct PointCloud2 {          // sensor_msgs/PointCloud2 (header reduced to stamp + frame)
-    double stamp = 0.0;
+struct Header {               // std_msgs/Header
+    uint32_t seq = 0;
+    uint32_t stamp_sec = 0, stamp_nsec = 0;
     std::string frame_id;
+    bool operator==(const Header& o) const {
+        return seq == o.seq && stamp_sec == o.stamp_sec && stamp_nsec == o.stamp_nsec && frame_id == o.frame_id;
+    }
+};
+
+// The header after pcl::fromROSMsg then pcl::toROSMsg (pcl_conversions, PCL 1.10): the stamp
+// travels as microseconds (toNSec() / 1000, then * 1000), so nanoseconds truncate.
+inline Header pcl_header(Header h) {
+    h.stamp_nsec = h.stamp_nsec / 1000u * 1000u;
+    return h;
+}
+
+struct PointCloud2 {          // sensor_msgs/PointCloud2
+    Header header;
     uint32_t height = 1, width = 0;
     std::vector<PointField> fields;
     bool is_bigendian = false;
@@ -77,6 +94,14 @@ public:
     Handle(const Handle&) = delete;
     Handle& operator=(const Handle&) = delete;
 protected:
+    std::vector<std::vector<float>> crops(const std::vector<float>& centres_xy) {
+        cg_crop_result r{};
+        check(cg_recrop(h_, centres_xy.empty() ? nullptr : centres_xy.data(), (uint32_t)(centres_xy.size() / 2), &r));
+        std::vector<std::vector<float>> out(r.n_centers);
+        for (uint32_t c = 0; c < r.n_centers; c++)
+            out[c].assign(r.points + 4 * (size_t)r.offsets[c], r.points + 4 * (size_t)r.offsets[c + 1]);
+        return out;
+    }
     cg_handle* h_ = nullptr;
 };
 
@@ -102,7 +127,8 @@ public:
         cg_ground_result r{};
         check(cg_ground_remove(h_, &v, &r));
         PointCloud2 out;
-        out.stamp = msg.stamp; out.frame_id = msg.frame_id;
+        // lines 83-86: header and fields set before toROSMsg, which replaces both
+        out.header = pcl_header(msg.header);
         out.width = r.width; out.height = r.height;
         out.fields = {{"x", 0}, {"y", 4}, {"z", 8}, {"intensity", 16}};
         out.point_step = 32; out.row_step = 32 * r.width;
@@ -119,6 +145,9 @@ public:
 class ConeDetector : public Handle {
 public:
     explicit ConeDetector(const cg_params& p, int device = 0) : Handle(p, device) {}
+    // get_reconstructed_cone (lines 222-238) around each centre over the last call's whole
+    // cloud: one x,y,z,intensity array per centre.
+    std::vector<std::vector<float>> recrop(const std::vector<float>& centres_xy) { return crops(centres_xy); }
     Detection cloud_handler(const PointCloud2& msg) {
         if (!intensity_in_cloud_checked) {                         // lines 131-136
             if (!msg.has_field("intensity")) intensity_in_cloud = false;
@@ -144,6 +173,104 @@ public:
         check(cg_pipeline(h_, &v, &r));
         return to_detection(r);
     }
+    std::vector<std::vector<float>> recrop(const std::vector<float>& centres_xy) {   // over the groundless cloud
+        return crops(centres_xy);
+    }
+};
+
+// pcl::toROSMsg of a PointCloud<PointXYZI> filled by push_back (PCL 1.10): height 1, width n,
+// PointXYZI's fields, point_step 32, is_dense; x, y, z, 1.0f, intensity, 12 zero padding bytes.
+inline PointCloud2 to_ros_msg(const std::vector<float>& xyzi) {
+    PointCloud2 m;
+    const size_t n = xyzi.size() / 4;
+    m.width = (uint32_t)n; m.height = 1;
+    m.fields = {{"x", 0}, {"y", 4}, {"z", 8}, {"intensity", 16}};
+    m.point_step = 32; m.row_step = 32 * m.width;
+    m.data.assign(32 * n, 0);
+    for (size_t i = 0; i < n; i++) {
+        const float rec[5] = {xyzi[4 * i], xyzi[4 * i + 1], xyzi[4 * i + 2], 1.0f, xyzi[4 * i + 3]};
+        std::memcpy(m.data.data() + 32 * i, rec, sizeof rec);
+    }
+    return m;
+}
+
+// Tracking and the colour clouds, get_centroid_clouds (src/cone_detection.cpp:251-339).
+class ConeTracker {
+public:
+    explicit ConeTracker(const cg_track_params& p) { check(cg_tracker_create(&p, &t_)); }
+    ~ConeTracker() { cg_tracker_destroy(t_); }
+    ConeTracker(const ConeTracker&) = delete;
+    ConeTracker& operator=(const ConeTracker&) = delete;
+    std::vector<int32_t> match(const std::vector<float>& centroids_xy, uint32_t& n_need) {
+        std::vector<int32_t> st(centroids_xy.size() / 2);
+        check(cg_tracker_match(t_, centroids_xy.empty() ? nullptr : centroids_xy.data(), (uint32_t)st.size(),
+                               st.empty() ? nullptr : st.data(), &n_need));
+        return st;
+    }
+    void commit(const std::vector<int32_t>* colours) {   // nullptr: the service call failed
+        check(cg_tracker_commit(t_, colours ? colours->data() : nullptr, colours ? (uint32_t)colours->size() : 0u));
+    }
+    std::vector<float> cloud(int colour) const {          // (x, y) pairs
+        const float* xy = nullptr;
+        uint32_t n = 0;
+        check(cg_tracker_cloud(t_, colour, &xy, &n));
+        return std::vector<float>(xy, xy + 2 * (size_t)n);
+    }
+private:
+    cg_tracker* t_ = nullptr;
+};
+
+// The whole ConeDetector::cloud_handler (src/cone_detection.cpp:130-187): the hot path, tracking,
+// the re-crop of cones that need a colour, the colour service (a callback standing in for
+// ClassifyColorSrv: it gets one PointXYZI message per cone, frame_id = cones_frame_id, and returns
+// false for a failed call) and the four messages published on cones_topics (index = colour),
+// each with the input's header and field list (lines 182-183). DETECTOR is ConeDetector, or
+// ConePipeline for the fused ground_removal:=true composition.
+using ColourService = std::function<bool(const std::vector<PointCloud2>& cones, std::vector<int32_t>& colours)>;
+
+template <class DETECTOR>
+class ConeDetectorNode {
+public:
+    ConeDetectorNode(const cg_params& p, const cg_track_params& tp, ColourService service = nullptr,
+                     std::string cones_frame_id = "cloud", int device = 0)
+        : detector(p, device), tracker(tp), service_(std::move(service)), frame_id_(std::move(cones_frame_id)) {}
+
+    std::array<PointCloud2, CG_NUM_COLORS> cloud_handler(const PointCloud2& msg) {
+        last = detector.cloud_handler(msg);
+        uint32_t n_need = 0;
+        const std::vector<int32_t> st = tracker.match(last.centroids, n_need);
+        std::vector<int32_t> colours;
+        bool ok = false;
+        if (n_need) {
+            std::vector<float> need;
+            for (size_t c = 0; c < st.size(); c++)
+                if (st[c] == CG_TRACK_NEED_COLOR) need.insert(need.end(), {last.centroids[2 * c], last.centroids[2 * c + 1]});
+            std::vector<PointCloud2> cones;
+            for (const auto& crop : detector.recrop(need)) {
+                cones.push_back(to_ros_msg(crop));
+                cones.back().header.frame_id = frame_id_;
+            }
+            ok = service_ && service_(cones, colours) && colours.size() == n_need;
+        }
+        tracker.commit(ok ? &colours : nullptr);
+        std::array<PointCloud2, CG_NUM_COLORS> out;
+        for (int i = 0; i < CG_NUM_COLORS; i++) {
+            const std::vector<float> xy = tracker.cloud(i);
+            std::vector<float> xyzi;
+            for (size_t k = 0; k < xy.size() / 2; k++) xyzi.insert(xyzi.end(), {xy[2 * k], xy[2 * k + 1], 0.f, 0.f});
+            out[i] = to_ros_msg(xyzi);
+            out[i].header = msg.header;   // line 182
+            out[i].fields = msg.fields;   // line 183
+        }
+        return out;
+    }
+
+    DETECTOR detector;
+    ConeTracker tracker;
+    Detection last;
+private:
+    ColourService service_;
+    std::string frame_id_;
 };
 
 }  // namespace cones_gpu

@@ -60,6 +60,50 @@ int main(int argc, char** argv) {
                             b.centroids[2 * c], b.centroids[2 * c + 1]);
             if (!ok) return 1;
         }
+        // the whole detector node over one scene seen from a creeping vehicle: fused pipeline vs
+        // the two-node chain (ground node -> detector node); published clouds must agree
+        cg_track_params tp;
+        cg_track_params_init(&tp);
+        tp.classify_colors = 1;
+        tp.use_points_buffer = 1;
+        ColourService service = [](const std::vector<PointCloud2>& cones, std::vector<int32_t>& colours) {
+            colours.clear();
+            for (const PointCloud2& c : cones) {   // a stand-in classifier: point count + intensity sum
+                double s = 0.0;
+                for (uint32_t i = 0; i < c.width; i++) {
+                    float v;
+                    std::memcpy(&v, c.data.data() + 32 * (size_t)i + 16, 4);
+                    s += v;
+                }
+                colours.push_back((int32_t)((c.width + (uint64_t)std::floor(s)) % CG_NUM_COLORS));
+            }
+            return true;
+        };
+        ConeDetectorNode<ConePipeline> fused_node(p, tp, service);
+        ConeDetectorNode<ConeDetector> chain_node(p, tp, service);
+        const PointCloud2 scene = synth_cloud(10);
+        for (int f = 0; f < frames; f++) {
+            PointCloud2 msg = scene;
+            msg.header.seq = (uint32_t)f;
+            msg.header.stamp_sec = 1000 + (uint32_t)f;
+            msg.header.stamp_nsec = 123456789;
+            for (uint32_t i = 0; i < msg.width; i++) {   // x -= 0.07 m per frame
+                float x;
+                std::memcpy(&x, msg.data.data() + 16 * (size_t)i, 4);
+                x -= 0.07f * (float)f;
+                std::memcpy(msg.data.data() + 16 * (size_t)i, &x, 4);
+            }
+            const auto a = fused_node.cloud_handler(msg);
+            const auto b = chain_node.cloud_handler(ground.cloud_handler(msg));
+            bool ok = true;
+            std::printf("node frame %d:", f);
+            for (int i = 0; i < CG_NUM_COLORS; i++) {
+                ok = ok && a[i].data == b[i].data && a[i].header == msg.header;
+                std::printf(" %s=%u", i == 0 ? "unknown" : i == 1 ? "yellow" : i == 2 ? "blue" : "orange", a[i].width);
+            }
+            std::printf(" %s\n", ok ? "fused == two-node" : "MISMATCH");
+            if (!ok) return 1;
+        }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 2;

@@ -177,3 +177,16 @@ def test_handles_leave_no_sticky_hip_error(params):
                 h.recrop([[2.0, 1.0], [0.0, 0.0]])
             h.close()
             assert hip.hipGetLastError() == 0, (cls.__name__, rings)
+
+
+def test_cpp_node_mirror_demo():
+    """host/nodes_demo.cpp: the C++ mirror's two-node chain equals the fused call (hot path), and
+    its ConeDetectorNode over a tracked sequence publishes the same clouds either way."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(_abi.LIB_PATH), "nodes_demo")
+    r = subprocess.run([exe, "5"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("node frame")]
+    assert len(lines) == 5 and all("fused == two-node" in l for l in lines)
+    assert any(" unknown=0" not in l or " yellow=0" not in l for l in lines[1:])   # something published
