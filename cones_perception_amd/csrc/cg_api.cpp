@@ -157,6 +157,7 @@ struct cg_handle {
     uint32_t large_points = 0;
     LgScratch lg{};
     int route = 0;                // cg_debug_route
+    unsigned long long* next_span = nullptr;   // cg_debug_launch_span
     cg_tile tile{};               // the rank's tile (cg_tile_front .. cg_tile_decide)
     bool tile_ready = false;
     // the last single-frame call, for cg_recrop
@@ -632,6 +633,8 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
         if (rc) return rc;
     }
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    L.span = h->next_span;
+    h->next_span = nullptr;
     rc = launch_frames(h, L, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s);
     if (rc) return rc;
     h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
@@ -779,6 +782,12 @@ int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
     const uint64_t cap = which == 0 ? LG_META_WORDS * 4 : which == 1 ? nch * LG_CHUNK : nch * CG_BLOCK * 16;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, src, std::min(bytes, cap), hipMemcpyDeviceToHost));
+    return CG_OK;
+}
+
+int cg_debug_launch_span(cg_handle* h, void* d_span) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    h->next_span = (unsigned long long*)d_span;
     return CG_OK;
 }
 

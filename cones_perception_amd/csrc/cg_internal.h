@@ -63,6 +63,9 @@ struct CgLaunch {
     uint64_t* stamps;
     // per-frame final sector-minimum keys (18 words) for cg_recrop, or null (ground modes)
     uint32_t* seckeys;
+    // timing: [first workgroup start, last workgroup end] of the launch (s_memrealtime,
+    // 100 MHz), or null (cg_debug_launch_span)
+    unsigned long long* span;
 };
 
 #ifndef CG_BLOCK

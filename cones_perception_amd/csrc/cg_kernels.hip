@@ -585,6 +585,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
     const uint32_t N = L.n_points;
     STAMP(0);
+    if (L.span && tid == 0) atomicMin(&L.span[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
     if (tid < 64) fs->scal[tid] = (tid >= S_BMIN0 && tid <= S_BMIN2) ? 0xffffffffu : 0u;
@@ -780,11 +781,6 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     STAMP(26);
     __syncthreads();
     STAMP(5);
-#ifdef CG_EXPERIMENT_FRONT_ONLY
-    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[2] = M; h[3] = 0; h[4] = 0; h[5] = 0; }
-    STAMP(20);
-    return;
-#endif
     if (use_lds) {
         Work WL;
         WL.P = bl->P; WL.KEY = bl->KEY; WL.VOX = bl->VOX; WL.A = bl->A; WL.PAR = bl->PAR; WL.CNT = bl->CNT;
@@ -793,6 +789,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     } else {
         backend(W, M, fs, L, P, f, flags);
     }
+    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------------------------------

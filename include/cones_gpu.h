@@ -4,8 +4,9 @@
  * (reference paths relative to its repository root):
  *   - GroundRemover::cloud_handler   src/ground_removal.cpp:50-89  (lines 51-79 replaced)
  *   - ConeDetector::cloud_handler    src/cone_detection.cpp:130-187 (lines 138-167 and the
- *     centroid arithmetic 261-279 replaced; tracking 282-339, colour RPC 342-363 and the
- *     4-topic publish 177-186 stay in the node)
+ *     centroid arithmetic 261-279 replaced; the colour RPC 342-363 and the 4-topic publish
+ *     177-186 stay in the node; the tracking 282-339 and the cone re-crop 222-238 are
+ *     offered as cg_tracker_* and cg_recrop below)
  * The reference has no plugin API; its seam is those callback bodies, which call PCL
  * (fromROSMsg, VoxelGrid, search::KdTree, EuclideanClusterExtraction, toROSMsg) and libm.
  * INTEGRATION.md shows the patched callbacks. Plain C types only: no torch, no C++ in
@@ -247,6 +248,11 @@ int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
 /* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz; 32 slots per frame) for the
  * next batch calls; enable = 0 frees the buffer. Fetch synchronises the batch stream. */
 int cg_debug_stamps(cg_handle* h, int enable);
+/* Timing: the next cg_run_batch launch of the frame kernel records its execution span in
+ * d_span (device memory, 2 x uint64 the caller sets to {UINT64_MAX, 0}): the first workgroup's
+ * start and the last workgroup's end, s_memrealtime ticks (100 MHz). One atomic per workgroup
+ * at each end; frames of more than 65,536 points (large-frame path) do not record. */
+int cg_debug_launch_span(cg_handle* h, void* d_span);
 int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
 
 /* Diagnostics: route every frame through the large-frame path (1), and also through its
