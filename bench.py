@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--scatter", action="store_true",
                     help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
                          "scatter to ranks, process, gather per-frame headers (reported separately)")
+    ap.add_argument("--no-events", action="store_true", help="experiment: no per-launch HIP events")
     ap.add_argument("--streams", type=int, default=3,
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
@@ -110,15 +111,18 @@ def main():
     for s in range(args.steps):
         st = streams[(counter[0]) % S]
         lib.cg_debug_launch_span(engines[counter[0] % S].handle, spans[s].data_ptr())
-        evs[s][0].record(st)
+        if not args.no_events:
+            evs[s][0].record(st)
         step()
-        evs[s][1].record(st)
+        if not args.no_events:
+            evs[s][1].record(st)
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    kern_ms = [a.elapsed_time(b) for a, b in evs] if not args.no_events else [0.0]
     avg_event_ms = sum(kern_ms) / len(kern_ms)
     sp = spans.cpu().numpy()
     spans_ok = bool((sp[:, 0] < 2 ** 63 - 1).all() and (sp[:, 1] > sp[:, 0]).all())
@@ -193,6 +197,7 @@ def main():
                          "aggregate_achieved": bytes_per_launch * args.steps * world / elapsed / 1e9 / world,
                          "aggregate_frac": bytes_per_launch * args.steps / elapsed / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
+            "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
         }
         if single is not None:
             line["single_frame"] = single

@@ -619,6 +619,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     }
     __syncthreads();
     STAMP(1);
+
+#if defined(CG_EXP_STOP) && CG_EXP_STOP == 1
+    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
+    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    return;
+#endif
     if (GROUND && tid < 64) {
         sector_thresholds(fs->sec_key, fs->scal[S_TOUCHED], P, fs->thr, fs->tkey, &fs->scal[S_TKMIN], &fs->scal[S_TKMAX]);
         if (L.seckeys && tid <= CG_NUM_BINS) L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = fs->sec_key[tid];
@@ -692,6 +698,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     uint32_t pos = wbase + incl - nsv;
     __syncthreads();   // counts complete; z-code overlay in LDS is dead from here on
     STAMP(3);
+
+#if defined(CG_EXP_STOP) && CG_EXP_STOP == 2
+    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
+    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    return;
+#endif
     const uint32_t Ms = fs->scal[S_MS];
     const uint32_t K = GROUND ? fs->scal[S_K] : N;
     // pipeline: the detector input is the groundless cloud, whose N-K trailing
@@ -781,6 +793,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     STAMP(26);
     __syncthreads();
     STAMP(5);
+
+#if defined(CG_EXP_STOP) && CG_EXP_STOP == 3
+    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
+    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    return;
+#endif
     if (use_lds) {
         Work WL;
         WL.P = bl->P; WL.KEY = bl->KEY; WL.VOX = bl->VOX; WL.A = bl->A; WL.PAR = bl->PAR; WL.CNT = bl->CNT;
