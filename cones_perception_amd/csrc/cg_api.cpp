@@ -85,6 +85,27 @@ int prepare(const cg_params& p, CgDevParams& d) {
     d.ang_hi = cg_ceil_to_float(theta);
     d.ang_cert_hi = cg_ceil_to_float((double)d.ang_hi + (double)CG_ANG_MARGIN);
     d.ang_cert_lo = cg_floor_to_float((double)d.ang_hi - (double)CG_ANG_MARGIN);
+    // sector rays and the angle-filter class of each sector's wedge (cg_device.h ray_inside)
+    for (int sct = 0; sct < CG_NUM_BINS; sct++) {
+        const double lo = sct * (double)CG_SECTOR_ANGLE_RAD;             // exact product
+        const double hi = sct + 1 < CG_NUM_BINS ? (sct + 1) * (double)CG_SECTOR_ANGLE_RAD : 2.0 * M_PI;
+        d.ray[sct] = make_float4((float)std::cos(lo), (float)std::sin(lo), (float)std::cos(hi), (float)std::sin(hi));
+        // unwrapped angles a in (-pi, pi] of the padded wedge: one or two intervals
+        const double wl = lo - CG_RAY_WEDGE_PAD, wh = hi + CG_RAY_WEDGE_PAD;
+        double iv[2][2];
+        int niv = 0;
+        if (wh <= M_PI) { iv[0][0] = wl; iv[0][1] = wh; niv = 1; }
+        else if (wl >= M_PI) { iv[0][0] = wl - 2 * M_PI; iv[0][1] = wh - 2 * M_PI; niv = 1; }
+        else { iv[0][0] = wl; iv[0][1] = M_PI; iv[1][0] = -M_PI; iv[1][1] = wh - 2 * M_PI; niv = 2; }
+        bool keep = true, rm = true;
+        for (int k = 0; k < niv; k++) {
+            // keep: ang_lo < a < ang_hi on the whole interval; remove: a <= ang_lo or a >= ang_hi
+            keep = keep && iv[k][0] > (double)d.ang_lo && iv[k][1] < (double)d.ang_hi;
+            rm = rm && (iv[k][1] <= (double)d.ang_lo || iv[k][0] >= (double)d.ang_hi);
+        }
+        if (keep || rm) d.ray_filter_ok |= 1u << sct;
+        if (rm) d.ray_arm |= 1u << sct;
+    }
     // pcl::VoxelGrid::setLeafSize(float, float, float): inverse = 1.0f / leaf
     d.inv_leaf[0] = 1.0f / (float)p.voxel_filter_leaf_size_x;
     d.inv_leaf[1] = 1.0f / (float)p.voxel_filter_leaf_size_y;

@@ -377,6 +377,32 @@ __device__ __forceinline__ bool zc_not_ground(uint32_t c, uint32_t qhi) { return
 
 
 // ------------------------------------------------------------------------------------------
+// Sector-coherent fast path. A lane's consecutive points are CG_BLOCK apart; on a spinning
+// sensor stored column by column that is a few degrees of azimuth, and the 64 lanes of a wave
+// are one column. So the lane's current sector is re-certified per point by two cross products
+// against the sector's edge rays (7 VALU), and the approximate atan2 of
+// classify_angle_fast runs only where that fails: at sector changes (wave-uniform on such
+// data), in sectors the angle filter cuts through, and near edges. Any point order is
+// correct; only the speed depends on it.
+static_assert(sizeof(((CgDevParams*)0)->ray) / sizeof(float4) == CG_NUM_BINS, "one ray pair per bin");
+// The lane-table of rays (LDS, CG_NUM_BINS entries) for this mode: with the angle filter on,
+// a sector the filter cuts through gets zero rays, which certify nothing.
+template <bool FILTER>
+__device__ __forceinline__ void init_rays(const CgDevParams& P, float4* rays, uint32_t t) {
+    if (t < CG_NUM_BINS)
+        rays[t] = (!FILTER || ((P.ray_filter_ok >> t) & 1u)) ? P.ray[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// (x, y) strictly inside the wedge of rays r (lower edge r.xy, upper edge r.zw) by the margin
+// CG_RAY_EPS (cg_internal.h): y cos(b) - x sin(b) = |p| sin(angle - b), computed with <= 3
+// roundings of |x| + |y|. Tiny, huge and NaN points fail (the 1e-30 floor, inf/NaN compares).
+__device__ __forceinline__ bool ray_inside(float x, float y, const float4& r) {
+    const float m = fmaf(fabsf(x) + fabsf(y), CG_RAY_EPS, 1.0e-30f);
+    const float dlo = fmaf(y, r.x, -(x * r.y));
+    const float dhi = fmaf(y, r.z, -(x * r.w));
+    return (dlo > m) & (dhi < -m);
+}
+
+// ------------------------------------------------------------------------------------------
 // Pass 1 over N points at fb (lane t owns points k*512 + t, k < PPT): the certified
 // classification of every point, the lane's sector-minimum runs flushed into the 17 bins of
 // sec_key (LDS, order-preserving keys), the position-filter bits of the lane's points (posm)
@@ -385,7 +411,7 @@ __device__ __forceinline__ bool zc_not_ground(uint32_t c, uint32_t qhi) { return
 // the loop. touched returns the lane's used sector bins (bit 17: NaN angle).
 template <int PPT, int LAYOUT, bool GROUND, bool FILTER, class STORE>
 __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, const CgLaunch& L,
-                                             const CgDevParams& P, uint32_t* sec_key,
+                                             const CgDevParams& P, uint32_t* sec_key, const float4* rays,
                                              LaneBits<(PPT + 63) / 64>& posm, uint32_t& touched,
                                              STORE store_codes) {
     constexpr int G = 8;                          // points per load group (double-buffered)
@@ -403,7 +429,9 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
     LaneBits<NW> uncm;
     posm.clear();
     uncm.clear();
-    int cur_s = 0;
+    int cur_s = -1;              // the lane's current sector (-1: none yet)
+    float4 cur_r = make_float4(0.f, 0.f, 0.f, 0.f);   // its rays (zero: certify nothing)
+    bool cur_arm = false;        // the angle filter removes all of it
     float cur_m = INFINITY;      // minimum z of the lane's current run of sector cur_s
     touched = 0;                 // sector bins this lane saw (bit 17: NaN angle)
     const uint32_t nlast = N ? N - 1 : 0u;
@@ -423,9 +451,10 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
 #pragma unroll
         for (int j = 0; j < G; j++) {
             const float x = buf[j].x, y = buf[j].y, z = buf[j].z;
-            int s = 0;
-            bool ang_rm = false, drm = false;
-            bool ok = classify_angle_fast<GROUND, FILTER>(P, x, y, s, ang_rm);
+            int s = cur_s;
+            bool ang_rm = cur_arm, drm = false;
+            bool ok = true;
+            if (!ray_inside(x, y, cur_r)) ok = classify_angle_fast<true, FILTER>(P, x, y, s, ang_rm);
             if (FILTER) {
                 ok = dist_level_fast(P, x, y, z, drm) & ok;
                 rpos = shl1_add_if(rpos, ok & !ang_rm & !drm);
@@ -450,8 +479,17 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
                         touched |= 1u << cur_s;
                     }
                     cur_m = INFINITY;
+                    cur_r = rays[ss];
+                    if (FILTER) cur_arm = (P.ray_arm >> ss) & 1u;
                 }
                 if (ok & (z < cur_m)) cur_m = z;   // a NaN z never lowers it
+                cur_s = ss;
+            } else {
+                const int ss = ok ? s : cur_s;
+                if (ss != cur_s) {
+                    cur_r = rays[ss];
+                    cur_arm = (P.ray_arm >> ss) & 1u;
+                }
                 cur_s = ss;
             }
         }

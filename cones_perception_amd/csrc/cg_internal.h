@@ -28,6 +28,12 @@ struct CgDevParams {
     // angle-filter certificates: |a| >= ang_cert_hi removes and |a| < ang_cert_lo keeps for
     // every exact angle within CG_ANG_MARGIN of the fast approximation a
     float ang_cert_lo, ang_cert_hi;
+    // sector rays for the coherent fast path (cg_device.h ray_inside): sector s is the wedge
+    // between the unit vectors ray[s].xy = (cos, sin)(s * SEC) and ray[s].zw at its upper
+    // edge ((s + 1) * SEC; 2 pi for sector 16). ray_filter_ok: sectors whose whole wedge (plus
+    // CG_RAY_WEDGE_PAD) lies on one side of the angle filter; ray_arm: those it removes.
+    float4 ray[17];
+    uint32_t ray_filter_ok, ray_arm;
 };
 
 // Sets the thread-local message cg_last_error returns; returns code.
@@ -39,6 +45,13 @@ int cg_set_error(int code, const char* msg);
 // margins from a boundary (radians / sector units), everything else takes the exact path.
 #define CG_ANG_MARGIN 8.0e-6f
 #define CG_SEC_MARGIN_T 2.5e-5f
+// Sector-ray certificate: a point is certified inside its lane's current sector when both
+// edge cross products clear CG_RAY_EPS * (|x| + |y|), i.e. its true angle lies >= 1.9e-5 rad
+// inside the wedge, against <= 8.5e-7 rad between the true edge and the reference's own
+// floor(fl(wrap(atan2f)) / SEC) edge. The angle-filter class of a sector is decided over the
+// wedge widened by CG_RAY_WEDGE_PAD on both sides.
+#define CG_RAY_EPS 2.0e-5f
+#define CG_RAY_WEDGE_PAD 1.0e-4
 
 // One batch launch: uniform frames, device-resident input and outputs.
 struct CgLaunch {

@@ -39,6 +39,7 @@
 // LDS map. The frontend's 16-bit z-key prefixes (zq) overlay the backend arrays, which are
 // dead until pass 3 begins; pass 2 leaves its decisions in registers.
 struct FrontShared {
+    float4 rays[CG_NUM_BINS];      // sector edge rays of the pass-1 fast path
     uint32_t sec_key[CG_NUM_BINS + 1];
     float thr[CG_NUM_BINS + 1];
     uint32_t tkey[CG_NUM_BINS + 1];
@@ -588,13 +589,14 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     if (L.span && tid == 0) atomicMin(&L.span[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
+    init_rays<FILTER>(P, fs->rays, tid);
     if (tid < 64) fs->scal[tid] = (tid >= S_BMIN0 && tid <= S_BMIN2) ? 0xffffffffu : 0u;
     __syncthreads();
 
     // ---- pass 1: stream the frame ----
     LaneBits<NW> posm;
     uint32_t touched = 0;
-    stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, posm, touched,
+    stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, fs->rays, posm, touched,
                                              [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; });
     const uint32_t nlast = N ? N - 1 : 0u;
     if (GROUND) {

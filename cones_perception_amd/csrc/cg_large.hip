@@ -75,16 +75,18 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
     constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
     __shared__ uint32_t sec_key[CG_NUM_BINS + 1];
+    __shared__ float4 rays[CG_NUM_BINS];
     const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id();
     const uint64_t base = (uint64_t)c * LG_CHUNK;
     const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
     if (tid <= CG_NUM_BINS) sec_key[tid] = cg_fkey(P.default_low);
+    init_rays<FILTER>(P, rays, tid);
     __syncthreads();
     LaneBits<NW> posm;
     uint32_t touched = 0;
     uint2* codes = (uint2*)S.codes + (uint64_t)c * (LG_CHUNK / 8);
-    stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, Nc, L, P, sec_key, posm, touched,
+    stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, Nc, L, P, sec_key, rays, posm, touched,
                                              [&](int g, uint2 cw) { codes[g * CG_BLOCK + tid] = cw; });
     if (GROUND) {
         touched = wave_or(touched);
