@@ -632,7 +632,7 @@ __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const 
 // pcl::VoxelGrid::applyFilter setup (PCL 1.10, src/cone_detection.cpp:240-249) from the
 // getMinMax3D bounds of the nfin finite points: the int64 overflow guard (pass = 1: output the
 // input unchanged) and min_b / div_b of the idx computation.
-__device__ __forceinline__ void voxel_grid_setup(uint32_t nfin, const float* bmn, const float* bmx,
+__host__ __device__ __forceinline__ void voxel_grid_setup(uint32_t nfin, const float* bmn, const float* bmx,
                                                  const CgDevParams& P, uint32_t& pass, int* min_b,
                                                  int* div_b) {
     pass = 0;

@@ -92,21 +92,24 @@ enum { CG_LAYOUT_GENERIC = 0, CG_LAYOUT_XYZI16 = 1, CG_LAYOUT_PCL32 = 2 };
 enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };
 
 // ---- frames of more than CG_MAX_POINTS points (cg_large.hip) ----
+// dense neighbour grid of the global backend: at most LG_DGRID_AXIS cells per axis
+#define LG_DGRID_AXIS 128
+#define LG_DCELLS_MAX (LG_DGRID_AXIS * LG_DGRID_AXIS * LG_DGRID_AXIS)
 #define LG_CHUNK 8192          // points per front workgroup (16 per lane): a 1M frame fills 128
 // per-frame meta words in HBM
 enum {
     LG_SECKEY = 0,             // 18 words: sector minima (order-preserving keys)
-    LG_TOUCHED = 18, LG_K, LG_MC, LG_MS, LG_NFIN,
+    LG_TOUCHED = 18, LG_K, LG_RESERVED, LG_MS, LG_NFIN,
     LG_BMIN, LG_BMAX = LG_BMIN + 3, LG_V = LG_BMAX + 3, LG_C, LG_U, LG_PASS,
     LG_MINB, LG_MUL1 = LG_MINB + 3, LG_MUL2, LG_ORG, LG_NFIN_ALL = LG_ORG + 3, LG_SCAN_N,
+    LG_DGINV, LG_DGN = LG_DGINV + 3, LG_NCELL = LG_DGN + 3,   // dense neighbour grid
     LG_META_WORDS = 64
 };
 struct LgScratch {
     uint32_t* meta;
     uint64_t* codes;          // z codes, [chunk][group][lane] words of 8
-    uint64_t* keep;           // ground-only mode: kept bits, [chunk][lane][2]
+    uint64_t* keep;           // kept bits (ground-only mode) / filter bits (pipeline), [chunk][lane]
     uint32_t* chunk_cnt;      // ground-only mode: kept points per chunk
-    float4* cand_p; uint32_t* cand_i;   // filter candidates (pipeline) and their frame index
     float4* surv_p; uint32_t* surv_i;   // survivors (detector input points)
     uint64_t* key0; uint64_t* key1;     // radix sort ping-pong
     uint32_t* val0; uint32_t* val1;
@@ -115,6 +118,7 @@ struct LgScratch {
     float4* vox;              // voxel points
     uint32_t* run;            // voxel run starts
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
+    uint32_t* cstart;         // dense neighbour grid: per-cell start in ord (LG_DCELLS_MAX + 2)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };

@@ -67,6 +67,46 @@ struct Bounds {
 };
 
 // ------------------------------------------------------------------------------------------
+// Append the lane's points selected by m (point k*CG_BLOCK + tid of the chunk at fb) to the
+// survivor arrays: one wave-wide slot reservation, then four loads in flight per lane. Each
+// survivor carries its frame index (pidx0 + its chunk index), so the order is free.
+template <int LAYOUT, int NW>
+__device__ __forceinline__ void lg_append(const uint8_t* fb, const CgLaunch& L, LgScratch& S, LaneBits<NW> m,
+                                          uint32_t pidx0, Bounds& bd) {
+    const uint32_t tid = threadIdx.x, l = lane_id();
+    const uint32_t n = m.count();
+    const uint32_t incl = wave_incl_scan(n);
+    uint32_t wbase = 0;
+    if (l == 63 && incl) wbase = atomicAdd(&S.meta[LG_MS], incl);
+    wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
+    uint32_t pos = wbase + incl - n;
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) {
+        uint64_t w = m.w[wi];
+        while (w) {
+            int ks[4];
+            float4 pt[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ks[q] = w ? 64 * wi + __builtin_ctzll(w) : -1;
+                if (w) w &= w - 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (ks[q] >= 0) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (ks[q] < 0) continue;
+                S.surv_p[pos] = pt[q];
+                S.surv_i[pos] = pidx0 + (uint32_t)ks[q] * CG_BLOCK + tid;
+                bd.add(pt[q]);
+                pos++;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Front: pass 1 per chunk.
 template <int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
@@ -95,34 +135,18 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
     __syncthreads();
     if (GROUND && tid <= CG_NUM_BINS) atomicMin(&S.meta[LG_SECKEY + tid], sec_key[tid]);
     if (!FILTER) return;
-    // pipeline: filter candidates (ground decided later); detector: the survivors themselves
-    const uint32_t n = posm.count();
-    const uint32_t incl = wave_incl_scan(n);
-    uint32_t wbase = 0;
-    if (l == 63 && incl) wbase = atomicAdd(&S.meta[GROUND ? LG_MC : LG_MS], incl);
-    wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
-    uint32_t pos = wbase + incl - n;
-    float4* const op = GROUND ? S.cand_p : S.surv_p;
-    uint32_t* const oi = GROUND ? S.cand_i : S.surv_i;
-    Bounds bd;
+    if (GROUND) {   // pipeline: the filter bits wait for the ground decision (lg_decide)
 #pragma unroll
-    for (int wi = 0; wi < NW; wi++) {
-        uint64_t m = posm.w[wi];
-        while (m) {
-            const uint32_t k = 64 * wi + __builtin_ctzll(m);
-            m &= m - 1;
-            const uint32_t i = k * CG_BLOCK + tid;
-            const float4 p = load_xyzi<LAYOUT>(fb, i, L);
-            op[pos] = p;
-            oi[pos] = S.pidx_base + (uint32_t)base + i;
-            pos++;
-            if (!GROUND) bd.add(p);
-        }
+        for (int wi = 0; wi < NW; wi++) S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi] = posm.w[wi];
+        return;
     }
-    if (!GROUND) bd.merge(S.meta);
+    // detector: the filter survivors themselves
+    Bounds bd;
+    lg_append<LAYOUT, NW>(fb, L, S, posm, S.pidx_base + (uint32_t)base, bd);
+    bd.merge(S.meta);
 }
 
-// Decide: thresholds, pass 2 per chunk, candidates -> survivors.
+// Decide: thresholds, pass 2 per chunk, survivors = ground-kept & filter bits (from lg_front).
 template <int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
     constexpr int PPT = LG_CHUNK / CG_BLOCK;
@@ -142,9 +166,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
     pass2_keep<PPT, LAYOUT>(fb, Nc, L, P, qlo, qhi, tkey, [&](int g) { return codes[g * CG_BLOCK + tid]; }, keep);
     const uint32_t kc = wave_sum(keep.count());
     if (l == 0) atomicAdd(&kcount, kc);
-    if (KMODE == CG_KMODE_GROUND) {
+    LaneBits<NW> surv;
 #pragma unroll
-        for (int wi = 0; wi < NW; wi++) S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi] = keep.w[wi];
+    for (int wi = 0; wi < NW; wi++) {
+        uint64_t* const kw = S.keep + ((uint64_t)c * CG_BLOCK + tid) * NW + wi;
+        if (KMODE == CG_KMODE_GROUND) *kw = keep.w[wi];
+        else surv.w[wi] = keep.w[wi] & *kw;   // kept by the ground filter and by the position filter
     }
     __syncthreads();
     if (tid == 0) {
@@ -152,43 +179,8 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
         if (KMODE == CG_KMODE_GROUND) S.chunk_cnt[c] = kcount;
     }
     if (KMODE == CG_KMODE_GROUND) return;
-    // this chunk's share of the candidates (written by lg_front, complete at kernel entry)
-    const uint32_t Mc = S.meta[LG_MC];
-    const uint32_t per = (Mc + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = min(Mc, c * per), hi = min(Mc, lo + per);
-    const uint8_t* cb = (const uint8_t*)S.codes;
     Bounds bd;
-    for (uint32_t i0 = lo; i0 < hi; i0 += CG_BLOCK) {   // uniform trip count
-        const uint32_t i = i0 + tid;
-        bool kp = false;
-        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t pidx = 0;
-        if (i < hi) {
-            pidx = S.cand_i[i];
-            p = S.cand_p[i];
-            const uint32_t lp = pidx - S.pidx_base;   // index within this launch's points
-            const uint32_t cc = lp / LG_CHUNK, r = lp % LG_CHUNK, k = r / CG_BLOCK, ln = r % CG_BLOCK;
-            const uint32_t code = cb[(uint64_t)cc * LG_CHUNK + ((k >> 3) * CG_BLOCK + ln) * 8 + (k & 7)];
-            if (zc_kept(code, qlo)) {
-                kp = true;
-            } else if (zc_not_ground(code, qhi)) {   // ambiguous: exact sector and threshold
-                int sx = 0;
-                bool unused = false;
-                classify_angle<true, false>(P, p.x, p.y, sx, unused);
-                kp = !(cg_zkey(p.z) < tkey[sx]);
-            }
-        }
-        const uint64_t bal = __ballot(kp);
-        uint32_t wb = 0;
-        if (l == 0 && bal) wb = atomicAdd(&S.meta[LG_MS], (uint32_t)__popcll(bal));
-        wb = (uint32_t)__builtin_amdgcn_readlane((int)wb, 0);
-        if (kp) {
-            const uint32_t pos = wb + mbcnt(bal);
-            S.surv_p[pos] = p;
-            S.surv_i[pos] = pidx;
-            bd.add(p);
-        }
-    }
+    lg_append<LAYOUT, NW>(fb, L, S, surv, S.pidx_base + (uint32_t)base, bd);
     bd.merge(S.meta);
 }
 
@@ -365,14 +357,15 @@ uint32_t tiles_of(uint64_t n) { return (uint32_t)((n + LG_TILE - 1) / LG_TILE); 
 uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + CG_BLOCK - 1) / CG_BLOCK); }
 uint32_t bits_of(uint64_t v) { uint32_t b = 0; while (b < 64 && (1ull << b) <= v) b++; return b ? b : 1; }
 
-// Sort n pairs in (k[0], v[0]); returns the buffer index (0 or 1) that holds the result.
-int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s) {
+// Stable sort of n pairs in (k[0], v[0]) by key bits [lo, bits); returns the buffer index (0 or
+// 1) that holds the result. The pairs are already in order of the bits below lo.
+int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t lo = 0) {
     uint64_t* k[2] = {S.key0, S.key1};
     uint32_t* v[2] = {S.val0, S.val1};
     int cur = 0;
     if (n <= 1) return cur;
     const uint32_t nt = tiles_of(n);
-    for (uint32_t shift = 0; shift < bits; shift += 8) {
+    for (uint32_t shift = lo; shift < bits; shift += 8) {
         hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist);
         hipLaunchKernelGGL(lg_scan_tiles, dim3(1), dim3(CG_BLOCK), 0, s, S.hist, 256 * nt, (uint32_t*)nullptr);
         hipLaunchKernelGGL(lg_rs_scatter, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
@@ -425,6 +418,25 @@ __global__ void lg_grid_setup(LgScratch S, CgDevParams P, uint32_t npad, uint32_
     m[LG_ORG + 0] = __float_as_uint(nfin ? bmn[0] : 0.f);
     m[LG_ORG + 1] = __float_as_uint(nfin ? bmn[1] : 0.f);
     m[LG_ORG + 2] = __float_as_uint(nfin ? bmn[2] : 0.f);
+    // dense neighbour grid over the bounds: cells of edge >= 1.0625 tol (so an edge joins
+    // voxels in adjacent cells), widened where an axis would need more than LG_DGRID_AXIS
+    uint32_t ncell = 1;
+    for (int a = 0; a < 3; a++) {
+        const float ext = nfin ? bmx[a] - bmn[a] : 0.f;
+        const float q = floorf(ext * P.cell_inv);
+        float inv = P.cell_inv;
+        uint32_t n = 1;
+        if (q >= (float)(LG_DGRID_AXIS - 1)) {          // ext / 127 > 1.0625 tol
+            inv = (float)(LG_DGRID_AXIS - 1) / ext;     // an infinite extent: one cell (inv 0)
+            n = LG_DGRID_AXIS;
+        } else if (q >= 0.f) {
+            n = (uint32_t)q + 1;
+        }
+        m[LG_DGINV + a] = __float_as_uint(inv);
+        m[LG_DGN + a] = n;
+        ncell *= n;
+    }
+    m[LG_NCELL] = ncell;
 }
 
 // keys: passthrough -> pidx; else (PCL idx << PB | pidx), non-finite idx = 0xffffffff (last)
@@ -485,7 +497,15 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
     }
     const uint32_t s = S.run[v], e = v + 1 < V ? S.run[v + 1] : m[LG_NFIN_ALL];
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-    for (uint32_t r = s; r < e; r++) {
+    uint32_t r = s;
+    for (; r + 4 <= e; r += 4) {   // four members in flight, summed in order
+        float4 pv[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) pv[b] = lg_point(S, val[r + b], Ms);
+#pragma unroll
+        for (int b = 0; b < 4; b++) { sx += pv[b].x; sy += pv[b].y; sz += pv[b].z; si += pv[b].w; }
+    }
+    for (; r < e; r++) {
         const float4 p = lg_point(S, val[r], Ms);
         sx += p.x; sy += p.y; sz += p.z; si += p.w;
     }
@@ -495,84 +515,181 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
     vox_out[v] = c;
 }
 
-// neighbour grid: cells of edge >= tolerance, so an edge joins voxels in adjacent cells
-__device__ __forceinline__ uint32_t lg_cell(float c, float o, float inv) {
+// ------------------------------------------------------------------------------------------
+// Euclidean clustering over the V voxels (FLANN L2_Simple predicate, PCL's seed = the lowest
+// index of each component):
+//   dense neighbour grid: voxel -> cell (atomic slot), exclusive scan of the cell counts,
+//   fill: ord holds the voxels cell by cell, cstart[c] the first of cell c;
+//   forest: every voxel points at its lowest adjacent voxel (<= itself), no atomics; the
+//   trees lie inside components and are rooted at their lowest index;
+//   flatten: pointer jumping;
+//   cross: only edges between different trees are united (uf_union hooks the larger root
+//   under the smaller, so roots stay the components' lowest indices).
+__device__ __forceinline__ uint32_t lg_dcell(float c, float o, float inv, uint32_t n) {
     const float q = floorf((c - o) * inv);
-    if (!(q >= 0.f)) return 0u;
-    return q >= 1023.f ? 1023u : (uint32_t)q;
+    if (!(q >= 0.f)) return 0u;                      // NaN or below the origin
+    return q >= (float)(n - 1) ? n - 1 : (uint32_t)q;   // clamped: a superset of neighbours
 }
-__global__ __launch_bounds__(CG_BLOCK) void lg_cell_keys(LgScratch S, CgDevParams P, uint32_t V, uint32_t VB) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
-    if (v >= V) return;
-    const float ox = __uint_as_float(S.meta[LG_ORG]), oy = __uint_as_float(S.meta[LG_ORG + 1]),
-                oz = __uint_as_float(S.meta[LG_ORG + 2]);
-    const float4 q = S.vox[v];
-    const uint32_t ck = (lg_cell(q.z, oz, P.cell_inv) << 20) | (lg_cell(q.y, oy, P.cell_inv) << 10) |
-                        lg_cell(q.x, ox, P.cell_inv);
-    S.key0[v] = ((uint64_t)ck << VB) | v;
-    S.val0[v] = v;
-}
-struct CellHead {
-    const uint64_t* key; uint32_t VB;
-    __device__ uint32_t operator()(uint32_t r) const {
-        return (r == 0 || (key[r] >> VB) != (key[r - 1] >> VB)) ? 1u : 0u;
-    }
-};
-struct CellEmit {
-    const uint64_t* key; uint32_t VB; uint32_t* uk; uint32_t* ca;
-    __device__ void operator()(uint32_t r, uint32_t u) const { uk[u] = (uint32_t)(key[r] >> VB); ca[u] = r; }
-};
-__global__ __launch_bounds__(CG_BLOCK) void lg_cell_order(LgScratch S, uint32_t V, uint32_t VB, int buf) {
-    const uint32_t r = blockIdx.x * CG_BLOCK + threadIdx.x;
-    const uint64_t* key = buf ? S.key1 : S.key0;
-    if (r < V) S.ord[r] = (uint32_t)(key[r] & ((1ull << VB) - 1ull));
-    if (r == 0) S.ca[S.meta[LG_U]] = V;
-}
-
-// union over all pairs (v < u) with fl(((dx^2) + dy^2) + dz^2) < r2 (FLANN L2_Simple). One
-// wave per voxel: for each of the 9 (z, y) rows of neighbour cells, the cells x-1..x+1 are
-// consecutive in the cell-sorted order, so their voxels form one contiguous range of ord[]
-// that the 64 lanes stride over.
-__global__ __launch_bounds__(CG_BLOCK) void lg_union(LgScratch S, CgDevParams P, uint32_t V) {
-    const uint32_t v = blockIdx.x * WAVES + wave_id(), l = lane_id();
-    if (v >= V) return;
-    const uint32_t U = S.meta[LG_U];
-    const float ox = __uint_as_float(S.meta[LG_ORG]), oy = __uint_as_float(S.meta[LG_ORG + 1]),
-                oz = __uint_as_float(S.meta[LG_ORG + 2]);
-    const float4 q = S.vox[v];
-    const uint32_t cx = lg_cell(q.x, ox, P.cell_inv), cy = lg_cell(q.y, oy, P.cell_inv), cz = lg_cell(q.z, oz, P.cell_inv);
-    const uint32_t xlo = cx > 0 ? cx - 1 : 0, xhi = cx < 1023 ? cx + 1 : 1023;
-    for (int dz = -1; dz <= 1; dz++) {
-        const int zz = (int)cz + dz;
-        if (zz < 0 || zz > 1023) continue;
-        for (int dy = -1; dy <= 1; dy++) {
-            const int yy = (int)cy + dy;
-            if (yy < 0 || yy > 1023) continue;
-            const uint32_t lo = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xlo;
-            const uint32_t hi = ((uint32_t)zz << 20) | ((uint32_t)yy << 10) | xhi;
-            uint32_t a = 0, b = U;       // first cell >= lo
-            while (a < b) {
-                const uint32_t mid = (a + b) >> 1;
-                if (S.uk[mid] < lo) a = mid + 1; else b = mid;
-            }
-            uint32_t e = a, b2 = U;      // first cell > hi
-            while (e < b2) {
-                const uint32_t mid = (e + b2) >> 1;
-                if (S.uk[mid] <= hi) e = mid + 1; else b2 = mid;
-            }
-            const uint32_t j1 = S.ca[e];
-            for (uint32_t j = S.ca[a] + l; j < j1; j += 64) {
-                const uint32_t o = S.ord[j];
-                if (o <= v) continue;
-                const float4 p = S.vox[o];
-                const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
-                float acc = ddx * ddx;
-                acc = acc + ddy * ddy;
-                acc = acc + ddz * ddz;
-                if (acc < P.r2) uf_union(S.par, v, o);
-            }
+struct LgGrid {
+    float o[3], inv[3];
+    uint32_t n[3];
+    __device__ explicit LgGrid(const uint32_t* m) {
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            o[a] = __uint_as_float(m[LG_ORG + a]);
+            inv[a] = __uint_as_float(m[LG_DGINV + a]);
+            n[a] = m[LG_DGN + a];
         }
     }
+    __device__ void cell(const float4& q, uint32_t& cx, uint32_t& cy, uint32_t& cz) const {
+        cx = lg_dcell(q.x, o[0], inv[0], n[0]);
+        cy = lg_dcell(q.y, o[1], inv[1], n[1]);
+        cz = lg_dcell(q.z, o[2], inv[2], n[2]);
+    }
+    __device__ uint32_t id(uint32_t cx, uint32_t cy, uint32_t cz) const { return cx + n[0] * (cy + n[1] * cz); }
+};
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_zero(LgScratch S) {
+    const uint32_t n = S.meta[LG_NCELL] + 1;
+    for (uint32_t i = blockIdx.x * CG_BLOCK + threadIdx.x; i < n; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_count(LgScratch S, uint32_t V) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const LgGrid g(S.meta);
+    uint32_t cx, cy, cz;
+    g.cell(S.vox[v], cx, cy, cz);
+    const uint32_t c = g.id(cx, cy, cz);
+    S.uk[v] = c;
+    S.ca[v] = atomicAdd(&S.cstart[c], 1u);
+}
+// exclusive scan of cstart[0, ncell] in place: tile sums (LG_TILE per block), one-block scan of
+// the tile sums (in S.hist), then each tile rescanned with its base
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_tiles(LgScratch S) {
+    __shared__ uint32_t red[WAVES];
+    const uint32_t n = S.meta[LG_NCELL] + 1;
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
+    if ((uint64_t)blockIdx.x * LG_TILE >= n) return;
+    uint32_t c = 0;
+    for (int q = 0; q < 8; q++) c += (b0 + q < n) ? S.cstart[b0 + q] : 0u;
+    c = wave_sum(c);
+    if (lane_id() == 0) red[wave_id()] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < WAVES; w++) t += red[w];
+        S.hist[blockIdx.x] = t;
+    }
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_scan(LgScratch S) {
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t nt = (S.meta[LG_NCELL] + 1 + LG_TILE - 1) / LG_TILE;
+    block_scan(nt, [&](uint32_t i) -> uint32_t { return S.hist[i]; },
+               [&](uint32_t i, uint32_t e) { S.hist[i] = e; }, red);
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_emit(LgScratch S) {
+    __shared__ uint32_t red[WAVES];
+    const uint32_t n = S.meta[LG_NCELL] + 1;
+    if ((uint64_t)blockIdx.x * LG_TILE >= n) return;
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
+    uint32_t x[8], c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) { x[q] = (b0 + q < n) ? S.cstart[b0 + q] : 0u; c += x[q]; }
+    const uint32_t inc = wave_incl_scan(c);
+    if (lane_id() == 63) red[wave_id()] = inc;
+    __syncthreads();
+    uint32_t pos = S.hist[blockIdx.x] + inc - c;
+    for (uint32_t w = 0; w < wave_id(); w++) pos += red[w];
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if (b0 + q < n) { S.cstart[b0 + q] = pos; pos += x[q]; }
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_fill(LgScratch S, uint32_t V) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v < V) S.ord[S.cstart[S.uk[v]] + S.ca[v]] = v;
+}
+// The voxels of the 27 cells around voxel q, visited by one wave: lanes 0-8 look up the nine
+// (z, y) rows, whose cells x-1..x+1 are consecutive in ord; then the 64 lanes stride each row.
+template <class F>
+__device__ __forceinline__ void lg_neighbours(const LgScratch& S, const LgGrid& g, const float4& q, F visit) {
+    const uint32_t l = lane_id();
+    uint32_t cx, cy, cz;
+    g.cell(q, cx, cy, cz);
+    uint32_t b = 0, e = 0;
+    if (l < 9) {
+        const int zz = (int)cz + (int)(l / 3) - 1, yy = (int)cy + (int)(l % 3) - 1;
+        if (zz >= 0 && zz < (int)g.n[2] && yy >= 0 && yy < (int)g.n[1]) {
+            const uint32_t xlo = cx > 0 ? cx - 1 : 0u, xhi = cx + 1 < g.n[0] ? cx + 1 : g.n[0] - 1;
+            b = S.cstart[g.id(xlo, (uint32_t)yy, (uint32_t)zz)];
+            e = S.cstart[g.id(xhi, (uint32_t)yy, (uint32_t)zz) + 1];
+        }
+    }
+    for (int r = 0; r < 9; r++) {
+        const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)b, r);
+        const uint32_t re = (uint32_t)__builtin_amdgcn_readlane((int)e, r);
+        for (uint32_t j = rb + l; j < re; j += 64) visit(S.ord[j]);
+    }
+}
+__device__ __forceinline__ bool lg_adjacent(const float4& q, const float4& p, float r2) {
+    const float ddx = q.x - p.x, ddy = q.y - p.y, ddz = q.z - p.z;
+    float acc = ddx * ddx;
+    acc = acc + ddy * ddy;
+    acc = acc + ddz * ddz;
+    return acc < r2;
+}
+// forest: par[v] = lowest adjacent voxel index, or v (one wave per voxel)
+__global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P, uint32_t V) {
+    const uint32_t v = blockIdx.x * WAVES + wave_id();
+    if (v >= V) return;
+    const LgGrid g(S.meta);
+    const float4 q = S.vox[v];
+    uint32_t lo = v;
+    lg_neighbours(S, g, q, [&](uint32_t o) {
+        if (o < lo && lg_adjacent(q, S.vox[o], P.r2)) lo = o;
+    });
+    lo = wave_umin(lo);
+    if (lane_id() == 0) S.par[v] = lo;
+}
+// flatten in LDS (V <= LG_FLAT_LDS): rounds of par[x] = par[par[x]] until nothing changes
+#define LG_FLAT_LDS 32768
+__global__ __launch_bounds__(CG_BLOCK) void lg_flatten_lds(LgScratch S, uint32_t V) {
+    __shared__ uint32_t par[LG_FLAT_LDS];
+    __shared__ uint32_t changed[2];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t x = tid; x < V; x += CG_BLOCK) par[x] = S.par[x];
+    if (tid < 2) changed[tid] = 0;
+    __syncthreads();
+    for (uint32_t r = 0;; r++) {
+        bool ch = false;
+        for (uint32_t x = tid; x < V; x += CG_BLOCK) {
+            const uint32_t p = par[x], pp = par[p];
+            if (pp != p) { par[x] = pp; ch = true; }
+        }
+        if (__ballot(ch) && lane_id() == 0) changed[r & 1] = 1;
+        __syncthreads();
+        const bool any = changed[r & 1] != 0;
+        if (tid == 0) changed[(r + 1) & 1] = 0;
+        __syncthreads();
+        if (!any) break;
+    }
+    for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = par[x];
+}
+// one global pointer-jumping round (larger V; the cross step's finds finish any leftover depth)
+__global__ __launch_bounds__(CG_BLOCK) void lg_jump(LgScratch S, uint32_t V) {
+    const uint32_t x = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (x >= V) return;
+    const uint32_t p = ld_rlx(S.par + x), pp = ld_rlx(S.par + p);
+    if (pp != p) st_rlx(S.par + x, pp);
+}
+// cross-tree edges (v < o): united unless both ends already share a parent
+__global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P, uint32_t V) {
+    const uint32_t v = blockIdx.x * WAVES + wave_id();
+    if (v >= V) return;
+    const LgGrid g(S.meta);
+    const float4 q = S.vox[v];
+    lg_neighbours(S, g, q, [&](uint32_t o) {
+        if (o > v && lg_adjacent(q, S.vox[o], P.r2) && ld_rlx(S.par + o) != ld_rlx(S.par + v))
+            uf_union(S.par, v, o);
+    });
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_find(LgScratch S, uint32_t V) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
@@ -593,6 +710,7 @@ struct KeepEmit {
     __device__ void operator()(uint32_t v, uint32_t d) const { droot[d] = v; dsz[d] = cnt[v]; }
 };
 
+#define LG_ORDER_LDS 8192
 // cluster order: PCL sorts the reversed discovery list ascending by size with std::sort
 // (restated, cg_sort.h); <= 16 clusters is an insertion sort: (size desc, seed asc)
 __global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
@@ -601,18 +719,21 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
     const uint32_t tid = threadIdx.x;
     const uint32_t C = S.meta[LG_C];
     if (C > CG_SORT_THRESHOLD) {
-        if (tid == 0) {
-            uint64_t* rec = S.key0;
-            for (uint32_t i = 0; i < C; i++) {
-                const uint32_t d = C - 1 - i;
-                rec[i] = ((uint64_t)S.dsz[d] << 32) | d;
-            }
+        // one lane runs the introsort restatement, on LDS records when they fit
+        __shared__ uint64_t lrec[LG_ORDER_LDS];
+        uint64_t* rec = C <= LG_ORDER_LDS ? lrec : S.key0;
+        for (uint32_t i = tid; i < C; i += CG_BLOCK) {
+            const uint32_t d = C - 1 - i;
+            rec[i] = ((uint64_t)S.dsz[d] << 32) | d;
+        }
+        __syncthreads();
+        if (tid == 0)
             cg_std_sort(rec, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, stk);
-            for (uint32_t k = 0; k < C; k++) {
-                const uint32_t d = (uint32_t)rec[C - 1 - k];
-                S.fin[k] = d;
-                S.rank[d] = k;
-            }
+        __syncthreads();
+        for (uint32_t k = tid; k < C; k += CG_BLOCK) {
+            const uint32_t d = (uint32_t)rec[C - 1 - k];
+            S.fin[k] = d;
+            S.rank[d] = k;
         }
     } else {
         for (uint32_t d = tid; d < C; d += CG_BLOCK) {
@@ -662,25 +783,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr(CgLaunch L, LgScratch S, uint
     }
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
-    const uint32_t k = blockIdx.x * CG_BLOCK + threadIdx.x;
+    // one wave per cluster: the lanes fetch 64 members at a time, the sums run through them in
+    // ascending member order (lane order), as the reference's loop does
+    const uint32_t k = blockIdx.x * WAVES + wave_id(), l = lane_id();
     const uint32_t C = S.meta[LG_C];
     if (k >= C) return;
     const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const uint32_t s = S.off[k], e = S.off[k + 1];
     float x = 0.0f, y = 0.0f;
-    uint32_t i = s;
-    for (; i + 8 <= e; i += 8) {   // members fetched eight at a time, summed in order
-        float2 pv[8];
-#pragma unroll
-        for (int b = 0; b < 8; b++) { const float4 p = S.vox[idx[i + b]]; pv[b] = make_float2(p.x, p.y); }
-#pragma unroll
-        for (int b = 0; b < 8; b++) { x += pv[b].x; y += pv[b].y; }
+    for (uint32_t i0 = s; i0 < e; i0 += 64) {
+        const uint32_t n = min(64u, e - i0);
+        float px = 0.f, py = 0.f;
+        if (l < n) { const float4 p = S.vox[idx[i0 + l]]; px = p.x; py = p.y; }
+        for (uint32_t b = 0; b < n; b++) {
+            x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), (int)b));
+            y += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), (int)b));
+        }
     }
-    for (; i < e; i++) {
-        const float4 p = S.vox[idx[i]];
-        x += p.x;
-        y += p.y;
-    }
+    if (l != 0) return;
     const int j = (int)(e - s);
     const float px = x / (float)j, py = y / (float)j;
     const double Sq = ((double)px * (double)px + (double)py * (double)py) + 0.0;
@@ -770,9 +890,28 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     if (Mtot <= CG_MMAX && !S.force_global) return cg_launch_lg_back_small(Lh, P, S, f, npad, K, s);
     const uint32_t PB = bits_of((uint64_t)N + npad);
     const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
+    // the voxel keys' idx width from the bounds the host already holds (lg_grid_setup's own
+    // computation): one bit above the largest idx keeps non-finite points (idx all ones) last
+    uint32_t key_bits = 32 + PB;
+    {
+        float bmn[3], bmx[3];
+        uint32_t nfin = hm[LG_NFIN];
+        for (int a = 0; a < 3; a++) {
+            bmn[a] = nfin ? cg_fkey_inv(hm[LG_BMIN + a]) : INFINITY;
+            bmx[a] = nfin ? cg_fkey_inv(hm[LG_BMAX + a]) : -INFINITY;
+            if (npad) { bmn[a] = std::min(bmn[a], 0.f); bmx[a] = std::max(bmx[a], 0.f); }
+        }
+        nfin += npad;
+        uint32_t pass = 0;
+        int min_b[3], div_b[3];
+        voxel_grid_setup(nfin, bmn, bmx, P, pass, min_b, div_b);
+        if (pass) key_bits = PB;
+        else key_bits = PB + 1 + bits_of((uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2]);
+        key_bits = std::min<uint32_t>(key_bits, 32 + PB);
+    }
     hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad, Mtot);
     hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
-    int buf = radix_sort(S, Mtot, 32 + PB, s);
+    int buf = radix_sort(S, Mtot, key_bits, s);
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     // runs over the finite points (non-finite keys sort last); passthrough: every point
     scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
@@ -783,19 +922,30 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     const uint32_t VB = bits_of(V);
     const uint32_t vb = std::max<uint32_t>(1, blocks_of(V));
     if (V > 0) {
-        hipLaunchKernelGGL(lg_cell_keys, dim3(vb), dim3(CG_BLOCK), 0, s, S, P, V, VB);
-        const int cb = radix_sort(S, V, 30 + VB, s);
-        const uint64_t* ckey = cb ? S.key1 : S.key0;
-        scan_emit(S, V, -1, CellHead{ckey, VB}, CellEmit{ckey, VB, S.uk, S.ca}, LG_U, s);
-        hipLaunchKernelGGL(lg_cell_order, dim3(vb), dim3(CG_BLOCK), 0, s, S, V, VB, cb);
-        hipLaunchKernelGGL(lg_union, dim3((V + WAVES - 1) / WAVES), dim3(CG_BLOCK), 0, s, S, P, V);
+        const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;   // tiles past ncell return at once
+        hipLaunchKernelGGL(lg_dgrid_zero, dim3(256), dim3(CG_BLOCK), 0, s, S);
+        hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
+        hipLaunchKernelGGL(lg_dgrid_tiles, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+        hipLaunchKernelGGL(lg_dgrid_scan, dim3(1), dim3(CG_BLOCK), 0, s, S);
+        hipLaunchKernelGGL(lg_dgrid_emit, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+        hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
+        const uint32_t wb = (V + WAVES - 1) / WAVES;
+        hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P, V);
+        if (V <= LG_FLAT_LDS) {
+            hipLaunchKernelGGL(lg_flatten_lds, dim3(1), dim3(CG_BLOCK), 0, s, S, V);
+        } else {
+            for (int r = 0; r < 12; r++) hipLaunchKernelGGL(lg_jump, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
+        }
+        hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P, V);
         hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
         scan_emit(S, V, -1, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
         hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
         hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, S, f, V, VB);
-        const int kb = radix_sort(S, V, 2 * VB, s);
+        // (rank, voxel) keys are written in voxel order: only the rank bits need sorting, and
+        // rank < C <= V, one bit more than V needs tells ranks from the non-members' ~0 keys
+        const int kb = radix_sort(S, V, VB + bits_of(V) + 1, s, VB);
         hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)V + 1)), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, kb, Mtot, K);
-        hipLaunchKernelGGL(lg_centroids, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
+        hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
     } else {
         hipLaunchKernelGGL(lg_csr, dim3(1), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, 0, Mtot, K);
     }
@@ -839,15 +989,15 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(1, take(nch * LG_CHUNK));
     place(2, take(nch * CG_BLOCK * 2 * 8));
     place(3, take(nch * 4 + 4));
-    place(4, take(N * 16)); place(5, take(N * 4));
     place(6, take(N * 16)); place(7, take(N * 4));
     place(8, take(N * 8)); place(9, take(N * 8));
     place(10, take(N * 4)); place(11, take(N * 4));
-    place(12, take((256 * nt + 2) * 4));
+    place(12, take((std::max<uint64_t>(256 * nt, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
     place(13, take((nt + 2) * 4));
     place(14, take(N * 16));
     place(15, take((N + 2) * 4));
     for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));
+    place(28, take((uint64_t)(LG_DCELLS_MAX + 2) * 4));
     return off;
 }
 }  // namespace
@@ -861,8 +1011,6 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 1: S.codes = (uint64_t*)p; break;
             case 2: S.keep = (uint64_t*)p; break;
             case 3: S.chunk_cnt = (uint32_t*)p; break;
-            case 4: S.cand_p = (float4*)p; break;
-            case 5: S.cand_i = (uint32_t*)p; break;
             case 6: S.surv_p = (float4*)p; break;
             case 7: S.surv_i = (uint32_t*)p; break;
             case 8: S.key0 = (uint64_t*)p; break;
@@ -873,6 +1021,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 13: S.tsum = (uint32_t*)p; break;
             case 14: S.vox = (float4*)p; break;
             case 15: S.run = (uint32_t*)p; break;
+            case 28: S.cstart = (uint32_t*)p; break;
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
     });
