@@ -134,6 +134,7 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
 int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                    bool init);
 int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f);
+#define CG_K_FROM_META 0xffffffffu   // cg_large_backend: read K from the frame's meta words
 int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t n_total, uint32_t K);
 // A tiled frame's gathered survivors and merged counts (K, Ms, nfin, bounds keys) into S.

@@ -271,10 +271,32 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_tiles(uint32_t* a, uint32_t 
     }
 }
 template <class FLAG, class EMIT>
-__global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, const uint32_t* meta, FLAG flag,
-                                                         EMIT emit, const uint32_t* tsum) {
+__global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, uint32_t* meta, FLAG flag,
+                                                         EMIT emit, const uint32_t* tsum, int total_word) {
     __shared__ uint32_t red[WAVES];
+    __shared__ uint32_t tbase;
     if (n_word >= 0) n = meta[n_word];
+    {   // this tile's base: the raw counts of the tiles before it (block 0 also writes the total)
+        __shared__ uint32_t pw[WAVES], tw[WAVES];
+        const uint32_t nt = gridDim.x, b = blockIdx.x;
+        uint32_t pre = 0, tot = 0;
+        for (uint32_t t = threadIdx.x; t < nt; t += CG_BLOCK) {
+            const uint32_t c = tsum[t];
+            tot += c;
+            pre += t < b ? c : 0u;
+        }
+        pre = wave_sum(pre);
+        tot = wave_sum(tot);
+        if (lane_id() == 0) { pw[wave_id()] = pre; tw[wave_id()] = tot; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t p = 0, t = 0;
+            for (int w = 0; w < WAVES; w++) { p += pw[w]; t += tw[w]; }
+            tbase = p;
+            if (b == 0) meta[total_word] = t;
+        }
+        __syncthreads();
+    }
     const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
     uint32_t fl[8], c = 0;
 #pragma unroll
@@ -284,7 +306,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word,
     __syncthreads();
     uint32_t wo = 0;
     for (uint32_t w = 0; w < wave_id(); w++) wo += red[w];
-    uint32_t pos = tsum[blockIdx.x] + wo + inc - c;
+    uint32_t pos = tbase + wo + inc - c;
 #pragma unroll
     for (int q = 0; q < 8; q++)
         if (fl[q]) emit((uint32_t)(b0 + q), pos++);
@@ -293,8 +315,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word,
 // ------------------------------------------------------------------------------------------
 // Stable LSD radix sort of (64-bit key, 32-bit value) pairs, 8 bits per pass.
 __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint32_t n, uint32_t shift,
-                                                       uint32_t* hist) {
+                                                       uint32_t* hist, const uint32_t* n_dev) {
     __shared__ uint32_t h[256];
+    if (n_dev) n = *n_dev;   // count known on the device only (grid sized for an upper bound)
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE;
@@ -305,17 +328,35 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint
     __syncthreads();
     if (threadIdx.x < 256) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
-// hist (scanned, digit-major) gives each (digit, tile) its output base. Within a tile the
+// hist (raw counts, digit-major) gives each (digit, tile) its output base. Within a tile the
 // elements go in 8 rounds of 512 in index order; a round ranks equal digits per wave with
 // eight ballots (the wave's lanes whose digit matches bit for bit) and offsets waves by the
 // per-wave digit counts of the round, so equal keys keep their input order (stable).
 __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                                           uint32_t* vout, uint32_t n, uint32_t shift,
-                                                          const uint32_t* hist) {
+                                                          const uint32_t* hist, const uint32_t* n_dev) {
+    if (n_dev) n = *n_dev;
     __shared__ uint32_t run[256];
     __shared__ uint32_t wcnt[WAVES][256];
+    __shared__ uint32_t red[8 * WAVES];
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
-    if (tid < 256) run[tid] = hist[tid * gridDim.x + blockIdx.x];
+    // this tile's base per digit from the raw (digit-major) counts: the digit's offset (all
+    // tiles' counts of smaller digits) plus its count in the tiles before this one
+    {
+        const uint32_t nt = gridDim.x, b = blockIdx.x;
+        uint32_t tot = 0, pre = 0;
+        if (tid < 256) {
+            const uint32_t* h = hist + (uint64_t)tid * nt;
+            for (uint32_t t = 0; t < nt; t++) {
+                const uint32_t c = h[t];
+                tot += c;
+                pre += t < b ? c : 0u;
+            }
+        }
+        block_scan(256, [&](uint32_t i) -> uint32_t { return tot; },
+                   [&](uint32_t i, uint32_t e) { run[i] = e + pre; }, red);
+    }
+    __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE;
     const uint64_t lt = (1ull << l) - 1ull;
     for (int q = 0; q < 8; q++) {
@@ -358,18 +399,19 @@ uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + CG_BLOCK - 1) / CG_BLOCK
 uint32_t bits_of(uint64_t v) { uint32_t b = 0; while (b < 64 && (1ull << b) <= v) b++; return b ? b : 1; }
 
 // Stable sort of n pairs in (k[0], v[0]) by key bits [lo, bits); returns the buffer index (0 or
-// 1) that holds the result. The pairs are already in order of the bits below lo.
-int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t lo = 0) {
+// 1) that holds the result. The pairs are already in order of the bits below lo. With n_dev,
+// the count is read on the device and n is only its upper bound.
+int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t lo = 0,
+               const uint32_t* n_dev = nullptr) {
     uint64_t* k[2] = {S.key0, S.key1};
     uint32_t* v[2] = {S.val0, S.val1};
     int cur = 0;
     if (n <= 1) return cur;
     const uint32_t nt = tiles_of(n);
     for (uint32_t shift = lo; shift < bits; shift += 8) {
-        hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist);
-        hipLaunchKernelGGL(lg_scan_tiles, dim3(1), dim3(CG_BLOCK), 0, s, S.hist, 256 * nt, (uint32_t*)nullptr);
+        hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist, n_dev);
         hipLaunchKernelGGL(lg_rs_scatter, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
-                           shift, S.hist);
+                           shift, S.hist, n_dev);
         cur ^= 1;
     }
     return cur;
@@ -379,9 +421,8 @@ template <class FLAG, class EMIT>
 void scan_emit(LgScratch& S, uint32_t n_max, int n_word, FLAG flag, EMIT emit, int total_word, hipStream_t s) {
     const uint32_t nt = std::max<uint32_t>(1, tiles_of(n_max));
     hipLaunchKernelGGL((lg_scan_count<FLAG>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, S.tsum);
-    hipLaunchKernelGGL(lg_scan_tiles, dim3(1), dim3(CG_BLOCK), 0, s, S.tsum, nt, S.meta + total_word);
     hipLaunchKernelGGL((lg_scan_emit<FLAG, EMIT>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, emit,
-                       S.tsum);
+                       S.tsum, total_word);
 }
 
 }  // namespace
@@ -552,8 +593,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_zero(LgScratch S) {
     const uint32_t n = S.meta[LG_NCELL] + 1;
     for (uint32_t i = blockIdx.x * CG_BLOCK + threadIdx.x; i < n; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
 }
-__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_count(LgScratch S, uint32_t V) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_count(LgScratch S) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
     if (v >= V) return;
     const LgGrid g(S.meta);
     uint32_t cx, cy, cz;
@@ -603,8 +644,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_emit(LgScratch S) {
     for (int q = 0; q < 8; q++)
         if (b0 + q < n) { S.cstart[b0 + q] = pos; pos += x[q]; }
 }
-__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_fill(LgScratch S, uint32_t V) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_fill(LgScratch S) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
     if (v < V) S.ord[S.cstart[S.uk[v]] + S.ca[v]] = v;
 }
 // The voxels of the 27 cells around voxel q, visited by one wave: lanes 0-8 look up the nine
@@ -637,8 +678,8 @@ __device__ __forceinline__ bool lg_adjacent(const float4& q, const float4& p, fl
     return acc < r2;
 }
 // forest: par[v] = lowest adjacent voxel index, or v (one wave per voxel)
-__global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P, uint32_t V) {
-    const uint32_t v = blockIdx.x * WAVES + wave_id();
+__global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P) {
+    const uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V];
     if (v >= V) return;
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
@@ -649,13 +690,16 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P
     lo = wave_umin(lo);
     if (lane_id() == 0) S.par[v] = lo;
 }
-// flatten in LDS (V <= LG_FLAT_LDS): rounds of par[x] = par[par[x]] until nothing changes
+// flatten: rounds of par[x] = par[par[x]] until nothing changes, in LDS when V <= LG_FLAT_LDS
+// (else on the HBM array, still one workgroup: its barriers order the rounds)
 #define LG_FLAT_LDS 32768
-__global__ __launch_bounds__(CG_BLOCK) void lg_flatten_lds(LgScratch S, uint32_t V) {
-    __shared__ uint32_t par[LG_FLAT_LDS];
+__global__ __launch_bounds__(CG_BLOCK) void lg_flatten(LgScratch S) {
+    __shared__ uint32_t lpar[LG_FLAT_LDS];
     __shared__ uint32_t changed[2];
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t x = tid; x < V; x += CG_BLOCK) par[x] = S.par[x];
+    const uint32_t tid = threadIdx.x, V = S.meta[LG_V];
+    uint32_t* const par = V <= LG_FLAT_LDS ? lpar : S.par;
+    if (V <= LG_FLAT_LDS)
+        for (uint32_t x = tid; x < V; x += CG_BLOCK) lpar[x] = S.par[x];
     if (tid < 2) changed[tid] = 0;
     __syncthreads();
     for (uint32_t r = 0;; r++) {
@@ -671,18 +715,12 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_flatten_lds(LgScratch S, uint32_t
         __syncthreads();
         if (!any) break;
     }
-    for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = par[x];
-}
-// one global pointer-jumping round (larger V; the cross step's finds finish any leftover depth)
-__global__ __launch_bounds__(CG_BLOCK) void lg_jump(LgScratch S, uint32_t V) {
-    const uint32_t x = blockIdx.x * CG_BLOCK + threadIdx.x;
-    if (x >= V) return;
-    const uint32_t p = ld_rlx(S.par + x), pp = ld_rlx(S.par + p);
-    if (pp != p) st_rlx(S.par + x, pp);
+    if (V <= LG_FLAT_LDS)
+        for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = lpar[x];
 }
 // cross-tree edges (v < o): united unless both ends already share a parent
-__global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P, uint32_t V) {
-    const uint32_t v = blockIdx.x * WAVES + wave_id();
+__global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P) {
+    const uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V];
     if (v >= V) return;
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
@@ -691,8 +729,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P,
             uf_union(S.par, v, o);
     });
 }
-__global__ __launch_bounds__(CG_BLOCK) void lg_find(LgScratch S, uint32_t V) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+__global__ __launch_bounds__(CG_BLOCK) void lg_find(LgScratch S) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
     if (v >= V) return;
     const uint32_t r = uf_find(S.par, v);
     S.lab[v] = r;
@@ -754,8 +792,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
     for (uint32_t d = tid; d < C; d += CG_BLOCK) S.rk[S.droot[d]] = S.rank[d];
 }
 // labels (cluster rank or -1) and the (rank, voxel) keys of the CSR sort
-__global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, uint32_t f, uint32_t V, uint32_t VB) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+__global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, uint32_t f, uint32_t VB) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
     if (v >= V) return;
     const uint32_t rk = S.rk[S.lab[v]];
     (L.lab + (uint64_t)f * L.cap)[v] = rk == 0xffffffffu ? -1 : (int32_t)rk;
@@ -883,6 +921,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     const uint32_t Ms = hm[LG_MS];
+    if (K == CG_K_FROM_META) K = hm[LG_K];   // pipeline frames: the ground stage's kept count
     const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
     const uint32_t Mtot = Ms + npad;
     CgLaunch Lh = L;
@@ -916,45 +955,36 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     // runs over the finite points (non-finite keys sort last); passthrough: every point
     scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
     hipLaunchKernelGGL(lg_voxel_centroids, dim3(mb), dim3(CG_BLOCK), 0, s, Lh, S, f, Mtot, buf);
-    if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    const uint32_t V = hm[LG_V];
-    const uint32_t VB = bits_of(V);
-    const uint32_t vb = std::max<uint32_t>(1, blocks_of(V));
-    if (V > 0) {
-        const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;   // tiles past ncell return at once
-        hipLaunchKernelGGL(lg_dgrid_zero, dim3(256), dim3(CG_BLOCK), 0, s, S);
-        hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
-        hipLaunchKernelGGL(lg_dgrid_tiles, dim3(gt), dim3(CG_BLOCK), 0, s, S);
-        hipLaunchKernelGGL(lg_dgrid_scan, dim3(1), dim3(CG_BLOCK), 0, s, S);
-        hipLaunchKernelGGL(lg_dgrid_emit, dim3(gt), dim3(CG_BLOCK), 0, s, S);
-        hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
-        const uint32_t wb = (V + WAVES - 1) / WAVES;
-        hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P, V);
-        if (V <= LG_FLAT_LDS) {
-            hipLaunchKernelGGL(lg_flatten_lds, dim3(1), dim3(CG_BLOCK), 0, s, S, V);
-        } else {
-            for (int r = 0; r < 12; r++) hipLaunchKernelGGL(lg_jump, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
-        }
-        hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P, V);
-        hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S, V);
-        scan_emit(S, V, -1, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
-        hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
-        hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, S, f, V, VB);
-        // (rank, voxel) keys are written in voxel order: only the rank bits need sorting, and
-        // rank < C <= V, one bit more than V needs tells ranks from the non-members' ~0 keys
-        const int kb = radix_sort(S, V, VB + bits_of(V) + 1, s, VB);
-        hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)V + 1)), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, kb, Mtot, K);
-        hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
-    } else {
-        hipLaunchKernelGGL(lg_csr, dim3(1), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, 0, Mtot, K);
-    }
+    // V is known on the device only: the clustering launches are sized for V <= Mtot and read
+    // V from the meta words (no host round trip)
+    const uint32_t VB = bits_of(Mtot);
+    const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES);
+    const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;   // tiles past ncell return at once
+    hipLaunchKernelGGL(lg_dgrid_zero, dim3(256), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_tiles, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_scan, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_emit, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
+    hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
+    hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    scan_emit(S, Mtot, LG_V, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
+    hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, S, f, VB);
+    // (rank, voxel) keys are written in voxel order: only the rank bits need sorting. rank < C
+    // <= Mtot / min_cluster_size; one bit more tells ranks from the non-members' ~0 keys
+    const uint32_t cmax = P.min_cl > 1 ? Mtot / P.min_cl : Mtot;
+    const int kb = radix_sort(S, Mtot, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V);
+    hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)Mtot + 1)), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, kb, Mtot, K);
+    hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
-// Host driver: one frame at a time on stream s. Synchronises twice per frame (survivor count
-// and voxel count size the backend launches).
+// Host driver: one frame at a time on stream s. Synchronises once per frame: the survivor
+// count and bounds size the backend launches.
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s) {
     const uint32_t N = L.n_points;
     hipError_t e;
@@ -967,11 +997,7 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
                                 (CG_NUM_BINS + 1) * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess)
             return e;
         if (kmode == CG_KMODE_PIPELINE && (e = (hipError_t)cg_large_decide(L, P, S, s, f)) != hipSuccess) return e;
-        uint32_t K = N;
-        if (kmode == CG_KMODE_PIPELINE) {
-            if ((e = hipMemcpyAsync(&K, S.meta + LG_K, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        }
+        const uint32_t K = kmode == CG_KMODE_PIPELINE ? CG_K_FROM_META : N;
         if ((e = (hipError_t)cg_large_backend(L, P, kmode, S, s, f, N, K)) != hipSuccess) return e;
     }
     return hipSuccess;
