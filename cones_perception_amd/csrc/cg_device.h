@@ -613,18 +613,29 @@ __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const 
             amb.w[wi] &= vm;
         }
     }
-    // ambiguous: exact z and sector from HBM, one point at a time (rare: tens per frame)
+    // ambiguous: exact z and sector from HBM (rare: tens per frame), four loads in flight
 #pragma unroll
     for (int wi = 0; wi < NW; wi++) {
         uint64_t m = amb.w[wi];
         while (m) {
-            const int k = __builtin_ctzll(m);
-            m &= m - 1;
-            const float3 p = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + k) * CG_BLOCK + tid, L);
-            int sx = 0;
-            bool unused = false;
-            classify_angle<true, false>(P, p.x, p.y, sx, unused);
-            if (!(cg_zkey(p.z) < tkey[sx])) keep.w[wi] |= 1ull << k;
+            int ks[4];
+            float3 pt[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ks[q] = m ? __builtin_ctzll(m) : -1;
+                if (m) m &= m - 1;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (ks[q] >= 0) pt[q] = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid, L);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (ks[q] < 0) continue;
+                int sx = 0;
+                bool unused = false;
+                classify_angle<true, false>(P, pt[q].x, pt[q].y, sx, unused);
+                if (!(cg_zkey(pt[q].z) < tkey[sx])) keep.w[wi] |= 1ull << ks[q];
+            }
         }
     }
 }

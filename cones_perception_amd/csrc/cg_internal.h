@@ -99,7 +99,7 @@ enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };
 // per-frame meta words in HBM
 enum {
     LG_SECKEY = 0,             // 18 words: sector minima (order-preserving keys)
-    LG_TOUCHED = 18, LG_K, LG_RESERVED, LG_MS, LG_NFIN,
+    LG_TOUCHED = 18, LG_K, LG_UNSORTED, LG_MS, LG_NFIN,
     LG_BMIN, LG_BMAX = LG_BMIN + 3, LG_V = LG_BMAX + 3, LG_C, LG_U, LG_PASS,
     LG_MINB, LG_MUL1 = LG_MINB + 3, LG_MUL2, LG_ORG, LG_NFIN_ALL = LG_ORG + 3, LG_SCAN_N,
     LG_DGINV, LG_DGN = LG_DGINV + 3, LG_NCELL = LG_DGN + 3,   // dense neighbour grid
@@ -108,7 +108,8 @@ enum {
 struct LgScratch {
     uint32_t* meta;
     uint64_t* codes;          // z codes, [chunk][group][lane] words of 8
-    uint64_t* keep;           // kept bits (ground-only mode) / filter bits (pipeline), [chunk][lane]
+    uint64_t* keep;           // per chunk and lane: kept bits (ground-only mode), else filter bits
+                              // (pipeline, until lg_decide leaves the survivor bits there)
     uint32_t* chunk_cnt;      // ground-only mode: kept points per chunk
     float4* surv_p; uint32_t* surv_i;   // survivors (detector input points)
     uint64_t* key0; uint64_t* key1;     // radix sort ping-pong

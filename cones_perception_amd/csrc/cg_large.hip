@@ -67,42 +67,22 @@ struct Bounds {
 };
 
 // ------------------------------------------------------------------------------------------
-// Append the lane's points selected by m (point k*CG_BLOCK + tid of the chunk at fb) to the
-// survivor arrays: one wave-wide slot reservation, then four loads in flight per lane. Each
-// survivor carries its frame index (pidx0 + its chunk index), so the order is free.
-template <int LAYOUT, int NW>
-__device__ __forceinline__ void lg_append(const uint8_t* fb, const CgLaunch& L, LgScratch& S, LaneBits<NW> m,
-                                          uint32_t pidx0, Bounds& bd) {
-    const uint32_t tid = threadIdx.x, l = lane_id();
-    const uint32_t n = m.count();
-    const uint32_t incl = wave_incl_scan(n);
-    uint32_t wbase = 0;
-    if (l == 63 && incl) wbase = atomicAdd(&S.meta[LG_MS], incl);
-    wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
-    uint32_t pos = wbase + incl - n;
+// The chunk's survivor bits m (point k*CG_BLOCK + tid of the chunk, bit k of the lane) go to
+// S.keep, their count to S.chunk_cnt[c]; lg_surv_write then writes the survivors in frame-index
+// order (every workgroup of the launch calls this).
+template <int NW>
+__device__ __forceinline__ void lg_store_survivor_bits(LgScratch& S, uint32_t c, const LaneBits<NW>& m,
+                                                       uint32_t* red) {
+    const uint32_t tid = threadIdx.x;
 #pragma unroll
-    for (int wi = 0; wi < NW; wi++) {
-        uint64_t w = m.w[wi];
-        while (w) {
-            int ks[4];
-            float4 pt[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                ks[q] = w ? 64 * wi + __builtin_ctzll(w) : -1;
-                if (w) w &= w - 1;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (ks[q] >= 0) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ks[q] < 0) continue;
-                S.surv_p[pos] = pt[q];
-                S.surv_i[pos] = pidx0 + (uint32_t)ks[q] * CG_BLOCK + tid;
-                bd.add(pt[q]);
-                pos++;
-            }
-        }
+    for (int wi = 0; wi < NW; wi++) S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi] = m.w[wi];
+    const uint32_t n = wave_sum(m.count());
+    if (lane_id() == 0) red[wave_id()] = n;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < WAVES; w++) t += red[w];
+        S.chunk_cnt[c] = t;
     }
 }
 
@@ -141,9 +121,8 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
         return;
     }
     // detector: the filter survivors themselves
-    Bounds bd;
-    lg_append<LAYOUT, NW>(fb, L, S, posm, S.pidx_base + (uint32_t)base, bd);
-    bd.merge(S.meta);
+    __shared__ uint32_t red[WAVES];
+    lg_store_survivor_bits<NW>(S, c, posm, red);
 }
 
 // Decide: thresholds, pass 2 per chunk, survivors = ground-kept & filter bits (from lg_front).
@@ -179,8 +158,70 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
         if (KMODE == CG_KMODE_GROUND) S.chunk_cnt[c] = kcount;
     }
     if (KMODE == CG_KMODE_GROUND) return;
+    __shared__ uint32_t red[WAVES];
+    lg_store_survivor_bits<NW>(S, c, surv, red);
+}
+
+// Survivors of every chunk in frame-index order: the chunk's base is the count of the chunks
+// before it, and within the chunk the order is (k, lane), i.e. the point index. VoxelGrid bounds
+// of the finite survivors merged into the meta words.
+template <int LAYOUT>
+__global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch S, uint32_t f) {
+    constexpr int PPT = LG_CHUNK / CG_BLOCK;
+    constexpr int NW = (PPT + 63) / 64;
+    __shared__ uint32_t cnt[PPT * WAVES];
+    __shared__ uint32_t red[8 * WAVES];
+    __shared__ uint32_t cbase;
+    const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint64_t base = (uint64_t)c * LG_CHUNK;
+    const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
+    __shared__ uint32_t pw[WAVES];
+    uint32_t pre = 0;
+    for (uint32_t t = tid; t < c; t += CG_BLOCK) pre += S.chunk_cnt[t];
+    pre = wave_sum(pre);
+    if (l == 0) pw[w] = pre;
+    LaneBits<NW> m;
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) m.w[wi] = S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const uint64_t bb = __ballot(m.get(k));
+        if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(bb);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int q = 0; q < WAVES; q++) t += pw[q];
+        cbase = t;
+    }
+    const uint32_t tot = block_scan(PPT * WAVES, [&](uint32_t i) -> uint32_t { return cnt[i]; },
+                                    [&](uint32_t i, uint32_t e) { cnt[i] = e; }, red);
+    if (tid == 0 && tot) atomicAdd(&S.meta[LG_MS], tot);
+    const uint32_t b0 = cbase;
+    const uint64_t lt = (1ull << l) - 1ull;
+    const uint32_t pidx0 = S.pidx_base + (uint32_t)base;
     Bounds bd;
-    lg_append<LAYOUT, NW>(fb, L, S, surv, S.pidx_base + (uint32_t)base, bd);
+#pragma unroll
+    for (int k0 = 0; k0 < PPT; k0 += 4) {   // four loads in flight
+        bool has[4];
+        uint32_t pos[4];
+        float4 pt[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = k0 + q;
+            has[q] = m.get(k);
+            const uint64_t bb = __ballot(has[q]);
+            pos[q] = b0 + cnt[k * WAVES + w] + (uint32_t)__popcll(bb & lt);
+            if (has[q]) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)k * CG_BLOCK + tid, L);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (!has[q]) continue;
+            S.surv_p[pos[q]] = pt[q];
+            S.surv_i[pos[q]] = pidx0 + (uint32_t)(k0 + q) * CG_BLOCK + tid;
+            bd.add(pt[q]);
+        }
+    }
     bd.merge(S.meta);
 }
 
@@ -489,18 +530,20 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevPara
     const uint32_t Ms = m[LG_MS];
     const float4 p = lg_point(S, j, Ms);
     const uint64_t pidx = j < Ms ? S.surv_i[j] : (uint64_t)N + (j - Ms);
+    // PB = 0 (survivors in frame-index order): a stable sort by idx alone keeps each voxel's
+    // points in frame-index order; otherwise the frame index is the key's low part
     uint64_t key;
     if (m[LG_PASS]) {
-        key = pidx;
+        key = PB ? pidx : 0ull;
     } else if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
-        key = (0xffffffffull << PB) | pidx;
+        key = (0xffffffffull << PB) | (PB ? pidx : 0ull);
     } else {
         const float mnb0 = (float)(int)m[LG_MINB], mnb1 = (float)(int)m[LG_MINB + 1], mnb2 = (float)(int)m[LG_MINB + 2];
         const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
         const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
         const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
         const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * m[LG_MUL1] + (uint32_t)i2 * m[LG_MUL2];
-        key = ((uint64_t)idx << PB) | pidx;
+        key = ((uint64_t)idx << PB) | (PB ? pidx : 0ull);
     }
     S.key0[j] = key;
     S.val0[j] = j;
@@ -829,13 +872,22 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams
     const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const uint32_t s = S.off[k], e = S.off[k + 1];
     float x = 0.0f, y = 0.0f;
-    for (uint32_t i0 = s; i0 < e; i0 += 64) {
-        const uint32_t n = min(64u, e - i0);
-        float px = 0.f, py = 0.f;
-        if (l < n) { const float4 p = S.vox[idx[i0 + l]]; px = p.x; py = p.y; }
-        for (uint32_t b = 0; b < n; b++) {
-            x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px), (int)b));
-            y += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py), (int)b));
+    for (uint32_t g0 = s; g0 < e; g0 += 4 * 64) {   // four chunks of 64 members in flight
+        float px[4], py[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t i = g0 + 64 * c + l;
+            px[c] = py[c] = 0.f;
+            if (i < e) { const float4 p = S.vox[idx[i]]; px[c] = p.x; py[c] = p.y; }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t i0 = g0 + 64 * c;
+            const uint32_t n = i0 < e ? min(64u, e - i0) : 0u;
+            for (uint32_t b = 0; b < n; b++) {
+                x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[c]), (int)b));
+                y += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[c]), (int)b));
+            }
         }
     }
     if (l != 0) return;
@@ -858,6 +910,10 @@ __global__ void lg_set_counts(LgScratch S, uint32_t K, uint32_t Ms, uint32_t nfi
     m[LG_BMIN] = b0; m[LG_BMIN + 1] = b1; m[LG_BMIN + 2] = b2;
     m[LG_BMAX] = b3; m[LG_BMAX + 1] = b4; m[LG_BMAX + 2] = b5;
 }
+__global__ __launch_bounds__(CG_BLOCK) void lg_check_sorted(LgScratch S, uint32_t n) {
+    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (j + 1 < n && !(S.surv_i[j] < S.surv_i[j + 1])) S.meta[LG_UNSORTED] = 1;
+}
 int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_points, const uint32_t* d_index,
                            uint32_t n, const uint32_t* c, hipStream_t s) {
     hipError_t e;
@@ -866,6 +922,7 @@ int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_poi
         if ((e = hipMemcpyAsync(S.surv_p, d_points, (size_t)n * 16, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(S.surv_i, d_index, (size_t)n * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     }
+    if (n > 1) hipLaunchKernelGGL(lg_check_sorted, dim3((n + CG_BLOCK - 1) / CG_BLOCK), dim3(CG_BLOCK), 0, s, S, n);
     hipLaunchKernelGGL(lg_set_counts, dim3(1), dim3(64), 0, s, S, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8]);
     return hipGetLastError();
 }
@@ -882,16 +939,20 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
 #define LG_FRONT(LAY, KM) hipLaunchKernelGGL((lg_front<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
     if (xyzi16) {
         if (kmode == CG_KMODE_PIPELINE) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE);
-        else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_DETECT);
-        else {
+        else if (kmode == CG_KMODE_DETECT) {
+            LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_DETECT);
+            hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
+        } else {
             LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_GROUND);
             hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_GROUND>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
             hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_XYZI16>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
         }
     } else {
         if (kmode == CG_KMODE_PIPELINE) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE);
-        else if (kmode == CG_KMODE_DETECT) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_DETECT);
-        else {
+        else if (kmode == CG_KMODE_DETECT) {
+            LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_DETECT);
+            hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
+        } else {
             LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_GROUND);
             hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_GROUND>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
             hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_GENERIC>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
@@ -905,10 +966,13 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
     const uint32_t nch = (uint32_t)(((uint64_t)L.n_points + LG_CHUNK - 1) / LG_CHUNK);
     if (nch == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
-    if (xyzi16)
+    if (xyzi16) {
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-    else
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
+    } else {
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
+    }
     return hipGetLastError();
 }
 
@@ -927,7 +991,9 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     CgLaunch Lh = L;
     Lh.n_points = N;   // the header's N is the whole frame's
     if (Mtot <= CG_MMAX && !S.force_global) return cg_launch_lg_back_small(Lh, P, S, f, npad, K, s);
-    const uint32_t PB = bits_of((uint64_t)N + npad);
+    // survivors arrive in frame-index order (lg_surv_write; tiles checked by lg_check_sorted):
+    // then the voxel keys need no frame-index bits (PB = 0)
+    const uint32_t PB = hm[LG_UNSORTED] ? bits_of((uint64_t)N + npad) : 0u;
     const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
     // the voxel keys' idx width from the bounds the host already holds (lg_grid_setup's own
     // computation): one bit above the largest idx keeps non-finite points (idx all ones) last
@@ -944,7 +1010,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
         uint32_t pass = 0;
         int min_b[3], div_b[3];
         voxel_grid_setup(nfin, bmn, bmx, P, pass, min_b, div_b);
-        if (pass) key_bits = PB;
+        if (pass) key_bits = PB;   // passthrough: frame-index order (nothing to sort when ordered)
         else key_bits = PB + 1 + bits_of((uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2]);
         key_bits = std::min<uint32_t>(key_bits, 32 + PB);
     }
