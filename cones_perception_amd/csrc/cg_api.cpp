@@ -175,6 +175,7 @@ struct cg_handle {
     size_t h_ground_bytes = 0;
     // frames of more than CG_MAX_POINTS points (cg_large.hip): scratch for one frame
     uint8_t* d_large = nullptr;
+    uint32_t* h_meta = nullptr;      // pinned: the large path's per-frame meta read
     uint32_t large_points = 0;
     LgScratch lg{};
     int route = 0;                // cg_debug_route
@@ -340,6 +341,8 @@ int ensure_large(cg_handle* h, uint32_t n) {
     h->large_points = 0;
     HIPCHK(hipMalloc(&h->d_large, cg_large_bytes(n)));
     cg_large_layout(h->d_large, n, h->lg);
+    if (!h->h_meta) HIPCHK(hipHostMalloc((void**)&h->h_meta, LG_META_WORDS * 4, hipHostMallocDefault));
+    h->lg.hmeta = h->h_meta;
     h->large_points = n;
     return CG_OK;
 }
@@ -516,6 +519,7 @@ int cg_destroy(cg_handle* h) {
     free_batch(h);
     if (h->d_stamps) (void)hipFree(h->d_stamps);
     if (h->d_in) (void)hipFree(h->d_in);
+    if (h->h_meta) (void)hipHostFree(h->h_meta);
     if (h->d_large) (void)hipFree(h->d_large);
     if (h->d_boxes) (void)hipFree(h->d_boxes);
     if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);

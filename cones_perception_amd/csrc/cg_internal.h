@@ -120,6 +120,7 @@ struct LgScratch {
     uint32_t* run;            // voxel run starts
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
     uint32_t* cstart;         // dense neighbour grid: per-cell start in ord (LG_DCELLS_MAX + 2)
+    uint32_t* hmeta;          // pinned host copy of the meta words (the one round trip per frame)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };

@@ -50,6 +50,38 @@ struct Bounds {
             n++;
         }
     }
+    // whole workgroup: wave partials through LDS (part: 7 * WAVES words), then one lane's
+    // atomics per workgroup instead of per wave (same-address atomics serialise in L2)
+    __device__ __forceinline__ void merge_block(uint32_t* meta, uint32_t* part) {
+        float r[6];
+#pragma unroll
+        for (int a = 0; a < 3; a++) { r[a] = wave_min(mn[a]); r[3 + a] = wave_max(mx[a]); }
+        const uint32_t nf = wave_sum(n), w = wave_id();
+        if (lane_id() == 0) {
+#pragma unroll
+            for (int a = 0; a < 6; a++) part[7 * w + a] = __float_as_uint(r[a]);
+            part[7 * w + 6] = nf;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float q[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            uint32_t t = 0;
+            for (int v = 0; v < WAVES; v++) {
+                for (int a = 0; a < 3; a++) {
+                    q[a] = fminf(q[a], __uint_as_float(part[7 * v + a]));
+                    q[3 + a] = fmaxf(q[3 + a], __uint_as_float(part[7 * v + 3 + a]));
+                }
+                t += part[7 * v + 6];
+            }
+            if (t) {
+                for (int a = 0; a < 3; a++) {
+                    atomicMin(&meta[LG_BMIN + a], cg_fkey(q[a]));
+                    atomicMax(&meta[LG_BMAX + a], cg_fkey(q[3 + a]));
+                }
+                atomicAdd(&meta[LG_NFIN], t);
+            }
+        }
+    }
     __device__ __forceinline__ void merge(uint32_t* meta) {   // every lane of the wave calls
         float r[6];
 #pragma unroll
@@ -222,7 +254,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
             bd.add(pt[q]);
         }
     }
-    bd.merge(S.meta);
+    __shared__ uint32_t part[7 * WAVES];
+    bd.merge_block(S.meta, part);
 }
 
 // Ground-only output: each chunk's kept points at its stable offset, then the zero pads.
@@ -561,40 +594,46 @@ struct VoxelEmit {
     __device__ void operator()(uint32_t r, uint32_t v) const { run[v] = r; }
 };
 
-// CentroidPoint: float sums in ascending frame index / float(n); passthrough copies the point
+// CentroidPoint: float sums in ascending frame index / float(n); passthrough copies the point.
+// One wave per voxel: the lanes fetch 64 members at a time, the sums run through them in
+// member order.
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScratch S, uint32_t f, uint32_t Mtot,
                                                                int buf) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint32_t v = blockIdx.x * WAVES + wave_id(), l = lane_id();
     const uint32_t* m = S.meta;
     const uint32_t V = m[LG_V], Ms = m[LG_MS];
     if (v >= V) return;
     const uint32_t* val = buf ? S.val1 : S.val0;
     float4* vox_out = L.vox + (uint64_t)f * L.cap;
-    S.par[v] = v;
-    S.cnt[v] = 0;
-    S.rk[v] = 0xffffffffu;
+    if (l == 0) {
+        S.par[v] = v;
+        S.cnt[v] = 0;
+        S.rk[v] = 0xffffffffu;
+    }
     if (m[LG_PASS]) {
-        const float4 p = lg_point(S, val[v], Ms);
-        S.vox[v] = p;
-        vox_out[v] = p;
+        if (l == 0) {
+            const float4 p = lg_point(S, val[v], Ms);
+            S.vox[v] = p;
+            vox_out[v] = p;
+        }
         return;
     }
     const uint32_t s = S.run[v], e = v + 1 < V ? S.run[v + 1] : m[LG_NFIN_ALL];
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
-    uint32_t r = s;
-    for (; r + 4 <= e; r += 4) {   // four members in flight, summed in order
-        float4 pv[4];
-#pragma unroll
-        for (int b = 0; b < 4; b++) pv[b] = lg_point(S, val[r + b], Ms);
-#pragma unroll
-        for (int b = 0; b < 4; b++) { sx += pv[b].x; sy += pv[b].y; sz += pv[b].z; si += pv[b].w; }
+    for (uint32_t g0 = s; g0 < e; g0 += 64) {
+        const uint32_t n = min(64u, e - g0);
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (l < n) p = lg_point(S, val[g0 + l], Ms);
+        for (uint32_t b = 0; b < n; b++) {
+            sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), (int)b));
+            sy += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), (int)b));
+            sz += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), (int)b));
+            si += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.w), (int)b));
+        }
     }
-    for (; r < e; r++) {
-        const float4 p = lg_point(S, val[r], Ms);
-        sx += p.x; sy += p.y; sz += p.z; si += p.w;
-    }
-    const float n = (float)(e - s);
-    const float4 c = make_float4(sx / n, sy / n, sz / n, si / n);
+    if (l != 0) return;
+    const float nn = (float)(e - s);
+    const float4 c = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
     S.vox[v] = c;
     vox_out[v] = c;
 }
@@ -981,8 +1020,9 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
 int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t N, uint32_t K) {
     hipError_t e;
-    uint32_t hm[LG_META_WORDS];
-    if ((e = hipMemcpyAsync(hm, S.meta, sizeof(hm), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    uint32_t hstack[LG_META_WORDS];
+    uint32_t* const hm = S.hmeta ? S.hmeta : hstack;   // pinned when the handle has one
+    if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     const uint32_t Ms = hm[LG_MS];
     if (K == CG_K_FROM_META) K = hm[LG_K];   // pipeline frames: the ground stage's kept count
@@ -1020,7 +1060,8 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     // runs over the finite points (non-finite keys sort last); passthrough: every point
     scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
-    hipLaunchKernelGGL(lg_voxel_centroids, dim3(mb), dim3(CG_BLOCK), 0, s, Lh, S, f, Mtot, buf);
+    hipLaunchKernelGGL(lg_voxel_centroids, dim3(std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES)), dim3(CG_BLOCK), 0, s,
+                       Lh, S, f, Mtot, buf);
     // V is known on the device only: the clustering launches are sized for V <= Mtot and read
     // V from the meta words (no host round trip)
     const uint32_t VB = bits_of(Mtot);
