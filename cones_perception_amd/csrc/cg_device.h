@@ -417,7 +417,7 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
     constexpr int G = 8;                          // points per load group (double-buffered)
     constexpr int NG = PPT / G;
     constexpr int NW = (PPT + 63) / 64;
-    static_assert(PPT % (2 * G) == 0, "PPT must be a multiple of two load groups");
+    static_assert(PPT == G || PPT % (2 * G) == 0, "PPT must be one load group or a multiple of two");
     const uint32_t tid = threadIdx.x;
     // ---- pass 1: stream the frame ----
     // Two explicit load buffers (A, B), the loop unrolled by two: group g+1 is in flight while
@@ -497,7 +497,11 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
         uncm.template set_bits<G>(g, __builtin_bitreverse32(runc) >> (32 - G));
         if (GROUND) store_codes(g, make_uint2(clo, chi));
     };
-    if (N) {
+    if (N && NG == 1) {
+        float3 A[G];
+        load_group(A, 0);
+        run_group(A, 0);
+    } else if (N) {
         float3 A[G], B[G];
         load_group(A, 0);
 #pragma unroll 1

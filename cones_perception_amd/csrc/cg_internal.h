@@ -95,7 +95,10 @@ enum { CG_KMODE_PIPELINE = 0, CG_KMODE_DETECT = 1, CG_KMODE_GROUND = 2 };
 // dense neighbour grid of the global backend: at most LG_DGRID_AXIS cells per axis
 #define LG_DGRID_AXIS 128
 #define LG_DCELLS_MAX (LG_DGRID_AXIS * LG_DGRID_AXIS * LG_DGRID_AXIS)
-#define LG_CHUNK 8192          // points per front workgroup (16 per lane): a 1M frame fills 128
+// per-chunk statistics words (LgScratch::cstat)
+enum { LG_CS_KEYS = 0, LG_CS_TOUCHED = 18, LG_CS_K, LG_CS_MS, LG_CS_BMIN, LG_CS_BMAX = LG_CS_BMIN + 3,
+       LG_CS_NFIN = LG_CS_BMAX + 3, LG_CS_WORDS = 32 };
+#define LG_CHUNK 4096          // points per front workgroup (8 per lane): a 1M frame fills 256
 // per-frame meta words in HBM
 enum {
     LG_SECKEY = 0,             // 18 words: sector minima (order-preserving keys)
@@ -121,6 +124,8 @@ struct LgScratch {
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
     uint32_t* cstart;         // dense neighbour grid: per-cell start in ord (LG_DCELLS_MAX + 2)
     uint32_t* hmeta;          // pinned host copy of the meta words (the one round trip per frame)
+    uint32_t* cstat;          // per-chunk statistics [chunk][LG_CS_WORDS], reduced into meta by
+                              // one workgroup (same-address atomics from every chunk serialise)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };

@@ -50,8 +50,8 @@ struct Bounds {
             n++;
         }
     }
-    // whole workgroup: wave partials through LDS (part: 7 * WAVES words), then one lane's
-    // atomics per workgroup instead of per wave (same-address atomics serialise in L2)
+    // whole workgroup: wave partials through LDS (part: 7 * WAVES words), then one lane writes
+    // the workgroup's bounds keys and finite count into its chunk statistics words cs
     __device__ __forceinline__ void merge_block(uint32_t* meta, uint32_t* part) {
         float r[6];
 #pragma unroll
@@ -73,13 +73,11 @@ struct Bounds {
                 }
                 t += part[7 * v + 6];
             }
-            if (t) {
-                for (int a = 0; a < 3; a++) {
-                    atomicMin(&meta[LG_BMIN + a], cg_fkey(q[a]));
-                    atomicMax(&meta[LG_BMAX + a], cg_fkey(q[3 + a]));
-                }
-                atomicAdd(&meta[LG_NFIN], t);
+            for (int a = 0; a < 3; a++) {   // (no finite point: keys that change no MIN / MAX)
+                meta[LG_CS_BMIN + a] = t ? cg_fkey(q[a]) : 0xffffffffu;
+                meta[LG_CS_BMAX + a] = t ? cg_fkey(q[3 + a]) : 0u;
             }
+            meta[LG_CS_NFIN] = t;
         }
     }
     __device__ __forceinline__ void merge(uint32_t* meta) {   // every lane of the wave calls
@@ -140,12 +138,19 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
     uint2* codes = (uint2*)S.codes + (uint64_t)c * (LG_CHUNK / 8);
     stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, Nc, L, P, sec_key, rays, posm, touched,
                                              [&](int g, uint2 cw) { codes[g * CG_BLOCK + tid] = cw; });
+    __shared__ uint32_t tw[WAVES];
     if (GROUND) {
         touched = wave_or(touched);
-        if (l == 0 && touched) atomicOr(&S.meta[LG_TOUCHED], touched);
+        if (l == 0) tw[wave_id()] = touched;
     }
     __syncthreads();
-    if (GROUND && tid <= CG_NUM_BINS) atomicMin(&S.meta[LG_SECKEY + tid], sec_key[tid]);
+    uint32_t* const cs = S.cstat + (uint64_t)c * LG_CS_WORDS;
+    if (GROUND && tid <= CG_NUM_BINS) cs[LG_CS_KEYS + tid] = sec_key[tid];
+    if (GROUND && tid == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < WAVES; w++) t |= tw[w];
+        cs[LG_CS_TOUCHED] = t;
+    }
     if (!FILTER) return;
     if (GROUND) {   // pipeline: the filter bits wait for the ground decision (lg_decide)
 #pragma unroll
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
     }
     __syncthreads();
     if (tid == 0) {
-        atomicAdd(&S.meta[LG_K], kcount);
+        S.cstat[(uint64_t)c * LG_CS_WORDS + LG_CS_K] = kcount;
         if (KMODE == CG_KMODE_GROUND) S.chunk_cnt[c] = kcount;
     }
     if (KMODE == CG_KMODE_GROUND) return;
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
     }
     const uint32_t tot = block_scan(PPT * WAVES, [&](uint32_t i) -> uint32_t { return cnt[i]; },
                                     [&](uint32_t i, uint32_t e) { cnt[i] = e; }, red);
-    if (tid == 0 && tot) atomicAdd(&S.meta[LG_MS], tot);
+    if (tid == 0) S.cstat[(uint64_t)c * LG_CS_WORDS + LG_CS_MS] = tot;
     const uint32_t b0 = cbase;
     const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t pidx0 = S.pidx_base + (uint32_t)base;
@@ -255,7 +260,45 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
         }
     }
     __shared__ uint32_t part[7 * WAVES];
-    bd.merge_block(S.meta, part);
+    bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, part);
+}
+
+// One workgroup folds the per-chunk statistics into the meta words: the sector keys (MIN) and
+// used bins (OR) after the front; K, survivor count, finite count (SUM) and the VoxelGrid
+// bounds (MIN / MAX keys) after the decisions. what: bit 0 keys, bit 1 K, bit 2 survivors.
+__global__ __launch_bounds__(CG_BLOCK) void lg_reduce_chunks(LgScratch S, uint32_t nch, uint32_t what) {
+    __shared__ uint32_t part[16][LG_CS_WORDS];
+    const uint32_t tid = threadIdx.x, w = tid & 31, q = tid >> 5;   // word, one of 16 chunk strides
+    const bool mn = (w <= CG_NUM_BINS) || (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3);
+    const bool mx = w >= LG_CS_BMAX && w < LG_CS_BMAX + 3;
+    const bool orw = w == LG_CS_TOUCHED;
+    uint32_t acc = mn ? 0xffffffffu : 0u;
+    auto fold = [&](uint32_t a, uint32_t v) { return mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v; };
+    uint32_t c = q;
+    for (; c + 48 < nch; c += 64) {   // four independent loads per trip
+        const uint32_t v0 = S.cstat[(uint64_t)c * LG_CS_WORDS + w], v1 = S.cstat[(uint64_t)(c + 16) * LG_CS_WORDS + w],
+                       v2 = S.cstat[(uint64_t)(c + 32) * LG_CS_WORDS + w], v3 = S.cstat[(uint64_t)(c + 48) * LG_CS_WORDS + w];
+        acc = fold(fold(acc, v0), fold(v1, fold(v2, v3)));
+    }
+    for (; c < nch; c += 16) acc = fold(acc, S.cstat[(uint64_t)c * LG_CS_WORDS + w]);
+    part[q][w] = acc;
+    __syncthreads();
+    if (tid >= LG_CS_WORDS) return;
+    uint32_t a = part[0][w];
+    for (int k = 1; k < 16; k++) {
+        const uint32_t v = part[k][w];
+        a = mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v;
+    }
+    uint32_t* m = S.meta;
+    if ((what & 1u) && w <= CG_NUM_BINS) m[LG_SECKEY + w] = a;
+    if ((what & 1u) && w == LG_CS_TOUCHED) m[LG_TOUCHED] = a;
+    if ((what & 2u) && w == LG_CS_K) m[LG_K] = a;
+    if (what & 4u) {
+        if (w == LG_CS_MS) m[LG_MS] = a;
+        if (w == LG_CS_NFIN) m[LG_NFIN] = a;
+        if (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3) m[LG_BMIN + (w - LG_CS_BMIN)] = a;
+        if (w >= LG_CS_BMAX && w < LG_CS_BMAX + 3) m[LG_BMAX + (w - LG_CS_BMAX)] = a;
+    }
 }
 
 // Ground-only output: each chunk's kept points at its stable offset, then the zero pads.
@@ -387,15 +430,18 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word,
 }
 
 // ------------------------------------------------------------------------------------------
-// Stable LSD radix sort of (64-bit key, 32-bit value) pairs, 8 bits per pass.
+// Stable LSD radix sort of (64-bit key, 32-bit value) pairs, 8 bits per pass, tiles of
+// LG_RS_TILE elements (LG_RS_ROUNDS rounds of 512 per workgroup).
+#define LG_RS_ROUNDS 2
+#define LG_RS_TILE (LG_RS_ROUNDS * CG_BLOCK)
 __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint32_t n, uint32_t shift,
                                                        uint32_t* hist, const uint32_t* n_dev) {
     __shared__ uint32_t h[256];
     if (n_dev) n = *n_dev;   // count known on the device only (grid sized for an upper bound)
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE;
-    for (int q = 0; q < 8; q++) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_RS_TILE;
+    for (int q = 0; q < LG_RS_ROUNDS; q++) {
         const uint64_t i = b0 + (uint64_t)q * CG_BLOCK + threadIdx.x;
         if (i < n) atomicAdd(&h[(key[i] >> shift) & 255u], 1u);
     }
@@ -431,9 +477,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, c
                    [&](uint32_t i, uint32_t e) { run[i] = e + pre; }, red);
     }
     __syncthreads();
-    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE;
+    const uint64_t b0 = (uint64_t)blockIdx.x * LG_RS_TILE;
     const uint64_t lt = (1ull << l) - 1ull;
-    for (int q = 0; q < 8; q++) {
+    for (int q = 0; q < LG_RS_ROUNDS; q++) {
         for (uint32_t x = tid; x < WAVES * 256; x += CG_BLOCK) (&wcnt[0][0])[x] = 0;
         __syncthreads();
         const uint64_t i = b0 + (uint64_t)q * CG_BLOCK + tid;
@@ -481,7 +527,7 @@ int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t 
     uint32_t* v[2] = {S.val0, S.val1};
     int cur = 0;
     if (n <= 1) return cur;
-    const uint32_t nt = tiles_of(n);
+    const uint32_t nt = (uint32_t)(((uint64_t)n + LG_RS_TILE - 1) / LG_RS_TILE);
     for (uint32_t shift = lo; shift < bits; shift += 8) {
         hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist, n_dev);
         hipLaunchKernelGGL(lg_rs_scatter, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
@@ -806,9 +852,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P)
     if (v >= V) return;
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
+    const uint32_t pv = S.par[v];
     lg_neighbours(S, g, q, [&](uint32_t o) {
-        if (o > v && lg_adjacent(q, S.vox[o], P.r2) && ld_rlx(S.par + o) != ld_rlx(S.par + v))
-            uf_union(S.par, v, o);
+        // plain loads, issued together: a stale pair of equal parents still lies in one tree
+        // (trees only merge); different ones go through uf_union, which re-reads
+        const float4 p = S.vox[o];
+        const uint32_t po = S.par[o];
+        if (o > v && po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, v, o);
     });
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_find(LgScratch S) {
@@ -975,29 +1025,28 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
     if (init) hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
     if (nch == 0) return hipGetLastError();
-#define LG_FRONT(LAY, KM) hipLaunchKernelGGL((lg_front<LAY, KM>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f)
-    if (xyzi16) {
-        if (kmode == CG_KMODE_PIPELINE) LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE);
-        else if (kmode == CG_KMODE_DETECT) {
-            LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_DETECT);
-            hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
-        } else {
-            LG_FRONT(CG_LAYOUT_XYZI16, CG_KMODE_GROUND);
-            hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_GROUND>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-            hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_XYZI16>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-        }
-    } else {
-        if (kmode == CG_KMODE_PIPELINE) LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE);
-        else if (kmode == CG_KMODE_DETECT) {
-            LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_DETECT);
-            hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
-        } else {
-            LG_FRONT(CG_LAYOUT_GENERIC, CG_KMODE_GROUND);
-            hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_GROUND>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-            hipLaunchKernelGGL((lg_ground_out<CG_LAYOUT_GENERIC>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-        }
+    const dim3 g(nch), b(CG_BLOCK);
+#define LG_FRONT_MODES(LAY)                                                                       \
+    if (kmode == CG_KMODE_PIPELINE) {                                                             \
+        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);           \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u);                      \
+    } else if (kmode == CG_KMODE_DETECT) {                                                        \
+        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f);             \
+        hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f);                              \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u);                      \
+    } else {                                                                                      \
+        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);             \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u);                      \
+        hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);            \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u);                      \
+        hipLaunchKernelGGL(lg_ground_out<LAY>, g, b, 0, s, L, P, S, f);                           \
     }
-#undef LG_FRONT
+    if (xyzi16) {
+        LG_FRONT_MODES(CG_LAYOUT_XYZI16)
+    } else {
+        LG_FRONT_MODES(CG_LAYOUT_GENERIC)
+    }
+#undef LG_FRONT_MODES
     return hipGetLastError();
 }
 
@@ -1005,13 +1054,15 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
     const uint32_t nch = (uint32_t)(((uint64_t)L.n_points + LG_CHUNK - 1) / LG_CHUNK);
     if (nch == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
+    const dim3 g(nch), b(CG_BLOCK);
     if (xyzi16) {
-        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f);
     } else {
-        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), dim3(nch), dim3(CG_BLOCK), 0, s, L, P, S, f);
-        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, dim3(nch), dim3(CG_BLOCK), 0, s, L, S, f);
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f);
     }
+    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u);
     return hipGetLastError();
 }
 
@@ -1125,12 +1176,14 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(6, take(N * 16)); place(7, take(N * 4));
     place(8, take(N * 8)); place(9, take(N * 8));
     place(10, take(N * 4)); place(11, take(N * 4));
-    place(12, take((std::max<uint64_t>(256 * nt, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
+    const uint64_t nrs = (N + LG_RS_TILE - 1) / LG_RS_TILE;
+    place(12, take((std::max<uint64_t>(256 * nrs, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
     place(13, take((nt + 2) * 4));
     place(14, take(N * 16));
     place(15, take((N + 2) * 4));
     for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));
     place(28, take((uint64_t)(LG_DCELLS_MAX + 2) * 4));
+    place(29, take(nch * LG_CS_WORDS * 4));
     return off;
 }
 }  // namespace
@@ -1155,6 +1208,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 14: S.vox = (float4*)p; break;
             case 15: S.run = (uint32_t*)p; break;
             case 28: S.cstart = (uint32_t*)p; break;
+            case 29: S.cstat = (uint32_t*)p; break;
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
     });
