@@ -45,7 +45,8 @@ def main():
                          "(128 rings x 8192 columns + clutter) through the large-frame path")
     ap.add_argument("--c5-tiled", action="store_true",
                     help="also time C5 tiled over the ranks: each rank holds a contiguous tile of "
-                         "the 1M-point frame; sector keys / counts merged, survivors gathered to rank 0")
+                         "the 1M-point frame; sector keys / counts merged, then (a) survivors gathered to rank 0, "
+                         "(b) voxel slabs per rank with a halo exchange (both reported)")
     ap.add_argument("--scatter", action="store_true",
                     help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
                          "scatter to ranks, process, gather per-frame headers (reported separately)")
@@ -172,7 +173,8 @@ def main():
 
     c5t = None
     if args.c5_tiled:
-        c5t = c5_tiled(cp, cd, params, local, rank, world)
+        c5t = {"gather": c5_tiled(cp, cd, params, local, rank, world),
+               "halo": c5_tiled(cp, cd, params, local, rank, world, halo=True)}
 
     single = None
     if args.single_frame and rank == 0:
@@ -370,7 +372,7 @@ def c5_single_gpu(cp, params, device, reps=50):
                         "and bounds size the backend); backend latency-bound (sorts, union-find)"}
 
 
-def c5_tiled(cp, cd, params, device, rank, world, reps=20):
+def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):
     """C5 tiled over the ranks (one GPU each): rank r holds points tile_range(r) of the
     1M-point frame in its HBM. Per frame: pass 1 on the tile, one MIN all-reduce of the sector
     keys, the keep decision, one all-gather of count words, one all-gather of survivors to
@@ -385,7 +387,7 @@ def c5_tiled(cp, cd, params, device, rank, world, reps=20):
     lo, hi = cd.tile_range(n_total, rank, world)
     tile = torch.from_numpy(np.ascontiguousarray(raw[0, lo * 16: hi * 16])).to(dev)
     eng = cp.BatchEngine(params, device=device)
-    run = lambda: cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev)
+    run = lambda: cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev, halo=halo)
     for _ in range(3):
         run()
     torch.cuda.synchronize(dev)
@@ -398,7 +400,12 @@ def c5_tiled(cp, cd, params, device, rank, world, reps=20):
     el = cd.max_over_ranks(time.perf_counter() - t0, dev)
     out = {"ms_per_frame": el / reps * 1e3, "frames_per_s": reps / el, "ranks": world,
            "points": n_total, "tile_points": hi - lo,
-           "includes": "device-resident tiles; 3 collectives + host syncs per frame; backend on rank 0"}
+           "includes": ("device-resident tiles; 2 collectives to decide the points, then voxel slabs per rank: "
+                        "all-to-all of the survivors, point-to-point halo to the slab below, gather of voxel "
+                        "records and component pairs to rank 0, merge there") if halo else
+                       "device-resident tiles; 3 collectives + host syncs per frame; backend on rank 0"}
+    if halo:
+        out["halo"] = dict(cd.last_halo_stats)
     if rank == 0:
         full = torch.from_numpy(raw).to(dev)
         ref_eng = cp.BatchEngine(params, device=device)

@@ -90,6 +90,13 @@ class cg_tile(C.Structure):
 
 
 CG_TILE_KEYS, CG_TILE_COUNTS = 19, 9
+CG_HALO_REC_WORDS = 8
+
+
+class cg_halo_plan(C.Structure):
+    _fields_ = [("passthrough", C.c_uint32), ("min_b", C.c_int32 * 3), ("div_b", C.c_uint32 * 3),
+                ("slabs", C.c_uint32), ("slab_w", C.c_uint32), ("band", C.c_uint32), ("pad_slab", C.c_int32),
+                ("n_pads", C.c_uint32), ("key_bits", C.c_uint32)]
 
 
 class cg_crop_result(C.Structure):
@@ -130,6 +137,14 @@ _SIGS = {
     "cg_tile_decide": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cg_tile_survivors": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_tile_backend": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
+    "cg_halo_plan_frame": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(cg_halo_plan)]),
+    "cg_halo_owner": (C.c_int, [C.c_void_p, C.POINTER(cg_halo_plan), C.c_void_p, C.c_uint32, C.c_void_p]),
+    "cg_halo_local": (C.c_int, [C.c_void_p, C.POINTER(cg_halo_plan), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "cg_halo_edges": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                C.POINTER(C.c_uint32)]),
+    "cg_halo_merge": (C.c_int, [C.c_void_p, C.POINTER(cg_halo_plan), C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                C.c_void_p, C.c_uint32]),
     "cg_batch_results_get": (C.c_int, [C.c_void_p, C.POINTER(cg_batch_results)]),
     "cg_batch_fetch": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(cg_detect_result)]),
     "cg_selftest_atan2f": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),

@@ -794,6 +794,122 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
     return CG_OK;
 }
 
+// ---- C5 halo tiling (cg_halo_*): argument checks and the handle's scratch; the work is in
+// cg_large.hip
+namespace {
+int halo_counts_ok(const uint32_t* c, uint32_t n_total) {
+    if (!c) return fail(CG_E_INVALID, "null merged counts");
+    if (n_total == 0 || n_total > CG_MAX_FRAME_POINTS || c[0] > n_total || c[1] > n_total || c[2] > c[1])
+        return fail(CG_E_INVALID, "inconsistent tile counts (K %u, survivors %u, finite %u, N %u)", c[0], c[1], c[2],
+                    n_total);
+    return CG_OK;
+}
+int halo_plan_ok(const cg_halo_plan* p) {
+    if (!p) return fail(CG_E_INVALID, "null plan");
+    if (p->passthrough) return fail(CG_E_INVALID, "passthrough frame: no voxel lattice to tile");
+    if (p->slabs == 0 || p->slab_w == 0) return fail(CG_E_INVALID, "empty slab plan");
+    return CG_OK;
+}
+}  // namespace
+
+int cg_halo_plan_frame(cg_handle* h, const uint32_t* merged_counts, uint32_t n_total, uint32_t n_ranks,
+                       cg_halo_plan* plan) {
+    if (!h || !plan) return fail(CG_E_INVALID, "null argument");
+    int rc = halo_counts_ok(merged_counts, n_total);
+    if (rc) return rc;
+    cg_halo_plan_compute(h->dp, merged_counts, n_total, n_ranks, plan);
+    return CG_OK;
+}
+
+int cg_halo_owner(cg_handle* h, const cg_halo_plan* plan, const float* d_points, uint32_t n, int32_t* d_slab) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    int rc = halo_plan_ok(plan);
+    if (rc) return rc;
+    if (n && (!d_points || !d_slab)) return fail(CG_E_INVALID, "null buffers");
+    HIPCHK(hipSetDevice(h->device));
+    rc = own_stream(h);
+    if (rc) return rc;
+    HIPCHK((hipError_t)cg_launch_halo_owner(d_points, n, h->dp.inv_leaf[0], plan->min_b[0], plan->slab_w, plan->slabs,
+                                            d_slab, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CG_OK;
+}
+
+int cg_halo_local(cg_handle* h, const cg_halo_plan* plan, const float* d_points, const uint32_t* d_index,
+                  uint32_t n, uint32_t n_pads, const uint32_t* merged_counts, uint32_t n_total, uint32_t* d_rec,
+                  uint32_t capacity, uint32_t* n_vox) {
+    if (!h || !n_vox) return fail(CG_E_INVALID, "null argument");
+    int rc = halo_plan_ok(plan);
+    if (!rc) rc = halo_counts_ok(merged_counts, n_total);
+    if (rc) return rc;
+    if (n && (!d_points || !d_index)) return fail(CG_E_INVALID, "null survivors");
+    if ((uint64_t)n + n_pads > n_total || n > merged_counts[2] || (n_pads && n_pads != plan->n_pads))
+        return fail(CG_E_INVALID, "%u survivors + %u pads do not fit the frame's counts", n, n_pads);
+    if ((uint64_t)n + n_pads > capacity || (capacity && !d_rec))
+        return fail(CG_E_INVALID, "record capacity %u < %u possible voxels", capacity, n + n_pads);
+    HIPCHK(hipSetDevice(h->device));
+    rc = own_stream(h);
+    if (!rc) rc = ensure_large(h, n_total);
+    if (!rc) rc = ensure_batch(h, 1, n_total, false);
+    if (rc) return rc;
+    LgScratch S = h->lg;
+    S.pidx_base = 0;
+    CgLaunch L{};
+    L.n_frames = 1;
+    L.n_points = n_total;
+    fill_launch_outputs(h, L);
+    L.stamps = nullptr;
+    HIPCHK((hipError_t)cg_halo_local_run(L, h->dp, S, h->stream, d_points, d_index, n, n_pads, plan->n_pads,
+                                         merged_counts, n_total, plan->key_bits, d_rec, capacity, n_vox));
+    return CG_OK;
+}
+
+int cg_halo_edges(cg_handle* h, const uint32_t* d_own, uint32_t n_own, const uint32_t* d_halo, uint32_t n_halo,
+                  uint32_t* d_pairs, uint32_t capacity, uint32_t* n_pairs) {
+    if (!h || !n_pairs) return fail(CG_E_INVALID, "null argument");
+    if ((n_own && !d_own) || (n_halo && !d_halo) || (capacity && !d_pairs)) return fail(CG_E_INVALID, "null buffers");
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (!rc) rc = ensure_large(h, 1);
+    if (rc) return rc;
+    uint32_t* d_count = h->lg.meta + LG_META_WORDS - 1;
+    HIPCHK((hipError_t)cg_halo_edges_run(d_own, n_own, d_halo, n_halo, h->dp.r2, d_pairs, capacity, d_count,
+                                         h->stream));
+    HIPCHK(hipMemcpyAsync(n_pairs, d_count, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CG_OK;
+}
+
+int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec, uint32_t n_rec,
+                  const uint32_t* d_pairs, uint32_t n_pairs, const uint32_t* merged_counts, uint32_t n_total) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    int rc = halo_plan_ok(plan);
+    if (!rc) rc = halo_counts_ok(merged_counts, n_total);
+    if (rc) return rc;
+    if ((n_rec && !d_rec) || (n_pairs && !d_pairs)) return fail(CG_E_INVALID, "null buffers");
+    const uint64_t Mtot = (uint64_t)merged_counts[1] + plan->n_pads;
+    if (n_rec > Mtot) return fail(CG_E_INVALID, "%u voxel records for %llu detector points", n_rec,
+                                  (unsigned long long)Mtot);
+    HIPCHK(hipSetDevice(h->device));
+    rc = own_stream(h);
+    if (!rc) rc = ensure_large(h, n_total);
+    if (!rc) rc = ensure_batch(h, 1, n_total, false);
+    if (rc) return rc;
+    LgScratch S = h->lg;
+    S.pidx_base = 0;
+    CgLaunch L{};
+    L.n_frames = 1;
+    L.n_points = n_total;
+    fill_launch_outputs(h, L);
+    L.stamps = nullptr;
+    HIPCHK((hipError_t)cg_halo_merge_run(L, h->dp, S, h->stream, d_rec, n_rec, d_pairs, n_pairs, plan->key_bits,
+                                         (uint32_t)Mtot, merged_counts[0]));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
+    h->last_single = false;
+    return CG_OK;
+}
+
 int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words) {
     return cg_debug_large_buffer(h, 0, out, (uint64_t)n_words * 4);
 }

@@ -147,6 +147,21 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
 // A tiled frame's gathered survivors and merged counts (K, Ms, nfin, bounds keys) into S.
 int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_points, const uint32_t* d_index,
                            uint32_t n, const uint32_t* counts, hipStream_t s);
+// C5 halo tiling (cg_large.hip): a slab's voxels and components -> records; cross-slab
+// edges -> component pairs (count at d_count); the merge of all slabs -> results in slot 0.
+int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, const float* d_points,
+                      const uint32_t* d_index, uint32_t n, uint32_t npad_local, uint32_t npad_all,
+                      const uint32_t* counts, uint32_t N, uint32_t key_bits, uint32_t* d_rec, uint32_t cap,
+                      uint32_t* n_vox);
+int cg_halo_edges_run(const uint32_t* own, uint32_t n_own, const uint32_t* halo, uint32_t n_halo, float r2,
+                      uint32_t* pairs, uint32_t cap, uint32_t* d_count, hipStream_t s);
+int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, const uint32_t* d_rec,
+                      uint32_t V, const uint32_t* d_pairs, uint32_t np, uint32_t key_bits, uint32_t Mtot,
+                      uint32_t K);
+void cg_halo_plan_compute(const CgDevParams& P, const uint32_t* merged_counts, uint32_t N, uint32_t n_ranks,
+                          struct cg_halo_plan* out);
+int cg_launch_halo_owner(const float* pts, uint32_t n, float inv0, int32_t min_b0, uint32_t slab_w, uint32_t slabs,
+                         int32_t* out, hipStream_t s);
 // The LDS backend of the frame kernel on a large frame's survivors (M <= CG_MMAX).
 int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
                             uint32_t npad, uint32_t K, hipStream_t s);

@@ -1213,3 +1213,257 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
         }
     });
 }
+
+// ------------------------------------------------------------------------------------------
+// C5 spatial tiling with a halo exchange (include/cones_gpu.h, cg_halo_*). The frame's PCL
+// voxel lattice (global bounds, so idx is the whole frame's) is cut into slabs of voxel columns
+// along x. A voxel lies in one slab, so each rank's voxel sums are the whole frame's (its
+// survivors arrive in frame-index order); clustering runs per slab, and only the edges across
+// a slab boundary need the neighbour's voxels: those within `band` columns of the boundary.
+//
+// Records (CG_HALO_REC_WORDS words): x, y, z, intensity (voxel centroid), idx, idx of the
+// lowest voxel of the voxel's component in its slab, 0, 0.
+
+// slab of each survivor by its voxel column (lg_voxel_keys's arithmetic); -1: non-finite
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_owner(const float4* pts, uint32_t n, float inv0, int32_t min_b0,
+                                                          uint32_t slab_w, uint32_t slabs, int32_t* out) {
+    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const float4 p = pts[j];
+    int32_t s = -1;
+    if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+        const int i0 = (int)(floorf(p.x * inv0) - (float)min_b0);
+        s = (int32_t)min((uint32_t)i0 / slab_w, slabs - 1);
+    }
+    out[j] = s;
+}
+// the local backend's run ends and scan length cover the slab's points only (the lattice
+// came from the whole frame's bounds)
+__global__ void lg_halo_counts(LgScratch S, uint32_t nfin_local) {
+    if (threadIdx.x != 0) return;
+    S.meta[LG_NFIN_ALL] = nfin_local;
+    S.meta[LG_SCAN_N] = nfin_local;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_records(LgScratch S, int buf, uint32_t PB, uint32_t* rec,
+                                                            uint32_t cap) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
+    if (v >= V || v >= cap) return;
+    const uint64_t* vkey = buf ? S.key1 : S.key0;
+    const float4 c = S.vox[v];
+    const uint32_t root = S.lab[v];
+    uint4* r = (uint4*)(rec + (uint64_t)v * CG_HALO_REC_WORDS);
+    r[0] = make_uint4(__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), __float_as_uint(c.w));
+    r[1] = make_uint4((uint32_t)(vkey[S.run[v]] >> PB), (uint32_t)(vkey[S.run[root]] >> PB), 0u, 0u);
+}
+
+int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, const float* d_points,
+                      const uint32_t* d_index, uint32_t n, uint32_t npad_local, uint32_t npad_all,
+                      const uint32_t* counts, uint32_t N, uint32_t key_bits, uint32_t* d_rec, uint32_t cap,
+                      uint32_t* n_vox) {
+    hipError_t e;
+    uint32_t c[CG_TILE_COUNTS];
+    for (int a = 0; a < CG_TILE_COUNTS; a++) c[a] = counts[a];
+    c[1] = n;   // the slab's survivors; nfin and bounds stay the whole frame's (the lattice)
+    int rc = cg_large_set_survivors(S, P, d_points, d_index, n, c, s);
+    if (rc) return rc;
+    uint32_t hstack[LG_META_WORDS];
+    uint32_t* const hm = S.hmeta ? S.hmeta : hstack;
+    if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint32_t Mtot = n + npad_local;
+    *n_vox = 0;
+    if (Mtot == 0) return hipSuccess;
+    const uint32_t PB = hm[LG_UNSORTED] ? bits_of((uint64_t)N + npad_all) : 0u;
+    key_bits = std::min<uint32_t>(key_bits + PB, 32 + PB);
+    const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
+    hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad_all, Mtot);
+    hipLaunchKernelGGL(lg_halo_counts, dim3(1), dim3(64), 0, s, S, Mtot);
+    hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
+    const int buf = radix_sort(S, Mtot, key_bits, s);
+    const uint64_t* vkey = buf ? S.key1 : S.key0;
+    scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
+    hipLaunchKernelGGL(lg_voxel_centroids, dim3(std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES)), dim3(CG_BLOCK), 0, s,
+                       L, S, 0u, Mtot, buf);
+    const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES);
+    const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
+    hipLaunchKernelGGL(lg_dgrid_zero, dim3(256), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_tiles, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_scan, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_emit, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
+    hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
+    hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_halo_records, dim3(vb), dim3(CG_BLOCK), 0, s, S, buf, PB, d_rec, cap);
+    if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *n_vox = hm[LG_V];
+    return hipGetLastError();
+}
+
+// Cross-slab edges: one wave per halo record, the lanes test 64 own records at a time with the
+// clustering predicate; every distinct own component a halo voxel touches gives one pair
+// (own component key, halo component key). The count is exact; pairs past cap are dropped.
+#define LG_HALO_SEEN 8
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_edges(const uint32_t* own, uint32_t n_own, const uint32_t* halo,
+                                                          uint32_t n_halo, float r2, uint32_t* pairs, uint32_t cap,
+                                                          uint32_t* count) {
+    const uint32_t t = blockIdx.x * WAVES + wave_id(), l = lane_id();
+    if (t >= n_halo) return;
+    const uint4* hr = (const uint4*)(halo + (uint64_t)t * CG_HALO_REC_WORDS);
+    const uint4 h0 = hr[0], h1 = hr[1];
+    const float4 q = make_float4(__uint_as_float(h0.x), __uint_as_float(h0.y), __uint_as_float(h0.z), 0.f);
+    uint32_t seen[LG_HALO_SEEN];
+    uint32_t nseen = 0;
+    for (uint32_t g0 = 0; g0 < n_own; g0 += 64) {
+        const uint32_t j = g0 + l;
+        bool adj = false;
+        uint32_t root = 0;
+        if (j < n_own) {
+            const uint4* orr = (const uint4*)(own + (uint64_t)j * CG_HALO_REC_WORDS);
+            const uint4 o0 = orr[0];
+            const float4 p = make_float4(__uint_as_float(o0.x), __uint_as_float(o0.y), __uint_as_float(o0.z), 0.f);
+            adj = lg_adjacent(p, q, r2);
+            if (adj) root = orr[1].y;
+        }
+        for (uint32_t k = 0; k < nseen; k++) adj = adj && root != seen[k];
+        uint64_t m = __ballot(adj);
+        while (m) {
+            const uint32_t key = __builtin_amdgcn_readlane(root, (int)__builtin_ctzll(m));
+            if (l == 0) {
+                const uint32_t at = atomicAdd(count, 1u);
+                if (at < cap) { pairs[2 * at] = key; pairs[2 * at + 1] = h1.y; }
+            }
+            if (nseen < LG_HALO_SEEN) seen[nseen++] = key;
+            adj = adj && root != key;
+            m = __ballot(adj);
+        }
+    }
+}
+int cg_halo_edges_run(const uint32_t* own, uint32_t n_own, const uint32_t* halo, uint32_t n_halo, float r2,
+                      uint32_t* pairs, uint32_t cap, uint32_t* d_count, hipStream_t s) {
+    if (hipMemsetAsync(d_count, 0, 4, s) != hipSuccess) return hipGetLastError();
+    if (n_halo && n_own)
+        hipLaunchKernelGGL(lg_halo_edges, dim3((n_halo + WAVES - 1) / WAVES), dim3(CG_BLOCK), 0, s, own, n_own, halo,
+                           n_halo, r2, pairs, cap, d_count);
+    return hipGetLastError();
+}
+
+// Merge on one rank: the records of every slab sorted by idx (the global voxel order), the
+// slab components as a forest (every voxel under its component's lowest voxel), the pairs
+// united; then the backend's tail (size filter, PCL's cluster order, CSR, centroids).
+__global__ void lg_halo_meta(LgScratch S, uint32_t V) {
+    if (threadIdx.x != 0) return;
+    S.meta[LG_V] = V;
+    S.meta[LG_PASS] = 0;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_keys(LgScratch S, const uint32_t* rec, uint32_t V) {
+    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (j >= V) return;
+    S.key0[j] = rec[(uint64_t)j * CG_HALO_REC_WORDS + 4];
+    S.val0[j] = j;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_place(CgLaunch L, LgScratch S, const uint32_t* rec, uint32_t V,
+                                                          int buf) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const uint32_t j = (buf ? S.val1 : S.val0)[v];
+    const uint4 r0 = ((const uint4*)(rec + (uint64_t)j * CG_HALO_REC_WORDS))[0];
+    const float4 c = make_float4(__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z),
+                                 __uint_as_float(r0.w));
+    S.vox[v] = c;
+    L.vox[v] = c;
+    S.uk[v] = (uint32_t)(buf ? S.key1 : S.key0)[v];
+    S.cnt[v] = 0;
+    S.rk[v] = 0xffffffffu;
+}
+__device__ __forceinline__ uint32_t lg_halo_find_key(const uint32_t* uk, uint32_t V, uint32_t key) {
+    uint32_t lo = 0, hi = V;   // first position with uk >= key (keys are unique and present)
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (uk[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo < V ? lo : V - 1;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_forest(LgScratch S, const uint32_t* rec, uint32_t V, int buf) {
+    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (v >= V) return;
+    const uint32_t j = (buf ? S.val1 : S.val0)[v];
+    S.par[v] = lg_halo_find_key(S.uk, V, rec[(uint64_t)j * CG_HALO_REC_WORDS + 5]);
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_halo_unite(LgScratch S, const uint32_t* pairs, uint32_t np, uint32_t V) {
+    const uint32_t i = blockIdx.x * CG_BLOCK + threadIdx.x;
+    if (i >= np) return;
+    uf_union(S.par, lg_halo_find_key(S.uk, V, pairs[2 * i]), lg_halo_find_key(S.uk, V, pairs[2 * i + 1]));
+}
+
+int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, const uint32_t* d_rec,
+                      uint32_t V, const uint32_t* d_pairs, uint32_t np, uint32_t key_bits, uint32_t Mtot,
+                      uint32_t K) {
+    hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
+    hipLaunchKernelGGL(lg_halo_meta, dim3(1), dim3(64), 0, s, S, V);
+    const uint32_t n = std::max<uint32_t>(V, 1);
+    const uint32_t vb = blocks_of(n), wb = (n + WAVES - 1) / WAVES;
+    int buf = 0;
+    if (V) {
+        hipLaunchKernelGGL(lg_halo_keys, dim3(vb), dim3(CG_BLOCK), 0, s, S, d_rec, V);
+        buf = radix_sort(S, V, key_bits, s);
+        hipLaunchKernelGGL(lg_halo_place, dim3(vb), dim3(CG_BLOCK), 0, s, L, S, d_rec, V, buf);
+        hipLaunchKernelGGL(lg_halo_forest, dim3(vb), dim3(CG_BLOCK), 0, s, S, d_rec, V, buf);
+        if (np) hipLaunchKernelGGL(lg_halo_unite, dim3(blocks_of(np)), dim3(CG_BLOCK), 0, s, S, d_pairs, np, V);
+        hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    }
+    scan_emit(S, n, LG_V, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
+    hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    const uint32_t VB = bits_of(n);
+    hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, L, S, 0u, VB);
+    const uint32_t cmax = P.min_cl > 1 ? n / P.min_cl : n;
+    const int kb = radix_sort(S, n, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V);
+    hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)n + 1)), dim3(CG_BLOCK), 0, s, L, S, 0u, VB, kb, Mtot, K);
+    hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, L, P, S, 0u);
+    return hipGetLastError();
+}
+int cg_launch_halo_owner(const float* pts, uint32_t n, float inv0, int32_t min_b0, uint32_t slab_w, uint32_t slabs,
+                         int32_t* out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(lg_halo_owner, dim3(blocks_of(n)), dim3(CG_BLOCK), 0, s, (const float4*)pts, n, inv0,
+                              min_b0, slab_w, slabs, out);
+    return hipGetLastError();
+}
+// The plan (cg_halo_plan_frame): the whole frame's lattice from the merged counts, as
+// cg_large_backend computes it, cut into slabs at least `band` columns wide.
+void cg_halo_plan_compute(const CgDevParams& P, const uint32_t* c, uint32_t N, uint32_t n_ranks, struct cg_halo_plan* out) {
+    const uint32_t K = c[0];
+    const uint32_t npad = P.zero_pass ? N - K : 0u;
+    float bmn[3], bmx[3];
+    uint32_t nfin = c[2];
+    for (int a = 0; a < 3; a++) {
+        bmn[a] = nfin ? cg_fkey_inv(c[3 + a]) : INFINITY;
+        bmx[a] = nfin ? cg_fkey_inv(c[6 + a]) : -INFINITY;
+        if (npad) { bmn[a] = std::min(bmn[a], 0.f); bmx[a] = std::max(bmx[a], 0.f); }
+    }
+    nfin += npad;
+    uint32_t pass = 0;
+    int min_b[3], div_b[3];
+    voxel_grid_setup(nfin, bmn, bmx, P, pass, min_b, div_b);
+    *out = cg_halo_plan{};
+    out->passthrough = pass;
+    for (int a = 0; a < 3; a++) { out->min_b[a] = min_b[a]; out->div_b[a] = (uint32_t)div_b[a]; }
+    // |x1 - x2| < tol between centroids of columns i1 < i2 needs i2 - i1 <= tol / leaf + 1;
+    // one column more covers a centroid rounded across its cell edge
+    out->band = (uint32_t)std::ceil((double)std::sqrt(P.r2) * (double)P.inv_leaf[0]) + 2u;
+    const uint32_t dx = (uint32_t)div_b[0];
+    out->slabs = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(n_ranks, 1), dx / out->band));
+    out->slab_w = (dx + out->slabs - 1) / out->slabs;
+    out->n_pads = npad;
+    out->pad_slab = -1;
+    if (npad && !pass) {
+        const int i0 = (int)(floorf(0.f * P.inv_leaf[0]) - (float)min_b[0]);
+        out->pad_slab = (int32_t)std::min<uint32_t>((uint32_t)i0 / out->slab_w, out->slabs - 1);
+    }
+    out->key_bits = pass ? 0u
+                         : 1u + bits_of((uint64_t)(uint32_t)div_b[0] * (uint64_t)(uint32_t)div_b[1] *
+                                        (uint64_t)(uint32_t)div_b[2]);
+    out->key_bits = std::min<uint32_t>(out->key_bits, 32u);
+}

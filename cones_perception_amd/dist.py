@@ -136,11 +136,9 @@ def gather_survivors(points, index, device, dst: int = 0, sizes=None):
     return allr[:, :4].contiguous(), allr[:, 4].contiguous().view(torch.int32)
 
 
-def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, device, point_step: int = 16,
-                    offsets=(0, 4, 8, 12), dst: int = 0):
-    """Pipeline one frame of n_total points whose points [first, first + n) are at d_tile_ptr
-    on this rank's GPU. `engine` is a cones_perception_amd.BatchEngine (the handle). Returns the
-    frame's Detection on dst (bit-identical to the single-GPU call on the whole frame)."""
+def _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets):
+    """Steps 1-2 of the tile protocol plus the rank's survivors: (merged counts, every rank's
+    survivor count, survivor points (ns, 4), frame indices (ns,))."""
     import ctypes as C
     import numpy as np
     from . import _abi
@@ -156,8 +154,148 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
     si = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
     _abi.check(lib.cg_tile_survivors(h, sp.data_ptr(), si.data_ptr(), sp.shape[0]))
     total, sizes = merge_tile_counts(counts, device, per_rank=True)
-    gp, gi = gather_survivors(sp[:ns], si[:ns], device, dst, sizes=sizes)
+    return total, sizes, sp[:ns], si[:ns]
+
+
+def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, device, point_step: int = 16,
+                    offsets=(0, 4, 8, 12), dst: int = 0, halo: bool = False):
+    """Pipeline one frame of n_total points whose points [first, first + n) are at d_tile_ptr
+    on this rank's GPU. `engine` is a cones_perception_amd.BatchEngine (the handle). Returns the
+    frame's Detection on dst (bit-identical to the single-GPU call on the whole frame).
+    halo=False gathers the survivors to dst, which runs the backend; halo=True tiles the
+    backend too (run_halo_backend: voxel slabs, a halo exchange between neighbouring slabs)."""
+    from . import _abi
+    total, sizes, sp, si = _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets)
+    if halo:
+        det = run_halo_backend(engine, total, sp, si, n_total, device, dst)
+        if det is not False:
+            return det
+    gp, gi = gather_survivors(sp, si, device, dst, sizes=sizes)
     if _distributed() and dist.get_rank() != dst:
         return None
-    _abi.check(lib.cg_tile_backend(h, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]), total.ctypes.data, n_total))
+    _abi.check(_abi.lib().cg_tile_backend(engine.handle, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]),
+                                          total.ctypes.data, n_total))
+    return engine.fetch(0)
+
+
+# ---------------------------------------------------------------------------------------------
+# C5 backend tiled by voxel slabs with a halo exchange (include/cones_gpu.h, cg_halo_*).
+# Collectives per frame after the survivors are known: one all-to-all of the slab counts and
+# one of the survivors (each to its slab's rank), one all-gather of the record counts, one
+# point-to-point halo (each slab's lowest `band` voxel columns to the slab below), one
+# all-gather of the pair counts and one gather of the records and pairs to dst.
+
+def _split_exchange(rows, dest, world_size, device):
+    """rows (n, k) float32 with dest (n,) int32 in [-1, world): rows go to rank dest (in their
+    order; -1 dropped). Returns the rows this rank receives, in source-rank order."""
+    cd = _coll_device(device)
+    keep = dest >= 0
+    order = torch.argsort(dest[keep].to(torch.int64), stable=True)
+    send = rows[keep][order].to(cd).contiguous()
+    cnt = torch.bincount(dest[keep].to(torch.int64), minlength=world_size).to(cd)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt)
+    out = torch.empty((int(rcnt.sum().item()), rows.shape[1]), dtype=rows.dtype, device=cd)
+    dist.all_to_all_single(out, send, [int(x) for x in rcnt.tolist()], [int(x) for x in cnt.tolist()])
+    return out.to(device)
+
+
+def _all_gather_ints(vals, device):
+    cd = _coll_device(device)
+    t = torch.tensor(vals, dtype=torch.int64, device=cd)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return torch.stack(parts).cpu().tolist()
+
+
+last_halo_stats = {}   # the rank's figures of its last run_halo_backend call (tests, bench)
+
+
+def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0):
+    """The backend of a tiled frame from every rank's survivors (sp (ns, 4) float32, si (ns,)
+    frame indices) and the merged counts: slab voxelisation and clustering, halo edges, merge on
+    dst. Returns the Detection on dst, None elsewhere, or False when the frame has no voxel
+    lattice (PCL's overflow guard) and the caller must gather instead."""
+    import ctypes as C
+    from . import _abi
+    lib, h = _abi.lib(), engine.handle
+    ws = dist.get_world_size() if _distributed() else 1
+    rank = dist.get_rank() if _distributed() else 0
+    plan = _abi.cg_halo_plan()
+    _abi.check(lib.cg_halo_plan_frame(h, total.ctypes.data, n_total, ws, C.byref(plan)))
+    if plan.passthrough:
+        return False
+    ns = int(sp.shape[0])
+    slab = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
+    _abi.check(lib.cg_halo_owner(h, C.byref(plan), sp.data_ptr(), ns, slab.data_ptr()))
+    slab = slab[:ns]
+    # survivors to their slab's rank; sources hold ascending frame-index ranges, so every rank
+    # receives its slab's survivors in frame-index order
+    if ws > 1:
+        rows = torch.cat([sp, si.view(torch.float32).unsqueeze(1)], 1)
+        got = _split_exchange(rows, slab, ws, device)
+        mp_, mi = got[:, :4].contiguous(), got[:, 4].contiguous().view(torch.int32)
+    else:
+        keep = slab >= 0
+        mp_, mi = sp[keep].contiguous(), si[keep].contiguous()
+    n = int(mp_.shape[0])
+    npad = plan.n_pads if rank == plan.pad_slab else 0
+    cap = n + npad
+    rec = torch.empty((max(cap, 1), _abi.CG_HALO_REC_WORDS), dtype=torch.int32, device=device)
+    nv = C.c_uint32(0)
+    _abi.check(lib.cg_halo_local(h, C.byref(plan), mp_.data_ptr(), mi.data_ptr(), n, npad, total.ctypes.data,
+                                 n_total, rec.data_ptr(), rec.shape[0], C.byref(nv)))
+    rec = rec[: nv.value]
+    col = rec[:, 4] % int(plan.div_b[0])
+    lo = rank * plan.slab_w
+    top = rec[col >= lo + plan.slab_w - plan.band].contiguous()    # own side of the upper edge
+    low = rec[col < lo + plan.band].contiguous()                   # halo for the slab below
+    halo = torch.empty((0, _abi.CG_HALO_REC_WORDS), dtype=torch.int32, device=device)
+    if ws > 1:
+        counts = _all_gather_ints([int(rec.shape[0]), int(low.shape[0])], device)
+        cd = _coll_device(device)
+        ops = []
+        if 0 < rank < plan.slabs and low.shape[0]:
+            ops.append(dist.P2POp(dist.isend, low.to(cd), rank - 1))
+        nh = counts[rank + 1][1] if rank + 1 < min(ws, plan.slabs) else 0
+        if nh:
+            hbuf = torch.empty((nh, _abi.CG_HALO_REC_WORDS), dtype=torch.int32, device=cd)
+            ops.append(dist.P2POp(dist.irecv, hbuf, rank + 1))
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        if nh:
+            halo = hbuf.to(device)
+    pairs = torch.empty((max(4 * halo.shape[0], 64), 2), dtype=torch.int32, device=device)
+    npairs = C.c_uint32(0)
+    for _ in range(2):   # once more with room for every pair when the first guess was short
+        _abi.check(lib.cg_halo_edges(h, top.data_ptr(), top.shape[0], halo.data_ptr(), halo.shape[0],
+                                     pairs.data_ptr(), pairs.shape[0], C.byref(npairs)))
+        if npairs.value <= pairs.shape[0]:
+            break
+        pairs = torch.empty((npairs.value, 2), dtype=torch.int32, device=device)
+    pairs = pairs[: npairs.value]
+    last_halo_stats.clear()
+    last_halo_stats.update(slabs=int(plan.slabs), slab_w=int(plan.slab_w), band=int(plan.band), survivors=n,
+                           voxels=int(rec.shape[0]), halo_sent=int(low.shape[0]) if 0 < rank < plan.slabs else 0,
+                           halo_received=int(halo.shape[0]), pairs=int(pairs.shape[0]))
+    if ws > 1:
+        sizes = _all_gather_ints([int(rec.shape[0]), int(pairs.shape[0])], device)
+        vmax = max(1, max(s[0] for s in sizes))
+        pmax = max(1, max(s[1] for s in sizes))
+        cd = _coll_device(device)
+        W = _abi.CG_HALO_REC_WORDS
+        pack = torch.zeros((vmax * W + pmax * 2,), dtype=torch.int32, device=cd)
+        pack[: rec.numel()] = rec.reshape(-1).to(cd)
+        pack[vmax * W: vmax * W + pairs.numel()] = pairs.reshape(-1).to(cd)
+        bufs = [torch.empty_like(pack) for _ in range(ws)] if rank == dst else None
+        dist.gather(pack, bufs, dst=dst)
+        if rank != dst:
+            return None
+        rec = torch.cat([bufs[r][: sizes[r][0] * W].view(-1, W) for r in range(ws)], 0).to(device)
+        pairs = torch.cat([bufs[r][vmax * W: vmax * W + sizes[r][1] * 2].view(-1, 2) for r in range(ws)],
+                          0).to(device)
+    rec, pairs = rec.contiguous(), pairs.contiguous()
+    _abi.check(lib.cg_halo_merge(h, C.byref(plan), rec.data_ptr(), rec.shape[0], pairs.data_ptr(), pairs.shape[0],
+                                 total.ctypes.data, n_total))
     return engine.fetch(0)

@@ -191,6 +191,48 @@ int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t
 int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index, uint32_t n_survivors,
                     const uint32_t* merged_counts, uint32_t n_total);
 
+/* Spatial tiling with a halo exchange, in place of steps 3-4. The frame's
+ * PCL voxel lattice (from the merged bounds) is cut into slabs of voxel columns along x; a
+ * voxel lies in exactly one slab, and every rank voxelises and clusters its own slab:
+ *   a. cg_halo_plan_frame with the merged counts -> the lattice, slabs, band width and the
+ *      slab of the zero pads' voxel (host arithmetic, identical on every rank). A PCL
+ *      overflow-guard frame (passthrough) has no lattice: use steps 3-4;
+ *   b. cg_halo_owner: the slab of each of the rank's survivors (-1: non-finite, not
+ *      voxelised). Survivors go to their slab's rank (all-to-all, in frame-index order);
+ *   c. cg_halo_local on the slab's survivors (plus the pads on the pads' slab) -> one record
+ *      per voxel in idx order: x, y, z, intensity (PCL centroid), idx, idx of the lowest voxel
+ *      of its component within the slab, 0, 0;
+ *   d. the records of a slab's lowest `band` voxel columns go to the rank of the slab below
+ *      (point to point); there cg_halo_edges tests them against the own records of the top
+ *      `band` columns -> pairs (own component idx, neighbour component idx), one per distinct
+ *      component pair a halo voxel joins. n_pairs is exact; call again with capacity >=
+ *      n_pairs when it exceeds capacity;
+ *   e. every slab's records and pairs go to one rank: cg_halo_merge orders the voxels, unites
+ *      the components and writes the clusters, results as cg_tile_backend's.
+ * Results are bit-identical to the single-GPU call on the whole frame. */
+#define CG_HALO_REC_WORDS 8
+typedef struct cg_halo_plan {
+    uint32_t passthrough;   /* the voxel grid's overflow guard hit (no lattice) */
+    int32_t  min_b[3];      /* pcl::VoxelGrid min_b_ and div_b_ of the whole frame */
+    uint32_t div_b[3];
+    uint32_t slabs;         /* slab s owns voxel columns [s * slab_w, (s + 1) * slab_w) (last: to div_b[0]) */
+    uint32_t slab_w;
+    uint32_t band;          /* voxel columns within which an edge can cross a slab boundary */
+    int32_t  pad_slab;      /* slab of the zero pads' voxel; -1 when no pad reaches the detector */
+    uint32_t n_pads;
+    uint32_t key_bits;      /* bits of idx (plus one: non-finite points sort last) */
+} cg_halo_plan;
+int cg_halo_plan_frame(cg_handle* h, const uint32_t* merged_counts, uint32_t n_total, uint32_t n_ranks,
+                       cg_halo_plan* plan);
+int cg_halo_owner(cg_handle* h, const cg_halo_plan* plan, const float* d_points, uint32_t n, int32_t* d_slab);
+int cg_halo_local(cg_handle* h, const cg_halo_plan* plan, const float* d_points, const uint32_t* d_index,
+                  uint32_t n, uint32_t n_pads, const uint32_t* merged_counts, uint32_t n_total, uint32_t* d_rec,
+                  uint32_t capacity, uint32_t* n_vox);
+int cg_halo_edges(cg_handle* h, const uint32_t* d_own, uint32_t n_own, const uint32_t* d_halo, uint32_t n_halo,
+                  uint32_t* d_pairs, uint32_t capacity, uint32_t* n_pairs);
+int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec, uint32_t n_rec,
+                  const uint32_t* d_pairs, uint32_t n_pairs, const uint32_t* merged_counts, uint32_t n_total);
+
 /* ---- detector node after the hot path (src/cone_detection.cpp:171-186, 222-339) -------- */
 /* Cone re-crop, ConeDetector::get_reconstructed_cone (src/cone_detection.cpp:222-238): for each
  * cone centre (x, y), every point of the last single-frame call's detector input (the "whole

@@ -2,6 +2,7 @@
 (torch.distributed, gloo here so that 2-3 ranks can share the box's single GPU; RCCL on a
 multi-GPU node), merged with the cg_tile_* protocol, backend on rank 0. The result must be
 bit-identical to the CPU restatement on the whole frame."""
+import json
 import os
 import socket
 
@@ -26,7 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out, rings, cols, over):
+def _worker(rank, world, port, out, rings, cols, over, halo=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
@@ -40,31 +41,50 @@ def _worker(rank, world, port, out, rings, cols, over):
     dev = torch.device("cuda", 0)
     tile = torch.from_numpy(np.ascontiguousarray(raw[0, lo * 16: hi * 16])).to(dev)
     eng = cpp.BatchEngine(params, device=0)
-    det = cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev)
+    det = cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev, halo=halo)
+    st = [dict(cd.last_halo_stats)]
+    if halo and dist.get_world_size() > 1:
+        allst = [None] * world
+        dist.all_gather_object(allst, st[0])
+        st = allst
     if rank == 0:
-        np.savez(out, **{k: np.asarray(getattr(det, k)) for k in FIELDS})
+        np.savez(out, stats=np.array(json.dumps(st)), **{k: np.asarray(getattr(det, k)) for k in FIELDS})
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rings,cols,over", [
-    (2, 128, 2048, {}),
-    (3, 96, 2048, {}),
-    (2, 64, 2048, {"distance_treshold_min": 0.0}),   # zero pads survive: global backend on rank 0
+@pytest.mark.parametrize("world,rings,cols,over,halo", [
+    (2, 128, 2048, {}, False),
+    (3, 96, 2048, {}, False),
+    (2, 64, 2048, {"distance_treshold_min": 0.0}, False),   # zero pads survive: global backend on rank 0
+    # voxel slabs with a halo exchange: clusters cross slab edges, pads on one slab
+    (2, 128, 2048, {}, True),
+    (3, 96, 2048, {}, True),
+    (4, 64, 2048, {"distance_treshold_min": 0.0}, True),
+    (4, 64, 2048, {"distance_treshold_max": 30.0, "max_cluster_size": 100000}, True),   # the wall: long clusters
 ])
-def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over):
+def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over, halo):
     out = str(tmp_path / "r0.npz")
-    mp.spawn(_worker, args=(world, _free_port(), out, rings, cols, over), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, rings, cols, over, halo), nprocs=world, join=True)
     z = np.load(out)
     got = Detection(*(z[k].item() if z[k].ndim == 0 else z[k] for k in FIELDS))
     params = cp.load_params("simulation", over)
     raw = cp.synth_frames(1, first_frame=4, rings=rings, cols=cols, clutter=40, cones_per_row=10)
     ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE)
     assert got.n_points == rings * cols
-    assert_same_detection(got, ref, f"tiled x{world}")
+    assert_same_detection(got, ref, f"tiled x{world} halo={halo}")
+    if halo:
+        # the halo path ran on every slab; the wall case's clusters cross every slab edge
+        st = json.loads(str(z["stats"]))
+        assert all(s["slabs"] == world for s in st), st
+        assert sum(s["voxels"] for s in st) == got.voxels.shape[0], st
+        assert all(s["halo_received"] > 0 for s in st[:-1]), st
+        if "max_cluster_size" in over:
+            assert all(s["pairs"] > 0 for s in st[:-1]), st
 
 
-def test_tiled_single_rank_matches_oracle():
+@pytest.mark.parametrize("halo", [False, True])
+def test_tiled_single_rank_matches_oracle(halo):
     """World size 1 (no process group): the tile protocol on one tile = the whole frame."""
     import torch
     from cones_perception_amd import dist as cd
@@ -72,6 +92,7 @@ def test_tiled_single_rank_matches_oracle():
     raw = cp.synth_frames(1, first_frame=9, rings=80, cols=1024, clutter=40, cones_per_row=8)
     n = raw.shape[1] // 16
     d = torch.from_numpy(raw[0].copy()).to(torch.device("cuda", 0))
-    got = cd.run_tiled_frame(cp.BatchEngine(params, device=0), d.data_ptr(), 0, n, n, torch.device("cuda", 0))
+    got = cd.run_tiled_frame(cp.BatchEngine(params, device=0), d.data_ptr(), 0, n, n, torch.device("cuda", 0),
+                             halo=halo)
     ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE)
     assert_same_detection(got, ref, "tiled x1")
