@@ -465,9 +465,20 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, c
     {
         const uint32_t nt = gridDim.x, b = blockIdx.x;
         uint32_t tot = 0, pre = 0;
-        if (tid < 256) {
+        if (tid < 256) {   // eight count loads in flight (a dependent walk costs an L2 trip per tile)
             const uint32_t* h = hist + (uint64_t)tid * nt;
-            for (uint32_t t = 0; t < nt; t++) {
+            uint32_t t = 0;
+            for (; t + 8 <= nt; t += 8) {
+                uint32_t c[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) c[u] = h[t + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    tot += c[u];
+                    pre += t + u < b ? c[u] : 0u;
+                }
+            }
+            for (; t < nt; t++) {
                 const uint32_t c = h[t];
                 tot += c;
                 pre += t < b ? c : 0u;
@@ -861,12 +872,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P)
         if (o > v && po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, v, o);
     });
 }
+// roots and component sizes: the lanes of a wave that share a root add their count with one
+// atomic (a component's voxels are mostly neighbours in idx order; same-address atomics from
+// every voxel of a large component serialise)
 __global__ __launch_bounds__(CG_BLOCK) void lg_find(LgScratch S) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
-    if (v >= V) return;
-    const uint32_t r = uf_find(S.par, v);
-    S.lab[v] = r;
-    atomicAdd(&S.cnt[r], 1u);
+    const bool in = v < V;
+    uint32_t r = 0;
+    if (in) {
+        r = uf_find(S.par, v);
+        S.lab[v] = r;
+    }
+    uint64_t m = __ballot(in);
+    while (m) {
+        const uint32_t lead = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)__builtin_ctzll(m));
+        const uint64_t same = __ballot(in && r == lead) & m;
+        if (lane_id() == (uint32_t)__builtin_ctzll(m)) atomicAdd(&S.cnt[lead], (uint32_t)__builtin_popcountll(same));
+        m &= ~same;
+    }
 }
 struct KeepRoot {   // component seeds whose size passes min <= size <= max, in seed order
     const uint32_t* lab; const uint32_t* cnt; uint32_t lo, hi;
@@ -887,8 +910,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
     __shared__ int32_t stk[3 * CG_SORT_STACK];
     __shared__ uint32_t red[8 * WAVES];
     const uint32_t tid = threadIdx.x;
-    const uint32_t C = S.meta[LG_C];
-    if (C > CG_SORT_THRESHOLD) {
+    const uint32_t C = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.meta[LG_C]);
+    if (C > CG_SORT_THRESHOLD && C <= 64) {
+        // wave 0 runs the introsort restatement on records held one per lane (scalar control,
+        // v_readlane / v_writelane element accesses instead of dependent LDS round trips)
+        if (wave_id() == 0) {
+            const uint32_t l = lane_id();
+            uint32_t lo = 0, hi = 0;
+            if (l < C) { lo = C - 1 - l; hi = S.dsz[lo]; }
+            int32_t st[3] = {0, 0, 0};
+            const CgWaveRegs64 f{&lo, &hi, 0};
+            const CgWaveStack sk{st};
+            cg_std_sort(f, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, sk);
+            if (l < C) {
+                S.fin[C - 1 - l] = lo;
+                S.rank[lo] = C - 1 - l;
+            }
+        }
+    } else if (C > CG_SORT_THRESHOLD) {
         // one lane runs the introsort restatement, on LDS records when they fit
         __shared__ uint64_t lrec[LG_ORDER_LDS];
         uint64_t* rec = C <= LG_ORDER_LDS ? lrec : S.key0;

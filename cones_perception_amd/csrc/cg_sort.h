@@ -9,21 +9,31 @@
 // libstdc++'s algorithm step for step: median-of-three pivot moved to first, unguarded Hoare
 // partition, depth limit 2*floor(log2 n) with heapsort fallback, threshold 16, final insertion
 // sort (guarded on the first 16, unguarded after). The GCC 9-13 implementation is unchanged
-// across those releases. tests/test_sort_host.py checks this restatement against the host
-// std::sort permutation for many tie-heavy inputs.
+// across those releases. The GPU parity tests check it against the oracle's host std::sort on
+// tie-heavy cluster lists (frames with more than 16 clusters of repeated sizes).
 //
-// Single-threaded by design (runs in one lane over short arrays such as the cluster list).
+// Sequential by design. The array is any A with f[i] (read, assign) and f + d (a view at
+// offset d): a pointer (one lane over LDS or memory), or CgWaveRegs64 below (every lane of
+// one wave runs the same uniform program over records held one per lane, so that indices
+// and compares stay scalar and element accesses are v_readlane / v_writelane).
 #pragma once
 #include <stdint.h>
 #include "cg_math.h"
 
 #define CG_SORT_THRESHOLD 16
 
-template <class T>
-CG_HD void cg_iter_swap(T* a, long i, long j) { T t = a[i]; a[i] = a[j]; a[j] = t; }
+template <class A> struct cg_elem { using type = typename A::value_type; };
+template <class T> struct cg_elem<T*> { using type = T; };
 
-template <class T, class L>
-CG_HD void cg_adjust_heap(T* f, long hole, long len, T value, L less) {
+template <class A>
+CG_HD void cg_iter_swap(A a, long i, long j) {
+    typename cg_elem<A>::type t = a[i];
+    a[i] = a[j];
+    a[j] = t;
+}
+
+template <class A, class T, class L>
+CG_HD void cg_adjust_heap(A f, long hole, long len, T value, L less) {
     const long top = hole;
     long second = hole;
     while (second < (len - 1) / 2) {
@@ -46,31 +56,31 @@ CG_HD void cg_adjust_heap(T* f, long hole, long len, T value, L less) {
     f[hole] = value;
 }
 
-template <class T, class L>
-CG_HD void cg_make_heap(T* f, long len, L less) {
+template <class A, class L>
+CG_HD void cg_make_heap(A f, long len, L less) {
     if (len < 2) return;
     long parent = (len - 2) / 2;
     while (true) {
-        T v = f[parent];
+        typename cg_elem<A>::type v = f[parent];
         cg_adjust_heap(f, parent, len, v, less);
         if (parent == 0) return;
         parent--;
     }
 }
 
-template <class T, class L>
-CG_HD void cg_heap_sort_range(T* f, long len, L less) {   // __partial_sort(first, last, last)
+template <class A, class L>
+CG_HD void cg_heap_sort_range(A f, long len, L less) {   // __partial_sort(first, last, last)
     cg_make_heap(f, len, less);
     while (len > 1) {
         --len;
-        T v = f[len];
+        typename cg_elem<A>::type v = f[len];
         f[len] = f[0];
         cg_adjust_heap(f, 0L, len, v, less);
     }
 }
 
-template <class T, class L>
-CG_HD void cg_move_median_to_first(T* f, long result, long a, long b, long c, L less) {
+template <class A, class L>
+CG_HD void cg_move_median_to_first(A f, long result, long a, long b, long c, L less) {
     if (less(f[a], f[b])) {
         if (less(f[b], f[c])) cg_iter_swap(f, result, b);
         else if (less(f[a], f[c])) cg_iter_swap(f, result, c);
@@ -80,8 +90,8 @@ CG_HD void cg_move_median_to_first(T* f, long result, long a, long b, long c, L 
     else cg_iter_swap(f, result, b);
 }
 
-template <class T, class L>
-CG_HD long cg_unguarded_partition(T* f, long first, long last, long pivot, L less) {
+template <class A, class L>
+CG_HD long cg_unguarded_partition(A f, long first, long last, long pivot, L less) {
     while (true) {
         while (less(f[first], f[pivot])) ++first;
         --last;
@@ -92,11 +102,11 @@ CG_HD long cg_unguarded_partition(T* f, long first, long last, long pivot, L les
     }
 }
 
-template <class T, class L>
-CG_HD void cg_insertion_sort(T* f, long first, long last, L less) {
+template <class A, class L>
+CG_HD void cg_insertion_sort(A f, long first, long last, L less) {
     if (first == last) return;
     for (long i = first + 1; i != last; ++i) {
-        T val = f[i];
+        typename cg_elem<A>::type val = f[i];
         if (less(val, f[first])) {
             for (long k = i; k > first; --k) f[k] = f[k - 1];
             f[first] = val;
@@ -108,10 +118,10 @@ CG_HD void cg_insertion_sort(T* f, long first, long last, L less) {
     }
 }
 
-template <class T, class L>
-CG_HD void cg_unguarded_insertion_sort(T* f, long first, long last, L less) {
+template <class A, class L>
+CG_HD void cg_unguarded_insertion_sort(A f, long first, long last, L less) {
     for (long i = first; i != last; ++i) {
-        T val = f[i];
+        typename cg_elem<A>::type val = f[i];
         long hole = i, next = i - 1;
         while (less(val, f[next])) { f[hole] = f[next]; hole = next; --next; }
         f[hole] = val;
@@ -125,8 +135,8 @@ CG_HD int cg_lg(long n) { int r = 0; while (n > 1) { n >>= 1; r++; } return r; }
 // result, only each range's depth budget matters (kept per stack entry). `stk` holds
 // 3 * CG_SORT_STACK ints (LDS on the device); pending entries never exceed 2*floor(log2 n).
 #define CG_SORT_STACK 64
-template <class T, class L>
-CG_HD void cg_std_sort(T* f, long n, L less, int* stk) {
+template <class A, class L, class STK>
+CG_HD void cg_std_sort(A f, long n, L less, STK stk) {
     if (n <= 1) return;
     int sp = 0;
     stk[0] = 0; stk[1] = (int)n; stk[2] = cg_lg(n) * 2; sp = 1;
@@ -151,3 +161,57 @@ CG_HD void cg_std_sort(T* f, long n, L less, int* stk) {
         cg_insertion_sort(f, 0L, n, less);
     }
 }
+
+#ifdef __HIPCC__
+// v_writelane: lane k of v takes x (k uniform)
+__device__ __forceinline__ int cg_writelane(int x, int k, int v) {
+    return (int)(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))) == k ? x : v;
+}
+// Records of one wave, element i in lane i (64-bit: two VGPRs). Every lane of the wave must
+// run the same program with uniform indices (the sort above, called by the whole wave).
+struct CgWaveRegs64 {
+    using value_type = uint64_t;
+    uint32_t* lo;
+    uint32_t* hi;
+    long base;
+    struct Ref {
+        const CgWaveRegs64* a;
+        long i;
+        __device__ __forceinline__ operator uint64_t() const { return a->get(i); }
+        __device__ __forceinline__ Ref& operator=(uint64_t v) { a->set(i, v); return *this; }
+        __device__ __forceinline__ Ref& operator=(const Ref& o) { a->set(i, (uint64_t)o); return *this; }
+    };
+    __device__ __forceinline__ uint64_t get(long i) const {
+        const int k = (int)(base + i);
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)*hi, k) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)*lo, k);
+    }
+    __device__ __forceinline__ void set(long i, uint64_t v) const {
+        const int k = (int)(base + i);
+        *lo = (uint32_t)cg_writelane((int)(uint32_t)v, k, (int)*lo);
+        *hi = (uint32_t)cg_writelane((int)(uint32_t)(v >> 32), k, (int)*hi);
+    }
+    __device__ __forceinline__ Ref operator[](long i) const { return Ref{this, i}; }
+    __device__ __forceinline__ CgWaveRegs64 operator+(long d) const { return CgWaveRegs64{lo, hi, base + d}; }
+};
+// cg_std_sort's stack of (first, last, depth) triples, entry s in lane s of three VGPRs
+struct CgWaveStack {
+    int32_t* r;   // r[0..2]
+    struct Ref {
+        const CgWaveStack* a;
+        int i;
+        __device__ __forceinline__ operator int() const {
+            const int q = i / 3, k = i - 3 * q;
+            return __builtin_amdgcn_readlane(k == 0 ? a->r[0] : k == 1 ? a->r[1] : a->r[2], q);
+        }
+        __device__ __forceinline__ Ref& operator=(int v) {
+            const int q = i / 3, k = i - 3 * q;
+            if (k == 0) a->r[0] = cg_writelane(v, q, a->r[0]);
+            else if (k == 1) a->r[1] = cg_writelane(v, q, a->r[1]);
+            else a->r[2] = cg_writelane(v, q, a->r[2]);
+            return *this;
+        }
+    };
+    __device__ __forceinline__ Ref operator[](int i) const { return Ref{this, i}; }
+};
+#endif
