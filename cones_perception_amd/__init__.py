@@ -23,7 +23,8 @@ from ._abi import (CG_MODE_DETECT, CG_MODE_PIPELINE, CG_F_GLOBAL_SCRATCH, CG_F_O
 lib()   # fail loudly at import if the gfx950 library is missing
 
 __all__ = ["PROFILES", "load_params", "PointField", "PointCloud2", "Detection", "GroundRemover",
-           "ConeDetector", "ConePipeline", "BatchEngine", "synth_frames", "CgError"]
+           "ConeDetector", "ConePipeline", "BatchEngine", "synth_frames", "CgError", "ColorClassifier",
+           "read_tflite"]
 
 # ---------------------------------------------------------------------------------------
 # Parameter profiles: the reference's config/*.yaml (keys verbatim, misspellings kept).
@@ -475,3 +476,6 @@ def frame_cloud(raw: np.ndarray, point_step=16) -> PointCloud2:
     else:
         fields = [PointField("x", 0), PointField("y", 4), PointField("z", 8), PointField("intensity", 16)]
     return PointCloud2(n, 1, fields, point_step, n * point_step, raw.reshape(-1), True)
+
+
+from .colornet import ColorClassifier, read_tflite  # noqa: E402  (the colour service, §8f row 4)

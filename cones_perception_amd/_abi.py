@@ -145,6 +145,9 @@ _SIGS = {
                                 C.POINTER(C.c_uint32)]),
     "cg_halo_merge": (C.c_int, [C.c_void_p, C.POINTER(cg_halo_plan), C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                 C.c_void_p, C.c_uint32]),
+    "cg_colornet_set": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "cg_classify_colors": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                     C.c_void_p]),
     "cg_batch_results_get": (C.c_int, [C.c_void_p, C.POINTER(cg_batch_results)]),
     "cg_batch_fetch": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(cg_detect_result)]),
     "cg_selftest_atan2f": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),

@@ -48,7 +48,7 @@ def build(verbose=False, force=False):
     if force or _stale(o, [src] + HEADERS):
         _run(["gcc", "-O2", "-fPIC", "-ffp-contract=off", "-std=c11", "-Wall", "-c", src, "-o", o], verbose)
     objs.append(o)
-    for name in ("cg_kernels.hip", "cg_large.hip", "cg_recrop.hip", "cg_api.cpp", "cg_track.cpp"):
+    for name in ("cg_kernels.hip", "cg_large.hip", "cg_recrop.hip", "cg_colornet.hip", "cg_api.cpp", "cg_track.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(OBJ, name.rsplit(".", 1)[0] + ".o")
         if force or _stale(o, [src] + HEADERS):

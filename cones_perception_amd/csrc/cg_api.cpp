@@ -194,6 +194,12 @@ struct cg_handle {
     size_t rc_out_cap = 0;
     std::vector<uint32_t> h_rc_cnt, h_rc_off;
     std::vector<float> h_rc_pts, h_rc_dev;
+    // colour classifier (cg_colornet_set / cg_classify_colors)
+    float* d_cn_w = nullptr;
+    float4* d_cn_pts = nullptr;
+    size_t cn_pts_cap = 0;
+    uint32_t* d_cn_offs = nullptr;   // offsets, then colors (int32), probs (float), images (bytes)
+    size_t cn_cap = 0;
     // diagnostics
     bool stamps_on = false;
     uint64_t* d_stamps = nullptr;
@@ -337,6 +343,9 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
 int ensure_large(cg_handle* h, uint32_t n) {
     if (n <= h->large_points && h->d_large) return CG_OK;
     if (h->d_large) (void)hipFree(h->d_large);
+    if (h->d_cn_w) (void)hipFree(h->d_cn_w);
+    if (h->d_cn_pts) (void)hipFree(h->d_cn_pts);
+    if (h->d_cn_offs) (void)hipFree(h->d_cn_offs);
     h->d_large = nullptr;
     h->large_points = 0;
     HIPCHK(hipMalloc(&h->d_large, cg_large_bytes(n)));
@@ -907,6 +916,62 @@ int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec,
     HIPCHK(hipStreamSynchronize(h->stream));
     h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
     h->last_single = false;
+    return CG_OK;
+}
+
+// ---- colour classifier (cg_colornet.hip) --------------------------------------------------
+int cg_colornet_set(cg_handle* h, const float* weights, uint32_t n_weights) {
+    if (!h || !weights) return fail(CG_E_INVALID, "null argument");
+    if (n_weights != CG_COLORNET_WEIGHTS)
+        return fail(CG_E_INVALID, "colour net weights: %u floats, expected %u", n_weights, CG_COLORNET_WEIGHTS);
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
+    if (!h->d_cn_w) HIPCHK(hipMalloc(&h->d_cn_w, CG_COLORNET_WEIGHTS * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(h->d_cn_w, weights, CG_COLORNET_WEIGHTS * sizeof(float), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return CG_OK;
+}
+
+int cg_classify_colors(cg_handle* h, const float* points, const uint32_t* offsets, uint32_t n_cones,
+                       int32_t* colors, float* probs, uint8_t* images) {
+    if (!h || !offsets || (n_cones && !colors)) return fail(CG_E_INVALID, "null argument");
+    if (!h->d_cn_w) return fail(CG_E_INVALID, "no colour net weights: call cg_colornet_set first");
+    if (n_cones == 0) return CG_OK;
+    if (offsets[0] != 0) return fail(CG_E_INVALID, "offsets[0] must be 0");
+    for (uint32_t c = 0; c < n_cones; c++)
+        if (offsets[c + 1] < offsets[c]) return fail(CG_E_INVALID, "offsets decrease at cone %u", c);
+    const uint32_t np = offsets[n_cones];
+    if (np && !points) return fail(CG_E_INVALID, "null points");
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
+    if (np > h->cn_pts_cap) {
+        if (h->d_cn_pts) HIPCHK(hipFree(h->d_cn_pts));
+        h->d_cn_pts = nullptr;
+        h->cn_pts_cap = std::max<size_t>(np, 4096);
+        HIPCHK(hipMalloc(&h->d_cn_pts, h->cn_pts_cap * sizeof(float4)));
+    }
+    // per cone: offset (n + 1), colour, 3 probabilities, 180 image bytes (45 words)
+    const size_t words = (size_t)n_cones + 1 + n_cones + 3 * (size_t)n_cones + 45 * (size_t)n_cones;
+    if (words > h->cn_cap) {
+        if (h->d_cn_offs) HIPCHK(hipFree(h->d_cn_offs));
+        h->d_cn_offs = nullptr;
+        h->cn_cap = std::max<size_t>(words, 1024);
+        HIPCHK(hipMalloc(&h->d_cn_offs, h->cn_cap * 4));
+    }
+    uint32_t* d_offs = h->d_cn_offs;
+    int32_t* d_col = (int32_t*)(d_offs + n_cones + 1);
+    float* d_prob = (float*)(d_col + n_cones);
+    uint8_t* d_img = (uint8_t*)(d_prob + 3 * (size_t)n_cones);
+    if (np) HIPCHK(hipMemcpyAsync(h->d_cn_pts, points, (size_t)np * 16, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(d_offs, offsets, ((size_t)n_cones + 1) * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK((hipError_t)cg_launch_colornet(h->d_cn_pts, d_offs, n_cones, h->d_cn_w, d_col, d_prob,
+                                          images ? d_img : nullptr, h->stream));
+    HIPCHK(hipMemcpyAsync(colors, d_col, (size_t)n_cones * 4, hipMemcpyDeviceToHost, h->stream));
+    if (probs) HIPCHK(hipMemcpyAsync(probs, d_prob, (size_t)n_cones * 12, hipMemcpyDeviceToHost, h->stream));
+    if (images) HIPCHK(hipMemcpyAsync(images, d_img, (size_t)n_cones * 180, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
     return CG_OK;
 }
 

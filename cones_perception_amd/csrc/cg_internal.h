@@ -181,5 +181,8 @@ int cg_launch_recrop(const CgLaunch& L, const CgDevParams& P, bool pipeline, con
                      const RcBox* d_boxes, uint32_t nb, uint32_t* d_cnt, const uint32_t* d_off, float4* d_out,
                      bool write, hipStream_t s);
 
+// Colour classifier (cg_colornet.hip): one workgroup per cone cloud.
+int cg_launch_colornet(const float4* pts, const uint32_t* offs, uint32_t n_cones, const float* w, int32_t* colors,
+                       float* probs, uint8_t* images, hipStream_t s);
 int cg_launch_selftest_atan2f(const float* y, const float* x, float* out, uint32_t n, hipStream_t s);
 int cg_launch_selftest_sqrt(const double* in, double* out, uint32_t n, hipStream_t s);

@@ -220,6 +220,47 @@ private:
     cg_tracker* t_ = nullptr;
 };
 
+// The colour classifier service (scripts/color_classifier_server.py:81-124) on the GPU: usable
+// as the ColourService below. weights: CG_COLORNET_WEIGHTS floats (python -m
+// cones_perception_amd.colornet dam_net.tflite dam_net.f32 writes them). Like the reference's
+// handler it answers one colour per non-empty cloud, and fails the call (false) where the
+// reference raises (a point outside the 15 image rows, an intensity outside [0, 255]).
+class ColorClassifier : public Handle {
+public:
+    ColorClassifier(const std::vector<float>& weights, int device = 0) : Handle(default_params(), device) {
+        check(cg_colornet_set(h_, weights.data(), (uint32_t)weights.size()));
+    }
+    bool operator()(const std::vector<PointCloud2>& cones, std::vector<int32_t>& colours) {
+        std::vector<float> pts;
+        std::vector<uint32_t> offs{0};
+        for (const auto& m : cones) {   // pc2.read_points: x, y, z, intensity by field name
+            const int32_t o[4] = {m.offset_of("x"), m.offset_of("y"), m.offset_of("z"), m.offset_of("intensity")};
+            for (uint32_t r = 0; r < m.height; r++)
+                for (uint32_t c = 0; c < m.width; c++) {
+                    const uint8_t* p = m.data.data() + (size_t)r * m.row_step + (size_t)c * m.point_step;
+                    for (int a = 0; a < 4; a++) {
+                        float v = 0.f;
+                        if (o[a] >= 0) std::memcpy(&v, p + o[a], 4);
+                        pts.push_back(v);
+                    }
+                }
+            offs.push_back((uint32_t)(pts.size() / 4));
+        }
+        std::vector<int32_t> st(cones.size());
+        check(cg_classify_colors(h_, pts.empty() ? nullptr : pts.data(), offs.data(), (uint32_t)cones.size(),
+                                 st.data(), nullptr, nullptr));
+        colours.clear();
+        for (int32_t c : st) {
+            if (c == CG_COLOR_SKIPPED) continue;
+            if (c < 0) return false;
+            colours.push_back(c);
+        }
+        return true;
+    }
+private:
+    static cg_params default_params() { cg_params p; cg_params_init(&p); return p; }
+};
+
 // The whole ConeDetector::cloud_handler (src/cone_detection.cpp:130-187): the hot path, tracking,
 // the re-crop of cones that need a colour, the colour service (a callback standing in for
 // ClassifyColorSrv: it gets one PointXYZI message per cone, frame_id = cones_frame_id, and returns

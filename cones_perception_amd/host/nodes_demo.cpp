@@ -104,6 +104,29 @@ int main(int argc, char** argv) {
             std::printf(" %s\n", ok ? "fused == two-node" : "MISMATCH");
             if (!ok) return 1;
         }
+        // with a weights file (argv[2], CG_COLORNET_WEIGHTS raw float32): the colour service
+        // served on the GPU by the dam_net classifier
+        if (argc > 2) {
+            std::vector<float> w(CG_COLORNET_WEIGHTS);
+            FILE* fw = std::fopen(argv[2], "rb");
+            if (!fw || std::fread(w.data(), 4, w.size(), fw) != w.size()) throw std::runtime_error("bad weights file");
+            std::fclose(fw);
+            ColorClassifier clf(w);
+            ConeDetectorNode<ConePipeline> gpu_node(p, tp, [&clf](const std::vector<PointCloud2>& c, std::vector<int32_t>& k) {
+                return clf(c, k);
+            });
+            uint32_t published = 0;
+            for (int f = 0; f < frames; f++) {
+                const auto a = gpu_node.cloud_handler(synth_cloud(10));
+                std::printf("gpu colour service frame %d:", f);
+                for (int i = 0; i < CG_NUM_COLORS; i++) {
+                    std::printf(" %u", a[i].width);
+                    published += a[i].width;
+                }
+                std::printf("\n");
+            }
+            if (frames > 1 && published == 0) return 1;
+        }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 2;

@@ -233,6 +233,27 @@ int cg_halo_edges(cg_handle* h, const uint32_t* d_own, uint32_t n_own, const uin
 int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec, uint32_t n_rec,
                   const uint32_t* d_pairs, uint32_t n_pairs, const uint32_t* merged_counts, uint32_t n_total);
 
+/* ---- colour classifier service ----------------------------------- */
+/* ColorClassifier.handle_classify_color (scripts/color_classifier_server.py:81-124) with its
+ * to_image (131-156) and the dam_net CNN it runs through TFLite (models/dam_net/dam_net.tflite),
+ * on the GPU. The node's colour-service call (src/cone_detection.cpp:342-363) can be served by
+ * it in process. Weights: the .tflite graph's constants packed as float32, in this order
+ * (shapes as in the graph): conv2d kernel [16][3][3] (OHW, one input channel), conv2d bias [16],
+ * conv2d_1 kernel [32][3][3][16] (OHWI), conv2d_1 bias [32], batch-norm MUL [32], batch-norm
+ * ADD [32], dense kernel [3][64], dense bias [3]. cones_perception_amd.colornet reads them from
+ * the .tflite file (the reference's ~model_path). */
+#define CG_COLORNET_WEIGHTS 5059
+#define CG_COLOR_SKIPPED     (-1)  /* empty cloud: the reference's response has no entry for it */
+#define CG_COLOR_INDEX_ERROR (-2)  /* a point's image row falls outside the 15 rows: the reference raises IndexError */
+#define CG_COLOR_RANGE_ERROR (-3)  /* an intensity outside [0, 255]: the reference's interp1d raises ValueError */
+int cg_colornet_set(cg_handle* h, const float* weights, uint32_t n_weights);
+/* points: host x, y, z, intensity float32, cone c's points at [offsets[c], offsets[c + 1]).
+ * colors[c]: 1 yellow, 2 blue, 3 orange, 0 unknown (max probability < 0.8), or a negative code
+ * above. probs (n_cones x 3) and images (n_cones x 15 x 12 uint8, to_image's pixels) are
+ * optional (NULL). Synchronous. */
+int cg_classify_colors(cg_handle* h, const float* points, const uint32_t* offsets, uint32_t n_cones,
+                       int32_t* colors, float* probs, uint8_t* images);
+
 /* ---- detector node after the hot path (src/cone_detection.cpp:171-186, 222-339) -------- */
 /* Cone re-crop, ConeDetector::get_reconstructed_cone (src/cone_detection.cpp:222-238): for each
  * cone centre (x, y), every point of the last single-frame call's detector input (the "whole

@@ -1,0 +1,79 @@
+"""Colour classifier service on CPU: the .tflite reading and its pin to
+the reference's SavedModel checkpoint, and the restatement's to_image rules
+(scripts/color_classifier_server.py:131-156). The GPU comparison is tests/test_gpu_colornet.py."""
+import os
+
+import numpy as np
+import pytest
+
+import colornet_ref as R
+from cones_perception_amd import colornet
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIXTURE = os.path.join(HERE, "golden", "dam_net_weights.npy")
+TFLITE = "/root/reference/models/dam_net/dam_net.tflite"
+
+
+def test_fixture_layout():
+    w = np.load(FIXTURE)
+    assert w.dtype == np.float32 and w.shape == (colornet.WEIGHTS,)
+    assert np.all(np.isfinite(w))
+
+
+@pytest.mark.skipif(not os.path.exists(TFLITE), reason="reference model not present (GPU box)")
+def test_tflite_reading_matches_fixture_and_checkpoint():
+    import importlib.util
+    w = colornet.read_tflite(TFLITE)
+    assert np.array_equal(w.view(np.uint32), np.load(FIXTURE).view(np.uint32))
+    spec = importlib.util.spec_from_file_location("make_dam_net", os.path.join(HERE, "golden", "make_dam_net.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    mk.pin(w)
+
+
+def test_tflite_reader_rejects_other_files(tmp_path):
+    p = tmp_path / "x.tflite"
+    p.write_bytes(b"\x00" * 64)
+    with pytest.raises(ValueError):
+        colornet.read_tflite(str(p))
+
+
+def _cone(n, seed, x0=6.0, y0=1.0):
+    g = np.random.default_rng(seed)
+    pts = np.zeros((n, 4), np.float32)
+    pts[:, 0] = x0 + g.uniform(-0.1, 0.1, n)
+    pts[:, 1] = y0 + g.uniform(-0.1, 0.1, n)
+    pts[:, 2] = g.uniform(-0.5, -0.18, n)
+    pts[:, 3] = g.uniform(0, 100, n)
+    return pts
+
+
+def test_to_image_rules():
+    pts = _cone(40, 1)
+    img = R.to_image(pts)
+    assert img.shape == (15, 12) and img.dtype == np.uint8
+    assert img[:, 0].any() and img[:, 11].any()              # the angle range spans all columns
+    # the last point of a pixel wins
+    dup = np.vstack([pts, pts[:1] * [1, 1, 1, 0] + [0, 0, 0, 77.9]]).astype(np.float32)
+    img2 = R.to_image(dup)
+    r, c = np.argwhere(img2 != img)[0] if (img2 != img).any() else (None, None)
+    assert (img2 == 77).any() and r is not None
+    # rows outside [-15, 14] raise, as the reference's indexing does
+    far = pts.copy()
+    far[0, 2] = 50.0
+    with pytest.raises(IndexError):
+        R.to_image(far)
+    hot = pts.copy()
+    hot[3, 3] = 255.5
+    with pytest.raises(ValueError):
+        R.to_image(hot)
+    one = pts[:1]                                            # a single point: slope 11 / 1e-16
+    assert R.to_image(one).sum() == int(pts[0, 3])
+
+
+def test_forward_is_a_distribution():
+    w = np.load(FIXTURE)
+    out = R.classify([_cone(60, s) for s in range(5)] + [np.zeros((0, 4), np.float32)], w)
+    for col, pr, _ in out[:5]:
+        assert 0 <= col <= 3 and abs(pr.sum() - 1) < 1e-12
+    assert out[5][0] == colornet.SKIPPED

@@ -185,8 +185,16 @@ def test_cpp_node_mirror_demo():
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(_abi.LIB_PATH), "nodes_demo")
-    r = subprocess.run([exe, "5"], capture_output=True, text=True, timeout=300)
+    import tempfile
+    import numpy as np
+    wpath = os.path.join(tempfile.mkdtemp(), "dam_net.f32")
+    np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "dam_net_weights.npy")).astype(
+        "<f4").tofile(wpath)
+    r = subprocess.run([exe, "5", wpath], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("node frame")]
     assert len(lines) == 5 and all("fused == two-node" in l for l in lines)
     assert any(" unknown=0" not in l or " yellow=0" not in l for l in lines[1:])   # something published
+    # the GPU colour classifier (ColorClassifier, cg_classify_colors) as the node's service
+    gl = [l for l in r.stdout.splitlines() if l.startswith("gpu colour service frame")]
+    assert len(gl) == 5

@@ -12,6 +12,7 @@ C=$R/cones_perception_amd/csrc
 /opt/rocm/bin/hipcc $F "$@" -c $C/cg_kernels.hip -o $O/cg_kernels.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_large.hip -o $O/cg_large.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_recrop.hip -o $O/cg_recrop.o &
+/opt/rocm/bin/hipcc $F -c $C/cg_colornet.hip -o $O/cg_colornet.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_track.cpp -o $O/cg_track.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_api.cpp -o $O/cg_api.o &
 gcc -O2 -fPIC -ffp-contract=off -std=c11 -Wall -c $C/cg_synth.c -o $O/cg_synth.o
