@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the frame-parallel CPU leg (the box's CPU share is 16)")
     ap.add_argument("--single-frame", action="store_true", help="also time C2 single-frame latency")
+    ap.add_argument("--colornet", action="store_true",
+                    help="also time the colour classifier service (cg_classify_colors) on re-crops of "
+                         "the synthetic frames: one call per frame's cones, and batched calls")
     ap.add_argument("--stamps", action="store_true", help="diagnostic: per-phase in-kernel timing")
     ap.add_argument("--no-c5", action="store_true", help="skip the default C5 single-GPU leg (N=1)")
     ap.add_argument("--c5", action="store_true",
@@ -179,6 +182,9 @@ def main():
     single = None
     if args.single_frame and rank == 0:
         single = single_frame_latency(cp, params, raw, local)
+    colornet = None
+    if args.colornet and rank == 0:
+        colornet = colornet_service(cp, params, raw, local)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -217,6 +223,8 @@ def main():
         }
         if single is not None:
             line["single_frame"] = single
+        if colornet is not None:
+            line["colornet"] = colornet
         if c5 is not None:
             line["c5_single_gpu"] = c5
         if c5t is not None:
@@ -418,6 +426,37 @@ def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):
             and np.array_equal(det.centroids.view(np.uint32), ref.centroids.view(np.uint32)))
         out["C"] = int(det.centroids.shape[0])
     return out
+
+
+def colornet_service(cp, params, raw, device, frames=16, reps=50):
+    """The colour service (cg_classify_colors, host clouds in, colours out) on the re-crops of
+    the first frames' cones: per-frame calls (the node's regime) and one batched call."""
+    import numpy as np
+    from cones_perception_amd import colornet
+    w = np.load(os.path.join(ROOT, "tests", "golden", "dam_net_weights.npy"))
+    pipe = cp.ConePipeline(params, device=device)
+    per_frame = []
+    for f in range(frames):
+        det = pipe.cloud_handler(cp.frame_cloud(raw[f]))
+        per_frame.append(pipe.recrop(det.centroids))
+    clf = colornet.ColorClassifier(w, device=device)
+    for crops in per_frame[:2]:
+        clf.classify(crops)
+    t0 = time.perf_counter()
+    for r in range(reps):
+        clf.classify(per_frame[r % frames])
+    per_call = (time.perf_counter() - t0) / reps
+    batch = [c for crops in per_frame for c in crops] * 16
+    clf.classify(batch)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        clf.classify(batch)
+    bt = (time.perf_counter() - t0) / 10
+    n_cones = sum(len(c) for c in per_frame) / frames
+    return {"cones_per_frame": n_cones, "points_per_cone": float(np.mean([len(c) for c in batch])),
+            "ms_per_frame_call": per_call * 1e3, "batched_cones": len(batch), "batched_ms": bt * 1e3,
+            "batched_cones_per_s": len(batch) / bt,
+            "includes": "host clouds -> H2D, one workgroup per cone (to_image + dam_net), colours D2H"}
 
 
 def single_frame_latency(cp, params, raw, device, reps=200):
