@@ -27,7 +27,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out, rings, cols, over, halo=False):
+def _frame(rings, cols, mutate=None):
+    raw = cp.synth_frames(1, first_frame=4, rings=rings, cols=cols, clutter=40, cones_per_row=10)
+    pts = raw[0].view(np.float32).reshape(-1, 4)
+    if mutate == "passthrough":       # a few points 1 km up: PCL's int32 voxel-count guard trips
+        pts[5::20011, 2] = 1000.0
+    elif mutate == "narrow":          # x squeezed to a few voxel columns: fewer slabs than ranks
+        pts[:, 0] *= np.float32(0.01)
+    elif mutate == "nonfinite":       # NaN / inf survivors are not voxelised
+        pts[7::9973, 0] = np.nan
+        pts[11::7919, 1] = np.inf
+    return raw
+
+
+def _worker(rank, world, port, out, rings, cols, over, halo=False, mutate=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
@@ -35,7 +48,7 @@ def _worker(rank, world, port, out, rings, cols, over, halo=False):
     import cones_perception_amd as cpp
     from cones_perception_amd import dist as cd
     params = cpp.load_params("simulation", over)
-    raw = cpp.synth_frames(1, first_frame=4, rings=rings, cols=cols, clutter=40, cones_per_row=10)
+    raw = _frame(rings, cols, mutate)
     n_total = rings * cols
     lo, hi = cd.tile_range(n_total, rank, world)
     dev = torch.device("cuda", 0)
@@ -53,29 +66,37 @@ def _worker(rank, world, port, out, rings, cols, over, halo=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rings,cols,over,halo", [
-    (2, 128, 2048, {}, False),
-    (3, 96, 2048, {}, False),
-    (2, 64, 2048, {"distance_treshold_min": 0.0}, False),   # zero pads survive: global backend on rank 0
+@pytest.mark.parametrize("world,rings,cols,over,halo,mutate", [
+    (2, 128, 2048, {}, False, None),
+    (3, 96, 2048, {}, False, None),
+    (2, 64, 2048, {"distance_treshold_min": 0.0}, False, None),   # zero pads survive: global backend on rank 0
     # voxel slabs with a halo exchange: clusters cross slab edges, pads on one slab
-    (2, 128, 2048, {}, True),
-    (3, 96, 2048, {}, True),
-    (4, 64, 2048, {"distance_treshold_min": 0.0}, True),
-    (4, 64, 2048, {"distance_treshold_max": 30.0, "max_cluster_size": 100000}, True),   # the wall: long clusters
+    (2, 128, 2048, {}, True, None),
+    (3, 96, 2048, {}, True, None),
+    (4, 64, 2048, {"distance_treshold_min": 0.0}, True, None),
+    (4, 64, 2048, {"distance_treshold_max": 30.0, "max_cluster_size": 100000}, True, None),   # the wall: long clusters
+    (3, 64, 2048, {"distance_treshold_max": 1e5}, True, "passthrough"),   # no lattice: falls back to the gather
+    (3, 64, 2048, {}, True, "narrow"),
+    (2, 64, 2048, {}, True, "nonfinite"),
 ])
-def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over, halo):
+def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over, halo, mutate):
     out = str(tmp_path / "r0.npz")
-    mp.spawn(_worker, args=(world, _free_port(), out, rings, cols, over, halo), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, rings, cols, over, halo, mutate), nprocs=world, join=True)
     z = np.load(out)
     got = Detection(*(z[k].item() if z[k].ndim == 0 else z[k] for k in FIELDS))
     params = cp.load_params("simulation", over)
-    raw = cp.synth_frames(1, first_frame=4, rings=rings, cols=cols, clutter=40, cones_per_row=10)
+    raw = _frame(rings, cols, mutate)
     ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE)
     assert got.n_points == rings * cols
     assert_same_detection(got, ref, f"tiled x{world} halo={halo}")
-    if halo:
+    if mutate == "passthrough":
+        assert got.flags & 1                                    # PCL's guard: voxel cloud = input
+    if halo and mutate != "passthrough":
         # the halo path ran on every slab; the wall case's clusters cross every slab edge
         st = json.loads(str(z["stats"]))
+        if mutate == "narrow":
+            assert all(s["slabs"] < world for s in st) and st[-1]["voxels"] == 0, st
+            return
         assert all(s["slabs"] == world for s in st), st
         assert sum(s["voxels"] for s in st) == got.voxels.shape[0], st
         assert all(s["halo_received"] > 0 for s in st[:-1]), st
