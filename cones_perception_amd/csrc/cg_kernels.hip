@@ -423,17 +423,13 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         // cluster order: PCL sorts the reversed discovery list ascending by size with std::sort
         if (C > CG_SORT_THRESHOLD && C <= 64) {
             // wave 0, records one per lane (cg_sort.h CgWaveRegs64): scalar control flow
-            if (tid < 64) {
+            if (tid < 64) {   // sizes <= V < 65536: (size << 16 | d) records in one VGPR
                 const uint32_t Cu = (uint32_t)__builtin_amdgcn_readfirstlane((int)C);
-                uint32_t lo = 0, hi = 0;
-                if (tid < Cu) { lo = Cu - 1 - tid; hi = DSZ[lo]; }
-                int32_t st[3] = {0, 0, 0};
-                const CgWaveRegs64 f{&lo, &hi, 0};
-                const CgWaveStack sk{st};
-                cg_std_sort(f, (long)Cu, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, sk);
+                uint32_t r = tid < Cu ? (DSZ[Cu - 1 - tid] << 16) | (Cu - 1 - tid) : 0u;
+                cg_std_sort_wave32(r, (int)Cu);
                 if (tid < Cu) {
-                    FIN[Cu - 1 - tid] = lo;
-                    RANK[lo] = Cu - 1 - tid;
+                    FIN[Cu - 1 - tid] = r & 0xffffu;
+                    RANK[r & 0xffffu] = Cu - 1 - tid;
                 }
             }
         } else if (C > CG_SORT_THRESHOLD) {

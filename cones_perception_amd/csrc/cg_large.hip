@@ -916,15 +916,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
         // v_readlane / v_writelane element accesses instead of dependent LDS round trips)
         if (wave_id() == 0) {
             const uint32_t l = lane_id();
-            uint32_t lo = 0, hi = 0;
-            if (l < C) { lo = C - 1 - l; hi = S.dsz[lo]; }
+            const uint32_t big = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_umax(l < C ? S.dsz[C - 1 - l] : 0u));
             int32_t st[3] = {0, 0, 0};
-            const CgWaveRegs64 f{&lo, &hi, 0};
             const CgWaveStack sk{st};
-            cg_std_sort(f, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, sk);
+            uint32_t d = 0;
+            if (big < 65536u) {   // (size << 16 | d) records in one VGPR, ballot-scan introsort
+                uint32_t r = l < C ? (S.dsz[C - 1 - l] << 16) | (C - 1 - l) : 0u;
+                cg_std_sort_wave32(r, (int)C);
+                d = r & 0xffffu;
+            } else {
+                uint32_t lo = 0, hi = 0;
+                if (l < C) { lo = C - 1 - l; hi = S.dsz[lo]; }
+                const CgWaveRegs64 f{&lo, &hi, 0};
+                cg_std_sort(f, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, sk);
+                d = lo;
+            }
             if (l < C) {
-                S.fin[C - 1 - l] = lo;
-                S.rank[lo] = C - 1 - l;
+                S.fin[C - 1 - l] = d;
+                S.rank[d] = C - 1 - l;
             }
         }
     } else if (C > CG_SORT_THRESHOLD) {
@@ -1000,16 +1009,21 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams
     const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const uint32_t s = S.off[k], e = S.off[k + 1];
     float x = 0.0f, y = 0.0f;
-    for (uint32_t g0 = s; g0 < e; g0 += 4 * 64) {   // four chunks of 64 members in flight
-        float px[4], py[4];
+    for (uint32_t g0 = s; g0 < e; g0 += 8 * 64) {   // eight chunks of 64 members in flight
+        float px[8], py[8];
+        uint32_t vi[8];
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
+        for (int c = 0; c < 8; c++) {   // all member indices first, then all voxel loads
             const uint32_t i = g0 + 64 * c + l;
-            px[c] = py[c] = 0.f;
-            if (i < e) { const float4 p = S.vox[idx[i]]; px[c] = p.x; py[c] = p.y; }
+            vi[c] = i < e ? (uint32_t)idx[i] : 0xffffffffu;
         }
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
+        for (int c = 0; c < 8; c++) {
+            px[c] = py[c] = 0.f;
+            if (vi[c] != 0xffffffffu) { const float4 p = S.vox[vi[c]]; px[c] = p.x; py[c] = p.y; }
+        }
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
             const uint32_t i0 = g0 + 64 * c;
             const uint32_t n = i0 < e ? min(64u, e - i0) : 0u;
             for (uint32_t b = 0; b < n; b++) {

@@ -194,6 +194,27 @@ struct CgWaveRegs64 {
     __device__ __forceinline__ Ref operator[](long i) const { return Ref{this, i}; }
     __device__ __forceinline__ CgWaveRegs64 operator+(long d) const { return CgWaveRegs64{lo, hi, base + d}; }
 };
+// 32-bit records of one wave, element i in lane i (one VGPR)
+struct CgWaveRegs32 {
+    using value_type = uint32_t;
+    uint32_t* v;
+    long base;
+    struct Ref {
+        const CgWaveRegs32* a;
+        long i;
+        __device__ __forceinline__ operator uint32_t() const { return a->get(i); }
+        __device__ __forceinline__ Ref& operator=(uint32_t x) { a->set(i, x); return *this; }
+        __device__ __forceinline__ Ref& operator=(const Ref& o) { a->set(i, (uint32_t)o); return *this; }
+    };
+    __device__ __forceinline__ uint32_t get(long i) const {
+        return (uint32_t)__builtin_amdgcn_readlane((int)*v, (int)(base + i));
+    }
+    __device__ __forceinline__ void set(long i, uint32_t x) const {
+        *v = (uint32_t)cg_writelane((int)x, (int)(base + i), (int)*v);
+    }
+    __device__ __forceinline__ Ref operator[](long i) const { return Ref{this, i}; }
+    __device__ __forceinline__ CgWaveRegs32 operator+(long d) const { return CgWaveRegs32{v, base + d}; }
+};
 // cg_std_sort's stack of (first, last, depth) triples, entry s in lane s of three VGPRs
 struct CgWaveStack {
     int32_t* r;   // r[0..2]
@@ -214,4 +235,89 @@ struct CgWaveStack {
     };
     __device__ __forceinline__ Ref operator[](int i) const { return Ref{this, i}; }
 };
+#endif
+
+#ifdef __HIPCC__
+// std::sort of n <= 64 records (size << 16 | payload, ordered by size only) held one per lane
+// of one wave (lane i: element i), with libstdc++'s control flow (the stack of ranges, depth
+// budget, median-of-three, Hoare partition, guarded then unguarded insertion sort, heapsort
+// fallback) but every linear scan replaced by one ballot: a scan that stops at the first (or
+// last) element satisfying a compare is the lowest (or highest) set bit of the compare's
+// ballot over the scanned range, and the final insertion passes are one stable rank sort.
+// Called by every lane of the wave with the same n. Same permutation as cg_std_sort.
+__device__ __forceinline__ uint32_t cg_wave_lane() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ uint32_t cg_wave_get(uint32_t v, int i) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+}
+__device__ __forceinline__ void cg_wave_swap(uint32_t& v, int i, int j) {
+    const uint32_t a = cg_wave_get(v, i), b = cg_wave_get(v, j);
+    const int l = (int)cg_wave_lane();
+    v = l == i ? b : (l == j ? a : v);
+}
+__device__ __forceinline__ uint64_t cg_lanes_below(int k) {   // lanes [0, k)
+    return k >= 64 ? ~0ull : (k <= 0 ? 0ull : (1ull << k) - 1ull);
+}
+// Stable sort of lanes [0, n) by size: each element's rank counts the smaller sizes and the
+// equal sizes before it; one forward permute moves it there. libstdc++'s final pass (a guarded
+// insertion sort of the first 16, then unguarded insertion of the rest into the sorted prefix)
+// is an insertion sort of the whole range, i.e. exactly this stable sort.
+__device__ __forceinline__ void cg_wave_stable_sort(uint32_t& v, int n) {
+    const int l = (int)cg_wave_lane();
+    const uint32_t k = v >> 16;
+    uint32_t rank = 0;
+    for (int j = 0; j < n; j++) {
+        const uint32_t kj = cg_wave_get(v, j) >> 16;
+        rank += (kj < k) || (kj == k && j < l);
+    }
+    if (l >= n) rank = (uint32_t)l;
+    v = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4), (int)v);
+}
+__device__ inline void cg_std_sort_wave32(uint32_t& v, int n) {
+    if (n <= 1) return;
+    const int l = (int)cg_wave_lane();
+    auto less = [](uint32_t a, uint32_t b) { return (a >> 16) < (b >> 16); };
+    int32_t st[3] = {0, 0, 0};
+    const CgWaveStack stk{st};
+    int sp = 0;
+    stk[0] = 0; stk[1] = n; stk[2] = cg_lg(n) * 2; sp = 1;
+    while (sp > 0) {
+        --sp;
+        int first = stk[3 * sp], last = stk[3 * sp + 1];
+        int depth = stk[3 * sp + 2];
+        while (last - first > CG_SORT_THRESHOLD) {
+            if (depth == 0) {
+                const CgWaveRegs32 f{&v, 0};
+                cg_heap_sort_range(f + first, (long)(last - first), less);
+                break;
+            }
+            --depth;
+            const int mid = first + (last - first) / 2;
+            {   // __move_median_to_first(first, first + 1, mid, last - 1)
+                const int a = first + 1, b = mid, c = last - 1;
+                const uint32_t fa = cg_wave_get(v, a), fb = cg_wave_get(v, b), fc = cg_wave_get(v, c);
+                int m;
+                if (less(fa, fb)) m = less(fb, fc) ? b : (less(fa, fc) ? c : a);
+                else m = less(fa, fc) ? a : (less(fb, fc) ? c : b);
+                cg_wave_swap(v, first, m);
+            }
+            // __unguarded_partition(first + 1, last, pivot = first): the pivot stays put
+            const uint32_t p = cg_wave_get(v, first) >> 16;
+            int lo = first + 1, hi = last;
+            while (true) {
+                lo = __builtin_ctzll(__ballot((v >> 16) >= p) & ~cg_lanes_below(lo));   // first f[i] >= p
+                --hi;
+                hi = 63 - __builtin_clzll(__ballot((v >> 16) <= p) & cg_lanes_below(hi + 1));   // last f[j] <= p
+                if (!(lo < hi)) break;
+                cg_wave_swap(v, lo, hi);
+                ++lo;
+            }
+            stk[3 * sp] = lo; stk[3 * sp + 1] = last; stk[3 * sp + 2] = depth; sp++;
+            last = lo;
+        }
+    }
+    (void)l;
+    cg_wave_stable_sort(v, n);   // the final insertion passes
+}
 #endif
