@@ -169,6 +169,8 @@ struct cg_handle {
     hipStream_t last_stream = nullptr;
     // host results
     uint32_t h_hdr[CG_HDR_WORDS] = {};
+    uint32_t* d_pack = nullptr;      // fetch_frame: one frame's results packed (CG_PACK_WORDS)
+    uint32_t* h_pack = nullptr;      // pinned copy of it; the results handed out point into it
     std::vector<float> h_vox, h_cen;
     std::vector<int32_t> h_lab, h_offs, h_idx;
     uint8_t* h_ground = nullptr;  // pinned
@@ -343,9 +345,6 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
 int ensure_large(cg_handle* h, uint32_t n) {
     if (n <= h->large_points && h->d_large) return CG_OK;
     if (h->d_large) (void)hipFree(h->d_large);
-    if (h->d_cn_w) (void)hipFree(h->d_cn_w);
-    if (h->d_cn_pts) (void)hipFree(h->d_cn_pts);
-    if (h->d_cn_offs) (void)hipFree(h->d_cn_offs);
     h->d_large = nullptr;
     h->large_points = 0;
     HIPCHK(hipMalloc(&h->d_large, cg_large_bytes(n)));
@@ -374,6 +373,38 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
 
 int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
     const uint64_t cap = h->cap_points;
+    // one packed copy into pinned memory and one synchronisation when the results fit
+    // CG_PACK_MAX entries per array (every frame of the LDS backend: V <= M <= CG_MMAX)
+    if (!h->d_pack) {
+        HIPCHK(hipMalloc(&h->d_pack, CG_PACK_WORDS * 4));
+        HIPCHK(hipHostMalloc((void**)&h->h_pack, CG_PACK_WORDS * 4, hipHostMallocDefault));
+    }
+    {
+        CgLaunch L{};   // the result arrays only (fill_launch_outputs would reset the stamps)
+        L.cap = h->cap_points;
+        L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
+        L.idx = h->d_idx; L.cen = h->d_cen;
+        HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
+        HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const uint32_t* p = h->h_pack;
+        const uint32_t V = p[CG_HDR_V], C = p[CG_HDR_C];
+        if (V <= CG_PACK_MAX && C <= CG_PACK_MAX && (C == 0 || p[CG_PACK_OFFS + C] <= CG_PACK_MAX)) {
+            std::memcpy(h->h_hdr, p, CG_HDR_WORDS * 4);
+            out->n_points = p[CG_HDR_N];
+            out->n_kept = p[CG_HDR_K];
+            out->n_filtered = p[CG_HDR_M];
+            out->n_voxels = V;
+            out->n_clusters = C;
+            out->flags = p[CG_HDR_FLAGS];
+            out->voxels = (float*)(h->h_pack + CG_PACK_VOX);
+            out->labels = (int32_t*)(h->h_pack + CG_PACK_LAB);
+            out->cluster_offsets = (int32_t*)(h->h_pack + CG_PACK_OFFS);
+            out->cluster_indices = (int32_t*)(h->h_pack + CG_PACK_IDX);
+            out->centroids = (float*)(h->h_pack + CG_PACK_CEN);
+            return CG_OK;
+        }
+    }
     HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, CG_HDR_WORDS * 4,
                           hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -530,6 +561,11 @@ int cg_destroy(cg_handle* h) {
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->h_meta) (void)hipHostFree(h->h_meta);
     if (h->d_large) (void)hipFree(h->d_large);
+    if (h->d_cn_w) (void)hipFree(h->d_cn_w);
+    if (h->d_cn_pts) (void)hipFree(h->d_cn_pts);
+    if (h->d_cn_offs) (void)hipFree(h->d_cn_offs);
+    if (h->d_pack) (void)hipFree(h->d_pack);
+    if (h->h_pack) (void)hipHostFree(h->h_pack);
     if (h->d_boxes) (void)hipFree(h->d_boxes);
     if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);
     if (h->d_rc_out) (void)hipFree(h->d_rc_out);

@@ -181,6 +181,16 @@ int cg_launch_recrop(const CgLaunch& L, const CgDevParams& P, bool pipeline, con
                      const RcBox* d_boxes, uint32_t nb, uint32_t* d_cnt, const uint32_t* d_off, float4* d_out,
                      bool write, hipStream_t s);
 
+// One frame's results packed for one device-to-host copy (word offsets; entries beyond
+// CG_PACK_MAX are fetched separately).
+#define CG_PACK_MAX 1024
+#define CG_PACK_VOX CG_HDR_WORDS
+#define CG_PACK_LAB (CG_PACK_VOX + 4 * CG_PACK_MAX)
+#define CG_PACK_OFFS (CG_PACK_LAB + CG_PACK_MAX)
+#define CG_PACK_IDX (CG_PACK_OFFS + CG_PACK_MAX + 1)
+#define CG_PACK_CEN (CG_PACK_IDX + CG_PACK_MAX)
+#define CG_PACK_WORDS (CG_PACK_CEN + 2 * CG_PACK_MAX)
+int cg_launch_pack(const CgLaunch& L, uint32_t f, uint32_t* out, hipStream_t s);
 // Colour classifier (cg_colornet.hip): one workgroup per cone cloud.
 int cg_launch_colornet(const float4* pts, const uint32_t* offs, uint32_t n_cones, const float* w, int32_t* colors,
                        float* probs, uint8_t* images, hipStream_t s);

@@ -914,6 +914,36 @@ int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 
 // ------------------------------------------------------------------------------------------
 // Self-test kernels: the device restatements, evaluated element-wise for host comparison.
+// Results of one frame packed for a single device-to-host copy (fetch_frame): the header, then
+// up to CG_PACK_MAX entries of each result array at fixed offsets (cg_internal.h CG_PACK_*).
+__global__ __launch_bounds__(256) void cg_pack_results(CgLaunch L, uint32_t f, uint32_t* out) {
+    const uint32_t* hdr = L.hdr + (uint64_t)f * CG_HDR_WORDS;
+    const uint32_t V = min(hdr[CG_HDR_V], (uint32_t)CG_PACK_MAX), C = min(hdr[CG_HDR_C], (uint32_t)CG_PACK_MAX);
+    const int32_t* offs = L.offs + (uint64_t)f * (L.cap + 1);
+    const uint32_t nidx = min(C ? (uint32_t)offs[C] : 0u, (uint32_t)CG_PACK_MAX);
+    const float4* vox = L.vox + (uint64_t)f * L.cap;
+    const int32_t* lab = L.lab + (uint64_t)f * L.cap;
+    const int32_t* idx = L.idx + (uint64_t)f * L.cap;
+    const float2* cen = L.cen + (uint64_t)f * L.cap;
+    for (uint32_t i = threadIdx.x; i < CG_HDR_WORDS; i += 256) out[i] = hdr[i];
+    for (uint32_t i = threadIdx.x; i < V; i += 256) {
+        const float4 p = vox[i];
+        uint32_t* q = out + CG_PACK_VOX + 4 * i;
+        q[0] = __float_as_uint(p.x); q[1] = __float_as_uint(p.y); q[2] = __float_as_uint(p.z); q[3] = __float_as_uint(p.w);
+        out[CG_PACK_LAB + i] = (uint32_t)lab[i];
+    }
+    for (uint32_t i = threadIdx.x; i <= C; i += 256) out[CG_PACK_OFFS + i] = (uint32_t)offs[i];
+    for (uint32_t i = threadIdx.x; i < nidx; i += 256) out[CG_PACK_IDX + i] = (uint32_t)idx[i];
+    for (uint32_t i = threadIdx.x; i < C; i += 256) {
+        out[CG_PACK_CEN + 2 * i] = __float_as_uint(cen[i].x);
+        out[CG_PACK_CEN + 2 * i + 1] = __float_as_uint(cen[i].y);
+    }
+}
+int cg_launch_pack(const CgLaunch& L, uint32_t f, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(cg_pack_results, dim3(1), dim3(256), 0, s, L, f, out);
+    return hipGetLastError();
+}
+
 __global__ void cg_selftest_atan2f_kernel(const float* y, const float* x, float* out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {

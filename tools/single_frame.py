@@ -1,0 +1,31 @@
+"""Diagnostic: C2 single-frame latency of the synchronous drop-in call (ConePipeline.cloud_handler:
+PointCloud2 bytes in host memory -> results on the host), by route (0: frame kernel, 1: the
+large-frame path's multi-workgroup front), with a host memcpy of the frame for scale."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import cones_perception_amd as cp  # noqa: E402
+from cones_perception_amd import _abi  # noqa: E402
+
+params = cp.load_params("simulation")
+raw = cp.synth_frames(8, first_frame=0, rings=64, cols=1024)
+msgs = [cp.frame_cloud(raw[i]) for i in range(8)]
+dst = np.empty_like(raw[0])
+t0 = time.perf_counter()
+for i in range(200):
+    np.copyto(dst, raw[i % 8])
+print(f"host memcpy of one 1 MiB frame: {(time.perf_counter() - t0) / 200 * 1e6:.1f} us")
+for route in (0, 1):
+    pipe = cp.ConePipeline(params, device=0)
+    _abi.check(_abi.lib().cg_debug_route(pipe.handle, route))
+    for i in range(20):
+        pipe.cloud_handler(msgs[i % 8])
+    t0 = time.perf_counter()
+    for i in range(200):
+        pipe.cloud_handler(msgs[i % 8])
+    print(f"route {route}: {(time.perf_counter() - t0) / 200 * 1e6:.1f} us per synchronous frame call")
