@@ -37,7 +37,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the frame-parallel CPU leg (the box's CPU share is 16)")
-    ap.add_argument("--single-frame", action="store_true", help="also time C2 single-frame latency")
+    ap.add_argument("--single-frame", action="store_true",
+                    help="also time C2 single-frame latency at N>1 (always at N=1)")
     ap.add_argument("--colornet", action="store_true",
                     help="also time the colour classifier service (cg_classify_colors) on re-crops of "
                          "the synthetic frames: one call per frame's cones, and batched calls")
@@ -180,8 +181,11 @@ def main():
                "halo": c5_tiled(cp, cd, params, local, rank, world, halo=True)}
 
     single = None
-    if args.single_frame and rank == 0:
-        single = single_frame_latency(cp, params, raw, local)
+    if rank == 0 and (args.single_frame or world == 1):   # C2: the ROS node's synchronous call
+        try:
+            single = single_frame_latency(cp, params, raw, local)
+        except Exception as e:  # noqa: BLE001
+            single = {"error": repr(e)}
     colornet = None
     if args.colornet and rank == 0:
         colornet = colornet_service(cp, params, raw, local)
@@ -469,7 +473,10 @@ def single_frame_latency(cp, params, raw, device, reps=200):
     for _ in range(reps):
         pipe.cloud_handler(msg)
     dt = (time.perf_counter() - t0) / reps
-    return {"latency_ms": dt * 1e3, "frames_per_s": 1.0 / dt, "includes": "PCIe H2D of 1 MiB + D2H of results"}
+    return {"latency_ms": dt * 1e3, "frames_per_s": 1.0 / dt,
+            "includes": "C2: one 64k-point PointCloud2 in pageable host memory through the synchronous "
+                        "ConePipeline.cloud_handler (staging + PCIe H2D of 1 MiB, frame kernel, packed D2H "
+                        "of the results, Python result objects)"}
 
 
 def cpu_baseline(cp, params, raw, budget_s, eng, threads):
