@@ -169,6 +169,7 @@ struct cg_handle {
     hipStream_t last_stream = nullptr;
     // host results
     uint32_t h_hdr[CG_HDR_WORDS] = {};
+    uint32_t* d_split = nullptr;     // split single-frame launch state (CG_SPLIT_WORDS)
     uint32_t* d_pack = nullptr;      // fetch_frame: one frame's results packed (CG_PACK_WORDS)
     uint32_t* h_pack = nullptr;      // pinned copy of it; the results handed out point into it
     std::vector<float> h_vox, h_cen;
@@ -358,7 +359,11 @@ int ensure_large(cg_handle* h, uint32_t n) {
 // Frames of <= CG_MAX_POINTS points run as one batch launch of the frame kernel; larger
 // frames (or every frame, under cg_debug_route) go through the multi-workgroup large path.
 int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
-    const bool large = L.n_points > CG_MAX_POINTS || (h->route != 0 && L.n_points > 0);
+    const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2) && L.n_points > 0);
+    if (!large && L.split) {
+        HIPCHK((hipError_t)cg_launch_split(L, h->dp, kmode, s));
+        return CG_OK;
+    }
     if (!large) {
         HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s));
         return CG_OK;
@@ -461,6 +466,16 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     h->last_single = false;
     if (kmode == CG_KMODE_PIPELINE) {
         L.seckeys = h->d_seckeys;
+    }
+    // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
+    // the one-workgroup frame kernel, for comparisons)
+    if (kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && h->route == 0) {
+        if (!h->d_split) {
+            HIPCHK(hipMalloc(&h->d_split, CG_SPLIT_WORDS * 4));
+            HIPCHK(hipMemsetAsync(h->d_split, 0, 8, h->stream));
+            HIPCHK(hipMemsetAsync(h->d_split + 2, 0xff, (CG_NUM_BINS + 1) * 4, h->stream));
+        }
+        L.split = h->d_split;
     }
     rc = launch_frames(h, L, kmode, h->stream);
     if (rc) return rc;
@@ -566,6 +581,7 @@ int cg_destroy(cg_handle* h) {
     if (h->d_cn_offs) (void)hipFree(h->d_cn_offs);
     if (h->d_pack) (void)hipFree(h->d_pack);
     if (h->h_pack) (void)hipHostFree(h->h_pack);
+    if (h->d_split) (void)hipFree(h->d_split);
     if (h->d_boxes) (void)hipFree(h->d_boxes);
     if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);
     if (h->d_rc_out) (void)hipFree(h->d_rc_out);
@@ -1035,7 +1051,7 @@ int cg_debug_launch_span(cg_handle* h, void* d_span) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 2) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 3) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

@@ -79,7 +79,19 @@ struct CgLaunch {
     // timing: [first workgroup start, last workgroup end] of the launch (s_memrealtime,
     // 100 MHz), or null (cg_debug_launch_span)
     unsigned long long* span;
+    // split single-frame launch (cg_launch_split): CG_SPLIT_WORDS of state, or null
+    uint32_t* split;
 };
+// A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
+// for pass 1; the last chunk to finish runs the rest of the frame kernel. State words: [0]
+// finished chunks, [1] used sector bins, [2, 20) sector-minimum keys (all reset by the last
+// workgroup), then the z codes (one uint2 per chunk and lane) and filter bits (one byte per
+// chunk and lane).
+#define CG_SPLIT_CHUNK 4096
+#define CG_SPLIT_CODES 64
+#define CG_SPLIT_POSM (CG_SPLIT_CODES + 2 * (CG_MAX_POINTS / 8))
+#define CG_SPLIT_WORDS (CG_SPLIT_POSM + CG_MAX_POINTS / 8 / 4)
+int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
 
 #ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU

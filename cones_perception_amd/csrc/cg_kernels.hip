@@ -72,7 +72,7 @@ enum {
     S_K = 0, S_MS, S_M, S_MF, S_V, S_C, S_U, S_FLAGS, S_PASS,
     S_MINB0, S_MINB1, S_MINB2, S_MUL1, S_MUL2,
     S_ORGX, S_ORGY, S_ORGZ, S_TKMIN, S_TKMAX, S_TOUCHED,
-    S_BMIN0, S_BMIN1, S_BMIN2, S_BMAX0, S_BMAX1, S_BMAX2, S_TMP
+    S_BMIN0, S_BMIN1, S_BMIN2, S_BMAX0, S_BMAX1, S_BMAX2, S_TMP, S_LAST
 };
 
 
@@ -581,7 +581,13 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
 // a code below q(min T) is ground in every sector, one above q(max T) is kept in every sector.
 // Only points whose code equals a band code re-read x, y, z from HBM and recompute their
 // sector (tens of points per frame on flat ground: the code step is 1/64 m).
-template <int PPT, int LAYOUT, int KMODE>
+//
+// SPLIT (single frames, cg_launch_split): pass 1 runs in one workgroup per 4,096-point chunk
+// (a frame alone on the GPU is VALU-bound on one CU), each writing its z codes and filter
+// bits to HBM and merging its sector minima into the frame's keys with atomics; the last
+// workgroup to finish (release/acquire on a counter) continues with the frame's thresholds,
+// pass 2 and backend below, codes and bits read back from L2.
+template <int PPT, int LAYOUT, int KMODE, bool SPLIT = false>
 __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
     constexpr int G = 8;                          // points per load group (double-buffered)
     constexpr int NW = (PPT + 63) / 64;
@@ -593,7 +599,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
     uint8_t* zq = (uint8_t*)bl;                   // z codes, [k/8][lane][k%8]
 
-    const uint32_t f = blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint32_t f = SPLIT ? 0u : blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
     const uint32_t N = L.n_points;
     STAMP(0);
@@ -607,10 +613,52 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     // ---- pass 1: stream the frame ----
     LaneBits<NW> posm;
     uint32_t touched = 0;
-    stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, fs->rays, posm, touched,
-                                             [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; });
+    uint2* const sp_codes = SPLIT ? (uint2*)(L.split + CG_SPLIT_CODES) : nullptr;
+    if constexpr (SPLIT) {
+        static_assert(PPT * CG_BLOCK == CG_MAX_POINTS, "split frames use the 64k tail");
+        const uint32_t c = blockIdx.x, c0 = c * CG_SPLIT_CHUNK;
+        const uint32_t Nc = N > c0 ? min((uint32_t)CG_SPLIT_CHUNK, N - c0) : 0u;
+        LaneBits<1> pm;
+        uint2 code = make_uint2(0u, 0u);
+        stream_pass1<CG_SPLIT_CHUNK / CG_BLOCK, LAYOUT, GROUND, FILTER>(
+            fb + (uint64_t)c0 * L.point_step, Nc, L, P, fs->sec_key, fs->rays, pm, touched,
+            [&](int, uint2 cw) { code = cw; });
+        sp_codes[c * CG_BLOCK + tid] = code;
+        ((uint8_t*)(L.split + CG_SPLIT_POSM))[c * CG_BLOCK + tid] = (uint8_t)pm.w[0];
+        if (GROUND) {
+            touched = wave_or(touched);
+            if (l == 0 && touched) atomicOr(L.split + 1, touched);
+        }
+        __syncthreads();   // the chunk's sector minima are final in LDS
+        if (GROUND && tid <= CG_NUM_BINS) atomicMin(L.split + 2 + tid, fs->sec_key[tid]);
+        __threadfence();
+        __syncthreads();
+        if (tid == 0)
+            fs->scal[S_LAST] = __hip_atomic_fetch_add(L.split, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                               gridDim.x - 1;
+        __syncthreads();
+        if (!fs->scal[S_LAST]) return;
+        __threadfence();
+        // the last workgroup: the frame's sector keys and used bins (state reset for the next
+        // frame), every lane's filter bits over the chunks
+        if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = atomicExch(L.split + 2 + tid, 0xffffffffu);
+        if (tid == 0) {
+            fs->scal[S_TOUCHED] = GROUND ? atomicExch(L.split + 1, 0u) : 0u;
+            atomicExch(L.split, 0u);
+        }
+        posm.clear();
+        const uint8_t* pb = (const uint8_t*)(L.split + CG_SPLIT_POSM);
+        const uint32_t nch = (N + CG_SPLIT_CHUNK - 1) / CG_SPLIT_CHUNK;
+#pragma unroll
+        for (int cc = 0; cc < PPT / 8; cc++)
+            if ((uint32_t)cc < nch) posm.set_byte(cc, pb[cc * CG_BLOCK + tid]);
+        __syncthreads();
+    } else {
+        stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, fs->rays, posm, touched,
+                                                 [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; });
+    }
     const uint32_t nlast = N ? N - 1 : 0u;
-    if (GROUND) {
+    if (GROUND && !SPLIT) {
         touched = wave_or(touched);
         if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
     }
@@ -650,7 +698,9 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     keepgm.clear();
     if (GROUND) {
         pass2_keep<PPT, LAYOUT>(fb, N, L, P, fs->scal[S_TKMIN], fs->scal[S_TKMAX], fs->tkey,
-                                [&](int g) { return ((const uint2*)zq)[g * CG_BLOCK + tid]; }, keepgm);
+                                [&](int g) {
+                                    return SPLIT ? sp_codes[g * CG_BLOCK + tid] : ((const uint2*)zq)[g * CG_BLOCK + tid];
+                                }, keepgm);
         const uint32_t kc = wave_sum(keepgm.count());
         if (l == 0) atomicAdd(&fs->scal[S_K], kc);
     } else {
@@ -896,6 +946,21 @@ static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hi
         default:
             hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_GROUND>), grid, block, 0, s, L, P);
             break;
+    }
+    return hipGetLastError();
+}
+
+int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
+    constexpr int PPT = CG_MAX_POINTS / CG_BLOCK;
+    const uint32_t nch = (L.n_points + CG_SPLIT_CHUNK - 1) / CG_SPLIT_CHUNK;
+    const dim3 grid(nch ? nch : 1u), block(CG_BLOCK);
+    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
+    if (kmode == CG_KMODE_PIPELINE) {
+        if (xyzi16) hipLaunchKernelGGL((cg_frame_kernel<PPT, CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE, true>), grid, block, 0, s, L, P);
+        else hipLaunchKernelGGL((cg_frame_kernel<PPT, CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE, true>), grid, block, 0, s, L, P);
+    } else {
+        if (xyzi16) hipLaunchKernelGGL((cg_frame_kernel<PPT, CG_LAYOUT_XYZI16, CG_KMODE_DETECT, true>), grid, block, 0, s, L, P);
+        else hipLaunchKernelGGL((cg_frame_kernel<PPT, CG_LAYOUT_GENERIC, CG_KMODE_DETECT, true>), grid, block, 0, s, L, P);
     }
     return hipGetLastError();
 }
