@@ -170,6 +170,7 @@ struct cg_handle {
     // host results
     uint32_t h_hdr[CG_HDR_WORDS] = {};
     uint32_t* d_split = nullptr;     // split single-frame launch state (CG_SPLIT_WORDS)
+    bool packed = false;             // the last single-frame launch left its results in d_pack
     uint32_t* d_pack = nullptr;      // fetch_frame: one frame's results packed (CG_PACK_WORDS)
     uint32_t* h_pack = nullptr;      // pinned copy of it; the results handed out point into it
     std::vector<float> h_vox, h_cen;
@@ -389,7 +390,9 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
         L.cap = h->cap_points;
         L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
         L.idx = h->d_idx; L.cen = h->d_cen;
-        HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
+        const bool prepacked = h->packed && frame == 0;   // by the single-frame launch just run
+        h->packed = false;
+        if (!prepacked) HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
         HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         const uint32_t* p = h->h_pack;
@@ -476,7 +479,13 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
             HIPCHK(hipMemsetAsync(h->d_split + 2, 0xff, (CG_NUM_BINS + 1) * 4, h->stream));
         }
         L.split = h->d_split;
+        if (!h->d_pack) {
+            HIPCHK(hipMalloc(&h->d_pack, CG_PACK_WORDS * 4));
+            HIPCHK(hipHostMalloc((void**)&h->h_pack, CG_PACK_WORDS * 4, hipHostMallocDefault));
+        }
+        L.pack = h->d_pack;   // the kernel packs the results itself
     }
+    h->packed = L.pack != nullptr;
     rc = launch_frames(h, L, kmode, h->stream);
     if (rc) return rc;
     h->last_frames = 1; h->last_points = n; h->last_mode = kmode; h->last_stream = h->stream;

@@ -81,6 +81,8 @@ struct CgLaunch {
     unsigned long long* span;
     // split single-frame launch (cg_launch_split): CG_SPLIT_WORDS of state, or null
     uint32_t* split;
+    // split launch: the frame's results also packed here (CG_PACK_WORDS) at the end, or null
+    uint32_t* pack;
 };
 // A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
 // for pass 1; the last chunk to finish runs the rest of the frame kernel. State words: [0]

@@ -581,6 +581,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
 // a code below q(min T) is ground in every sector, one above q(max T) is kept in every sector.
 // Only points whose code equals a band code re-read x, y, z from HBM and recompute their
 // sector (tens of points per frame on flat ground: the code step is 1/64 m).
+__device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32_t* out);
 //
 // SPLIT (single frames, cg_launch_split): pass 1 runs in one workgroup per 4,096-point chunk
 // (a frame alone on the GPU is VALU-bound on one CU), each writing its z codes and filter
@@ -870,6 +871,13 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     } else {
         backend(W, M, fs, L, P, f, flags);
     }
+    if constexpr (SPLIT) {   // the results packed for the host's one copy (fetch_frame)
+        if (L.pack) {
+            __threadfence();
+            __syncthreads();
+            pack_frame(L, f, L.pack);
+        }
+    }
     if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
@@ -981,7 +989,8 @@ int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 // Self-test kernels: the device restatements, evaluated element-wise for host comparison.
 // Results of one frame packed for a single device-to-host copy (fetch_frame): the header, then
 // up to CG_PACK_MAX entries of each result array at fixed offsets (cg_internal.h CG_PACK_*).
-__global__ __launch_bounds__(256) void cg_pack_results(CgLaunch L, uint32_t f, uint32_t* out) {
+__device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32_t* out) {
+    const uint32_t nt = blockDim.x;
     const uint32_t* hdr = L.hdr + (uint64_t)f * CG_HDR_WORDS;
     const uint32_t V = min(hdr[CG_HDR_V], (uint32_t)CG_PACK_MAX), C = min(hdr[CG_HDR_C], (uint32_t)CG_PACK_MAX);
     const int32_t* offs = L.offs + (uint64_t)f * (L.cap + 1);
@@ -990,19 +999,22 @@ __global__ __launch_bounds__(256) void cg_pack_results(CgLaunch L, uint32_t f, u
     const int32_t* lab = L.lab + (uint64_t)f * L.cap;
     const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const float2* cen = L.cen + (uint64_t)f * L.cap;
-    for (uint32_t i = threadIdx.x; i < CG_HDR_WORDS; i += 256) out[i] = hdr[i];
-    for (uint32_t i = threadIdx.x; i < V; i += 256) {
+    for (uint32_t i = threadIdx.x; i < CG_HDR_WORDS; i += nt) out[i] = hdr[i];
+    for (uint32_t i = threadIdx.x; i < V; i += nt) {
         const float4 p = vox[i];
         uint32_t* q = out + CG_PACK_VOX + 4 * i;
         q[0] = __float_as_uint(p.x); q[1] = __float_as_uint(p.y); q[2] = __float_as_uint(p.z); q[3] = __float_as_uint(p.w);
         out[CG_PACK_LAB + i] = (uint32_t)lab[i];
     }
-    for (uint32_t i = threadIdx.x; i <= C; i += 256) out[CG_PACK_OFFS + i] = (uint32_t)offs[i];
-    for (uint32_t i = threadIdx.x; i < nidx; i += 256) out[CG_PACK_IDX + i] = (uint32_t)idx[i];
-    for (uint32_t i = threadIdx.x; i < C; i += 256) {
+    for (uint32_t i = threadIdx.x; i <= C; i += nt) out[CG_PACK_OFFS + i] = (uint32_t)offs[i];
+    for (uint32_t i = threadIdx.x; i < nidx; i += nt) out[CG_PACK_IDX + i] = (uint32_t)idx[i];
+    for (uint32_t i = threadIdx.x; i < C; i += nt) {
         out[CG_PACK_CEN + 2 * i] = __float_as_uint(cen[i].x);
         out[CG_PACK_CEN + 2 * i + 1] = __float_as_uint(cen[i].y);
     }
+}
+__global__ __launch_bounds__(256) void cg_pack_results(CgLaunch L, uint32_t f, uint32_t* out) {
+    pack_frame(L, f, out);
 }
 int cg_launch_pack(const CgLaunch& L, uint32_t f, uint32_t* out, hipStream_t s) {
     hipLaunchKernelGGL(cg_pack_results, dim3(1), dim3(256), 0, s, L, f, out);

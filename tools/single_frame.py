@@ -30,3 +30,16 @@ for route in (0, 3, 1):
     for i in range(200):
         pipe.cloud_handler(msgs[i % 8])
     print(f"route {route}: {(time.perf_counter() - t0) / 200 * 1e6:.1f} us per synchronous frame call")
+
+# the bare C-ABI call (no Python result objects): what a C++ node pays
+import ctypes as C  # noqa: E402
+pipe = cp.ConePipeline(params, device=0)
+views = [m.view() for m in msgs]
+r = _abi.cg_detect_result()
+lib = _abi.lib()
+for i in range(20):
+    _abi.check(lib.cg_pipeline(pipe.handle, C.byref(views[i % 8]), C.byref(r)))
+t0 = time.perf_counter()
+for i in range(200):
+    lib.cg_pipeline(pipe.handle, C.byref(views[i % 8]), C.byref(r))
+print(f"bare cg_pipeline call: {(time.perf_counter() - t0) / 200 * 1e6:.1f} us")
