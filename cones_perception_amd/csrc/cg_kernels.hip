@@ -67,6 +67,10 @@ struct BackLds {
 static_assert(SMEM_BYTES <= 163840, "LDS budget");
 static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overlay must fit");
 
+#ifndef CG_PREFETCH
+#define CG_PREFETCH 2   // filter survivors per lane loaded right after pass 1
+#endif
+
 // Scalar slots in FrontShared::scal
 enum {
     S_K = 0, S_MS, S_M, S_MF, S_V, S_C, S_U, S_FLAGS, S_PASS,
@@ -663,20 +667,23 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
         touched = wave_or(touched);
         if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
     }
-    // the lane's first two filter survivors are the likely first gather loads: issue them now,
+    // the lane's first CG_PREFETCH filter survivors are the likely first gather loads: issue them now,
     // they land while the thresholds and pass 2 run (a survivor that turns out to be ground
     // costs one wasted load)
-    int pk[2] = {-1, -1};
-    float4 pv[2];
+    int pk[CG_PREFETCH];
+    float4 pv[CG_PREFETCH];
+#pragma unroll
+    for (int q = 0; q < CG_PREFETCH; q++) pk[q] = -1;
     if (FILTER) {
 #pragma unroll
         for (int wi = 0; wi < NW; wi++) {
             uint64_t m = posm.w[wi];
-            if (pk[0] < 0 && m) { pk[0] = 64 * wi + __builtin_ctzll(m); m &= m - 1; }
-            if (pk[1] < 0 && m) pk[1] = 64 * wi + __builtin_ctzll(m);
+#pragma unroll
+            for (int q = 0; q < CG_PREFETCH; q++)
+                if (pk[q] < 0 && m) { pk[q] = 64 * wi + __builtin_ctzll(m); m &= m - 1; }
         }
 #pragma unroll
-        for (int q = 0; q < 2; q++)
+        for (int q = 0; q < CG_PREFETCH; q++)
             pv[q] = load_xyzi<LAYOUT>(fb, min((uint32_t)(pk[q] < 0 ? 0 : pk[q]) * CG_BLOCK + tid, nlast), L);
     }
     __syncthreads();
@@ -800,7 +807,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
         }
     };
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < CG_PREFETCH; q++) {
         if (pk[q] >= 0 && keepm.get(pk[q])) {
             keepm.clear_bit(pk[q]);
             W.P[pos] = pv[q];
