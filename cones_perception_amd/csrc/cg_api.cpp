@@ -275,7 +275,7 @@ int check_view(const cg_cloud_view* v) {
 // Stage a PointCloud2 data block as one contiguous device frame. Aligned, unpadded rows are
 // uploaded verbatim; padded rows or unaligned fields are re-packed (pure byte moves, the
 // memcpy half of pcl::fromROSMsg) to x,y,z,intensity at 0,4,8,12.
-int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L) {
+int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L, bool zero_copy = false) {
     const uint32_t n = v->width * v->height;
     const bool aligned = v->point_step % 4 == 0 && (v->off_x < 0 || v->off_x % 4 == 0) &&
                          (v->off_y < 0 || v->off_y % 4 == 0) && (v->off_z < 0 || v->off_z % 4 == 0) &&
@@ -315,7 +315,10 @@ int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L) {
         L.point_step = 16;
         L.off_x = 0; L.off_y = 4; L.off_z = 8; L.off_i = 12;
     }
-    if (n) HIPCHK(hipMemcpyAsync(h->d_in, h->h_stage, (size_t)n * step, hipMemcpyHostToDevice, h->stream));
+    // zero_copy (split single frames): the kernel's chunk workgroups read the pinned staging
+    // buffer over PCIe and write the device copy themselves; no DMA, no DMA-to-kernel gap
+    if (zero_copy) L.in_host = h->h_stage;
+    else if (n) HIPCHK(hipMemcpyAsync(h->d_in, h->h_stage, (size_t)n * step, hipMemcpyHostToDevice, h->stream));
     L.in = h->d_in;
     L.frame_stride = (uint64_t)n * step;
     L.n_frames = 1;
@@ -463,16 +466,17 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     rc = ensure_batch(h, 1, n, kmode == CG_KMODE_GROUND);
     if (rc) return rc;
     CgLaunch L{};
-    rc = stage_frame(h, in, L);
+    // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
+    // the one-workgroup frame kernel, for comparisons)
+    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4);
+    rc = stage_frame(h, in, L, split && h->route == 0);   // route 4: split, input by DMA
     if (rc) return rc;
     fill_launch_outputs(h, L);
     h->last_single = false;
     if (kmode == CG_KMODE_PIPELINE) {
         L.seckeys = h->d_seckeys;
     }
-    // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
-    // the one-workgroup frame kernel, for comparisons)
-    if (kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && h->route == 0) {
+    if (split) {
         if (!h->d_split) {
             HIPCHK(hipMalloc(&h->d_split, CG_SPLIT_WORDS * 4));
             HIPCHK(hipMemsetAsync(h->d_split, 0, 8, h->stream));
@@ -1060,7 +1064,7 @@ int cg_debug_launch_span(cg_handle* h, void* d_span) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 3) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 4) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

@@ -83,6 +83,9 @@ struct CgLaunch {
     uint32_t* split;
     // split launch: the frame's results also packed here (CG_PACK_WORDS) at the end, or null
     uint32_t* pack;
+    // split launch: the frame in pinned host memory; each chunk workgroup copies its chunk to
+    // `in` (the device copy) before pass 1, or null (`in` already holds the frame)
+    const uint8_t* in_host;
 };
 // A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
 // for pass 1; the last chunk to finish runs the rest of the frame kernel. State words: [0]

@@ -623,6 +623,25 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
         static_assert(PPT * CG_BLOCK == CG_MAX_POINTS, "split frames use the 64k tail");
         const uint32_t c = blockIdx.x, c0 = c * CG_SPLIT_CHUNK;
         const uint32_t Nc = N > c0 ? min((uint32_t)CG_SPLIT_CHUNK, N - c0) : 0u;
+        if (L.in_host) {   // the chunk over PCIe from pinned host memory into the device copy
+            const uint64_t b0 = (uint64_t)c0 * L.point_step, nb = (uint64_t)Nc * L.point_step;
+            uint8_t* dst = (uint8_t*)L.in + b0;
+            const uint8_t* src = L.in_host + b0;
+            const uint64_t n16 = nb / 16;
+            for (uint64_t i = tid; i < n16; i += CG_BLOCK * 4) {
+                uint4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (i + (uint64_t)u * CG_BLOCK < n16) v[u] = ((const uint4*)src)[i + (uint64_t)u * CG_BLOCK];
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (i + (uint64_t)u * CG_BLOCK < n16) ((uint4*)dst)[i + (uint64_t)u * CG_BLOCK] = v[u];
+            }
+            for (uint64_t i = n16 * 16 + 4 * (uint64_t)tid; i < nb; i += 4 * CG_BLOCK)
+                *(uint32_t*)(dst + i) = *(const uint32_t*)(src + i);
+            __threadfence();
+            __syncthreads();
+        }
         LaneBits<1> pm;
         uint2 code = make_uint2(0u, 0u);
         stream_pass1<CG_SPLIT_CHUNK / CG_BLOCK, LAYOUT, GROUND, FILTER>(

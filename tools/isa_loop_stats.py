@@ -11,7 +11,7 @@ ROOT = __file__.rsplit("/tools/", 1)[0]
 
 def main(argv):
     defs = [a for a in argv if a.startswith("-D")]
-    kern = "_Z15cg_frame_kernelILi128ELi1ELi0EEv8CgLaunch11CgDevParams"
+    kern = "_Z15cg_frame_kernelILi128ELi1ELi0ELb0EEv8CgLaunch11CgDevParams"
     src = f"{ROOT}/cones_perception_amd/csrc/cg_kernels.hip"
     ppl = 16
     for i, a in enumerate(argv):

@@ -1,7 +1,8 @@
 """Diagnostic: C2 single-frame latency of the synchronous drop-in call (ConePipeline.cloud_handler:
 PointCloud2 bytes in host memory -> results on the host), by route (0: frame kernel, 1: the
-large-frame path's multi-workgroup front, 3: the frame kernel in one workgroup; 0 runs its
-pass 1 in one workgroup per 4,096-point chunk), with a host memcpy of the frame for scale."""
+large-frame path's multi-workgroup front, 3: the frame kernel in one workgroup, 4: pass 1 in one
+workgroup per 4,096-point chunk with the input copied by DMA; 0: the same with the chunks
+read by the kernel from pinned memory), with a host memcpy of the frame for scale."""
 import os
 import sys
 import time
@@ -21,7 +22,7 @@ t0 = time.perf_counter()
 for i in range(200):
     np.copyto(dst, raw[i % 8])
 print(f"host memcpy of one 1 MiB frame: {(time.perf_counter() - t0) / 200 * 1e6:.1f} us")
-for route in (0, 3, 1):
+for route in (0, 4, 3, 1):
     pipe = cp.ConePipeline(params, device=0)
     _abi.check(_abi.lib().cg_debug_route(pipe.handle, route))
     for i in range(20):
