@@ -116,6 +116,51 @@ __device__ __forceinline__ void lg_store_survivor_bits(LgScratch& S, uint32_t c,
     }
 }
 
+// One workgroup folds the per-chunk statistics into the meta words: the sector keys (MIN) and
+// used bins (OR) after the front; K, survivor count, finite count (SUM) and the VoxelGrid
+// bounds (MIN / MAX keys) after the decisions. what: bit 0 keys, bit 1 K, bit 2 survivors.
+__device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32_t what) {
+    __shared__ uint32_t part[16][LG_CS_WORDS];
+    const uint32_t tid = threadIdx.x, w = tid & 31, q = tid >> 5;   // word, one of 16 chunk strides
+    const bool mn = (w <= CG_NUM_BINS) || (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3);
+    const bool mx = w >= LG_CS_BMAX && w < LG_CS_BMAX + 3;
+    const bool orw = w == LG_CS_TOUCHED;
+    uint32_t acc = mn ? 0xffffffffu : 0u;
+    auto fold = [&](uint32_t a, uint32_t v) { return mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v; };
+    uint32_t c = q;
+    for (; c + 48 < nch; c += 64) {   // four independent loads per trip
+        const uint32_t v0 = S.cstat[(uint64_t)c * LG_CS_WORDS + w], v1 = S.cstat[(uint64_t)(c + 16) * LG_CS_WORDS + w],
+                       v2 = S.cstat[(uint64_t)(c + 32) * LG_CS_WORDS + w], v3 = S.cstat[(uint64_t)(c + 48) * LG_CS_WORDS + w];
+        acc = fold(fold(acc, v0), fold(v1, fold(v2, v3)));
+    }
+    for (; c < nch; c += 16) acc = fold(acc, S.cstat[(uint64_t)c * LG_CS_WORDS + w]);
+    part[q][w] = acc;
+    __syncthreads();
+    if (tid >= LG_CS_WORDS) return;
+    uint32_t a = part[0][w];
+    for (int k = 1; k < 16; k++) {
+        const uint32_t v = part[k][w];
+        a = mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v;
+    }
+    uint32_t* m = S.meta;
+    if ((what & 1u) && w <= CG_NUM_BINS) m[LG_SECKEY + w] = a;
+    if ((what & 1u) && w == LG_CS_TOUCHED) m[LG_TOUCHED] = a;
+    if ((what & 2u) && w == LG_CS_K) m[LG_K] = a;
+    if (what & 4u) {
+        if (w == LG_CS_MS) m[LG_MS] = a;
+        if (w == LG_CS_NFIN) m[LG_NFIN] = a;
+        if (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3) m[LG_BMIN + (w - LG_CS_BMIN)] = a;
+        if (w >= LG_CS_BMAX && w < LG_CS_BMAX + 3) m[LG_BMAX + (w - LG_CS_BMAX)] = a;
+    }
+}
+
+__global__ __launch_bounds__(CG_BLOCK) void lg_reduce_chunks(LgScratch S, uint32_t nch, uint32_t what) {
+    lg_fold_chunks(S, nch, what);
+}
+// (Folding in the last workgroup of the chunk launch instead, behind a release/acquire counter,
+// measured 7 -> 53 us per launch on a 256-chunk frame: every workgroup's agent-scope release
+// writes back its XCD's L2.)
+
 // ------------------------------------------------------------------------------------------
 // Front: pass 1 per chunk.
 template <int LAYOUT, int KMODE>
@@ -151,10 +196,11 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
         for (int w = 0; w < WAVES; w++) t |= tw[w];
         cs[LG_CS_TOUCHED] = t;
     }
-    if (!FILTER) return;
-    if (GROUND) {   // pipeline: the filter bits wait for the ground decision (lg_decide)
+    if (GROUND) {
+        if (FILTER) {   // pipeline: the filter bits wait for the ground decision (lg_decide)
 #pragma unroll
-        for (int wi = 0; wi < NW; wi++) S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi] = posm.w[wi];
+            for (int wi = 0; wi < NW; wi++) S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi] = posm.w[wi];
+        }
         return;
     }
     // detector: the filter survivors themselves
@@ -261,44 +307,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
     }
     __shared__ uint32_t part[7 * WAVES];
     bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, part);
-}
-
-// One workgroup folds the per-chunk statistics into the meta words: the sector keys (MIN) and
-// used bins (OR) after the front; K, survivor count, finite count (SUM) and the VoxelGrid
-// bounds (MIN / MAX keys) after the decisions. what: bit 0 keys, bit 1 K, bit 2 survivors.
-__global__ __launch_bounds__(CG_BLOCK) void lg_reduce_chunks(LgScratch S, uint32_t nch, uint32_t what) {
-    __shared__ uint32_t part[16][LG_CS_WORDS];
-    const uint32_t tid = threadIdx.x, w = tid & 31, q = tid >> 5;   // word, one of 16 chunk strides
-    const bool mn = (w <= CG_NUM_BINS) || (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3);
-    const bool mx = w >= LG_CS_BMAX && w < LG_CS_BMAX + 3;
-    const bool orw = w == LG_CS_TOUCHED;
-    uint32_t acc = mn ? 0xffffffffu : 0u;
-    auto fold = [&](uint32_t a, uint32_t v) { return mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v; };
-    uint32_t c = q;
-    for (; c + 48 < nch; c += 64) {   // four independent loads per trip
-        const uint32_t v0 = S.cstat[(uint64_t)c * LG_CS_WORDS + w], v1 = S.cstat[(uint64_t)(c + 16) * LG_CS_WORDS + w],
-                       v2 = S.cstat[(uint64_t)(c + 32) * LG_CS_WORDS + w], v3 = S.cstat[(uint64_t)(c + 48) * LG_CS_WORDS + w];
-        acc = fold(fold(acc, v0), fold(v1, fold(v2, v3)));
-    }
-    for (; c < nch; c += 16) acc = fold(acc, S.cstat[(uint64_t)c * LG_CS_WORDS + w]);
-    part[q][w] = acc;
-    __syncthreads();
-    if (tid >= LG_CS_WORDS) return;
-    uint32_t a = part[0][w];
-    for (int k = 1; k < 16; k++) {
-        const uint32_t v = part[k][w];
-        a = mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v;
-    }
-    uint32_t* m = S.meta;
-    if ((what & 1u) && w <= CG_NUM_BINS) m[LG_SECKEY + w] = a;
-    if ((what & 1u) && w == LG_CS_TOUCHED) m[LG_TOUCHED] = a;
-    if ((what & 2u) && w == LG_CS_K) m[LG_K] = a;
-    if (what & 4u) {
-        if (w == LG_CS_MS) m[LG_MS] = a;
-        if (w == LG_CS_NFIN) m[LG_NFIN] = a;
-        if (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3) m[LG_BMIN + (w - LG_CS_BMIN)] = a;
-        if (w >= LG_CS_BMAX && w < LG_CS_BMAX + 3) m[LG_BMAX + (w - LG_CS_BMAX)] = a;
-    }
 }
 
 // Ground-only output: each chunk's kept points at its stable offset, then the zero pads.
@@ -865,11 +873,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P)
     const float4 q = S.vox[v];
     const uint32_t pv = S.par[v];
     lg_neighbours(S, g, q, [&](uint32_t o) {
-        // plain loads, issued together: a stale pair of equal parents still lies in one tree
-        // (trees only merge); different ones go through uf_union, which re-reads
+        // each edge once, from its lower end: the higher neighbours only are loaded. Plain loads,
+        // issued together: a stale pair of equal parents still lies in one tree (trees only
+        // merge); different ones go through uf_union, which re-reads
+        if (o <= v) return;
         const float4 p = S.vox[o];
         const uint32_t po = S.par[o];
-        if (o > v && po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, v, o);
+        if (po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, v, o);
     });
 }
 // roots and component sizes: the lanes of a wave that share a root add their count with one

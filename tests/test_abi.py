@@ -42,17 +42,23 @@ def test_header_compiles_as_c_and_cpp(tmp_path):
 
 def test_ctypes_struct_sizes_match_c(tmp_path):
     src = tmp_path / "sz.c"
-    src.write_text('#include <stdio.h>\n#include "cones_gpu.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",'
+    src.write_text('#include <stdio.h>\n#include "cones_gpu.h"\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",'
                    'sizeof(cg_params), sizeof(cg_cloud_view), sizeof(cg_ground_result), sizeof(cg_detect_result),'
                    'sizeof(cg_batch), sizeof(cg_batch_results), sizeof(cg_synth_cfg), sizeof(cg_tile),'
-                   'sizeof(cg_crop_result), sizeof(cg_track_params)); return 0;}\n')
+                   'sizeof(cg_crop_result), sizeof(cg_track_params), sizeof(cg_halo_plan)); return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [C.sizeof(t) for t in (_abi.cg_params, _abi.cg_cloud_view, _abi.cg_ground_result,
                                   _abi.cg_detect_result, _abi.cg_batch, _abi.cg_batch_results, _abi.cg_synth_cfg,
-                                  _abi.cg_tile, _abi.cg_crop_result, _abi.cg_track_params)]
+                                  _abi.cg_tile, _abi.cg_crop_result, _abi.cg_track_params, _abi.cg_halo_plan)]
     assert got == want
+
+
+def test_every_declared_function_has_a_ctypes_signature():
+    """Without argtypes ctypes passes a handle as a 32-bit int: a missing binding crashes."""
+    missing = [n for n in declared_functions() if n not in _abi._SIGS]
+    assert not missing, missing
 
 
 def test_params_defaults_mirror_reference():
