@@ -409,7 +409,7 @@ __device__ __forceinline__ bool ray_inside(float x, float y, const float4& r) {
 // and the 8-bit z codes, handed to store_codes(group, {codes of points 0-3, 4-7}) once per
 // group of 8 points. Points the fast classification cannot certify are redone exactly after
 // the loop. touched returns the lane's used sector bins (bit 17: NaN angle).
-template <int PPT, int LAYOUT, bool GROUND, bool FILTER, class STORE>
+template <int PPT, int LAYOUT, bool GROUND, bool FILTER, class STORE, bool FULL = false>
 __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, const CgLaunch& L,
                                              const CgDevParams& P, uint32_t* sec_key, const float4* rays,
                                              LaneBits<(PPT + 63) / 64>& posm, uint32_t& touched,
@@ -440,9 +440,26 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
     float zbias = P.zq_bias;
     asm volatile("" : "+v"(zbias));
     auto load_group = [&](float3* buf, int g) {
+        if (FULL && LAYOUT == CG_LAYOUT_XYZI16) {
+            // every group is whole (N = PPT * CG_BLOCK): the group past the end (the loop's last
+            // prefetch) is clamped as a whole, a scalar min on the uniform group base, so the
+            // per-point address is the loop-invariant lane offset (no per-point VALU)
+            // buffer loads: the row offset in an SGPR (soffset), the lane's offset a
+            // loop-invariant VGPR (voffset); gfx9 raw-buffer descriptor word 3 = 0x00020000
+            const uint32_t gc = (uint32_t)g < (uint32_t)NG ? (uint32_t)g : (uint32_t)NG - 1u;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)fb, (short)0, (int)(N * 16u), 0x00020000);
+            typedef uint32_t v3u __attribute__((ext_vector_type(3)));
 #pragma unroll
-        for (int j = 0; j < G; j++)
-            buf[j] = load_xyz3<LAYOUT>(fb, min((uint32_t)(g * G + j) * CG_BLOCK + tid, nlast), L);
+            for (int j = 0; j < G; j++) {
+                const v3u v = __builtin_amdgcn_raw_buffer_load_b96(rs, tid * 16u, (gc * G + (uint32_t)j) * (CG_BLOCK * 16u), 0);
+                buf[j] = make_float3(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < G; j++)
+                buf[j] = load_xyz3<LAYOUT>(fb, min((uint32_t)(g * G + j) * CG_BLOCK + tid, nlast), L);
+        }
     };
     auto run_group = [&](const float3* buf, int g) {
         // per-point bits are accumulated as v = 2v + bit (one add-with-carry from the compare

@@ -678,8 +678,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             if ((uint32_t)cc < nch) posm.set_byte(cc, pb[cc * CG_BLOCK + tid]);
         __syncthreads();
     } else {
-        stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, fs->rays, posm, touched,
-                                                 [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; });
+        auto store = [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; };
+        if (LAYOUT == CG_LAYOUT_XYZI16 && N == (uint32_t)(PPT * CG_BLOCK))   // whole groups only
+            stream_pass1<PPT, LAYOUT, GROUND, FILTER, decltype(store), true>(fb, N, L, P, fs->sec_key, fs->rays,
+                                                                          posm, touched, store);
+        else
+            stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, fs->rays, posm, touched, store);
     }
     const uint32_t nlast = N ? N - 1 : 0u;
     if (GROUND && !SPLIT) {
