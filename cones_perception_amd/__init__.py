@@ -281,10 +281,13 @@ class ConeDetector(_Handle):
         return _detection(r)
 
 
-def _recrop(h, centers) -> List[np.ndarray]:
+def _recrop(h, centers, frame: Optional[int] = None) -> List[np.ndarray]:
     cen = np.ascontiguousarray(np.asarray(centers, np.float32).reshape(-1, 2))
     r = _abi.cg_crop_result()
-    check(lib().cg_recrop(h, cen.ctypes.data if cen.size else None, cen.shape[0], C.byref(r)))
+    if frame is None:
+        check(lib().cg_recrop(h, cen.ctypes.data if cen.size else None, cen.shape[0], C.byref(r)))
+    else:
+        check(lib().cg_batch_recrop(h, frame, cen.ctypes.data if cen.size else None, cen.shape[0], C.byref(r)))
     n = r.n_centers
     offs = np.ctypeslib.as_array(r.offsets, (n + 1,)).copy()
     tot = int(offs[-1])
@@ -446,6 +449,11 @@ class BatchEngine(_Handle):
         r = _abi.cg_detect_result()
         check(lib().cg_batch_fetch(self._h, frame, C.byref(r)))
         return _detection(r)
+
+    def recrop(self, frame: int, centers) -> List[np.ndarray]:
+        """get_reconstructed_cone for frame `frame` of the last batch (cg_batch_recrop): the
+        batch's input must still be resident."""
+        return _recrop(self._h, centers, frame)
 
 
 # ---------------------------------------------------------------------------------------

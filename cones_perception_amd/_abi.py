@@ -159,6 +159,7 @@ _SIGS = {
     "cg_debug_large_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "cg_debug_stamps_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_recrop": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(cg_crop_result)]),
+    "cg_batch_recrop": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(cg_crop_result)]),
     "cg_track_params_init": (None, [C.POINTER(cg_track_params)]),
     "cg_tracker_create": (C.c_int, [C.POINTER(cg_track_params), C.POINTER(C.c_void_p)]),
     "cg_tracker_destroy": (C.c_int, [C.c_void_p]),

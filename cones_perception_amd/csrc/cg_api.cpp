@@ -189,6 +189,10 @@ struct cg_handle {
     // the last single-frame call, for cg_recrop
     bool last_single = false;
     CgLaunch last_in{};
+    // the last cg_run_batch, for cg_batch_recrop (its input stays the caller's device memory)
+    CgLaunch last_batch{};
+    int batch_kmode = 0;
+    bool batch_valid = false;
     uint32_t last_k = 0;
     uint32_t* d_seckeys = nullptr;   // 18 words per frame inside d_hdr (not owned)
     RcBox* d_boxes = nullptr;
@@ -628,15 +632,12 @@ int cg_pipeline(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out) {
     return run_single(h, in, CG_KMODE_PIPELINE, out, nullptr);
 }
 
-int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop_result* out) {
-    if (!h || !out || (n_centers && !centers_xy)) return fail(CG_E_INVALID, "null argument");
-    if (!h->last_single || (h->last_mode != CG_KMODE_DETECT && h->last_mode != CG_KMODE_PIPELINE))
-        return fail(CG_E_INVALID, "cg_recrop needs a preceding cg_detect or cg_pipeline call on the handle");
-    HIPCHK(hipSetDevice(h->device));
-    const bool pipe = h->last_mode == CG_KMODE_PIPELINE;
-    const CgLaunch& L = h->last_in;
+// The re-crop of one frame L (frame 0 of L) whose detector input was the groundless cloud
+// (pipe: sector keys at d_seckeys, K kept points) or the frame itself.
+static int recrop_frame(cg_handle* h, const CgLaunch& L, bool pipe, const uint32_t* d_seckeys, uint32_t K,
+                        const float* centers_xy, uint32_t n_centers, cg_crop_result* out) {
     const uint32_t N = L.n_points, nblk = cg_recrop_blocks(N);
-    const uint32_t npad = pipe ? N - h->last_k : 0u;   // the groundless cloud's PointXYZI() tail
+    const uint32_t npad = pipe ? N - K : 0u;   // the groundless cloud's PointXYZI() tail
     h->h_rc_off.assign((size_t)n_centers + 1, 0u);
     h->h_rc_pts.clear();
     std::vector<RcBox> boxes(std::min<uint32_t>(n_centers, CG_RECROP_MAX_BOXES));
@@ -655,7 +656,7 @@ int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop
         HIPCHK(hipMemcpyAsync(h->d_boxes, boxes.data(), nb * sizeof(RcBox), hipMemcpyHostToDevice, h->stream));
         h->h_rc_cnt.assign(ncnt, 0u);
         if (ncnt) {
-            HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, h->d_seckeys, h->d_boxes, nb, h->d_rc_cnt, nullptr,
+            HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, d_seckeys, h->d_boxes, nb, h->d_rc_cnt, nullptr,
                                                 nullptr, false, h->stream));
             HIPCHK(hipMemcpyAsync(h->h_rc_cnt.data(), h->d_rc_cnt, ncnt * 4, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
@@ -680,7 +681,7 @@ int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop
                 h->rc_out_cap = total;
             }
             HIPCHK(hipMemcpyAsync(h->d_rc_cnt + ncnt, off.data(), ncnt * 4, hipMemcpyHostToDevice, h->stream));
-            HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, h->d_seckeys, h->d_boxes, nb, nullptr,
+            HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, d_seckeys, h->d_boxes, nb, nullptr,
                                                 h->d_rc_cnt + ncnt, h->d_rc_out, true, h->stream));
             HIPCHK(hipMemcpyAsync(h->h_rc_dev.data(), h->d_rc_out, total * 16, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
@@ -699,6 +700,38 @@ int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop
     out->offsets = h->h_rc_off.data();
     out->points = h->h_rc_pts.empty() ? nullptr : h->h_rc_pts.data();
     return CG_OK;
+}
+
+int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop_result* out) {
+    if (!h || !out || (n_centers && !centers_xy)) return fail(CG_E_INVALID, "null argument");
+    if (!h->last_single || (h->last_mode != CG_KMODE_DETECT && h->last_mode != CG_KMODE_PIPELINE))
+        return fail(CG_E_INVALID, "cg_recrop needs a preceding cg_detect or cg_pipeline call on the handle");
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
+    return recrop_frame(h, h->last_in, h->last_mode == CG_KMODE_PIPELINE, h->d_seckeys, h->last_k, centers_xy,
+                        n_centers, out);
+}
+
+int cg_batch_recrop(cg_handle* h, uint32_t frame, const float* centers_xy, uint32_t n_centers, cg_crop_result* out) {
+    if (!h || !out || (n_centers && !centers_xy)) return fail(CG_E_INVALID, "null argument");
+    if (!h->batch_valid) return fail(CG_E_INVALID, "cg_batch_recrop needs a preceding cg_run_batch on the handle");
+    if (frame >= h->last_batch.n_frames)
+        return fail(CG_E_INVALID, "frame %u >= %u", frame, h->last_batch.n_frames);
+    HIPCHK(hipSetDevice(h->device));
+    int rc = own_stream(h);
+    if (rc) return rc;
+    // the batch ran on its own stream: its header (K) after it finishes
+    uint32_t hdr[CG_HDR_WORDS];
+    HIPCHK(hipMemcpyAsync(hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, sizeof(hdr), hipMemcpyDeviceToHost,
+                          h->last_stream));
+    HIPCHK(hipStreamSynchronize(h->last_stream));
+    CgLaunch L = h->last_batch;
+    L.in += (uint64_t)frame * L.frame_stride;
+    L.n_frames = 1;
+    const bool pipe = h->batch_kmode == CG_KMODE_PIPELINE;
+    return recrop_frame(h, L, pipe, h->d_seckeys + (uint64_t)frame * (CG_NUM_BINS + 1), hdr[CG_HDR_K], centers_xy,
+                        n_centers, out);
 }
 
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
@@ -734,8 +767,13 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     L.span = h->next_span;
     h->next_span = nullptr;
-    rc = launch_frames(h, L, mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT, s);
+    const int kmode = mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT;
+    if (kmode == CG_KMODE_PIPELINE) L.seckeys = h->d_seckeys;   // per frame, for cg_batch_recrop
+    rc = launch_frames(h, L, kmode, s);
     if (rc) return rc;
+    h->last_batch = L;
+    h->batch_kmode = kmode;
+    h->batch_valid = true;
     h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
     h->last_single = false;
     return CG_OK;

@@ -268,6 +268,11 @@ typedef struct cg_crop_result {
     const float*    points;   /* offsets[n_centers] x 4 */
 } cg_crop_result;
 int cg_recrop(cg_handle* h, const float* centers_xy, uint32_t n_centers, cg_crop_result* out);
+/* The same for frame `frame` of the last cg_run_batch on the handle (pipeline or detect
+ * mode). The batch's input must still be in the caller's device memory; the call waits for
+ * the batch's stream. */
+int cg_batch_recrop(cg_handle* h, uint32_t frame, const float* centers_xy, uint32_t n_centers,
+                    cg_crop_result* out);
 
 /* Tracking and the four colour clouds, ConeDetector::get_centroid_clouds
  * (src/cone_detection.cpp:251-339). Host code; no device. One frame is two calls, split where

@@ -198,3 +198,24 @@ def test_cpp_node_mirror_demo():
     # the GPU colour classifier (ColorClassifier, cg_classify_colors) as the node's service
     gl = [l for l in r.stdout.splitlines() if l.startswith("gpu colour service frame")]
     assert len(gl) == 5
+
+
+@pytest.mark.parametrize("mode,rings", [("pipeline", 64), ("detect", 64), ("pipeline", 128)])
+def test_batch_recrop_matches_oracle(params, mode, rings):
+    """cg_batch_recrop: the re-crop of any frame of a device-resident batch (frames of the
+    batch engine, 128-ring frames through the large path) equals the oracle's on that frame."""
+    import torch
+    F, cols = 3, 1024
+    raw = cp.synth_frames(F, first_frame=5, rings=rings, cols=cols, clutter=20, cones_per_row=6)
+    d = torch.from_numpy(raw).to(torch.device("cuda", 0))
+    eng = cp.BatchEngine(params, device=0)
+    m = _abi.CG_MODE_PIPELINE if mode == "pipeline" else _abi.CG_MODE_DETECT
+    eng.run(d.data_ptr(), F, rings * cols, 16, mode=m)
+    om = O.MODE_PIPELINE if mode == "pipeline" else O.MODE_DETECT
+    for f in (F - 1, 0):
+        det = eng.fetch(f)
+        cen = _centres(det, np.random.default_rng(f))
+        got = eng.recrop(f, cen)
+        ref = O.recrop(params, cp.frame_cloud(raw[f]), om, cen)
+        _same_crops(got, ref, f"batch {mode} frame {f}")
+        assert sum(len(c) for c in got) > 0
