@@ -2,19 +2,23 @@
 // and any LiDAR with more than 64 x 1024 returns). Same semantics as the frame kernel
 // (cg_kernels.hip), spread over many workgroups per frame and HBM scratch:
 //
-//   lg_front    one 512-lane workgroup per 8,192-point chunk: pass 1 (stream_pass1), z codes
-//               to HBM, per-chunk sector minima merged with global atomicMin, filter
-//               candidates appended with their frame index (detector mode: survivors + bounds)
-//   lg_decide   per chunk: thresholds, pass 2 over the chunk's codes (kept count K); the
-//               candidates of the chunk's share decided by their code (exactly when ambiguous),
-//               survivors appended, VoxelGrid bounds merged
+//   lg_front    one 512-lane workgroup per 4,096-point chunk: pass 1 (stream_pass1), z codes
+//               to HBM, per-chunk statistics (sector minima, used bins; detector mode: the
+//               filter survivors' bits and count)
+//   lg_reduce_chunks  one workgroup folds the chunk statistics into the frame's meta words
+//   lg_decide   per chunk: thresholds, pass 2 over the chunk's codes (kept count K), survivor
+//               bits = ground-kept & filter bits (ambiguous codes decided exactly)
+//   lg_surv_write  survivors in frame-index order (chunk-count prefix, then (k, lane) order)
+//               with their VoxelGrid bounds
 //   lg_ground_* ground-only mode: stable per-chunk output offsets, kept points then zero pads
 //   backend     M <= CG_MMAX: one workgroup from LDS (cg_kernels.hip, cg_launch_lg_back_small);
-//               otherwise the global backend below: voxel keys (PCL idx, frame index) sorted by
-//               a stable LSD radix sort, voxel runs + centroids in frame-index order, a
-//               neighbour grid (cells >= tolerance) sorted the same way, union-find with
-//               global atomics (roots = lowest voxel index = PCL's seed), size filter, PCL's
-//               cluster order, CSR by a (rank, voxel) sort, per-cluster centroids.
+//               otherwise the global backend below: PCL idx keys sorted by a stable LSD radix
+//               sort (the survivors are already in frame-index order), voxel runs + centroids
+//               in frame-index order, a dense neighbour grid, a lowest-neighbour forest, pointer
+//               jumping and cross-tree unions (roots = lowest voxel index = PCL's seed), size
+//               filter, PCL's cluster order, CSR by a sort of the rank bits, per-cluster
+//               centroids.
+//   cg_halo_*   C5 spatial tiling: the backend per voxel slab, cross-slab edges, merge.
 //
 // Every sum keeps the reference's order (PCL sorts by idx; ties in point order here, as in
 // the frame kernel), so results are bit-identical to the frame kernel's on the same input.
