@@ -357,6 +357,7 @@ int ensure_large(cg_handle* h, uint32_t n) {
     h->d_large = nullptr;
     h->large_points = 0;
     HIPCHK(hipMalloc(&h->d_large, cg_large_bytes(n)));
+    HIPCHK(hipMemset(h->d_large, 0, cg_large_bytes(n)));   // the scans' status words start zeroed
     cg_large_layout(h->d_large, n, h->lg);
     if (!h->h_meta) HIPCHK(hipHostMalloc((void**)&h->h_meta, LG_META_WORDS * 4, hipHostMallocDefault));
     h->lg.hmeta = h->h_meta;

@@ -135,7 +135,7 @@ struct LgScratch {
     uint64_t* key0; uint64_t* key1;     // radix sort ping-pong
     uint32_t* val0; uint32_t* val1;
     uint32_t* hist;           // 256 x tiles + 1
-    uint32_t* tsum;           // tiles + 2
+    uint32_t* sstat;          // single-pass scan status words (tickets, finished, per tile)
     float4* vox;              // voxel points
     uint32_t* run;            // voxel run starts
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;

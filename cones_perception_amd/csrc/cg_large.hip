@@ -369,76 +369,98 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void lg_ground_out(CgLaunch L, CgDevPa
 }
 
 // ------------------------------------------------------------------------------------------
-// Device-wide exclusive scan of flag(i) over i < n (count from meta[n_word] when n_word >= 0),
-// calling emit(i, position) for every flagged i; the total goes to meta[total_word].
-// Three launches: per-tile counts, one-block scan of the tile counts, emit.
-template <class FLAG>
-__global__ __launch_bounds__(CG_BLOCK) void lg_scan_count(uint32_t n, int n_word, const uint32_t* meta, FLAG flag,
-                                                          uint32_t* tsum) {
-    __shared__ uint32_t red[WAVES];
-    if (n_word >= 0) n = meta[n_word];
-    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
-    uint32_t c = 0;
-    for (int q = 0; q < 8; q++) c += (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u;
-    c = wave_sum(c);
-    if (lane_id() == 0) red[wave_id()] = c;
+// Single-pass device-wide scans (decoupled look-back). A tile takes a ticket when it starts,
+// so it only ever waits on tiles already running; it publishes its count (LG_ST_A), sums the
+// tiles before it (the nearest inclusive prefix, LG_ST_P, ends the walk) and publishes its own
+// prefix. The last tile to finish zeroes the status words for the next launch (the scratch
+// starts zeroed). st: [0] tickets, [1] finished tiles, [2 + t] tile t's status.
+#define LG_ST_A 0x40000000u
+#define LG_ST_P 0x80000000u
+#define LG_ST_V 0x3fffffffu   // counts < 2^30 (frames of <= CG_MAX_FRAME_POINTS points)
+__device__ __forceinline__ uint32_t lg_tile_ticket(uint32_t* st) {
+    __shared__ uint32_t tk;
+    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(&st[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int w = 0; w < WAVES; w++) t += red[w];
-        tsum[blockIdx.x] = t;
-    }
+    return tk;
 }
-// In-place exclusive scan of a[0, n) by one workgroup; a[n] = total, also to *total if set.
-__global__ __launch_bounds__(CG_BLOCK) void lg_scan_tiles(uint32_t* a, uint32_t n, uint32_t* total) {
-    __shared__ uint32_t red[8 * WAVES];
-    const uint32_t t = block_scan(n, [&](uint32_t i) -> uint32_t { return a[i]; },
-                                  [&](uint32_t i, uint32_t e) { a[i] = e; }, red);
-    if (threadIdx.x == 0) {
-        a[n] = t;
-        if (total) *total = t;
+// Wave 0 of tile t: publish count, return the exclusive prefix of the tiles before t.
+__device__ __forceinline__ uint32_t lg_lookback(uint32_t* st, uint32_t t, uint32_t count) {
+    uint32_t* ts = st + 2;
+    const uint32_t l = lane_id();
+    if (t == 0) {
+        if (l == 0) __hip_atomic_store(&ts[0], LG_ST_P | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
     }
+    if (l == 0) __hip_atomic_store(&ts[t], LG_ST_A | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t base = 0;
+    int32_t hi = (int32_t)t - 1;
+    for (;;) {
+        const int32_t j = hi - (int32_t)l;
+        const uint32_t w = j >= 0 ? __hip_atomic_load(&ts[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LG_ST_P;
+        const uint64_t pm = __ballot((w & LG_ST_P) != 0u);
+        const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
+        if (__ballot(w == 0u && l < first)) {   // a tile before the nearest prefix not published yet
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        base += wave_sum(l <= first ? (w & LG_ST_V) : 0u);
+        if (first < 64u) break;
+        hi -= 64;
+    }
+    if (l == 0) __hip_atomic_store(&ts[t], LG_ST_P | (base + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return base;
 }
-template <class FLAG, class EMIT>
-__global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, uint32_t* meta, FLAG flag,
-                                                         EMIT emit, const uint32_t* tsum, int total_word) {
+// Every thread of the block, after its look-back: the last tile resets the status words.
+__device__ __forceinline__ void lg_tile_done(uint32_t* st, uint32_t active) {
+    __shared__ uint32_t last;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(&st[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
+    __syncthreads();
+    if (last)
+        for (uint32_t i = threadIdx.x; i < active + 2; i += CG_BLOCK) st[i] = 0;
+}
+// Block-wide: this tile's eight-per-thread counts c -> each thread's exclusive position;
+// returns through tot_out the device-wide total when this is the last active tile.
+__device__ __forceinline__ uint32_t lg_tile_scan(uint32_t* st, uint32_t t, uint32_t active, uint32_t c,
+                                                 uint32_t* total) {
     __shared__ uint32_t red[WAVES];
     __shared__ uint32_t tbase;
-    if (n_word >= 0) n = meta[n_word];
-    {   // this tile's base: the raw counts of the tiles before it (block 0 also writes the total)
-        __shared__ uint32_t pw[WAVES], tw[WAVES];
-        const uint32_t nt = gridDim.x, b = blockIdx.x;
-        uint32_t pre = 0, tot = 0;
-        for (uint32_t t = threadIdx.x; t < nt; t += CG_BLOCK) {
-            const uint32_t c = tsum[t];
-            tot += c;
-            pre += t < b ? c : 0u;
-        }
-        pre = wave_sum(pre);
-        tot = wave_sum(tot);
-        if (lane_id() == 0) { pw[wave_id()] = pre; tw[wave_id()] = tot; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t p = 0, t = 0;
-            for (int w = 0; w < WAVES; w++) { p += pw[w]; t += tw[w]; }
-            tbase = p;
-            if (b == 0) meta[total_word] = t;
-        }
-        __syncthreads();
-    }
-    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
-    uint32_t fl[8], c = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) { fl[q] = (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u; c += fl[q]; }
     const uint32_t inc = wave_incl_scan(c);
     if (lane_id() == 63) red[wave_id()] = inc;
     __syncthreads();
-    uint32_t wo = 0;
-    for (uint32_t w = 0; w < wave_id(); w++) wo += red[w];
-    uint32_t pos = tbase + wo + inc - c;
+    if (wave_id() == 0) {
+        const uint32_t tot = wave_sum(lane_id() < WAVES ? red[lane_id()] : 0u);
+        const uint32_t base = lg_lookback(st, t, tot);
+        if (lane_id() == 0) {
+            tbase = base;
+            if (t == active - 1 && total) *total = base + tot;
+        }
+    }
+    __syncthreads();
+    uint32_t pos = tbase + inc - c;
+    for (uint32_t w = 0; w < wave_id(); w++) pos += red[w];
+    return pos;
+}
+
+// Exclusive scan of flag(i) over i < n (count from meta[n_word] when n_word >= 0), calling
+// emit(i, position) for every flagged i; the total goes to meta[total_word]. One launch.
+template <class FLAG, class EMIT>
+__global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, uint32_t* meta, FLAG flag,
+                                                         EMIT emit, uint32_t* st, int total_word) {
+    if (n_word >= 0) n = meta[n_word];
+    const uint32_t active = n ? (n + LG_TILE - 1) / LG_TILE : 1u;
+    if (blockIdx.x >= active) return;
+    const uint32_t t = lg_tile_ticket(st);
+    const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)threadIdx.x * 8;
+    uint32_t fl[8], c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) { fl[q] = (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u; c += fl[q]; }
+    uint32_t pos = lg_tile_scan(st, t, active, c, meta + total_word);
 #pragma unroll
     for (int q = 0; q < 8; q++)
         if (fl[q]) emit((uint32_t)(b0 + q), pos++);
+    lg_tile_done(st, active);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -563,9 +585,8 @@ int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t 
 template <class FLAG, class EMIT>
 void scan_emit(LgScratch& S, uint32_t n_max, int n_word, FLAG flag, EMIT emit, int total_word, hipStream_t s) {
     const uint32_t nt = std::max<uint32_t>(1, tiles_of(n_max));
-    hipLaunchKernelGGL((lg_scan_count<FLAG>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, S.tsum);
     hipLaunchKernelGGL((lg_scan_emit<FLAG, EMIT>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, emit,
-                       S.tsum, total_word);
+                       S.sstat, total_word);
 }
 
 }  // namespace
@@ -627,8 +648,12 @@ __global__ void lg_grid_setup(LgScratch S, CgDevParams P, uint32_t npad, uint32_
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevParams P, uint32_t Mtot, uint32_t N,
                                                           uint32_t PB) {
     const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
-    if (j >= Mtot) return;
     const uint32_t* m = S.meta;
+    {   // the dense neighbour grid's cell counts (lg_dgrid_count), ncell from lg_grid_setup
+        const uint32_t nc = m[LG_NCELL] + 1;
+        for (uint32_t i = j; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
+    }
+    if (j >= Mtot) return;
     const uint32_t Ms = m[LG_MS];
     const float4 p = lg_point(S, j, Ms);
     const uint64_t pidx = j < Ms ? S.surv_i[j] : (uint64_t)N + (j - Ms);
@@ -740,10 +765,6 @@ struct LgGrid {
     }
     __device__ uint32_t id(uint32_t cx, uint32_t cy, uint32_t cz) const { return cx + n[0] * (cy + n[1] * cz); }
 };
-__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_zero(LgScratch S) {
-    const uint32_t n = S.meta[LG_NCELL] + 1;
-    for (uint32_t i = blockIdx.x * CG_BLOCK + threadIdx.x; i < n; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
-}
 __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_count(LgScratch S) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
     if (v >= V) return;
@@ -754,46 +775,21 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_count(LgScratch S) {
     S.uk[v] = c;
     S.ca[v] = atomicAdd(&S.cstart[c], 1u);
 }
-// exclusive scan of cstart[0, ncell] in place: tile sums (LG_TILE per block), one-block scan of
-// the tile sums (in S.hist), then each tile rescanned with its base
-__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_tiles(LgScratch S) {
-    __shared__ uint32_t red[WAVES];
-    const uint32_t n = S.meta[LG_NCELL] + 1;
-    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
-    if ((uint64_t)blockIdx.x * LG_TILE >= n) return;
-    uint32_t c = 0;
-    for (int q = 0; q < 8; q++) c += (b0 + q < n) ? S.cstart[b0 + q] : 0u;
-    c = wave_sum(c);
-    if (lane_id() == 0) red[wave_id()] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int w = 0; w < WAVES; w++) t += red[w];
-        S.hist[blockIdx.x] = t;
-    }
-}
+// exclusive scan of cstart[0, ncell] in place (single pass, lg_tile_scan)
 __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_scan(LgScratch S) {
-    __shared__ uint32_t red[8 * WAVES];
-    const uint32_t nt = (S.meta[LG_NCELL] + 1 + LG_TILE - 1) / LG_TILE;
-    block_scan(nt, [&](uint32_t i) -> uint32_t { return S.hist[i]; },
-               [&](uint32_t i, uint32_t e) { S.hist[i] = e; }, red);
-}
-__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_emit(LgScratch S) {
-    __shared__ uint32_t red[WAVES];
     const uint32_t n = S.meta[LG_NCELL] + 1;
-    if ((uint64_t)blockIdx.x * LG_TILE >= n) return;
-    const uint64_t b0 = (uint64_t)blockIdx.x * LG_TILE + (uint64_t)threadIdx.x * 8;
+    const uint32_t active = (n + LG_TILE - 1) / LG_TILE;
+    if (blockIdx.x >= active) return;
+    const uint32_t t = lg_tile_ticket(S.sstat);
+    const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)threadIdx.x * 8;
     uint32_t x[8], c = 0;
 #pragma unroll
     for (int q = 0; q < 8; q++) { x[q] = (b0 + q < n) ? S.cstart[b0 + q] : 0u; c += x[q]; }
-    const uint32_t inc = wave_incl_scan(c);
-    if (lane_id() == 63) red[wave_id()] = inc;
-    __syncthreads();
-    uint32_t pos = S.hist[blockIdx.x] + inc - c;
-    for (uint32_t w = 0; w < wave_id(); w++) pos += red[w];
+    uint32_t pos = lg_tile_scan(S.sstat, t, active, c, nullptr);
 #pragma unroll
     for (int q = 0; q < 8; q++)
         if (b0 + q < n) { S.cstart[b0 + q] = pos; pos += x[q]; }
+    lg_tile_done(S.sstat, active);
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_fill(LgScratch S) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
@@ -1185,11 +1181,8 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     const uint32_t VB = bits_of(Mtot);
     const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;   // tiles past ncell return at once
-    hipLaunchKernelGGL(lg_dgrid_zero, dim3(256), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_tiles, dim3(gt), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_scan, dim3(1), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_emit, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
     hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
@@ -1245,7 +1238,7 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(10, take(N * 4)); place(11, take(N * 4));
     const uint64_t nrs = (N + LG_RS_TILE - 1) / LG_RS_TILE;
     place(12, take((std::max<uint64_t>(256 * nrs, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
-    place(13, take((nt + 2) * 4));
+    place(13, take((std::max<uint64_t>(nt, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
     place(14, take(N * 16));
     place(15, take((N + 2) * 4));
     for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));
@@ -1271,7 +1264,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 10: S.val0 = (uint32_t*)p; break;
             case 11: S.val1 = (uint32_t*)p; break;
             case 12: S.hist = (uint32_t*)p; break;
-            case 13: S.tsum = (uint32_t*)p; break;
+            case 13: S.sstat = (uint32_t*)p; break;
             case 14: S.vox = (float4*)p; break;
             case 15: S.run = (uint32_t*)p; break;
             case 28: S.cstart = (uint32_t*)p; break;
@@ -1353,11 +1346,8 @@ int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
                        L, S, 0u, Mtot, buf);
     const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
-    hipLaunchKernelGGL(lg_dgrid_zero, dim3(256), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_tiles, dim3(gt), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_scan, dim3(1), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_emit, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
     hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
