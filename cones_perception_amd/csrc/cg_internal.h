@@ -123,6 +123,7 @@ enum {
     LG_BMIN, LG_BMAX = LG_BMIN + 3, LG_V = LG_BMAX + 3, LG_C, LG_U, LG_PASS,
     LG_MINB, LG_MUL1 = LG_MINB + 3, LG_MUL2, LG_ORG, LG_NFIN_ALL = LG_ORG + 3, LG_SCAN_N,
     LG_DGINV, LG_DGN = LG_DGINV + 3, LG_NCELL = LG_DGN + 3,   // dense neighbour grid
+    LG_SORT_LIM,               // cluster-order sort: key bits in use (digits past it are skipped)
     LG_META_WORDS = 64
 };
 struct LgScratch {

@@ -469,9 +469,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word,
 #define LG_RS_ROUNDS 2
 #define LG_RS_TILE (LG_RS_ROUNDS * CG_BLOCK)
 __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint32_t n, uint32_t shift,
-                                                       uint32_t* hist, const uint32_t* n_dev) {
+                                                       uint32_t* hist, const uint32_t* n_dev, const uint32_t* lim) {
     __shared__ uint32_t h[256];
     if (n_dev) n = *n_dev;   // count known on the device only (grid sized for an upper bound)
+    if (lim && shift >= *lim) return;   // key width known on the device only: an identity pass
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * LG_RS_TILE;
@@ -488,8 +489,16 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint
 // per-wave digit counts of the round, so equal keys keep their input order (stable).
 __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                                           uint32_t* vout, uint32_t n, uint32_t shift,
-                                                          const uint32_t* hist, const uint32_t* n_dev) {
+                                                          const uint32_t* hist, const uint32_t* n_dev,
+                                                          const uint32_t* lim) {
     if (n_dev) n = *n_dev;
+    if (lim && shift >= *lim) {   // digits past the keys' width: the pass is a copy
+        for (int q = 0; q < LG_RS_ROUNDS; q++) {
+            const uint64_t i = (uint64_t)blockIdx.x * LG_RS_TILE + (uint64_t)q * CG_BLOCK + threadIdx.x;
+            if (i < n) { kout[i] = kin[i]; vout[i] = vin[i]; }
+        }
+        return;
+    }
     __shared__ uint32_t run[256];
     __shared__ uint32_t wcnt[WAVES][256];
     __shared__ uint32_t red[8 * WAVES];
@@ -560,6 +569,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, c
 namespace {
 
 uint32_t tiles_of(uint64_t n) { return (uint32_t)((n + LG_TILE - 1) / LG_TILE); }
+// wave-per-item launches whose count (V, C) is known on the device only: a grid-stride loop
+// over at most 1024 workgroups (the chip's 8192 wave slots) instead of one wave per upper bound
+uint32_t lg_wave_blocks(uint64_t n) {
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + WAVES - 1) / WAVES, 1024));
+}
 uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + CG_BLOCK - 1) / CG_BLOCK); }
 uint32_t bits_of(uint64_t v) { uint32_t b = 0; while (b < 64 && (1ull << b) <= v) b++; return b ? b : 1; }
 
@@ -567,16 +581,16 @@ uint32_t bits_of(uint64_t v) { uint32_t b = 0; while (b < 64 && (1ull << b) <= v
 // 1) that holds the result. The pairs are already in order of the bits below lo. With n_dev,
 // the count is read on the device and n is only its upper bound.
 int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t lo = 0,
-               const uint32_t* n_dev = nullptr) {
+               const uint32_t* n_dev = nullptr, const uint32_t* lim = nullptr) {
     uint64_t* k[2] = {S.key0, S.key1};
     uint32_t* v[2] = {S.val0, S.val1};
     int cur = 0;
     if (n <= 1) return cur;
     const uint32_t nt = (uint32_t)(((uint64_t)n + LG_RS_TILE - 1) / LG_RS_TILE);
     for (uint32_t shift = lo; shift < bits; shift += 8) {
-        hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist, n_dev);
+        hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist, n_dev, lim);
         hipLaunchKernelGGL(lg_rs_scatter, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
-                           shift, S.hist, n_dev);
+                           shift, S.hist, n_dev, lim);
         cur ^= 1;
     }
     return cur;
@@ -691,12 +705,11 @@ struct VoxelEmit {
 // CentroidPoint: float sums in ascending frame index / float(n); passthrough copies the point.
 // One wave per voxel: the lanes fetch 64 members at a time, the sums run through them in
 // member order.
-__global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScratch S, uint32_t f, uint32_t Mtot,
-                                                               int buf) {
-    const uint32_t v = blockIdx.x * WAVES + wave_id(), l = lane_id();
+__device__ __forceinline__ void lg_voxel_centroids_one(const CgLaunch& L, const LgScratch& S, uint32_t f, int buf,
+                                                       uint32_t v) {
+    const uint32_t l = lane_id();
     const uint32_t* m = S.meta;
     const uint32_t V = m[LG_V], Ms = m[LG_MS];
-    if (v >= V) return;
     const uint32_t* val = buf ? S.val1 : S.val0;
     float4* vox_out = L.vox + (uint64_t)f * L.cap;
     if (l == 0) {
@@ -730,6 +743,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
     const float4 c = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
     S.vox[v] = c;
     vox_out[v] = c;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScratch S, uint32_t f, uint32_t Mtot,
+                                                               int buf) {
+    for (uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V]; v < V; v += gridDim.x * WAVES)
+        lg_voxel_centroids_one(L, S, f, buf, v);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -825,9 +843,7 @@ __device__ __forceinline__ bool lg_adjacent(const float4& q, const float4& p, fl
     return acc < r2;
 }
 // forest: par[v] = lowest adjacent voxel index, or v (one wave per voxel)
-__global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P) {
-    const uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V];
-    if (v >= V) return;
+__device__ __forceinline__ void lg_forest_one(const LgScratch& S, const CgDevParams& P, uint32_t v) {
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
     uint32_t lo = v;
@@ -836,6 +852,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P
     });
     lo = wave_umin(lo);
     if (lane_id() == 0) S.par[v] = lo;
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P) {
+    for (uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V]; v < V; v += gridDim.x * WAVES)
+        lg_forest_one(S, P, v);
 }
 // flatten: rounds of par[x] = par[par[x]] until nothing changes, in LDS when V <= LG_FLAT_LDS
 // (else on the HBM array, still one workgroup: its barriers order the rounds)
@@ -866,9 +886,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_flatten(LgScratch S) {
         for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = lpar[x];
 }
 // cross-tree edges (v < o): united unless both ends already share a parent
-__global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P) {
-    const uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V];
-    if (v >= V) return;
+__device__ __forceinline__ void lg_cross_one(const LgScratch& S, const CgDevParams& P, uint32_t v) {
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
     const uint32_t pv = S.par[v];
@@ -881,6 +899,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P)
         const uint32_t po = S.par[o];
         if (po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, v, o);
     });
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P) {
+    for (uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V]; v < V; v += gridDim.x * WAVES)
+        lg_cross_one(S, P, v);
 }
 // roots and component sizes: the lanes of a wave that share a root add their count with one
 // atomic (a component's voxels are mostly neighbours in idx order; same-address atomics from
@@ -984,6 +1006,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_order(LgScratch S) {
 // labels (cluster rank or -1) and the (rank, voxel) keys of the CSR sort
 __global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, uint32_t f, uint32_t VB) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
+    // kept keys: rank < C in bits [VB, VB + bits(C)); dropped keys are all ones there, so one
+    // bit more orders them last and the digits above are skipped
+    if (v == 0) S.meta[LG_SORT_LIM] = VB + (32u - (uint32_t)__clz(S.meta[LG_C])) + 1u;
     if (v >= V) return;
     const uint32_t rk = S.rk[S.lab[v]];
     (L.lab + (uint64_t)f * L.cap)[v] = rk == 0xffffffffu ? -1 : (int32_t)rk;
@@ -1010,12 +1035,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr(CgLaunch L, LgScratch S, uint
         h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u);
     }
 }
-__global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+__device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S,
+                                                 uint32_t f, uint32_t k) {
     // one wave per cluster: the lanes fetch 64 members at a time, the sums run through them in
     // ascending member order (lane order), as the reference's loop does
-    const uint32_t k = blockIdx.x * WAVES + wave_id(), l = lane_id();
-    const uint32_t C = S.meta[LG_C];
-    if (k >= C) return;
+    const uint32_t l = lane_id();
     const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const uint32_t s = S.off[k], e = S.off[k + 1];
     float x = 0.0f, y = 0.0f;
@@ -1050,6 +1074,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams
     const float qx = (float)((double)px + (double)(px / len) * P.ext);
     const float qy = (float)((double)py + (double)(py / len) * P.ext);
     (L.cen + (uint64_t)f * L.cap)[k] = make_float2(qx, qy);
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+    for (uint32_t k = blockIdx.x * WAVES + wave_id(), C = S.meta[LG_C]; k < C; k += gridDim.x * WAVES)
+        lg_centroids_one(L, P, S, f, k);
 }
 
 // Gathered survivors of a tiled frame (cg_tile_backend): meta reset, survivors copied into
@@ -1174,12 +1202,12 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     // runs over the finite points (non-finite keys sort last); passthrough: every point
     scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
-    hipLaunchKernelGGL(lg_voxel_centroids, dim3(std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES)), dim3(CG_BLOCK), 0, s,
+    hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(Mtot)), dim3(CG_BLOCK), 0, s,
                        Lh, S, f, Mtot, buf);
     // V is known on the device only: the clustering launches are sized for V <= Mtot and read
     // V from the meta words (no host round trip)
     const uint32_t VB = bits_of(Mtot);
-    const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES);
+    const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = lg_wave_blocks(Mtot);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;   // tiles past ncell return at once
     hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
@@ -1194,7 +1222,8 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     // (rank, voxel) keys are written in voxel order: only the rank bits need sorting. rank < C
     // <= Mtot / min_cluster_size; one bit more tells ranks from the non-members' ~0 keys
     const uint32_t cmax = P.min_cl > 1 ? Mtot / P.min_cl : Mtot;
-    const int kb = radix_sort(S, Mtot, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V);
+    const int kb = radix_sort(S, Mtot, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V,
+                               S.meta + LG_SORT_LIM);
     hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)Mtot + 1)), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, kb, Mtot, K);
     hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
     return hipGetLastError();
@@ -1342,9 +1371,9 @@ int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     const int buf = radix_sort(S, Mtot, key_bits, s);
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
-    hipLaunchKernelGGL(lg_voxel_centroids, dim3(std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES)), dim3(CG_BLOCK), 0, s,
+    hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(Mtot)), dim3(CG_BLOCK), 0, s,
                        L, S, 0u, Mtot, buf);
-    const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = std::max<uint32_t>(1, (Mtot + WAVES - 1) / WAVES);
+    const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = lg_wave_blocks(Mtot);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
     hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
@@ -1462,7 +1491,7 @@ int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
     hipLaunchKernelGGL(lg_halo_meta, dim3(1), dim3(64), 0, s, S, V);
     const uint32_t n = std::max<uint32_t>(V, 1);
-    const uint32_t vb = blocks_of(n), wb = (n + WAVES - 1) / WAVES;
+    const uint32_t vb = blocks_of(n), wb = lg_wave_blocks(n);
     int buf = 0;
     if (V) {
         hipLaunchKernelGGL(lg_halo_keys, dim3(vb), dim3(CG_BLOCK), 0, s, S, d_rec, V);
@@ -1477,7 +1506,8 @@ int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     const uint32_t VB = bits_of(n);
     hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, L, S, 0u, VB);
     const uint32_t cmax = P.min_cl > 1 ? n / P.min_cl : n;
-    const int kb = radix_sort(S, n, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V);
+    const int kb = radix_sort(S, n, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V,
+                               S.meta + LG_SORT_LIM);
     hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)n + 1)), dim3(CG_BLOCK), 0, s, L, S, 0u, VB, kb, Mtot, K);
     hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, L, P, S, 0u);
     return hipGetLastError();
