@@ -614,14 +614,13 @@ __device__ __forceinline__ float4 lg_point(const LgScratch& S, uint32_t j, uint3
 }
 
 // pcl::VoxelGrid setup from the bounds (getMinMax3D + the int64 overflow guard)
-__global__ void lg_grid_setup(LgScratch S, CgDevParams P, uint32_t npad, uint32_t Mtot) {
-    if (threadIdx.x != 0) return;
-    uint32_t* m = S.meta;
+// (one thread; reads the bounds words of in, writes the grid words of m)
+__device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams& P, uint32_t npad, uint32_t Mtot) {
     float bmn[3], bmx[3];
-    uint32_t nfin = m[LG_NFIN];
+    uint32_t nfin = in[LG_NFIN];
     for (int a = 0; a < 3; a++) {
-        bmn[a] = nfin ? cg_fkey_inv(m[LG_BMIN + a]) : INFINITY;
-        bmx[a] = nfin ? cg_fkey_inv(m[LG_BMAX + a]) : -INFINITY;
+        bmn[a] = nfin ? cg_fkey_inv(in[LG_BMIN + a]) : INFINITY;
+        bmx[a] = nfin ? cg_fkey_inv(in[LG_BMAX + a]) : -INFINITY;
         if (npad) { bmn[a] = fminf(bmn[a], 0.f); bmx[a] = fmaxf(bmx[a], 0.f); }
     }
     nfin += npad;
@@ -659,16 +658,28 @@ __global__ void lg_grid_setup(LgScratch S, CgDevParams P, uint32_t npad, uint32_
 }
 
 // keys: passthrough -> pidx; else (PCL idx << PB | pidx), non-finite idx = 0xffffffff (last)
+// Every workgroup derives the grid words from the bounds (lg_grid_setup); workgroup 0 also
+// stores them in the meta words for the kernels after it (a halo slab: with its own count of
+// finite points, nfin_local, for the voxel runs).
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevParams P, uint32_t Mtot, uint32_t N,
-                                                          uint32_t PB) {
+                                                          uint32_t PB, uint32_t npad,
+                                                          uint32_t nfin_local = 0xffffffffu) {
+    __shared__ uint32_t m[LG_META_WORDS];
     const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
-    const uint32_t* m = S.meta;
+    if (threadIdx.x == 0) {
+        lg_grid_setup(S.meta, m, P, npad, Mtot);
+        if (blockIdx.x == 0) {
+            lg_grid_setup(S.meta, S.meta, P, npad, Mtot);
+            if (nfin_local != 0xffffffffu) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = nfin_local;
+        }
+    }
+    __syncthreads();
     {   // the dense neighbour grid's cell counts (lg_dgrid_count), ncell from lg_grid_setup
         const uint32_t nc = m[LG_NCELL] + 1;
         for (uint32_t i = j; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
     }
     if (j >= Mtot) return;
-    const uint32_t Ms = m[LG_MS];
+    const uint32_t Ms = S.meta[LG_MS];   // (m holds the grid words only)
     const float4 p = lg_point(S, j, Ms);
     const uint64_t pidx = j < Ms ? S.surv_i[j] : (uint64_t)N + (j - Ms);
     // PB = 0 (survivors in frame-index order): a stable sort by idx alone keeps each voxel's
@@ -1017,9 +1028,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, u
 }
 // CSR indices (ascending voxel index inside each cluster), per-cluster centroid + radial push
 // (src/cone_detection.cpp:261-279), offsets and the frame header
-__global__ __launch_bounds__(CG_BLOCK) void lg_csr(CgLaunch L, LgScratch S, uint32_t f, uint32_t VB, int buf,
-                                                   uint32_t Mtot, uint32_t K) {
-    const uint32_t i = blockIdx.x * CG_BLOCK + threadIdx.x;
+__device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const LgScratch& S, uint32_t f, uint32_t VB, int buf,
+                                           uint32_t Mtot, uint32_t K, uint32_t b) {
+    const uint32_t i = b * CG_BLOCK + threadIdx.x;
     const uint32_t* m = S.meta;
     const uint32_t C = m[LG_C], tot = C ? S.off[C] : 0u;
     const uint64_t* key = buf ? S.key1 : S.key0;
@@ -1036,11 +1047,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr(CgLaunch L, LgScratch S, uint
     }
 }
 __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S,
-                                                 uint32_t f, uint32_t k) {
+                                                 uint32_t f, uint32_t k, const uint64_t* key, uint64_t vmask) {
     // one wave per cluster: the lanes fetch 64 members at a time, the sums run through them in
     // ascending member order (lane order), as the reference's loop does
     const uint32_t l = lane_id();
-    const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const uint32_t s = S.off[k], e = S.off[k + 1];
     float x = 0.0f, y = 0.0f;
     for (uint32_t g0 = s; g0 < e; g0 += 8 * 64) {   // eight chunks of 64 members in flight
@@ -1049,7 +1059,7 @@ __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevP
 #pragma unroll
         for (int c = 0; c < 8; c++) {   // all member indices first, then all voxel loads
             const uint32_t i = g0 + 64 * c + l;
-            vi[c] = i < e ? (uint32_t)idx[i] : 0xffffffffu;
+            vi[c] = i < e ? (uint32_t)(key[i] & vmask) : 0xffffffffu;   // lg_csr's member index
         }
 #pragma unroll
         for (int c = 0; c < 8; c++) {
@@ -1075,9 +1085,19 @@ __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevP
     const float qy = (float)((double)py + (double)(py / len) * P.ext);
     (L.cen + (uint64_t)f * L.cap)[k] = make_float2(qx, qy);
 }
-__global__ __launch_bounds__(CG_BLOCK) void lg_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
-    for (uint32_t k = blockIdx.x * WAVES + wave_id(), C = S.meta[LG_C]; k < C; k += gridDim.x * WAVES)
-        lg_centroids_one(L, P, S, f, k);
+// CSR, header and cluster centroids in one launch: the first cb workgroups write the CSR
+// arrays, the others sum the clusters (member indices from the sorted keys, as lg_csr reads them)
+__global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
+                                                             uint32_t VB, int buf, uint32_t Mtot, uint32_t K,
+                                                             uint32_t cb) {
+    if (blockIdx.x < cb) {
+        lg_csr_one(L, S, f, VB, buf, Mtot, K, blockIdx.x);
+        return;
+    }
+    const uint64_t* key = buf ? S.key1 : S.key0;
+    const uint64_t vmask = (1ull << VB) - 1ull;
+    for (uint32_t k = (blockIdx.x - cb) * WAVES + wave_id(), C = S.meta[LG_C]; k < C; k += (gridDim.x - cb) * WAVES)
+        lg_centroids_one(L, P, S, f, k, key, vmask);
 }
 
 // Gathered survivors of a tiled frame (cg_tile_backend): meta reset, survivors copied into
@@ -1196,8 +1216,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
         else key_bits = PB + 1 + bits_of((uint64_t)div_b[0] * (uint64_t)div_b[1] * (uint64_t)div_b[2]);
         key_bits = std::min<uint32_t>(key_bits, 32 + PB);
     }
-    hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad, Mtot);
-    hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
+    hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB, npad);
     int buf = radix_sort(S, Mtot, key_bits, s);
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     // runs over the finite points (non-finite keys sort last); passthrough: every point
@@ -1224,8 +1243,8 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     const uint32_t cmax = P.min_cl > 1 ? Mtot / P.min_cl : Mtot;
     const int kb = radix_sort(S, Mtot, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V,
                                S.meta + LG_SORT_LIM);
-    hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)Mtot + 1)), dim3(CG_BLOCK), 0, s, Lh, S, f, VB, kb, Mtot, K);
-    hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
+    const uint32_t cb = blocks_of((uint64_t)Mtot + 1);
+    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, kb, Mtot, K, cb);
     return hipGetLastError();
 }
 
@@ -1328,11 +1347,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_halo_owner(const float4* pts, uin
 }
 // the local backend's run ends and scan length cover the slab's points only (the lattice
 // came from the whole frame's bounds)
-__global__ void lg_halo_counts(LgScratch S, uint32_t nfin_local) {
-    if (threadIdx.x != 0) return;
-    S.meta[LG_NFIN_ALL] = nfin_local;
-    S.meta[LG_SCAN_N] = nfin_local;
-}
 __global__ __launch_bounds__(CG_BLOCK) void lg_halo_records(LgScratch S, int buf, uint32_t PB, uint32_t* rec,
                                                             uint32_t cap) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
@@ -1365,9 +1379,7 @@ int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     const uint32_t PB = hm[LG_UNSORTED] ? bits_of((uint64_t)N + npad_all) : 0u;
     key_bits = std::min<uint32_t>(key_bits + PB, 32 + PB);
     const uint32_t mb = std::max<uint32_t>(1, blocks_of(Mtot));
-    hipLaunchKernelGGL(lg_grid_setup, dim3(1), dim3(64), 0, s, S, P, npad_all, Mtot);
-    hipLaunchKernelGGL(lg_halo_counts, dim3(1), dim3(64), 0, s, S, Mtot);
-    hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB);
+    hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB, npad_all, Mtot);
     const int buf = radix_sort(S, Mtot, key_bits, s);
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
@@ -1508,8 +1520,8 @@ int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     const uint32_t cmax = P.min_cl > 1 ? n / P.min_cl : n;
     const int kb = radix_sort(S, n, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V,
                                S.meta + LG_SORT_LIM);
-    hipLaunchKernelGGL(lg_csr, dim3(blocks_of((uint64_t)n + 1)), dim3(CG_BLOCK), 0, s, L, S, 0u, VB, kb, Mtot, K);
-    hipLaunchKernelGGL(lg_centroids, dim3(wb), dim3(CG_BLOCK), 0, s, L, P, S, 0u);
+    const uint32_t cb = blocks_of((uint64_t)n + 1);
+    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, L, P, S, 0u, VB, kb, Mtot, K, cb);
     return hipGetLastError();
 }
 int cg_launch_halo_owner(const float* pts, uint32_t n, float inv0, int32_t min_b0, uint32_t slab_w, uint32_t slabs,
