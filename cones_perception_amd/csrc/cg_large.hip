@@ -840,10 +840,21 @@ __device__ __forceinline__ void lg_neighbours(const LgScratch& S, const LgGrid& 
             e = S.cstart[g.id(xhi, (uint32_t)yy, (uint32_t)zz) + 1];
         }
     }
+    // the nine row ranges as one index space over the lanes: ceil(total / 64) rounds instead of
+    // one round (or more) per row
+    uint32_t rb[9], rx[9], tot = 0;
+#pragma unroll
     for (int r = 0; r < 9; r++) {
-        const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)b, r);
-        const uint32_t re = (uint32_t)__builtin_amdgcn_readlane((int)e, r);
-        for (uint32_t j = rb + l; j < re; j += 64) visit(S.ord[j]);
+        rb[r] = (uint32_t)__builtin_amdgcn_readlane((int)b, r);
+        rx[r] = tot;
+        tot += (uint32_t)__builtin_amdgcn_readlane((int)e, r) - rb[r];
+    }
+    for (uint32_t t = l; t < tot; t += 64) {
+        uint32_t j = 0;
+#pragma unroll
+        for (int r = 0; r < 9; r++)
+            if (t >= rx[r]) j = rb[r] + (t - rx[r]);   // the last row starting at or before t
+        visit(S.ord[j]);
     }
 }
 __device__ __forceinline__ bool lg_adjacent(const float4& q, const float4& p, float r2) {
