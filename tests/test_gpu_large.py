@@ -116,3 +116,14 @@ def test_c5_dense_million_point_frame(params):
     assert got.n_points == 1 << 20
     assert got.voxels.shape[0] > 1024          # the global backend ran
     assert_same_detection(got, ref, "C5")
+
+
+def test_c5_frame_through_detector(params):
+    """The detector alone on C5's frame: ~550k filtered points reach the voxel stage, so the
+    single-pass scan over them spans ~135 tiles and each tile's look-back crosses more than
+    one 64-tile window."""
+    msg = _frame(128, 8192, frame=0, clutter=60, cpr=12)
+    got = cp.ConeDetector(params).cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_DETECT)
+    assert ref.n_filtered > 64 * 4096
+    assert_same_detection(got, ref, "C5 detect")
