@@ -368,6 +368,8 @@ class ConeTracker:
         return st[: cen.shape[0]], need.value
 
     def commit(self, colors=None):
+        """colors: the colour service's response for the NEED_COLOR centroids in request order
+        (it may be shorter: the rest stay unknown), or None for a failed call."""
         if colors is None:
             check(lib().cg_tracker_commit(self._t, None, 0))
         else:
@@ -411,9 +413,9 @@ class ConeDetectorNode:
         if n_need:
             need = det.centroids[status == _abi.CG_TRACK_NEED_COLOR]
             crops = [to_ros_msg(c, {"frame_id": self.cones_frame_id}) for c in self.detector.recrop(need)]
+            # the service's response: possibly shorter than the request (the reference's server
+            # skips empty crops); the tracker applies it positionally (src/cone_detection.cpp:357-358)
             colors = self.classifier(crops) if self.classifier is not None else None
-            if colors is not None and len(colors) != n_need:
-                colors = None
         self.tracker.commit(colors)
         out = []
         for xy in self.tracker.clouds():

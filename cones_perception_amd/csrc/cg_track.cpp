@@ -121,19 +121,26 @@ extern "C" int cg_tracker_match(cg_tracker* t, const float* centroids_xy, uint32
 // src/cone_detection.cpp:320-339: the classified centroids follow the known-colour ones in
 // their clouds, in classification order; then prev_centroid_clouds = this frame's clouds and
 // prev_detected_cones = every centroid of this frame.
+//
+// The colours are the service's response, applied as the reference applies it: colors(n_need,
+// kUnknownColor) (line 328), then std::transform of the response over its first entries
+// (357-358). The reference's server answers only non-empty crops
+// (scripts/color_classifier_server.py:83-84), so n_colors < n_need colours the first n_colors
+// cones in request order and leaves the rest unknown. colors == NULL is a failed call (every
+// colour unknown, 359-361). n_colors > n_need would write past the reference's vector: refused.
 extern "C" int cg_tracker_commit(cg_tracker* t, const int32_t* colors, uint32_t n_colors) {
     if (!t) return fail(CG_E_INVALID, "null argument");
     if (!t->matched) return fail(CG_E_INVALID, "cg_tracker_commit without cg_tracker_match");
     uint32_t need = 0;
     for (int32_t s : t->status) need += s == CG_TRACK_NEED_COLOR;
-    if (colors && n_colors != need) return fail(CG_E_INVALID, "one colour per centroid that needs one");
-    for (uint32_t k = 0; colors && k < n_colors; k++)
+    if (!colors) n_colors = 0;
+    if (n_colors > need) return fail(CG_E_INVALID, "more colours than centroids that need one");
+    for (uint32_t k = 0; k < n_colors; k++)
         if (colors[k] < 0 || colors[k] >= CG_NUM_COLORS) return fail(CG_E_INVALID, "colour out of range");
-    // a failed service call leaves every colour kUnknownColor (src/cone_detection.cpp:321,359)
     uint32_t k = 0;
     for (size_t c = 0; c < t->status.size(); c++) {
         if (t->status[c] != CG_TRACK_NEED_COLOR) continue;
-        const int colour = colors ? colors[k] : 0;
+        const int colour = k < n_colors ? colors[k] : 0;   // kUnknownColor past the response
         k++;
         t->clouds[colour].insert(t->clouds[colour].end(), {t->cur[2 * c], t->cur[2 * c + 1]});
     }

@@ -291,7 +291,9 @@ public:
                 cones.push_back(to_ros_msg(crop));
                 cones.back().header.frame_id = frame_id_;
             }
-            ok = service_ && service_(cones, colours) && colours.size() == n_need;
+            // the response may be shorter than the request (the reference's server skips empty
+            // crops); the tracker applies it positionally (src/cone_detection.cpp:328,357-358)
+            ok = service_ && service_(cones, colours);
         }
         tracker.commit(ok ? &colours : nullptr);
         std::array<PointCloud2, CG_NUM_COLORS> out;

@@ -283,9 +283,13 @@ int cg_batch_recrop(cg_handle* h, uint32_t frame, const float* centers_xy, uint3
  *                     use_points_buffer), a colour 0..3 (published in that cloud: colour known
  *                     from the previous frame, or 0 = unknown when classify_colors is off), or
  *                     CG_TRACK_NEED_COLOR (re-crop with cg_recrop and classify);
- *   cg_tracker_commit with the classifier's colours for the CG_TRACK_NEED_COLOR centroids in
- *                     order (NULL: the service call failed, all unknown); builds the clouds in
- *                     the reference's push order and rolls the previous-frame state.
+ *   cg_tracker_commit with the colour service's response for the CG_TRACK_NEED_COLOR
+ *                     centroids in request order: n_colors <= n_need colours, applied to the
+ *                     first n_colors of them, the rest unknown (src/cone_detection.cpp:328,
+ *                     357-358; the reference's server skips empty crops, so a response can be
+ *                     short); NULL: the service call failed, all unknown; more colours than
+ *                     n_need: CG_E_INVALID. Builds the clouds in the reference's push order
+ *                     and rolls the previous-frame state.
  * cg_tracker_cloud then returns colour cloud `color` as (x, y) pairs (z = 0, intensity = 0):
  * the points the node publishes on cones_topics[color] (src/cone_detection.cpp:46-49). */
 #define CG_NUM_COLORS        4     /* perception_handling::Color: unknown, yellow, blue, orange */

@@ -405,9 +405,13 @@ std::vector<Pt> whole_cloud(const View& v, int mode, const Params& prm) {
     return cloud;
 }
 
-// One colour per crop from the test's stand-in for the colour service; a negative answer
-// fails the whole (single) service call, leaving every colour unknown (lines 321, 359).
-typedef int (*ClassifyFn)(void* ctx, const float* xyzi, uint32_t n);
+// The colour service call (src/cone_detection.cpp:342-363): the request is every crop
+// (xyzi floats, crop k at offsets[k]..offsets[k+1]); the callback writes the response colours
+// (at most cap) and returns their count, or -1 for a failed call. The reference's server
+// answers only non-empty crops (scripts/color_classifier_server.py:83-84), so a response may
+// be shorter than the request; the test's restatement of the server decides that.
+typedef int (*ServiceFn)(void* ctx, const float* xyzi, const uint32_t* offsets, uint32_t n_crops, int32_t* colours,
+                         uint32_t cap);
 
 // ConeDetector's tracking state (src/cone_detection.cpp:60-63): null until the first frame.
 struct Node {
@@ -423,8 +427,8 @@ bool matches(const Node& nd, const Pt& a, const Pt& b) {
 
 // get_centroid_clouds (src/cone_detection.cpp:251-339) after the centroid arithmetic: the
 // centroids arrive in cluster order; clouds[i] receives what cones_pubs[i] publishes.
-void centroid_clouds(Node& nd, const std::vector<Pt>& whole, const float* cen, uint32_t n, ClassifyFn classify,
-                     void* ctx, std::vector<Pt> clouds[4]) {
+int centroid_clouds(Node& nd, const std::vector<Pt>& whole, const float* cen, uint32_t n, ServiceFn service,
+                    void* ctx, std::vector<Pt> clouds[4]) {
     auto current = std::make_unique<std::vector<Pt>>();
     std::vector<std::vector<Pt>> to_classify;
     std::vector<Pt> to_classify_centroids;
@@ -455,20 +459,31 @@ void centroid_clouds(Node& nd, const std::vector<Pt>& whole, const float* cen, u
         }
     }
     if (nd.classify_colors) {
-        std::vector<int> colours(to_classify.size(), 0);
-        bool ok = true;
-        std::vector<int> answer(to_classify.size(), 0);
-        for (size_t k = 0; k < to_classify.size(); k++) {
-            std::vector<float> xyzi;
-            for (const Pt& q : to_classify[k]) xyzi.insert(xyzi.end(), {q.x, q.y, q.z, q.intensity});
-            answer[k] = classify ? classify(ctx, xyzi.data(), (uint32_t)to_classify[k].size()) : -1;
-            ok = ok && answer[k] >= 0 && answer[k] < 4;
+        // colors(n, kUnknownColor) (line 328); a successful call overwrites the first
+        // len(response) entries in order, std::transform(resp.begin(), resp.end(), colors.begin())
+        // (357-358); a failed call leaves them all unknown (359-361)
+        const size_t n_req = to_classify.size();
+        std::vector<int> colours(n_req, 0);
+        std::vector<float> xyzi;
+        std::vector<uint32_t> offs(1, 0);
+        for (const std::vector<Pt>& crop : to_classify) {
+            for (const Pt& q : crop) xyzi.insert(xyzi.end(), {q.x, q.y, q.z, q.intensity});
+            offs.push_back((uint32_t)(xyzi.size() / 4));
         }
-        if (ok) colours = answer;
-        for (size_t k = 0; k < to_classify.size(); k++) clouds[colours[k]].push_back(to_classify_centroids[k]);
+        std::vector<int32_t> resp(n_req + 1, 0);
+        const int r = service ? service(ctx, xyzi.data(), offs.data(), (uint32_t)n_req, resp.data(),
+                                        (uint32_t)resp.size())
+                              : -1;
+        if (r > (int)n_req) return -1;   // writes past colors' end in the reference (UB)
+        for (int k = 0; k < r; k++) {
+            if (resp[k] < 0 || resp[k] >= 4) return -1;
+            colours[k] = resp[k];
+        }
+        for (size_t k = 0; k < n_req; k++) clouds[colours[k]].push_back(to_classify_centroids[k]);
     }
     for (int i = 0; i < 4; i++) nd.prev_clouds[i] = std::make_unique<std::vector<Pt>>(clouds[i]);
     nd.prev_detected = std::move(current);
+    return 0;
 }
 
 }  // namespace
@@ -512,11 +527,11 @@ void oracle_node_destroy(void* node) { delete (Node*)node; }
 // whole cloud (view, mode as oracle_recrop). counts[4] = points per colour cloud; xy holds
 // colour i's points at xy + i * cap * 2.
 int oracle_node_step(void* node, const void* params, const void* view, int mode, const float* centroids,
-                     uint32_t n, ClassifyFn classify, void* ctx, uint32_t* counts, float* xy, uint32_t cap) {
+                     uint32_t n, ServiceFn service, void* ctx, uint32_t* counts, float* xy, uint32_t cap) {
     const Params& prm = *(const Params*)params;
     const std::vector<Pt> whole = whole_cloud(*(const View*)view, mode, prm);
     std::vector<Pt> clouds[4];
-    centroid_clouds(*(Node*)node, whole, centroids, n, classify, ctx, clouds);
+    if (centroid_clouds(*(Node*)node, whole, centroids, n, service, ctx, clouds) != 0) return -1;
     for (int i = 0; i < 4; i++) {
         counts[i] = (uint32_t)clouds[i].size();
         for (size_t k = 0; k < clouds[i].size() && k < cap; k++) {

@@ -35,11 +35,12 @@ def lib():
         _lib.oracle_node_destroy.argtypes = [C.c_void_p]
         _lib.oracle_node_step.restype = C.c_int
         _lib.oracle_node_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_uint32,
-                                          CLASSIFY_FN, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+                                          SERVICE_FN, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     return _lib
 
 
-CLASSIFY_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_uint32)
+SERVICE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_uint32,
+                         C.POINTER(C.c_int32), C.c_uint32)
 
 
 def recrop(params, msg: PointCloud2, mode, centres, intensity_offset=None):
@@ -71,24 +72,44 @@ class Node:
             lib().oracle_node_destroy(self._n)
             self._n = None
 
-    def step(self, params, msg: PointCloud2, mode, centroids, classify, intensity_offset=None):
-        """classify(xyzi (n, 4) array) -> colour 0..3, or -1 to fail the frame's service call.
-        Returns the four colour clouds as (k, 2) arrays."""
+    def step(self, params, msg: PointCloud2, mode, centroids, service, intensity_offset=None):
+        """service(list of (n_k, 4) xyzi crops, request order) -> the response's colours (a list,
+        possibly shorter than the request), or None for a failed call. Returns the four colour
+        clouds as (k, 2) arrays."""
         v = msg.view(intensity_offset=intensity_offset)
         cen = np.ascontiguousarray(np.asarray(centroids, np.float32).reshape(-1, 2))
 
-        def cb(_ctx, ptr, n):
-            a = np.ctypeslib.as_array(ptr, (n * 4,)).reshape(n, 4).copy() if n else np.zeros((0, 4), np.float32)
-            return int(classify(a))
+        def cb(_ctx, ptr, offs, n, out, cap):
+            tot = offs[n] if n else 0
+            pts = np.ctypeslib.as_array(ptr, (tot * 4,)).reshape(tot, 4).copy() if tot else np.zeros((0, 4), np.float32)
+            crops = [pts[offs[k]:offs[k + 1]] for k in range(n)]
+            resp = service(crops)
+            if resp is None:
+                return -1
+            resp = [int(c) for c in resp]
+            if len(resp) > cap:
+                return cap
+            for k, c in enumerate(resp):
+                out[k] = c
+            return len(resp)
 
-        fn = CLASSIFY_FN(cb)
+        fn = SERVICE_FN(cb)
         cap = max(cen.shape[0], 1)
         counts = np.zeros(4, np.uint32)
         xy = np.zeros((4, cap, 2), np.float32)
-        lib().oracle_node_step(self._n, C.addressof(params), C.addressof(v), mode,
-                               cen.ctypes.data if cen.size else None, cen.shape[0], fn, None,
-                               counts.ctypes.data, xy.ctypes.data, cap)
+        rc = lib().oracle_node_step(self._n, C.addressof(params), C.addressof(v), mode,
+                                    cen.ctypes.data if cen.size else None, cen.shape[0], fn, None,
+                                    counts.ctypes.data, xy.ctypes.data, cap)
+        if rc != 0:
+            raise ValueError("colour service response longer than the request, or a colour out of range")
         return [xy[i, : counts[i]].copy() for i in range(4)]
+
+
+def server(crops, classify):
+    """The reference's service handler (scripts/color_classifier_server.py:81-124) around a
+    per-crop classifier: empty crops get no answer (`continue`, lines 83-84), so the response
+    lists the non-empty crops' colours in request order."""
+    return [int(classify(c)) for c in crops if len(c)]
 
 
 def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_STABLE, intensity_offset=None):

@@ -116,7 +116,7 @@ def test_node_matches_oracle_over_frames(params, fused, classify, buffer):
         assert all(m.header.get("frame_id") == "cloud" and m.point_step == 32 for m in msgs)
         if state["frame"] in failing:
             return None
-        return [_service(m.xyzi()) for m in msgs]
+        return [_service(m.xyzi()) for m in msgs if m.width]   # the server skips empty crops
 
     node = cp.ConeDetectorNode(params, classify_colors=classify, use_points_buffer=buffer, classifier=classifier,
                                fused_ground_removal=fused)
@@ -135,7 +135,8 @@ def test_node_matches_oracle_over_frames(params, fused, classify, buffer):
         msg.header = {"seq": f, "stamp_sec": 100 + f, "stamp_nsec": 123456789, "frame_id": "lidar"}
         outs = node.cloud_handler(msg)
         det, _ = O.run(params, msg, mode)
-        ref = ref_node.step(params, msg, mode, det.centroids, lambda c: -1 if f in failing else _service(c))
+        ref = ref_node.step(params, msg, mode, det.centroids,
+                            lambda crops: None if f in failing else O.server(crops, _service))
         assert len(outs) == 4
         for i, m in enumerate(outs):
             assert m.header == msg.header                                          # line 182
@@ -147,6 +148,45 @@ def test_node_matches_oracle_over_frames(params, fused, classify, buffer):
             published += m.width
     assert published > 0
     assert (state["asked"] > 0) == classify
+
+
+def _ring_and_cone():
+    """A ring of 16 points (radius 0.35 m around (5, 0)): one cluster whose pushed centroid
+    (5.05, 0) has no point within the re-crop box (half-width 0.228 / 1.5 m), so its crop is
+    empty; and a 6-point cone at (7, 1), a smaller cluster, so it is classified second."""
+    a = np.arange(16) * (2 * np.pi / 16)
+    ring = np.stack([5 + 0.35 * np.cos(a), 0.35 * np.sin(a), np.zeros(16), np.full(16, 40.0)], 1)
+    cone = np.array([[7.0, 1.0, 0.0], [7.05, 1.0, 0.1], [7.0, 1.05, 0.2], [6.95, 1.0, 0.1],
+                     [7.0, 0.95, 0.2], [7.02, 1.02, 0.3]])
+    cone = np.concatenate([cone, np.full((6, 1), 70.0)], 1)
+    return cp.PointCloud2.from_xyzi(np.concatenate([ring, cone]).astype(np.float32), layout=16)
+
+
+def test_node_short_colour_response_is_positional(params):
+    """The reference's server answers only non-empty crops (scripts/color_classifier_server.py:
+    83-84) and the node writes the response over colors(n_need, Unknown) from the front
+    (src/cone_detection.cpp:328,357-358). With the ring's empty crop first in the request, the
+    cone's colour lands on the ring's centroid and the cone stays unknown; GPU node = oracle."""
+    msg = _ring_and_cone()
+    requests = []
+
+    def classifier(msgs):
+        requests.append([m.width for m in msgs])
+        return [3 for m in msgs if m.width]
+
+    node = cp.ConeDetectorNode(params, classify_colors=True, use_points_buffer=False, classifier=classifier)
+    ref_node = O.Node(True, False, params.cones_matching_dist_theshold)
+    for f in range(2):
+        outs = node.cloud_handler(msg)
+        det, _ = O.run(params, msg, O.MODE_DETECT)
+        assert len(det.centroids) == 2
+        ref = ref_node.step(params, msg, O.MODE_DETECT, det.centroids, lambda crops: O.server(crops, lambda c: 3))
+        for i, m in enumerate(outs):
+            got = m.data.view(np.float32).reshape(-1, 8)[:, 0:2]
+            assert np.array_equal(got.view(np.uint32), ref[i].view(np.uint32)), (f, i)
+    assert requests == [[0, 6]]
+    ring_c, cone_c = det.centroids
+    assert ref[3].tolist() == [ring_c.tolist()] and ref[0].tolist() == [cone_c.tolist()]
 
 
 def test_ground_node_message_header_and_fields(params):

@@ -1,7 +1,9 @@
 """Tracking and colour clouds (ConeDetector::get_centroid_clouds, src/cone_detection.cpp:251-339):
 the C-ABI tracker (host code, no GPU) against the CPU restatement over random multi-frame
 centroid sequences, for every combination of classify_colors / use_points_buffer, with failed
-colour-service calls and matches exactly at the threshold.
+colour-service calls, short service responses (the reference's server skips empty crops,
+scripts/color_classifier_server.py:83-84, and the node applies the response positionally,
+src/cone_detection.cpp:328,357-358) and matches exactly at the threshold.
 
 The colour service stands in as a deterministic answer sequence: the k-th classification of
 the run gets colour k*7+3 mod 4, so both sides must ask for the same cones in the same order.
@@ -41,7 +43,14 @@ def _sequences(seed, frames=40):
     return out
 
 
-def _run_product(seq, classify, buffer, fail):
+def _answers(k, need, f, short):
+    """The service's response: one colour per request entry, or only the first half of them on
+    the `short` frames (as when the server skipped empty crops)."""
+    n = (need + 1) // 2 if f in short else need
+    return [(kk * 7 + 3) % 4 for kk in range(k, k + n)]
+
+
+def _run_product(seq, classify, buffer, fail, short=()):
     t = cp.ConeTracker(classify, buffer, 0.5)
     k = 0
     clouds = []
@@ -50,30 +59,28 @@ def _run_product(seq, classify, buffer, fail):
         assert st.shape == (len(cen),) and need == int((st == _abi.CG_TRACK_NEED_COLOR).sum())
         colours = None
         if need and f not in fail:
-            colours = [(kk * 7 + 3) % 4 for kk in range(k, k + need)]
+            colours = _answers(k, need, f, short)
             k += need
         t.commit(colours)
         clouds.append(t.clouds())
     return clouds
 
 
-def _run_oracle(seq, classify, buffer, fail):
+def _run_oracle(seq, classify, buffer, fail, short=()):
     params = cp.load_params("simulation")
     empty = cp.PointCloud2.from_xyzi(np.zeros((0, 4), np.float32))
     node = O.Node(classify, buffer, 0.5)
     state = {"k": 0}
     clouds = []
     for f, cen in enumerate(seq):
-        asked = []
-
-        def service(_crop):
+        def service(crops):
             if f in fail:
-                return -1
-            asked.append(1)
-            return ((state["k"] + len(asked) - 1) * 7 + 3) % 4
+                return None
+            r = _answers(state["k"], len(crops), f, short)
+            state["k"] += len(crops)
+            return r
 
         clouds.append(node.step(params, empty, O.MODE_DETECT, cen, service))
-        state["k"] += len(asked)
     return clouds
 
 
@@ -82,8 +89,9 @@ def _run_oracle(seq, classify, buffer, fail):
 def test_tracker_matches_restatement(classify, buffer, seed):
     seq = _sequences(seed)
     fail = {7, 19} if classify else set()
-    got = _run_product(seq, classify, buffer, fail)
-    ref = _run_oracle(seq, classify, buffer, fail)
+    short = {4, 9, 13, 22, 30} if classify else set()
+    got = _run_product(seq, classify, buffer, fail, short)
+    ref = _run_oracle(seq, classify, buffer, fail, short)
     published = 0
     for f, (g, r) in enumerate(zip(got, ref)):
         for i in range(4):
@@ -108,7 +116,7 @@ def test_commit_validates_colours():
     _, need = t.match([[1.0, 1.0], [2.0, 2.0]])
     assert need == 2
     with pytest.raises(_abi.CgError):
-        t.commit([1])                                      # one colour per cone that needs one
+        t.commit([1, 2, 3])                                # more colours than cones that need one
     with pytest.raises(_abi.CgError):
         t.commit([1, 4])                                   # out of range
     t.commit([cp.BLUE, cp.ORANGE])
@@ -116,3 +124,20 @@ def test_commit_validates_colours():
     assert len(c[cp.BLUE]) == 1 and len(c[cp.ORANGE]) == 1
     st, need = t.match([[1.0, 1.05], [2.0, 2.0], [5.0, 5.0]])   # colours known from last frame
     assert list(st) == [cp.BLUE, cp.ORANGE, _abi.CG_TRACK_NEED_COLOR] and need == 1
+
+
+def test_short_response_is_positional():
+    """A response of L < n_need colours colours the first L cones that need one, in request
+    order; the rest stay unknown (src/cone_detection.cpp:328,357-358). A response longer than
+    the request is refused (the reference would write past its colour vector)."""
+    t = cp.ConeTracker(True, False)
+    t.match([[3.0, 1.0], [4.0, -1.0], [6.0, 2.0]])
+    t.commit()
+    st, need = t.match([[3.0, 1.0], [4.0, -1.0], [6.0, 2.0]])
+    assert need == 3
+    t.commit([2])
+    c = t.clouds()
+    assert c[2].tolist() == [[3.0, 1.0]] and c[0].tolist() == [[4.0, -1.0], [6.0, 2.0]]
+    t.match([[9.0, 9.0]])
+    with pytest.raises(RuntimeError):
+        t.commit([1, 2])
