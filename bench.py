@@ -11,7 +11,12 @@ over ranks is reported.
 The roofline object prices the dominant (only) kernel, cg_frame_kernel, by its algorithmic
 bytes B = 16 N + 20 V + 8 C + 64 per frame over its average duration from
 HIP events recorded on the launch stream. cpu_baseline times the CPU restatement
-(oracle/, single core, same frames) on a bounded sample on rank 0.
+(oracle/, single core, same frames) on a bounded sample on rank 0 (any N).
+
+`--gpus N` without a launcher environment starts N ranks itself (torch.distributed.run on
+127.0.0.1, before any GPU call); under a launcher WORLD_SIZE must equal N. At N > 1 the C4
+composition (rank 0 scatters the batch over RCCL, gathers per-frame headers) is reported as
+`c4_scatter_gather` with its own xGMI roofline; `value` stays the frame-sharded rate.
 """
 import argparse
 import json
@@ -23,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBS = 153.0   # one xGMI link, one direction (7 links x ~153 GB/s per GPU)
+METRIC = "LiDAR frames/sec @64k pts/frame, 1/2/4/8 MI355X; cluster-set match vs PCL"
 
 
 def main():
@@ -58,15 +65,28 @@ def main():
     ap.add_argument("--streams", type=int, default=3,
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
+    ap.add_argument("--no-scatter", action="store_true", help="at N>1, skip the C4 scatter/gather leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="plumbing rehearsal without a GPU: launcher, gloo ranks, barrier + max-over-ranks "
+                         "timing and the JSON line (value null); used by the CPU tests")
     args = ap.parse_args()
+
+    # one process per GPU: a plain `bench.py --gpus N` (no launcher environment) starts the N
+    # ranks itself, as a child torch.distributed.run, before anything here touches the GPU
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, args.dry_run))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     import numpy as np
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; CG_DIST_BACKEND=gloo only rehearses the N>1 logic with several
     # ranks sharing one GPU (the driver's multi-GPU runs use RCCL)
     backend = os.environ.get("CG_DIST_BACKEND", "nccl")
@@ -163,7 +183,7 @@ def main():
                          around=lambda: [step(i) for i in range(1, S)], tag="loaded")
 
     scatter = None
-    if args.scatter and world > 1:
+    if world > 1 and (args.scatter or not args.no_scatter):
         scatter = scatter_composition(cp, cd, engines[0], streams[0], raw, F, N, dev, rank, world, args.steps)
 
     # C5's frame shape on this GPU: by default at N=1 (no collective involved; a failure is
@@ -197,12 +217,14 @@ def main():
         colornet = colornet_service(cp, params, raw, local)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:   # rank 0's own batch, timed on this box's host cores
         cpu = cpu_baseline(cp, params, raw, args.cpu_seconds, engines[0], args.cpu_threads)
+    if world > 1:   # the other ranks wait for rank 0's CPU leg
+        dist.barrier()
 
     if rank == 0:
         line = {
-            "metric": "LiDAR frames/sec @64k pts/frame, 1/2/4/8 MI355X; cluster-set match vs PCL",
+            "metric": METRIC,
             "value": fps,
             "unit": "frames/s",
             "n_gpus": world,
@@ -244,6 +266,75 @@ def main():
         if scatter is not None:
             line["c4_scatter_gather"] = scatter
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def launch_ranks(n, dry_run):
+    """Start `n` rank processes of this script under torch.distributed.run on this node
+    (rendezvous on 127.0.0.1) and return their exit code. Called before any GPU call."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    if dry_run:
+        env["CG_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd, env=env).returncode
+
+
+def host_info():
+    """CPU model, logical CPUs of the machine and of this process's affinity set."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
+
+
+def dry_run(args, world, rank):
+    """The launcher and reporting path without device work: gloo ranks, barrier, a timed
+    host loop, max over ranks, rank 0's JSON line with value null."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.zeros(1)
+    for _ in range(args.warmup):
+        t += 1
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        t += 1
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        m = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        el = float(m.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": el / max(args.steps, 1) * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "none (dry run)",
+                          "dry_run": True, "ranks_seen": world, "host": host_info(),
+                          "config": {"workload": "dry run: no device work", "parallelism": f"frame-shard x{world}"}}),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -361,7 +452,14 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
     torch.cuda.synchronize(dev)
     dist.barrier()
     el = cd.max_over_ranks(time.perf_counter() - t0, dev)
+    # the root's egress: every peer's share of the batch leaves over that peer's direct link
+    egress = float(F * (world - 1) * raw.shape[1])
+    ach = egress / (el / steps) / 1e9
+    peak = XGMI_LINK_GBS * min(world - 1, 7)
     return {"frames_per_s": F * world * steps / el, "ms_per_step": el / steps * 1e3,
+            "roofline": {"bound": "xgmi", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
+                         "bytes_per_step": egress,
+                         "peak_basis": f"root egress over {min(world - 1, 7)} direct xGMI links x {XGMI_LINK_GBS} GB/s"},
             "includes": "RCCL scatter of the batch from rank 0, processing, gather of headers"}
 
 
@@ -534,7 +632,7 @@ def cpu_baseline(cp, params, raw, budget_s, eng, threads):
         el = time.perf_counter() - t0
         if el >= budget_s and n >= 20:
             break
-    out = {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+    out = {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port", "host": host_info(),
            "sample": f"{n} frames of this bench's 64k-point synthetic batch (cycling over its "
                      f"first {min(n, F)}), sequential, {el:.1f} s, oracle/cg_oracle.cpp "
                      "(g++ -O2 -ffp-contract=off)"}

@@ -234,6 +234,9 @@ void free_batch(cg_handle* h) {
 }
 
 int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
+    // every caller writes (or reallocates) the per-frame result slots: cg_batch_recrop may
+    // read them again only after the next cg_run_batch (which sets batch_valid afterwards)
+    h->batch_valid = false;
     const uint32_t pts = std::max<uint32_t>(points, 1);
     const bool need_ground = ground && h->d_ground == nullptr;
     if (frames <= h->cap_frames && pts <= h->cap_points && !need_ground) return CG_OK;

@@ -388,7 +388,7 @@ __device__ __forceinline__ uint32_t lg_lookback(uint32_t* st, uint32_t t, uint32
     uint32_t* ts = st + 2;
     const uint32_t l = lane_id();
     if (t == 0) {
-        if (l == 0) __hip_atomic_store(&ts[0], LG_ST_P | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0) __hip_atomic_store(&ts[0], LG_ST_P | count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
     if (l == 0) __hip_atomic_store(&ts[t], LG_ST_A | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -407,18 +407,22 @@ __device__ __forceinline__ uint32_t lg_lookback(uint32_t* st, uint32_t t, uint32
         if (first < 64u) break;
         hi -= 64;
     }
-    if (l == 0) __hip_atomic_store(&ts[t], LG_ST_P | (base + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l == 0) __hip_atomic_store(&ts[t], LG_ST_P | (base + count), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     return base;
 }
 // Every thread of the block, after its look-back: the last tile resets the status words.
 __device__ __forceinline__ void lg_tile_done(uint32_t* st, uint32_t active) {
     __shared__ uint32_t last;
     __syncthreads();
+    // release: this tile's status word (published above) is ordered before its count; the
+    // last tile's acquire sees every tile's final word before it zeroes them
     if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(&st[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
+        last = __hip_atomic_fetch_add(&st[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
     __syncthreads();
-    if (last)
+    if (last) {
+        __threadfence();
         for (uint32_t i = threadIdx.x; i < active + 2; i += CG_BLOCK) st[i] = 0;
+    }
 }
 // Block-wide: this tile's eight-per-thread counts c -> each thread's exclusive position;
 // returns through tot_out the device-wide total when this is the last active tile.

@@ -72,3 +72,30 @@ def test_sharded_batch_equals_single_rank(tmp_path):
     single = _headers(cp.synth_frames(ws * F, first_frame=0, rings=RINGS, cols=COLS))
     assert np.array_equal(gathered, single)
     assert tmax == ws
+
+
+def _bench(args, env=None):
+    import json
+    import subprocess
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=e)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher environment starts two ranks itself (gloo in the
+    dry run) and reports n_gpus 2 from rank 0, after a barrier and the max over ranks."""
+    rc, line, err = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["dry_run"] is True
+    assert line["config"]["parallelism"] == "frame-shard x2"
+
+
+def test_bench_refuses_mismatched_world_size():
+    rc, line, err = _bench(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc != 0 and line is None and "WORLD_SIZE=1" in err

@@ -259,3 +259,26 @@ def test_batch_recrop_matches_oracle(params, mode, rings):
         ref = O.recrop(params, cp.frame_cloud(raw[f]), om, cen)
         _same_crops(got, ref, f"batch {mode} frame {f}")
         assert sum(len(c) for c in got) > 0
+
+
+@pytest.mark.gpu
+def test_batch_recrop_refused_after_single_frame_call(params):
+    """A single-frame call on a batch engine's handle rewrites frame 0's result slots, so a
+    cg_batch_recrop of the earlier batch must fail (CG_E_INVALID), not crop with mixed state."""
+    import ctypes
+    import torch
+    raw = cp.synth_frames(2, first_frame=9, rings=64, cols=1024)
+    d = torch.from_numpy(raw).to(torch.device("cuda", 0))
+    eng = cp.BatchEngine(params, device=0)
+    eng.run(d.data_ptr(), 2, 64 * 1024, 16)
+    cen = _centres(eng.fetch(0), np.random.default_rng(3))
+    eng.recrop(0, cen)   # valid right after the batch
+    msg = cp.frame_cloud(raw[1])   # keeps the bytes the view points at alive
+    v = msg.view(intensity_offset=12)
+    r = _abi.cg_detect_result()
+    _abi.check(cp.lib().cg_pipeline(eng.handle, ctypes.byref(v), ctypes.byref(r)))
+    with pytest.raises(_abi.CgError):
+        eng.recrop(0, cen)
+    eng.run(d.data_ptr(), 2, 64 * 1024, 16)   # a new batch makes it valid again
+    got = eng.recrop(1, cen)
+    _same_crops(got, O.recrop(params, cp.frame_cloud(raw[1]), O.MODE_PIPELINE, cen), "after re-run")

@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit; the bench only runs when the tests pass.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -3 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
