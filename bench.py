@@ -66,6 +66,9 @@ def main():
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
     ap.add_argument("--no-scatter", action="store_true", help="at N>1, skip the C4 scatter/gather leg")
+    ap.add_argument("--voxel-order", choices=["pcl", "point"], default="pcl",
+                    help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
+                         "every voxel bit as the reference) or ascending point order")
     ap.add_argument("--dry-run", action="store_true",
                     help="plumbing rehearsal without a GPU: launcher, gloo ranks, barrier + max-over-ranks "
                          "timing and the JSON line (value null); used by the CPU tests")
@@ -112,7 +115,8 @@ def main():
     d_ins = [torch.from_numpy(raw).to(dev) for _ in range(S)]
     # one engine (own output buffers) per stream; dedicated streams: the default stream's
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
-    engines = [cp.BatchEngine(params, device=local) for _ in range(S)]
+    vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
+    engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
     assert all(st.cuda_stream != 0 for st in streams)
     eng, stream = engines[0], streams[0]
@@ -191,7 +195,7 @@ def main():
     c5 = None
     if rank == 0 and (args.c5 or (world == 1 and not args.no_c5)):
         try:
-            c5 = c5_single_gpu(cp, params, local)
+            c5 = c5_single_gpu(cp, params, local, order=vorder)
         except Exception as e:  # noqa: BLE001
             c5 = {"error": repr(e)}
 
@@ -203,7 +207,7 @@ def main():
     single = None
     if rank == 0 and (args.single_frame or world == 1):   # C2: the ROS node's synchronous call
         try:
-            single = single_frame_latency(cp, params, raw, local)
+            single = single_frame_latency(cp, params, raw, local, order=vorder)
         except Exception as e:  # noqa: BLE001
             single = {"error": repr(e)}
     pcie = None
@@ -239,7 +243,8 @@ def main():
             "config": {"workload": f"C3/C4: {F} frames x {N} pts per GPU per step (xyzi f32, "
                                    "simulation params), ground_removal + cone_detection fused",
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
-                       "parallelism": f"frame-shard x{world}", "streams_per_gpu": S},
+                       "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
+                       "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),
                          "kernel": "cg_frame_kernel", "avg_kernel_ms": avg_kernel_ms,
@@ -463,13 +468,15 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
             "includes": "RCCL scatter of the batch from rank 0, processing, gather of headers"}
 
 
-def c5_single_gpu(cp, params, device, reps=50):
+def c5_single_gpu(cp, params, device, reps=50, order=None):
     """C5's frame shape on one GPU, device-resident: one 1M-point dense frame per call of the
     batch engine (large-frame path; the call synchronises once the frame is done)."""
     import torch
     raw = cp.synth_frames(1, first_frame=0, rings=128, cols=8192, clutter=60, cones_per_row=12)
     d = torch.from_numpy(raw).to(torch.device("cuda", device))
     eng = cp.BatchEngine(params, device=device)
+    if order is not None:
+        eng.set_voxel_order(order)
     st = torch.cuda.Stream(torch.device("cuda", device))
     n = raw.shape[1] // 16
     for _ in range(5):
@@ -592,9 +599,11 @@ def colornet_service(cp, params, raw, device, frames=16, reps=50):
             "includes": "host clouds -> H2D, one workgroup per cone (to_image + dam_net), colours D2H"}
 
 
-def single_frame_latency(cp, params, raw, device, reps=200):
+def single_frame_latency(cp, params, raw, device, reps=200, order=None):
     """C2: one 64k frame through the synchronous ROS drop-in call (H2D + kernel + D2H)."""
     pipe = cp.ConePipeline(params, device=device)
+    if order is not None:
+        pipe.set_voxel_order(order)
     msg = cp.frame_cloud(raw[0])
     for _ in range(10):
         pipe.cloud_handler(msg)

@@ -17,7 +17,8 @@ from typing import List, Optional
 import numpy as np
 
 from . import _abi
-from ._abi import (CG_MODE_DETECT, CG_MODE_PIPELINE, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL,
+from ._abi import (CG_VOXEL_ORDER_PCL, CG_VOXEL_ORDER_POINT, CG_F_VOXEL_POINT_ORDER,  # noqa: F401
+                   CG_MODE_DETECT, CG_MODE_PIPELINE, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL,
                    CG_F_VOXEL_PASSTHROUGH, CgError, check, lib)
 
 lib()   # fail loudly at import if the gfx950 library is missing
@@ -212,6 +213,12 @@ class _Handle:
     @property
     def handle(self):
         return self._h
+
+    def set_voxel_order(self, order: int):
+        """CG_VOXEL_ORDER_PCL (default): each voxel's float sums in PCL's std::sort order, every
+        voxel bit as the reference; CG_VOXEL_ORDER_POINT: in ascending point order."""
+        check(lib().cg_set_voxel_order(self._h, order))
+        return self
 
     def debug_route(self, route: int):
         """Diagnostics: 1 = every frame through the large-frame path, 2 = also its global

@@ -12,7 +12,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CONES_GPU_LIB") or os.path.join(_HERE, "lib", "libcones_gpu.so")
 
 CG_OK, CG_E_INVALID, CG_E_DEVICE, CG_E_OOM, CG_E_CAPACITY = 0, 1, 2, 3, 4
-CG_F_VOXEL_PASSTHROUGH, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL = 0x1, 0x2, 0x4
+CG_F_VOXEL_PASSTHROUGH, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL, CG_F_VOXEL_POINT_ORDER = 0x1, 0x2, 0x4, 0x8
+CG_VOXEL_ORDER_POINT, CG_VOXEL_ORDER_PCL = 0, 1
 CG_MODE_PIPELINE, CG_MODE_DETECT = 0, 1
 CG_HDR_N, CG_HDR_K, CG_HDR_M, CG_HDR_V, CG_HDR_C, CG_HDR_FLAGS, CG_HDR_WORDS = 0, 1, 2, 3, 4, 5, 8
 
@@ -127,6 +128,7 @@ _SIGS = {
     "cg_create": (C.c_int, [C.POINTER(cg_params), C.c_int, C.POINTER(C.c_void_p)]),
     "cg_destroy": (C.c_int, [C.c_void_p]),
     "cg_set_params": (C.c_int, [C.c_void_p, C.POINTER(cg_params)]),
+    "cg_set_voxel_order": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_last_error": (C.c_char_p, []),
     "cg_version": (C.c_char_p, []),
     "cg_ground_remove": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_ground_result)]),

@@ -18,7 +18,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
-HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h", "cg_device.h")] + \
+HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h", "cg_device.h", "cg_pcl.h")] + \
           [os.path.join(ROOT, "include", "cones_gpu.h")]
 
 

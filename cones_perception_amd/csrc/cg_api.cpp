@@ -579,6 +579,7 @@ int cg_create(const cg_params* params, int device, cg_handle** out) {
     CgDevParams dp;
     int rc = prepare(p, dp);
     if (rc) return rc;
+    dp.voxel_order = CG_VOXEL_ORDER_PCL;
     HIPCHK(hipSetDevice(device));
     cg_handle* h = new cg_handle();
     h->device = device;
@@ -618,8 +619,17 @@ int cg_set_params(cg_handle* h, const cg_params* params) {
     CgDevParams dp;
     int rc = prepare(*params, dp);
     if (rc) return rc;
+    dp.voxel_order = h->dp.voxel_order;
     h->params = *params;
     h->dp = dp;
+    return CG_OK;
+}
+
+int cg_set_voxel_order(cg_handle* h, int order) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    if (order != CG_VOXEL_ORDER_POINT && order != CG_VOXEL_ORDER_PCL)
+        return fail(CG_E_INVALID, "unknown voxel order %d", order);
+    h->dp.voxel_order = order;
     return CG_OK;
 }
 

@@ -34,6 +34,9 @@ struct CgDevParams {
     // CG_RAY_WEDGE_PAD) lies on one side of the angle filter; ray_arm: those it removes.
     float4 ray[17];
     uint32_t ray_filter_ok, ray_arm;
+    // voxel summation order (cg_set_voxel_order): CG_VOXEL_ORDER_PCL = PCL's std::sort
+    // permutation (cg_pcl.h), CG_VOXEL_ORDER_POINT = ascending point index
+    int32_t voxel_order;
 };
 
 // Sets the thread-local message cg_last_error returns; returns code.
@@ -124,6 +127,7 @@ enum {
     LG_MINB, LG_MUL1 = LG_MINB + 3, LG_MUL2, LG_ORG, LG_NFIN_ALL = LG_ORG + 3, LG_SCAN_N,
     LG_DGINV, LG_DGN = LG_DGINV + 3, LG_NCELL = LG_DGN + 3,   // dense neighbour grid
     LG_SORT_LIM,               // cluster-order sort: key bits in use (digits past it are skipped)
+    LG_PCL_N,                  // PCL voxel order: finite points in index_vector (compaction total)
     LG_META_WORDS = 64
 };
 struct LgScratch {
@@ -144,6 +148,8 @@ struct LgScratch {
     uint32_t* hmeta;          // pinned host copy of the meta words (the one round trip per frame)
     uint32_t* cstat;          // per-chunk statistics [chunk][LG_CS_WORDS], reduced into meta by
                               // one workgroup (same-address atomics from every chunk serialise)
+    uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
+    uint32_t pq_cap;          //   entries
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };

@@ -32,6 +32,7 @@
 #include "cg_math.h"
 #include "cg_sort.h"
 #include "cg_device.h"
+#include "cg_pcl.h"
 
 #define CG_BRUTE_V 256        // voxel count up to which clustering tests all pairs
 
@@ -80,10 +81,6 @@ enum {
 };
 
 
-struct Work {
-    float4* P; uint64_t* KEY; float4* VOX; uint32_t* A; uint32_t* PAR; uint32_t* CNT;
-    uint32_t* UK; int32_t* LAB; uint32_t* ORD; uint32_t* IDX; uint32_t* OFF;
-};
 
 uint64_t cg_scratch_bytes(uint32_t n) {
     uint64_t n2 = 1; while (n2 < n) n2 <<= 1;
@@ -168,34 +165,46 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         const float mnb0 = (float)(int)fs->scal[S_MINB0], mnb1 = (float)(int)fs->scal[S_MINB1],
                     mnb2 = (float)(int)fs->scal[S_MINB2];
         const uint32_t mul1 = fs->scal[S_MUL1], mul2 = fs->scal[S_MUL2];
-        // keys (idx << 32 | point index << 16 | slot): unique, so any sort yields PCL's idx
-        // order with ties in point order. Non-finite points get idx 0xffffffff (beyond every
-        // real idx, which the overflow guard keeps below 2^31) and sort last.
-        auto voxel_key = [&](uint32_t j) -> uint64_t {
-            const float4 p = W.P[j];
-            const uint64_t lowbits = ((uint64_t)(W.IDX[j] & 0xffffu) << 16) | j;
-            if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return (0xffffffffull << 32) | lowbits;
+        const uint32_t Mf = fs->scal[S_MF];
+        auto voxel_idx = [&](const float4& p) -> uint32_t {
             const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
             const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
             const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
-            const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
-            return ((uint64_t)idx << 32) | lowbits;
+            return (uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2;
         };
-        if (M <= CG_RANK_SORT_MAX) {
-            uint64_t* tmp = (uint64_t*)W.VOX;      // VOX is free until the centroids
-            for (uint32_t j = tid; j < M; j += CG_BLOCK) tmp[j] = voxel_key(j);
-            __syncthreads();
+        if (P.voxel_order == CG_VOXEL_ORDER_PCL) {
+            // index_vector in cloud order (VOX is free until the centroids), then std::sort's
+            // permutation of it into KEY (cg_pcl.h)
+            uint64_t* E = (uint64_t*)W.VOX;
+            pcl_index_vector(W, M, fs->scal[S_MS], E, red, [&](uint32_t j) -> uint32_t { return voxel_idx(W.P[j]); });
             STAMP(7);
-            rank_sort(tmp, W.KEY, M);
+            pcl_sort(W, E, Mf, red);
         } else {
-            uint32_t n2 = 1;
-            while (n2 < M) n2 <<= 1;
-            for (uint32_t j = tid; j < n2; j += CG_BLOCK) W.KEY[j] = j < M ? voxel_key(j) : ~0ull;
-            __syncthreads();
-            STAMP(7);
-            bitonic_sort(W.KEY, n2);
+            // keys (idx << 32 | point index << 16 | slot): unique, so any sort yields PCL's idx
+            // order with ties in point order. Non-finite points get idx 0xffffffff (beyond every
+            // real idx, which the overflow guard keeps below 2^31) and sort last.
+            flags |= CG_F_VOXEL_POINT_ORDER;
+            auto voxel_key = [&](uint32_t j) -> uint64_t {
+                const float4 p = W.P[j];
+                const uint64_t lowbits = ((uint64_t)(W.IDX[j] & 0xffffu) << 16) | j;
+                if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) return (0xffffffffull << 32) | lowbits;
+                return ((uint64_t)voxel_idx(p) << 32) | lowbits;
+            };
+            if (M <= CG_RANK_SORT_MAX) {
+                uint64_t* tmp = (uint64_t*)W.VOX;      // VOX is free until the centroids
+                for (uint32_t j = tid; j < M; j += CG_BLOCK) tmp[j] = voxel_key(j);
+                __syncthreads();
+                STAMP(7);
+                rank_sort(tmp, W.KEY, M);
+            } else {
+                uint32_t n2 = 1;
+                while (n2 < M) n2 <<= 1;
+                for (uint32_t j = tid; j < n2; j += CG_BLOCK) W.KEY[j] = j < M ? voxel_key(j) : ~0ull;
+                __syncthreads();
+                STAMP(7);
+                bitonic_sort(W.KEY, n2);
+            }
         }
-        const uint32_t Mf = fs->scal[S_MF];
         STAMP(8);
         V = block_scan(
             Mf,
@@ -957,6 +966,7 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void cg_lg_back_small(CgLaunch L, CgDe
         bl->P[Ms + j] = make_float4(0.f, 0.f, 0.f, 0.f);
         bl->IDX[Ms + j] = 0xffffu;   // after every kept point
     }
+    if (tid == 0) fs->scal[S_MS] = Ms;   // kept survivors (slots [0, Ms)); pads follow
     __syncthreads();
     Work W;
     W.P = bl->P; W.KEY = bl->KEY; W.VOX = bl->VOX; W.A = bl->A; W.PAR = bl->PAR; W.CNT = bl->CNT;

@@ -23,11 +23,14 @@
 // Every sum keeps the reference's order (PCL sorts by idx; ties in point order here, as in
 // the frame kernel), so results are bit-identical to the frame kernel's on the same input.
 #include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
 #include "cg_internal.h"
 #include "../../include/cones_gpu.h"
 #include "cg_math.h"
 #include "cg_sort.h"
 #include "cg_device.h"
+#include "cg_pcl.h"
 
 #define LG_TILE 4096   // elements per scan / sort workgroup (512 threads x 8)
 
@@ -766,6 +769,186 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 }
 
 // ------------------------------------------------------------------------------------------
+// PCL's voxel order for the global backend (cg_pcl.h has the algorithm). index_vector is the
+// finite detector-input points in frame-index order; lg_scan_emit lists them as records
+// (idx << 32 | slot) (PclCompact*), then libstdc++'s introsort runs on them level by level:
+// lg_pcl_level partitions every range of the level longer than LG_PCL_LEAF with one workgroup
+// in HBM (median of three, the parallel Hoare partition: per-wave segment counts, the L and R
+// lists, the swaps), and lg_pcl_leaf finishes each remaining range with pcl_sort, in LDS when
+// it fits, with the depth left on its path, writing (idx, slot) pairs in std::sort's order.
+// Ranges are disjoint, so their order inside a level does not matter; the levels are separate
+// launches (no workgroup waits on another).
+#define LG_PCL_LEAF 2048
+#define LG_PQ_HDR 8            // list counts (four used)
+struct PclCompactFlag {   // finite points (non-finite keys carry idx 0xffffffff)
+    const uint64_t* key; uint32_t PB;
+    __device__ uint32_t operator()(uint32_t j) const { return (uint32_t)(key[j] >> PB) != 0xffffffffu ? 1u : 0u; }
+};
+struct PclCompactEmit {
+    const uint64_t* key; const uint32_t* val; uint64_t* E; uint32_t PB;
+    __device__ void operator()(uint32_t j, uint32_t r) const {
+        E[r] = ((uint64_t)(uint32_t)(key[j] >> PB) << 32) | val[j];
+    }
+};
+
+// Bytes of LDS for a leaf: E and KEY (8 B), seven word arrays (n + 4 each)
+#define LG_PCL_LDS (2 * 8 * LG_PCL_LEAF + 7 * 4 * (LG_PCL_LEAF + 4))
+
+__device__ __forceinline__ uint32_t pq_key(const uint64_t* E, uint32_t x) {
+    return ((const uint32_t*)E)[2 * x + 1];
+}
+// One workgroup: __unguarded_partition(first + 1, last, pivot = first) after the median of
+// three, over E in HBM; PL / PR hold the L and R lists. Returns the cut (all threads).
+__device__ uint32_t lg_pcl_partition(uint64_t* E, uint32_t* PL, uint32_t* PR, uint32_t first, uint32_t last) {
+    __shared__ uint32_t sh[4 * WAVES + 4];
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    if (tid == 0) {
+        cg_move_median_to_first(E, (long)first, (long)first + 1, (long)(first + (last - first) / 2), (long)last - 1,
+                                [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
+        sh[4 * WAVES] = pq_key(E, first);
+        sh[4 * WAVES + 1] = 0u;
+    }
+    __syncthreads();
+    const uint32_t p = sh[4 * WAVES];
+    const uint32_t a = first + 1, m = last - a;
+    const uint32_t seg = ((m + WAVES - 1) / WAVES + 63u) & ~63u;   // each wave: a contiguous segment
+    const uint32_t s0 = min(a + w * seg, last), s1 = min(s0 + seg, last);
+    uint32_t cge = 0, cle = 0;
+    for (uint32_t x0 = s0; x0 < s1; x0 += 256) {   // four strips of 64 in flight
+        uint32_t k[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) { const uint32_t x = x0 + 64 * q + l; k[q] = x < s1 ? pq_key(E, x) : 0u; }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool in = x0 + 64 * q + l < s1;
+            cge += (uint32_t)__popcll(__ballot(in && k[q] >= p));
+            cle += (uint32_t)__popcll(__ballot(in && k[q] <= p));
+        }
+    }
+    if (l == 0) { sh[w] = cge; sh[WAVES + w] = cle; }
+    __syncthreads();
+    uint32_t bge = 0, ble = 0, nL = 0, nR = 0;
+    for (uint32_t v = 0; v < WAVES; v++) {
+        bge += v < w ? sh[v] : 0u;
+        ble += v < w ? sh[WAVES + v] : 0u;
+        nL += sh[v];
+        nR += sh[WAVES + v];
+    }
+    for (uint32_t x0 = s0; x0 < s1; x0 += 64) {
+        const uint32_t x = x0 + l;
+        const uint32_t k = x < s1 ? pq_key(E, x) : 0u;
+        const uint64_t ge = __ballot(x < s1 && k >= p), le = __ballot(x < s1 && k <= p);
+        if (x < s1 && k >= p) PL[a + bge + mbcnt(ge)] = x;
+        if (x < s1 && k <= p) PR[a + (nR - 1u - (ble + mbcnt(le)))] = x;
+        bge += (uint32_t)__popcll(ge);
+        ble += (uint32_t)__popcll(le);
+    }
+    __syncthreads();
+    // swaps (L_k, R_k) while L_k < R_k (a prefix of k): count them, swap in parallel
+    const uint32_t m2 = min(nL, nR);
+    uint32_t cnt = 0;
+    for (uint32_t k = tid; k < m2; k += CG_BLOCK) {
+        const uint32_t i = PL[a + k], j = PR[a + k];
+        if (i < j) {
+            const uint64_t t = E[i];
+            E[i] = E[j];
+            E[j] = t;
+            cnt++;
+        }
+    }
+    cnt = wave_sum(cnt);
+    if (l == 0 && cnt) atomicAdd(&sh[4 * WAVES + 1], cnt);
+    __syncthreads();
+    const uint32_t sw = sh[4 * WAVES + 1];
+    const uint32_t cut = sw == 0 ? PL[a] : min(sw < nL ? PL[a + sw] : 0xffffffffu, PR[a + sw - 1]);
+    __syncthreads();
+    return cut;
+}
+
+// Range lists of the level-synchronous sort (S.pq): four counts, then four lists of
+// (first, last, depth) triples, S.pq_cap entries each. Level lv partitions the ranges of list
+// lv % 3, queues the parts on list (lv + 1) % 3 and clears list (lv + 2) % 3 for the level
+// after it; list 3 collects the leaves.
+#define PQ_LEAF 3
+__device__ __forceinline__ uint32_t* pq_list(const LgScratch& S, uint32_t which) {
+    return S.pq + LG_PQ_HDR + (uint64_t)which * 3 * S.pq_cap;
+}
+__device__ __forceinline__ void pq_push(const LgScratch& S, uint32_t which, uint32_t first, uint32_t last, uint32_t depth) {
+    const uint32_t i = atomicAdd(&S.pq[which], 1u);
+    if (i < S.pq_cap) {
+        uint32_t* e = pq_list(S, which) + 3 * i;
+        e[0] = first; e[1] = last; e[2] = depth;
+    }
+}
+// One level of __introsort_loop: workgroup b partitions range b of the level's list (level 0:
+// the whole index_vector). Parts longer than LG_PCL_LEAF with depth left are queued for the
+// next level (leaves after the last level); the others, and every range whose depth budget
+// is spent (pcl_sort runs the heapsort fallback), are leaves.
+__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_level(LgScratch S, uint64_t* E, uint32_t level, uint32_t last_level) {
+    const uint32_t cur = level % 3u, nxt = (level + 1u) % 3u;
+    uint32_t first, last, depth;
+    if (level == 0) {
+        if (blockIdx.x) return;
+        first = 0; last = S.meta[LG_PCL_N]; depth = (uint32_t)(2 * cg_lg((long)last));
+        if (threadIdx.x == 0) { S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAF] = 0; }
+        if (last <= LG_PCL_LEAF || depth == 0) {
+            if (threadIdx.x == 0) pq_push(S, PQ_LEAF, first, last, depth);
+            return;
+        }
+    } else {
+        if (blockIdx.x == 0 && threadIdx.x == 0) S.pq[(level + 2u) % 3u] = 0;
+        const uint32_t n = min(S.pq[cur], S.pq_cap);
+        if (blockIdx.x >= n) return;
+        const uint32_t* e = pq_list(S, cur) + 3 * blockIdx.x;
+        first = e[0]; last = e[1]; depth = e[2];
+    }
+    const uint32_t cut = lg_pcl_partition(E, S.par, S.cnt, first, last);
+    if (threadIdx.x == 0) {
+        for (int c = 0; c < 2; c++) {
+            const uint32_t f = c ? cut : first, l = c ? last : cut, d = depth - 1u;
+            pq_push(S, (l - f > LG_PCL_LEAF && d > 0 && level < last_level) ? nxt : PQ_LEAF, f, l, d);
+        }
+    }
+}
+// The rest of each leaf range (cg_pcl.h pcl_sort with the depth left on its path): in LDS
+// when it fits, else in HBM (ranges are disjoint, so each uses its own span of the scratch
+// arrays); out as (idx, slot) pairs in std::sort's order.
+__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E, uint64_t* kout, uint32_t* vout) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PCL_LDS];
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t n = min(S.pq[PQ_LEAF], S.pq_cap);
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const uint32_t* e = pq_list(S, PQ_LEAF) + 3 * b;
+        const uint32_t first = e[0], last = e[1], depth = e[2], size = last - first;
+        Work W{};
+        uint64_t* El;
+        if (size <= LG_PCL_LEAF) {
+            El = (uint64_t*)smem;
+            uint32_t* w0 = (uint32_t*)(El + 2 * LG_PCL_LEAF);
+            W.KEY = El + LG_PCL_LEAF;
+            W.A = w0; W.PAR = w0 + (LG_PCL_LEAF + 4); W.CNT = w0 + 2 * (LG_PCL_LEAF + 4);
+            W.UK = w0 + 3 * (LG_PCL_LEAF + 4); W.ORD = w0 + 4 * (LG_PCL_LEAF + 4);
+            W.LAB = (int32_t*)(w0 + 5 * (LG_PCL_LEAF + 4)); W.OFF = w0 + 6 * (LG_PCL_LEAF + 4);
+            for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
+            __syncthreads();
+        } else {   // the range's own span of the HBM arrays (A needs size + 1: first + size <= N)
+            El = E + first;
+            W.KEY = (uint64_t*)S.vox + 2ull * first;
+            W.A = S.lab + first; W.PAR = S.par + first; W.CNT = S.cnt + first; W.UK = S.uk + first;
+            W.ORD = S.ord + first; W.LAB = (int32_t*)S.rank + first; W.OFF = S.off + first;
+        }
+        pcl_sort(W, El, size, red, (int)depth);
+        for (uint32_t i = tid; i < size; i += CG_BLOCK) {
+            const uint64_t r = W.KEY[i];
+            kout[first + i] = r >> 32;
+            vout[first + i] = (uint32_t)r;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Euclidean clustering over the V voxels (FLANN L2_Simple predicate, PCL's seed = the lowest
 // index of each component):
 //   dense neighbour grid: voxel -> cell (atomic slot), exclusive scan of the cell counts,
@@ -1043,8 +1226,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, u
 }
 // CSR indices (ascending voxel index inside each cluster), per-cluster centroid + radial push
 // (src/cone_detection.cpp:261-279), offsets and the frame header
-__device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const LgScratch& S, uint32_t f, uint32_t VB, int buf,
-                                           uint32_t Mtot, uint32_t K, uint32_t b) {
+__device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
+                                           uint32_t VB, int buf, uint32_t Mtot, uint32_t K, uint32_t b) {
     const uint32_t i = b * CG_BLOCK + threadIdx.x;
     const uint32_t* m = S.meta;
     const uint32_t C = m[LG_C], tot = C ? S.off[C] : 0u;
@@ -1058,7 +1241,8 @@ __device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const LgScratch& S
         h[CG_HDR_M] = Mtot;
         h[CG_HDR_V] = m[LG_V];
         h[CG_HDR_C] = C;
-        h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u);
+        h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
+                          (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
     }
 }
 __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S,
@@ -1106,7 +1290,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
                                                              uint32_t VB, int buf, uint32_t Mtot, uint32_t K,
                                                              uint32_t cb) {
     if (blockIdx.x < cb) {
-        lg_csr_one(L, S, f, VB, buf, Mtot, K, blockIdx.x);
+        lg_csr_one(L, P, S, f, VB, buf, Mtot, K, blockIdx.x);
         return;
     }
     const uint64_t* key = buf ? S.key1 : S.key0;
@@ -1232,10 +1416,33 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
         key_bits = std::min<uint32_t>(key_bits, 32 + PB);
     }
     hipLaunchKernelGGL(lg_voxel_keys, dim3(mb), dim3(CG_BLOCK), 0, s, S, P, Mtot, N, PB, npad);
-    int buf = radix_sort(S, Mtot, key_bits, s);
+    int buf;
+    uint32_t run_pb = PB;
+    if (key_bits == PB || P.voxel_order != CG_VOXEL_ORDER_PCL) {
+        // passthrough (a sort of the frame-index bits), or point order: a stable radix sort
+        // of (idx, frame index) keys keeps each voxel's points in frame-index order
+        buf = radix_sort(S, Mtot, key_bits, s);
+    } else {
+        // PCL's order: index_vector (finite points in frame-index order) as (idx, slot)
+        // records, then std::sort's permutation of it (lg_pcl_level, lg_pcl_leaf)
+        buf = PB ? radix_sort(S, Mtot, PB, s) : 0;   // unsorted tiles: frame-index order first
+        uint64_t* kb[2] = {S.key0, S.key1};
+        uint32_t* vb2[2] = {S.val0, S.val1};
+        scan_emit(S, Mtot, -1, PclCompactFlag{kb[buf], PB}, PclCompactEmit{kb[buf], vb2[buf], kb[buf ^ 1], PB},
+                  LG_PCL_N, s);
+        // levels until every range fits a leaf (one more for uneven cuts), then the leaves
+        uint32_t levels = 1;
+        while (((uint64_t)LG_PCL_LEAF << (levels - 1)) < Mtot) levels++;
+        for (uint32_t lv = 0; lv < levels; lv++)
+            hipLaunchKernelGGL(lg_pcl_level, dim3(lv ? (1u << lv) : 1u), dim3(CG_BLOCK), 0, s, S, kb[buf ^ 1], lv,
+                               levels - 1);
+        hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (1u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
+                           kb[buf ^ 1], kb[buf], vb2[buf]);
+        run_pb = 0;   // sorted keys are the idx alone
+    }
     const uint64_t* vkey = buf ? S.key1 : S.key0;
     // runs over the finite points (non-finite keys sort last); passthrough: every point
-    scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, PB}, VoxelEmit{S.run}, LG_V, s);
+    scan_emit(S, Mtot, LG_SCAN_N, VoxelHead{vkey, S.meta, run_pb}, VoxelEmit{S.run}, LG_V, s);
     hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(Mtot)), dim3(CG_BLOCK), 0, s,
                        Lh, S, f, Mtot, buf);
     // V is known on the device only: the clustering launches are sized for V <= Mtot and read
@@ -1307,6 +1514,7 @@ uint64_t lg_walk(uint32_t n, F place) {
     for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));
     place(28, take((uint64_t)(LG_DCELLS_MAX + 2) * 4));
     place(29, take(nch * LG_CS_WORDS * 4));
+    place(30, take(LG_PQ_HDR * 4 + (N + 64) * 12 * 4));   // PCL sort range lists: 4 x (first, last, depth)
     return off;
 }
 }  // namespace
@@ -1332,6 +1540,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 15: S.run = (uint32_t*)p; break;
             case 28: S.cstart = (uint32_t*)p; break;
             case 29: S.cstat = (uint32_t*)p; break;
+            case 30: S.pq = (uint32_t*)p; S.pq_cap = std::max<uint32_t>(n, 1) + 64; break;
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
     });
@@ -1536,7 +1745,9 @@ int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     const int kb = radix_sort(S, n, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V,
                                S.meta + LG_SORT_LIM);
     const uint32_t cb = blocks_of((uint64_t)n + 1);
-    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, L, P, S, 0u, VB, kb, Mtot, K, cb);
+    CgDevParams Pm = P;
+    Pm.voxel_order = CG_VOXEL_ORDER_POINT;   // each slab summed its voxels in frame-index order
+    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, L, Pm, S, 0u, VB, kb, Mtot, K, cb);
     return hipGetLastError();
 }
 int cg_launch_halo_owner(const float* pts, uint32_t n, float inv0, int32_t min_b0, uint32_t slab_w, uint32_t slabs,

@@ -321,3 +321,4 @@ __device__ inline void cg_std_sort_wave32(uint32_t& v, int n) {
     cg_wave_stable_sort(v, n);   // the final insertion passes
 }
 #endif
+

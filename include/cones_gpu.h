@@ -37,6 +37,8 @@ extern "C" {
 #define CG_F_GLOBAL_SCRATCH    0x2u  /* detector input too large for the LDS backend; ran from HBM */
 #define CG_F_ORDER_CANONICAL   0x4u  /* >16 clusters: order is (size desc, seed asc); PCL's
                                         std::sort may order equal-size clusters differently */
+#define CG_F_VOXEL_POINT_ORDER 0x8u  /* voxel sums ran in ascending point order, not in PCL's
+                                        std::sort order (cg_set_voxel_order, the halo form) */
 
 /* ---- parameters --------------------------------------------------------------------- */
 /* Field names are the YAML keys, misspellings kept (config/ *.yaml). */
@@ -82,6 +84,15 @@ typedef struct cg_handle cg_handle;
 int  cg_create(const cg_params* params, int device, cg_handle** out);
 int  cg_destroy(cg_handle* h);
 int  cg_set_params(cg_handle* h, const cg_params* params);
+/* Voxel summation order of the VoxelGrid stage (src/cone_detection.cpp:240-249). PCL sorts
+ * index_vector with std::sort, an unstable introsort, so the float sums of a voxel's points
+ * run in libstdc++'s permutation of the equal-idx points; CG_VOXEL_ORDER_PCL reproduces that
+ * permutation and every voxel bit, CG_VOXEL_ORDER_POINT sums in ascending point index (same
+ * voxels, clusters and cluster sets; voxel coordinates may differ in the last bits).
+ * Default: CG_VOXEL_ORDER_PCL. */
+#define CG_VOXEL_ORDER_POINT 0
+#define CG_VOXEL_ORDER_PCL   1
+int  cg_set_voxel_order(cg_handle* h, int order);
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char* cg_last_error(void);
 

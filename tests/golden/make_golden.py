@@ -2,7 +2,7 @@
 """Regenerate tests/golden/*.npz: inputs and CPU-restatement outputs of the hot path.
 
 The reference has no golden data of its own and cannot run here, so these
-fixtures are produced by the oracle (oracle/cg_oracle.cpp) and cross-checked at generation time
+fixtures are produced by the oracle (oracle/cg_oracle.cpp, PCL's std::sort voxel order) and cross-checked at generation time
 against the independent numpy restatement (tests/np_reference.py). They pin both restatements
 (and the host libm they call) and give the GPU tests size-bounded vectors that need no
 generator. Cases: two C1 frames (16 rings x 1024 columns, simulation params) and every
@@ -41,12 +41,15 @@ def save_case(name, pts_raw, point_step, over):
     for mode, tag in ((O.MODE_PIPELINE, "pipeline"), (O.MODE_DETECT, "detect"), (O.MODE_GROUND, "ground")):
         for k, v in outputs(params, msg, mode).items():
             arrays[f"{tag}_{k}"] = v
-    # cross-check the pipeline outputs against the numpy restatement before saving
+    # cross-check against the numpy restatement before saving (it sums each voxel in point
+    # order: compared with the oracle's ORDER_STABLE; the fixtures hold PCL's order)
     prm = {**cp.GROUND_PARAMS, **cp.PROFILES["simulation"], **over}
     ref = R.pipeline(msg.xyzi(), prm, ground=True)
+    st, _ = O.run(params, msg, O.MODE_PIPELINE, O.ORDER_STABLE)
     assert int(arrays["pipeline_hdr"][2]) == ref["M"], name
-    assert np.array_equal(arrays["pipeline_voxels"].view(np.uint32), ref["vox"].view(np.uint32)) or \
+    assert np.array_equal(st.voxels.view(np.uint32), ref["vox"].view(np.uint32)) or \
         np.isnan(ref["vox"]).any(), name
+    assert [list(c) for c in st.clusters] == ref["clusters"] or len(ref["clusters"]) > 16, name
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
     print(f"{name}: N={n} K={int(arrays['pipeline_hdr'][1])} M={int(arrays['pipeline_hdr'][2])} "
           f"V={int(arrays['pipeline_hdr'][3])} C={int(arrays['pipeline_hdr'][4])}")

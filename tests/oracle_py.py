@@ -112,8 +112,10 @@ def server(crops, classify):
     return [int(classify(c)) for c in crops if len(c)]
 
 
-def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_STABLE, intensity_offset=None):
-    """Run the restatement on one cloud; returns (Detection or ground bytes, header)."""
+def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_PCL, intensity_offset=None):
+    """Run the restatement on one cloud; returns (Detection or ground bytes, header). order:
+    ORDER_PCL (default) sums each voxel in PCL's std::sort order, as the reference and the device
+    do; ORDER_STABLE in ascending point order (the numpy restatement's and the halo form's)."""
     n = msg.width * msg.height
     v = msg.view(intensity_offset=intensity_offset)
     cap = max(n, 1)

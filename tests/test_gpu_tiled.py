@@ -86,7 +86,9 @@ def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over, halo, mu
     got = Detection(*(z[k].item() if z[k].ndim == 0 else z[k] for k in FIELDS))
     params = cp.load_params("simulation", over)
     raw = _frame(rings, cols, mutate)
-    ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE)
+    # the halo form sums each voxel in frame-index order on its slab (ORDER_STABLE); the gather
+    # form runs the global backend, which reproduces PCL's std::sort order
+    ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_STABLE if halo else O.ORDER_PCL)
     assert got.n_points == rings * cols
     assert_same_detection(got, ref, f"tiled x{world} halo={halo}")
     if mutate == "passthrough":
@@ -115,5 +117,5 @@ def test_tiled_single_rank_matches_oracle(halo):
     d = torch.from_numpy(raw[0].copy()).to(torch.device("cuda", 0))
     got = cd.run_tiled_frame(cp.BatchEngine(params, device=0), d.data_ptr(), 0, n, n, torch.device("cuda", 0),
                              halo=halo)
-    ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE)
+    ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_STABLE if halo else O.ORDER_PCL)
     assert_same_detection(got, ref, "tiled x1")

@@ -30,7 +30,7 @@ def test_kat_oracle_vs_numpy(kat, mode):
     name, pts, over, _ = kat
     params, prm = params_for(over)
     msg = cp.PointCloud2.from_xyzi(pts)
-    det, hdr = O.run(params, msg, O.MODE_PIPELINE if mode == "pipeline" else O.MODE_DETECT)
+    det, hdr = O.run(params, msg, O.MODE_PIPELINE if mode == "pipeline" else O.MODE_DETECT, O.ORDER_STABLE)
     ref = R.pipeline(pts.copy(), prm, ground=(mode == "pipeline"))
     assert det.n_filtered == ref["M"], name
     assert same_f32(det.voxels, ref["vox"]), name

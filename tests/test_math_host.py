@@ -14,8 +14,54 @@ PROG = r'''
 #include <algorithm>
 #include <random>
 #include <vector>
+#include <climits>
 #include "cg_math.h"
 #include "cg_sort.h"
+struct R { unsigned key, id; };
+// level-parallel model of std::sort's permutation (keys compared alone)
+static void levels_sort(std::vector<R>& a) {
+  const int n = (int)a.size();
+  std::vector<char> head(n + 1, 0), heap(n, 0);
+  head[0] = 1; head[n] = 1;
+  struct Rg { int first, last, depth; };
+  std::vector<Rg> act;
+  if (n > 16) act.push_back({0, n, cg_lg(n) * 2});
+  auto lt = [](const R& p, const R& q) { return p.key < q.key; };
+  while (!act.empty()) {
+    std::vector<Rg> nx;
+    for (auto r : act) {
+      if (r.depth == 0) {
+        cg_heap_sort_range(a.data() + r.first, (long)(r.last - r.first), lt);
+        for (int i = r.first; i < r.last; i++) heap[i] = 1;
+        continue;
+      }
+      const int d = r.depth - 1, first = r.first, last = r.last, mid = first + (last - first) / 2;
+      cg_move_median_to_first(a.data(), first, first + 1, mid, last - 1, lt);
+      const unsigned p = a[first].key;
+      std::vector<int> L, Rr;
+      for (int i = first + 1; i < last; i++) if (a[i].key >= p) L.push_back(i);
+      for (int i = last - 1; i > first; i--) if (a[i].key <= p) Rr.push_back(i);
+      int s = 0;
+      while (s < (int)L.size() && s < (int)Rr.size() && L[s] < Rr[s]) s++;
+      const int cut = s == 0 ? L[0] : std::min(s < (int)L.size() ? L[s] : INT_MAX, Rr[s - 1]);
+      for (int k = 0; k < s; k++) std::swap(a[L[k]], a[Rr[k]]);
+      head[cut] = 1;
+      if (cut - first > 16) nx.push_back({first, cut, d});
+      if (last - cut > 16) nx.push_back({cut, last, d});
+    }
+    act = nx;
+  }
+  std::vector<R> out(n);
+  for (int i = 0; i < n; i++) {
+    if (heap[i]) { out[i] = a[i]; continue; }
+    int s = i; while (!head[s]) s--;
+    int e = i + 1; while (!head[e]) e++;
+    int rank = 0;
+    for (int j = s; j < e; j++) rank += a[j].key < a[i].key || (a[j].key == a[i].key && j < i);
+    out[s + rank] = a[i];
+  }
+  a = out;
+}
 int main() {
   std::mt19937_64 rng(12345);
   long bad = 0;
@@ -55,7 +101,6 @@ int main() {
   }
   if (bad) { printf("sector mismatches %ld\n", bad); return 3; }
   // std::sort permutation restatement
-  struct R { unsigned key, id; };
   for (int it = 0; it < 20000; it++) {
     int n = (it % 5 == 0) ? (int)(rng() % 3000) : (int)(rng() % 120);
     unsigned kr = 1 + (unsigned)(rng() % ((it % 2) ? 4 : 1000));
@@ -69,6 +114,22 @@ int main() {
     for (int i = 0; i < n; i++) if (a[i].id != b[i].id) { bad++; break; }
   }
   if (bad) { printf("sort mismatches %ld\n", bad); return 4; }
+  // the level-parallel formulas of the device's voxel sort (cg_kernels.hip pcl_sort): cut =
+  // L_0 or min(L_s, R_{s-1}), swaps (L_k, R_k) for k < s, stable sort inside the final ranges
+  for (int it = 0; it < 20000; it++) {
+    int n = (it % 7 == 0) ? (int)(rng() % 5000) : (int)(rng() % 400);
+    unsigned kr = 1 + (unsigned)(rng() % ((it % 3 == 0) ? 3 : (it % 3 == 1) ? 50 : 100000));
+    std::vector<R> a(n);
+    for (int i = 0; i < n; i++) a[i] = {(unsigned)(rng() % kr), (unsigned)i};
+    if (it % 11 == 0) std::sort(a.begin(), a.end(), [](const R& p, const R& q) { return p.key < q.key; });
+    if (it % 13 == 0) std::reverse(a.begin(), a.end());
+    for (int i = 0; i < n; i++) a[i].id = i;
+    auto b = a;
+    std::sort(a.begin(), a.end(), [](const R& p, const R& q) { return p.key < q.key; });
+    levels_sort(b);
+    for (int i = 0; i < n; i++) if (a[i].id != b[i].id) { bad++; break; }
+  }
+  if (bad) { printf("level model mismatches %ld\n", bad); return 5; }
   printf("ok\n");
   return 0;
 }

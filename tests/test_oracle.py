@@ -23,7 +23,7 @@ def test_oracle_matches_numpy_c1(frame):
     raw = cp.synth_frames(1, first_frame=frame, rings=16, cols=1024)
     msg = cp.frame_cloud(raw[0])
     params = cp.load_params("simulation")
-    det, _ = O.run(params, msg, O.MODE_PIPELINE)
+    det, _ = O.run(params, msg, O.MODE_PIPELINE, O.ORDER_STABLE)
     ref = R.pipeline(msg.xyzi(), PRM, ground=True)
     assert len(ref["clusters"]) > 0
     _compare(det, ref, f"frame {frame}")
@@ -33,7 +33,7 @@ def test_oracle_matches_numpy_detector_only():
     raw = cp.synth_frames(1, first_frame=4, rings=16, cols=1024)
     msg = cp.frame_cloud(raw[0])
     params = cp.load_params("simulation")
-    det, _ = O.run(params, msg, O.MODE_DETECT)
+    det, _ = O.run(params, msg, O.MODE_DETECT, O.ORDER_STABLE)
     _compare(det, R.pipeline(msg.xyzi(), PRM, ground=False), "detect")
 
 
@@ -41,7 +41,7 @@ def test_oracle_matches_numpy_our_profile():
     raw = cp.synth_frames(1, first_frame=6, rings=16, cols=1024)
     msg = cp.frame_cloud(raw[0])
     prm = {**cp.GROUND_PARAMS, **cp.PROFILES["our"]}
-    det, _ = O.run(cp.load_params("our"), msg, O.MODE_PIPELINE)
+    det, _ = O.run(cp.load_params("our"), msg, O.MODE_PIPELINE, O.ORDER_STABLE)
     _compare(det, R.pipeline(msg.xyzi(), prm, ground=True), "our")
 
 
