@@ -1430,9 +1430,13 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
         uint32_t* vb2[2] = {S.val0, S.val1};
         scan_emit(S, Mtot, -1, PclCompactFlag{kb[buf], PB}, PclCompactEmit{kb[buf], vb2[buf], kb[buf ^ 1], PB},
                   LG_PCL_N, s);
-        // levels until every range fits a leaf (one more for uneven cuts), then the leaves
+        // levels until every range fits a leaf, then the leaves
+        // (median-of-three cuts are uneven: three levels more than an even split needs keep the
+        // leaves within LG_PCL_LEAF and out of the slow HBM form; levels past the last range
+        // to cut return at once)
         uint32_t levels = 1;
         while (((uint64_t)LG_PCL_LEAF << (levels - 1)) < Mtot) levels++;
+        if (levels > 1) levels += 3;
         for (uint32_t lv = 0; lv < levels; lv++)
             hipLaunchKernelGGL(lg_pcl_level, dim3(lv ? (1u << lv) : 1u), dim3(CG_BLOCK), 0, s, S, kb[buf ^ 1], lv,
                                levels - 1);

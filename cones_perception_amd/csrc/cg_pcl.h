@@ -106,38 +106,57 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 }
 
 // One wave: __move_median_to_first + __unguarded_partition(first + 1, last, first) of E by
-// key, the parallel form (see above): L and R lists in PL / PR from first + 1, then the swaps
-// of the pairs (L_k, R_k) with L_k < R_k. Returns the cut (wave-uniform).
+// key, the parallel form (see above), for a range of at most PCL_WAVE_MAX: the keys held in
+// registers (one 64-element chunk per register), the L and R lists in PL / PR from first + 1,
+// then the swaps of the pairs (L_k, R_k) with L_k < R_k. Returns the cut (wave-uniform).
+#define PCL_WAVE_CHUNKS (PCL_WAVE_MAX / 64)
 __device__ inline uint32_t pcl_wave_partition(uint64_t* E, uint32_t* PL, uint32_t* PR, uint32_t first, uint32_t last) {
     const uint32_t l = lane_id();
-    if (l == 0)
-        cg_move_median_to_first(E, (long)first, (long)first + 1, (long)(first + (last - first) / 2), (long)last - 1,
-                                [](uint64_t a, uint64_t b) { return pcl_key(a) < pcl_key(b); });
+    const uint32_t a = first + 1, mid = first + (last - first) / 2;
+    // __move_median_to_first(first, first + 1, mid, last - 1): the three keys in one round trip
+    const uint32_t ka = pcl_key(E[a]), kb = pcl_key(E[mid]), kc = pcl_key(E[last - 1]);
+    uint32_t m, p;
+    if (ka < kb) { if (kb < kc) { m = mid; p = kb; } else if (ka < kc) { m = last - 1; p = kc; } else { m = a; p = ka; } }
+    else if (ka < kc) { m = a; p = ka; }
+    else if (kb < kc) { m = last - 1; p = kc; }
+    else { m = mid; p = kb; }
+    if (l == 0) {
+        const uint64_t t = E[first];
+        E[first] = E[m];
+        E[m] = t;
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint32_t p = pcl_key(E[first]);
-    const uint32_t a = first + 1;
+    // keys of [first + 1, last) in registers (after the median swap)
+    uint32_t kr[PCL_WAVE_CHUNKS];
+#pragma unroll
+    for (int c = 0; c < PCL_WAVE_CHUNKS; c++) {
+        const uint32_t x = a + 64u * c + l;
+        kr[c] = x < last ? pcl_key(E[x]) : 0u;
+    }
+    uint64_t gem[PCL_WAVE_CHUNKS], lem[PCL_WAVE_CHUNKS];
     uint32_t nL = 0, nR = 0;
-    for (uint32_t x0 = a; x0 < last; x0 += 64) {
-        const uint32_t x = x0 + l;
-        const uint32_t k = x < last ? pcl_key(E[x]) : 0u;
-        nL += (uint32_t)__popcll(__ballot(x < last && k >= p));
-        nR += (uint32_t)__popcll(__ballot(x < last && k <= p));
+#pragma unroll
+    for (int c = 0; c < PCL_WAVE_CHUNKS; c++) {
+        const uint32_t x = a + 64u * c + l;
+        gem[c] = __ballot(x < last && kr[c] >= p);
+        lem[c] = __ballot(x < last && kr[c] <= p);
+        nL += (uint32_t)__popcll(gem[c]);
+        nR += (uint32_t)__popcll(lem[c]);
     }
     uint32_t bge = 0, ble = 0;
-    for (uint32_t x0 = a; x0 < last; x0 += 64) {
-        const uint32_t x = x0 + l;
-        const uint32_t k = x < last ? pcl_key(E[x]) : 0u;
-        const uint64_t ge = __ballot(x < last && k >= p), le = __ballot(x < last && k <= p);
-        if (x < last && k >= p) PL[a + bge + mbcnt(ge)] = x;
-        if (x < last && k <= p) PR[a + nR - 1u - (ble + mbcnt(le))] = x;
-        bge += (uint32_t)__popcll(ge);
-        ble += (uint32_t)__popcll(le);
+#pragma unroll
+    for (int c = 0; c < PCL_WAVE_CHUNKS; c++) {
+        const uint32_t x = a + 64u * c + l;
+        if ((gem[c] >> l) & 1u) PL[a + bge + mbcnt(gem[c])] = x;
+        if ((lem[c] >> l) & 1u) PR[a + nR - 1u - (ble + mbcnt(lem[c]))] = x;
+        bge += (uint32_t)__popcll(gem[c]);
+        ble += (uint32_t)__popcll(lem[c]);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint32_t m2 = min(nL, nR);
     uint32_t sw = 0;
-    for (uint32_t k0 = 0; k0 < m2; k0 += 64) {
-        const uint32_t k = k0 + l;
+    for (uint32_t k0c = 0; k0c < m2; k0c += 64) {
+        const uint32_t k = k0c + l;
         bool c = false;
         if (k < m2) {
             const uint32_t i = PL[a + k], j = PR[a + k];
@@ -319,15 +338,19 @@ __device__ inline void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t
     __syncthreads();
     PCL_STAMP();
     // the final insertion passes: a stable sort inside each range of at most 16 (the ranges
-    // are weakly ordered); heapsorted ranges are final
+    // are weakly ordered); heapsorted ranges are final. Each range's first lists its positions.
+    uint32_t* SEG = PRE;
+    for (uint32_t i = tid; i < n; i += CG_BLOCK)
+        if ((FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD) {
+            const uint32_t e = i + (INFO[i] & 0xfffffu);
+            for (uint32_t j = i; j < e; j++) SEG[j] = i;
+        }
+    __syncthreads();
     uint64_t* KEY = W.KEY;
     for (uint32_t i = tid; i < n; i += CG_BLOCK) {
         const uint64_t ri = E[i];
         if (FLG[i] & PCL_HEAP) { KEY[i] = ri; continue; }
-        uint32_t s0 = i;
-        while (!(FLG[s0] & PCL_HEAD)) s0--;
-        uint32_t e0 = i + 1;
-        while (e0 < n && !(FLG[e0] & PCL_HEAD)) e0++;
+        const uint32_t s0 = SEG[i], e0 = s0 + (INFO[s0] & 0xfffffu);
         const uint32_t ki = pcl_key(ri);
         uint32_t rank = 0;
         for (uint32_t j = s0; j < e0; j++) {
