@@ -178,7 +178,8 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             uint64_t* E = (uint64_t*)W.VOX;
             pcl_index_vector(W, M, fs->scal[S_MS], E, red, [&](uint32_t j) -> uint32_t { return voxel_idx(W.P[j]); });
             STAMP(7);
-            pcl_sort(W, E, Mf, red);
+            if (flags & CG_F_GLOBAL_SCRATCH) pcl_sort<2, false>(W, E, Mf, red);
+            else pcl_sort<2, true>(W, E, Mf, red);
         } else {
             // keys (idx << 32 | point index << 16 | slot): unique, so any sort yields PCL's idx
             // order with ties in point order. Non-finite points get idx 0xffffffff (beyond every

@@ -938,7 +938,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
             W.A = S.lab + first; W.PAR = S.par + first; W.CNT = S.cnt + first; W.UK = S.uk + first;
             W.ORD = S.ord + first; W.LAB = (int32_t*)S.rank + first; W.OFF = S.off + first;
         }
-        pcl_sort(W, El, size, red, (int)depth);
+        if (size <= LG_PCL_LEAF) pcl_sort<4, true>(W, El, size, red, (int)depth);
+        else pcl_sort<4, false>(W, El, size, red, (int)depth);
         for (uint32_t i = tid; i < size; i += CG_BLOCK) {
             const uint64_t r = W.KEY[i];
             kout[first + i] = r >> 32;

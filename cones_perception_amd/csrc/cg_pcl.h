@@ -19,7 +19,7 @@ struct Work {
 // It is reproduced exactly:
 //  1. index_vector order: the rank of a kept survivor among the finite kept survivors by point
 //     index (a bitmap of point indices, popcount prefix), then the zero pads;
-//  2. __introsort_loop level-synchronously while any range is longer than PCL_WAVE_MAX: per range, the
+//  2. __introsort_loop level-synchronously: per range, the
 //     median of three moved to first, then the unguarded Hoare partition in parallel. Its
 //     k-th swap exchanges the k-th element >= pivot from the left (L_k) with the k-th element
 //     <= pivot from the right (R_k) while L_k < R_k; both lists are read off prefix counts of
@@ -27,10 +27,9 @@ struct Work {
 //     With s swaps the cut (where the left scan stops next) is L_0 if s = 0, else
 //     min(L_s, R_{s-1}). Depth budget and heapsort fallback per range as in the sequential
 //     code (cg_sort.h);
-//  3. ranges of at most PCL_WAVE_MAX on single waves, in rounds: each round every wave
-//     partitions ranges of the round's list with the same parallel formulas (ballots, LDS
-//     lists) and lists the parts longer than 16 for the next round (no wave waits on another
-//     except at the round's barrier);
+//  3. up to PMAX * CG_BLOCK elements (pcl_block_sort) each thread keeps its elements' ranges in
+//     registers; longer arrays (HBM scratch) run block levels until every range fits, then
+//     pcl_block_sort on each range;
 //  4. the final insertion passes: a stable sort inside each range of at most 16 (the ranges
 //     are weakly ordered, so this is the stable sort of the whole array).
 // The permutation is checked against std::sort on the host (tests/test_math_host.py, the
@@ -38,17 +37,22 @@ struct Work {
 #ifdef CG_PCL_PROBE
 __device__ unsigned long long g_pcl_probe[64];
 __device__ unsigned int g_pcl_probe_n;
+// workgroup 0 only (other workgroups of a probe launch share the counter), bounded slot
 #define PCL_STAMP()                                                                      \
     do {                                                                                 \
-        if (threadIdx.x == 0 && g_pcl_probe_n < 64) g_pcl_probe[g_pcl_probe_n++] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && blockIdx.x == 0) {                                      \
+            const unsigned int s_ = atomicAdd(&g_pcl_probe_n, 1u);                       \
+            if (s_ < 64) g_pcl_probe[s_] = __builtin_amdgcn_s_memrealtime();             \
+        }                                                                                \
     } while (0)
+#define PCL_STEP() PCL_STAMP()
 #else
 #define PCL_STAMP() ((void)0)
+#define PCL_STEP() ((void)0)
 #endif
 #define PCL_INACT 0xffffffffu
 #define PCL_HEAD 1u
 #define PCL_HEAP 2u
-#define PCL_WAVE_MAX 512   // ranges up to this length are partitioned by single waves
 __device__ __forceinline__ uint32_t pcl_key(uint64_t r) { return (uint32_t)(r >> 32); }
 
 // Records (idx << 32 | slot) of the Mf finite points of W.P in index_vector order -> E.
@@ -105,82 +109,261 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
     __syncthreads();
 }
 
-// One wave: __move_median_to_first + __unguarded_partition(first + 1, last, first) of E by
-// key, the parallel form (see above), for a range of at most PCL_WAVE_MAX: the keys held in
-// registers (one 64-element chunk per register), the L and R lists in PL / PR from first + 1,
-// then the swaps of the pairs (L_k, R_k) with L_k < R_k. Returns the cut (wave-uniform).
-#define PCL_WAVE_CHUNKS (PCL_WAVE_MAX / 64)
-__device__ inline uint32_t pcl_wave_partition(uint64_t* E, uint32_t* PL, uint32_t* PR, uint32_t first, uint32_t last) {
-    const uint32_t l = lane_id();
-    const uint32_t a = first + 1, mid = first + (last - first) / 2;
-    // __move_median_to_first(first, first + 1, mid, last - 1): the three keys in one round trip
-    const uint32_t ka = pcl_key(E[a]), kb = pcl_key(E[mid]), kc = pcl_key(E[last - 1]);
-    uint32_t m, p;
-    if (ka < kb) { if (kb < kc) { m = mid; p = kb; } else if (ka < kc) { m = last - 1; p = kc; } else { m = a; p = ka; } }
-    else if (ka < kc) { m = a; p = ka; }
-    else if (kb < kc) { m = last - 1; p = kc; }
-    else { m = mid; p = kb; }
-    if (l == 0) {
-        const uint64_t t = E[first];
-        E[first] = E[m];
-        E[m] = t;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // keys of [first + 1, last) in registers (after the median swap)
-    uint32_t kr[PCL_WAVE_CHUNKS];
-#pragma unroll
-    for (int c = 0; c < PCL_WAVE_CHUNKS; c++) {
-        const uint32_t x = a + 64u * c + l;
-        kr[c] = x < last ? pcl_key(E[x]) : 0u;
-    }
-    uint64_t gem[PCL_WAVE_CHUNKS], lem[PCL_WAVE_CHUNKS];
-    uint32_t nL = 0, nR = 0;
-#pragma unroll
-    for (int c = 0; c < PCL_WAVE_CHUNKS; c++) {
-        const uint32_t x = a + 64u * c + l;
-        gem[c] = __ballot(x < last && kr[c] >= p);
-        lem[c] = __ballot(x < last && kr[c] <= p);
-        nL += (uint32_t)__popcll(gem[c]);
-        nR += (uint32_t)__popcll(lem[c]);
-    }
-    uint32_t bge = 0, ble = 0;
-#pragma unroll
-    for (int c = 0; c < PCL_WAVE_CHUNKS; c++) {
-        const uint32_t x = a + 64u * c + l;
-        if ((gem[c] >> l) & 1u) PL[a + bge + mbcnt(gem[c])] = x;
-        if ((lem[c] >> l) & 1u) PR[a + nR - 1u - (ble + mbcnt(lem[c]))] = x;
-        bge += (uint32_t)__popcll(gem[c]);
-        ble += (uint32_t)__popcll(lem[c]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const uint32_t m2 = min(nL, nR);
-    uint32_t sw = 0;
-    for (uint32_t k0c = 0; k0c < m2; k0c += 64) {
-        const uint32_t k = k0c + l;
-        bool c = false;
-        if (k < m2) {
-            const uint32_t i = PL[a + k], j = PR[a + k];
-            c = i < j;
-            if (c) {
-                const uint64_t t = E[i];
-                E[i] = E[j];
-                E[j] = t;
-            }
-        }
-        const uint64_t cm = __ballot(c);
-        sw += (uint32_t)__popcll(cm);
-        if (~cm & __ballot(k < m2)) break;   // the pairs past the first failure all fail
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    return sw == 0 ? PL[a] : min(sw < nL ? PL[a + sw] : 0xffffffffu, PR[a + sw - 1u]);
+// ------------------------------------------------------------------------------------------
+// The whole workgroup sorts n <= CG_BLOCK * PER elements, every partition of a level of
+// __introsort_loop at once. Element x = tid + CG_BLOCK * k (k < PER); each thread keeps the
+// range [f, e) of its elements in registers and follows the cut after every level. Per level
+// (one LDS round trip and one barrier per step):
+//   S1. >= / <= pivot against the range's pivot; per (chunk, wave) counts;
+//   S2. exclusive counts over positions; the head and the last element of each partitioned
+//       range publish theirs (at f and f + 1: f + 1 is never a head while the range is longer
+//       than 16), so an element's index in its range's L / R list is a difference;
+//   S3. the L and R lists (from first + 1); heads reset the swap count;
+//   S4. the swaps (L_k, R_k) while L_k < R_k: every partner is read, then every element
+//       written; the last swap of a range records the swap count s;
+//   S5. each head: the cut (header: L_0 if s = 0, else min(L_s, R_{s-1})), then both children
+//       set up as __introsort_loop does (heapsort when the depth budget is spent, else the
+//       median of three moved to first and the pivot), the cut published for S0;
+//   S0. every element follows the cut into its child range.
+// Then the final insertion passes: a stable rank inside each range of at most 16; heapsorted
+// ranges are sorted already. Scratch: INFO (act | final | budget at heads), PIV, RLO, PL, PR,
+// CUT (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
+#define PB_ACT 0x100u
+#define PB_FIN 0x200u
+#define PB_BUDGET 0xffu
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+// Pointer kinds: LDS (ds_* instructions) when the arrays live in LDS, generic otherwise.
+struct PbLds { typedef lds_u32* P32; typedef lds_u64* P64; };
+struct PbGen { typedef uint32_t* P32; typedef uint64_t* P64; };
+template <class K> struct PbScratch { typename K::P32 INFO, PIV, RLO, PL, PR, CUT; };
+struct PwLess {   // a functor, not a function: a function pointer could become an indirect call
+    __device__ __forceinline__ bool operator()(uint64_t a, uint64_t b) const { return pcl_key(a) < pcl_key(b); }
+};
+
+// __move_median_to_first(first, first + 1, mid, last - 1) of a range longer than 16: the
+// index of the median, decided exactly as libstdc++ does on keys ka, kb, kc at a, b, c.
+__device__ __forceinline__ uint32_t pb_median(uint32_t a, uint32_t b, uint32_t c, uint32_t ka, uint32_t kb, uint32_t kc) {
+    if (ka < kb) return kb < kc ? b : (ka < kc ? c : a);
+    if (ka < kc) return a;
+    return kb < kc ? c : b;
 }
 
-// std::sort(E, E + n) by key (E in W.VOX) into KEY, libstdc++'s permutation. Scratch: W.A
-// (prefix, n + 1), W.PAR / W.CNT (L and R lists), W.UK (range of each position), W.ORD
-// (flags), W.LAB (size | depth << 20 at each range's first), W.OFF (pivot, later last),
-// KEY as words (s, later cut). Every thread calls it; ends with a barrier.
-__device__ inline void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t* red, int depth0 = -1) {
+// A head sets up the two children [f, cut) and [cut, e) of a partitioned range, children's
+// budget d (the body of __introsort_loop): a child longer than 16 is heapsorted when d == 0
+// (final), else its median of three is moved to its first and its pivot noted (partitioned in
+// the next level). The eight elements are read in one batch, then written. Returns whether a
+// child is partitioned next.
+template <class K>
+__device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K>& S, uint32_t f, uint32_t cut,
+                                            uint32_t e, uint32_t d) {
+    const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
+    bool med[2];
+    uint32_t ia[2], ib[2], ic[2];
+    uint64_t v0[2], va[2], vb[2], vc[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        med[c] = hi[c] - lo[c] > CG_SORT_THRESHOLD && d > 0;
+        ia[c] = lo[c] + 1; ib[c] = lo[c] + (hi[c] - lo[c]) / 2; ic[c] = hi[c] - 1;
+        if (med[c]) { v0[c] = E[lo[c]]; va[c] = E[ia[c]]; vb[c] = E[ib[c]]; vc[c] = E[ic[c]]; }
+    }
+    bool act = false;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        uint32_t info = d;
+        if (hi[c] - lo[c] > CG_SORT_THRESHOLD) {
+            if (d == 0) {   // __partial_sort(first, last, last): final
+                cg_heap_sort_range((uint64_t*)(E + lo[c]), (long)(hi[c] - lo[c]), PwLess{});
+                info |= PB_FIN;
+            } else {
+                const uint32_t m = pb_median(ia[c], ib[c], ic[c], pcl_key(va[c]), pcl_key(vb[c]), pcl_key(vc[c]));
+                const uint64_t vm = m == ia[c] ? va[c] : (m == ib[c] ? vb[c] : vc[c]);
+                E[lo[c]] = vm;
+                E[m] = v0[c];
+                S.PIV[lo[c]] = pcl_key(vm);
+                info |= PB_ACT;
+                act = true;
+            }
+        }
+        S.INFO[lo[c]] = info;
+    }
+    return act;
+}
+
+// Always inlined: an out-of-line call takes its arguments through scratch memory (and
+// tests/test_isa.py asserts that no kernel makes a call).
+template <int PER, class K>
+__device__ __forceinline__ void pcl_block_sort(typename K::P64 E, typename K::P64 out, uint32_t n, uint32_t depth0,
+                                               const PbScratch<K> S, typename K::P32 cnt) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    constexpr uint32_t GE = 1u << 24, LE = 1u << 25, IN = 1u << 26, PART = 1u << 27;
+    uint32_t fe[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) fe[k] = n << 16;
+    bool act = false;
+    if (tid == 0 && n) {   // the whole array as the right child of an empty range
+        act = pb_children<K>(E, S, 0, 0, n, depth0);
+    }
+    bool any = __syncthreads_or(act);
+    while (any) {
+        uint32_t st[PER], nn[PER];
+        // S1
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
+            uint32_t info = 0, p = 0, kx = 0;
+            if (x < n) {
+                info = S.INFO[f];
+                p = S.PIV[f];
+                kx = pcl_key(E[x]);
+            }
+            const bool part = (info & PB_ACT) != 0, in = part && x > f;
+            const bool ge = in && kx >= p, le = in && kx <= p;
+            const uint64_t gm = __ballot(ge), lm = __ballot(le);
+            if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
+            st[k] = mbcnt(gm) | (mbcnt(lm) << 12) | (ge ? GE : 0u) | (le ? LE : 0u) | (in ? IN : 0u) | (part ? PART : 0u);
+        }
+        __syncthreads();
+        PCL_STEP();
+        // S2: lane j of every wave scans the (chunk, wave) counts; element (k, w) reads entry
+        // k * WAVES + w of the exclusive scan
+        {
+            const uint32_t cj = l < PER * WAVES ? cnt[l] : 0u;
+            const uint32_t g = wave_incl_scan(cj & 0xffffu), h = wave_incl_scan(cj >> 16);
+            const uint32_t gex = g - (cj & 0xffffu), hex = h - (cj >> 16);
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+                const uint32_t src = (uint32_t)k * WAVES + w;
+                const uint32_t gx = (uint32_t)__builtin_amdgcn_readlane((int)gex, (int)src) + (st[k] & 0xfffu);
+                const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)hex, (int)src) + ((st[k] >> 12) & 0xfffu);
+                if ((st[k] & PART) && x == f) S.RLO[f] = gx | (lx << 16);
+                if ((st[k] & IN) && x == e - 1)
+                    S.RLO[f + 1] = (gx + ((st[k] & GE) ? 1u : 0u)) | ((lx + ((st[k] & LE) ? 1u : 0u)) << 16);
+                st[k] = gx | (lx << 12) | (st[k] & (GE | LE | IN | PART));
+            }
+        }
+        __syncthreads();
+        PCL_STEP();
+        // S3
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
+            nn[k] = 0;
+            if (st[k] & PART) {
+                const uint32_t lo = S.RLO[f], hi = S.RLO[f + 1];
+                const uint32_t gf = lo & 0xffffu, lf = lo >> 16, gend = hi & 0xffffu, lend = hi >> 16;
+                nn[k] = (gend - gf) | ((lend - lf) << 16);
+                if (x == f) S.CUT[f] = 0u;
+                if (st[k] & IN) {
+                    const uint32_t gx = st[k] & 0xfffu, lx = (st[k] >> 12) & 0xfffu;
+                    const uint32_t li = gx - gf, ri = lend - lx - 1u;
+                    if (st[k] & GE) S.PL[f + 1 + li] = x;
+                    if (st[k] & LE) S.PR[f + 1 + ri] = x;
+                    st[k] = li | ((ri & 0xfffu) << 12) | (st[k] & (GE | LE | IN | PART));
+                }
+            }
+        }
+        __syncthreads();
+        PCL_STEP();
+        // S4: the partners and the next pair in one batch, then the partners' elements
+        uint64_t val[PER];
+        uint32_t sw = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
+            val[k] = 0;
+            if (st[k] & IN) {
+                const uint32_t li = st[k] & 0xfffu, ri = (st[k] >> 12) & 0xfffu;
+                const uint32_t nL = nn[k] & 0xffffu, nR = nn[k] >> 16;
+                const bool hasL = (st[k] & GE) && li < nR, hasR = (st[k] & LE) && ri < nL;
+                const bool nxt = hasL && li + 1 < min(nL, nR);
+                const uint32_t j = hasL ? S.PR[f + 1 + li] : 0u;
+                const uint32_t i = hasR ? S.PL[f + 1 + ri] : 0xffffffffu;
+                const uint32_t pl2 = nxt ? S.PL[f + 2 + li] : 0u, pr2 = nxt ? S.PR[f + 2 + li] : 0u;
+                uint32_t partner = x;
+                if (hasL && x < j) {
+                    partner = j;
+                    if (!nxt || !(pl2 < pr2)) S.CUT[f] = li + 1;
+                }
+                if (hasR && i < x) partner = i;
+                if (partner != x) {
+                    val[k] = E[partner];
+                    sw |= 1u << k;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PER; k++)
+            if (sw & (1u << k)) E[tid + CG_BLOCK * k] = val[k];
+        __syncthreads();
+        PCL_STEP();
+        // S5: heads
+        act = false;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+            if ((st[k] & PART) && x == f) {
+                const uint32_t s = S.CUT[f], info = S.INFO[f], pl1 = S.PL[f + 1];
+                const uint32_t nL = nn[k] & 0xffffu;
+                const uint32_t pls = s < nL ? S.PL[f + 1 + s] : 0xffffffffu, prs = s ? S.PR[f + s] : 0u;
+                const uint32_t cut = s == 0 ? pl1 : min(pls, prs);
+                act |= pb_children<K>(E, S, f, cut, e, (info & PB_BUDGET) - 1u);
+                S.CUT[f] = cut;
+            }
+        }
+        any = __syncthreads_or(act);
+        PCL_STEP();
+        // S0
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+            if (st[k] & PART) {
+                const uint32_t c = S.CUT[f];
+                fe[k] = x < c ? (f | (c << 16)) : (c | (e << 16));
+            }
+        }
+    }
+    // the final insertion passes
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+        if (x < n) {
+            const uint64_t r = E[x];
+            const uint32_t info = S.INFO[f];
+            uint32_t kj[CG_SORT_THRESHOLD];
+#pragma unroll
+            for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++) kj[j] = f + j < e ? pcl_key(E[f + j]) : 0u;
+            if (info & PB_FIN) {
+                out[x] = r;
+            } else {
+                const uint32_t kx = pcl_key(r);
+                uint32_t rank = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++)
+                    rank += f + j < e && ((kj[j] < kx) || (kj[j] == kx && f + j < x));
+                out[f + rank] = r;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// std::sort(E, E + n) by key (E in W.VOX) into KEY, libstdc++'s permutation. Up to
+// PCL_BLOCK_MAX elements: pcl_block_sort (scratch W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD; red
+// for the counts). Longer arrays (the HBM-scratch backend, large-frame leaves in HBM): block
+// levels over W.A (prefix, n + 1), W.PAR / W.CNT (L and R lists), W.UK (range of each
+// position), W.ORD (flags), W.LAB (size | depth << 20 at each range's first), W.OFF (pivot,
+// later last), KEY as words (s, later cut), until every range is at most PCL_BLOCK_MAX; those
+// are then sorted one after another by pcl_block_sort. Every thread calls it; ends with a
+// barrier.
+// PMAX: the largest pcl_block_sort instantiation (elements per thread) the caller affords;
+// LDS: the arrays of W live in LDS (n <= PMAX * CG_BLOCK then).
+template <int PMAX, bool LDS>
+__device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t* red, int depth0 = -1) {
+    constexpr uint32_t PCL_BLOCK_MAX = PMAX * CG_BLOCK;
+    const uint32_t tid = threadIdx.x;
     uint32_t* PRE = W.A;
     uint32_t* PL = W.PAR;
     uint32_t* PR = W.CNT;
@@ -189,15 +372,30 @@ __device__ inline void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t
     uint32_t* INFO = (uint32_t*)W.LAB;
     uint32_t* PIV = W.OFF;
     uint32_t* SC = (uint32_t*)W.KEY;
-    const bool big = n > PCL_WAVE_MAX;
+    const uint32_t d0 = (uint32_t)(depth0 >= 0 ? depth0 : 2 * cg_lg((long)n));
+    PCL_STAMP();
+    if constexpr (LDS) {
+        const PbScratch<PbLds> PS{(lds_u32*)(uint32_t*)W.LAB, (lds_u32*)W.OFF, (lds_u32*)W.A, (lds_u32*)W.PAR,
+                                  (lds_u32*)W.CNT, (lds_u32*)W.ORD};
+        lds_u64* const El = (lds_u64*)E;
+        lds_u64* const Ko = (lds_u64*)W.KEY;
+        lds_u32* const Rl = (lds_u32*)red;
+        if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, Ko, n, d0, PS, Rl);
+        else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, Ko, n, d0, PS, Rl);
+        else pcl_block_sort<PMAX, PbLds>(El, Ko, n, d0, PS, Rl);
+        PCL_STAMP();
+        return;
+    }
+    const PbScratch<PbGen> PS{(uint32_t*)W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD};
+    if (n <= PMAX * CG_BLOCK) { pcl_block_sort<PMAX, PbGen>(E, W.KEY, n, d0, PS, red); PCL_STAMP(); return; }
+    const bool big = true;
     for (uint32_t i = tid; i < n; i += CG_BLOCK) {
         RID[i] = big ? 0u : PCL_INACT;
         FLG[i] = i == 0 ? PCL_HEAD : 0u;
     }
-    if (tid == 0 && n) INFO[0] = n | ((uint32_t)(depth0 >= 0 ? depth0 : 2 * cg_lg((long)n)) << 20);
+    if (tid == 0 && n) INFO[0] = n | (d0 << 20);
     __syncthreads();
     bool any = big;
-    PCL_STAMP();
     while (any) {
         // (1) per range: depth budget, heapsort fallback or median of three to first
         for (uint32_t i = tid; i < n; i += CG_BLOCK) {
@@ -281,21 +479,20 @@ __device__ inline void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t
             const uint32_t r = RID[i];
             if (r == PCL_INACT) continue;
             const uint32_t cut = SC[r], last = PIV[r];
-            const uint32_t nr = i < cut ? (cut - r > PCL_WAVE_MAX ? r : PCL_INACT)
-                                        : (last - cut > PCL_WAVE_MAX ? cut : PCL_INACT);
+            const uint32_t nr = i < cut ? (cut - r > PCL_BLOCK_MAX ? r : PCL_INACT)
+                                        : (last - cut > PCL_BLOCK_MAX ? cut : PCL_INACT);
             RID[i] = nr;
             mine |= nr != PCL_INACT;
         }
         any = __syncthreads_or(mine);
         PCL_STAMP();
     }
-    // the remaining ranges (at most PCL_WAVE_MAX, longer than 16) in rounds: in each round
-    // every wave takes ranges of the round's list (round robin), partitions each once by
-    // itself and lists the parts still longer than 16 for the next round
+    // the remaining ranges (at most PCL_BLOCK_MAX): those longer than 16 (not heapsorted) are
+    // listed as tasks; the others get their final insertion pass here, a stable rank
+    // inside the range (heapsorted ranges are sorted already)
     uint32_t* CUR = RID;                    // range firsts (RID is free after the block levels)
-    uint32_t* NXT = PIV;                    // (PIV too)
-    uint32_t* qc = red + 3 * WAVES;         // [0]: next round's count
-    uint32_t ncur = block_scan(
+    uint64_t* KEY = W.KEY;
+    const uint32_t ncur = block_scan(
         n,
         [&](uint32_t i) -> uint32_t {
             return (FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD && (INFO[i] & 0xfffffu) > CG_SORT_THRESHOLD ? 1u : 0u;
@@ -304,60 +501,33 @@ __device__ inline void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t
             if ((FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD && (INFO[i] & 0xfffffu) > CG_SORT_THRESHOLD) CUR[e] = i;
         },
         red);
-    if (tid == 0) qc[0] = 0u;
-    __syncthreads();
-    PCL_STAMP();
-    while (ncur) {
-        for (uint32_t q = w; q < ncur; q += WAVES) {
-            const uint32_t first = CUR[q];
-            const uint32_t last = first + (INFO[first] & 0xfffffu), depth = INFO[first] >> 20;
-            if (depth == 0) {   // __partial_sort (heapsort) of the range: final
-                if (l == 0)
-                    cg_heap_sort_range(E + first, (long)(last - first),
-                                       [](uint64_t a, uint64_t b) { return pcl_key(a) < pcl_key(b); });
-                for (uint32_t x = first + l; x < last; x += 64) FLG[x] |= PCL_HEAP;
-                continue;
-            }
-            const uint32_t cut = pcl_wave_partition(E, PL, PR, first, last);
-            if (l == 0) {
-                FLG[cut] |= PCL_HEAD;
-                const uint32_t d = (depth - 1u) << 20;
-                INFO[first] = (cut - first) | d;
-                INFO[cut] = (last - cut) | d;
-                if (cut - first > CG_SORT_THRESHOLD) NXT[atomicAdd(&qc[0], 1u)] = first;
-                if (last - cut > CG_SORT_THRESHOLD) NXT[atomicAdd(&qc[0], 1u)] = cut;
-            }
-        }
-        __syncthreads();
-        ncur = qc[0];
-        uint32_t* t = CUR; CUR = NXT; NXT = t;
-        __syncthreads();
-        if (tid == 0) qc[0] = 0u;
-        __syncthreads();
-    }
-    __syncthreads();
-    PCL_STAMP();
-    // the final insertion passes: a stable sort inside each range of at most 16 (the ranges
-    // are weakly ordered); heapsorted ranges are final. Each range's first lists its positions.
-    uint32_t* SEG = PRE;
-    for (uint32_t i = tid; i < n; i += CG_BLOCK)
-        if ((FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD) {
-            const uint32_t e = i + (INFO[i] & 0xfffffu);
-            for (uint32_t j = i; j < e; j++) SEG[j] = i;
-        }
-    __syncthreads();
-    uint64_t* KEY = W.KEY;
     for (uint32_t i = tid; i < n; i += CG_BLOCK) {
         const uint64_t ri = E[i];
         if (FLG[i] & PCL_HEAP) { KEY[i] = ri; continue; }
-        const uint32_t s0 = SEG[i], e0 = s0 + (INFO[s0] & 0xfffffu);
+        uint32_t s0 = i;   // the range's first, if within 16 positions
+        while (!(FLG[s0] & PCL_HEAD) && s0 + CG_SORT_THRESHOLD > i) s0--;
+        if (!(FLG[s0] & PCL_HEAD)) continue;
+        const uint32_t size = INFO[s0] & 0xfffffu;
+        if (size > CG_SORT_THRESHOLD) continue;   // a task
         const uint32_t ki = pcl_key(ri);
         uint32_t rank = 0;
-        for (uint32_t j = s0; j < e0; j++) {
+        for (uint32_t j = s0; j < s0 + size; j++) {
             const uint32_t kj = pcl_key(E[j]);
             rank += (kj < ki) || (kj == ki && j < i);
         }
         KEY[s0 + rank] = ri;
+    }
+    __syncthreads();
+    PCL_STAMP();
+    // tasks, one after another: each range by the whole workgroup, scratch at its own positions
+    for (uint32_t q = 0; q < ncur; q++) {
+        const uint32_t first = CUR[q];
+        const uint32_t size = INFO[first] & 0xfffffu, depth = INFO[first] >> 20;
+        __syncthreads();   // every thread has the range before pcl_block_sort rewrites INFO[first]
+        pcl_block_sort<PMAX, PbGen>(E + first, KEY + first, size, depth,
+                                    PbScratch<PbGen>{(uint32_t*)W.LAB + first, W.OFF + first, W.A + first,
+                                                     W.PAR + first, W.CNT + first, W.ORD + first},
+                                    red);
     }
     __syncthreads();
     PCL_STAMP();

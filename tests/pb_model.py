@@ -1,0 +1,276 @@
+"""Lane-by-lane model of cg_pcl.h pcl_block_sort (512 threads, PER elements each), with every
+array access bounds-checked, for tests/test_pcl_block_model.py: the same steps, ballots and
+index arithmetic as the device code, checked against libstdc++'s std::sort permutation
+(cg_sort.h restated in Python: tests/pb_model.std_sort)."""
+
+THRESH = 16
+HEAD, FIN, DEPTH, SC_SHIFT, SC_MASK = 0x80000000, 0x40000000, 0xFF, 8, 0x7FF
+
+
+class Arr:
+    """Fixed-size array that raises on any access outside [0, n)."""
+
+    def __init__(self, n, fill=0):
+        self.v = [fill] * n
+
+    def __getitem__(self, i):
+        if not 0 <= i < len(self.v):
+            raise IndexError(f"read {i} of {len(self.v)}")
+        return self.v[i]
+
+    def __setitem__(self, i, x):
+        if not 0 <= i < len(self.v):
+            raise IndexError(f"write {i} of {len(self.v)}")
+        self.v[i] = x
+
+
+def key(r):
+    return r >> 32
+
+
+# ---- libstdc++ std::sort (cg_sort.h restated) ----------------------------------------------
+def _lg(n):
+    r = 0
+    while n > 1:
+        n >>= 1
+        r += 1
+    return r
+
+
+def _adjust_heap(f, base, hole, ln, value):
+    top = hole
+    second = hole
+    while second < (ln - 1) // 2:
+        second = 2 * (second + 1)
+        if key(f[base + second]) < key(f[base + second - 1]):
+            second -= 1
+        f[base + hole] = f[base + second]
+        hole = second
+    if (ln & 1) == 0 and second == (ln - 2) // 2:
+        second = 2 * (second + 1)
+        f[base + hole] = f[base + second - 1]
+        hole = second - 1
+    parent = (hole - 1) // 2
+    while hole > top and key(f[base + parent]) < key(value):
+        f[base + hole] = f[base + parent]
+        hole = parent
+        parent = (hole - 1) // 2
+    f[base + hole] = value
+
+
+def heap_sort_range(f, base, ln):
+    if ln >= 2:
+        parent = (ln - 2) // 2
+        while True:
+            _adjust_heap(f, base, parent, ln, f[base + parent])
+            if parent == 0:
+                break
+            parent -= 1
+    while ln > 1:
+        ln -= 1
+        v = f[base + ln]
+        f[base + ln] = f[base]
+        _adjust_heap(f, base, 0, ln, v)
+
+
+def move_median_to_first(f, result, a, b, c):
+    def lt(i, j):
+        return key(f[i]) < key(f[j])
+
+    def sw(i, j):
+        f[i], f[j] = f[j], f[i]
+
+    if lt(a, b):
+        if lt(b, c):
+            sw(result, b)
+        elif lt(a, c):
+            sw(result, c)
+        else:
+            sw(result, a)
+    elif lt(a, c):
+        sw(result, a)
+    elif lt(b, c):
+        sw(result, c)
+    else:
+        sw(result, b)
+
+
+def std_sort(a, depth0=None):
+    """std::sort(a, a + n) by key; depth0 overrides the depth budget 2 * floor(log2 n)."""
+    f = list(a)
+    n = len(f)
+    if n <= 1:
+        return f
+    stk = [(0, n, 2 * _lg(n) if depth0 is None else depth0)]
+    while stk:
+        first, last, depth = stk.pop()
+        while last - first > THRESH:
+            if depth == 0:
+                heap_sort_range(f, first, last - first)
+                break
+            depth -= 1
+            move_median_to_first(f, first, first + 1, first + (last - first) // 2, last - 1)
+            lo, hi, p = first + 1, last, key(f[first])
+            while True:
+                while key(f[lo]) < p:
+                    lo += 1
+                hi -= 1
+                while p < key(f[hi]):
+                    hi -= 1
+                if not lo < hi:
+                    break
+                f[lo], f[hi] = f[hi], f[lo]
+                lo += 1
+            stk.append((lo, last, depth))
+            last = lo
+    # insertion sort: stable by key
+    return sorted(f, key=key)
+
+
+# ---- the block model ------------------------------------------------------------------------
+BLOCK, WAVES = 512, 8
+ACT, FINB, BUDGET = 0x100, 0x200, 0xFF
+
+
+def _popc(m):
+    return bin(m).count("1")
+
+
+def _setup(E, S, cf, ce, d):
+    info, act = d, False
+    if ce - cf > THRESH:
+        if d == 0:
+            heap_sort_range(E, cf, ce - cf)
+            info |= FINB
+        else:
+            move_median_to_first(E, cf, cf + 1, cf + (ce - cf) // 2, ce - 1)
+            S["PIV"][cf] = key(E[cf])
+            info |= ACT
+            act = True
+    S["INFO"][cf] = info
+    return act
+
+
+def block_sort(E_in, PER=None, depth0=None):
+    """cg_pcl.h pcl_block_sort, thread by thread: element x = tid + 512 k."""
+    n = len(E_in)
+    if PER is None:
+        PER = 1 if n <= 512 else 2 if n <= 1024 else 4
+    assert n <= BLOCK * PER
+    if depth0 is None:
+        depth0 = 2 * _lg(n) if n else 0
+    E = Arr(n)
+    E.v = list(E_in)
+    out = Arr(n)
+    S = {k: Arr(n + 1) for k in ("INFO", "PIV", "RLO", "PL", "PR", "CUT")}
+    cnt = Arr(8 * PER)
+    T = range(BLOCK)
+    fe = [[n << 16] * PER for _ in T]
+    anyact = _setup(E, S, 0, n, depth0) if n else False
+    while anyact:
+        st = [[0] * PER for _ in T]
+        nn = [[0] * PER for _ in T]
+        for k in range(PER):                         # S1
+            ge = [False] * BLOCK
+            le = [False] * BLOCK
+            for t in T:
+                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
+                info = p = kx = 0
+                if x < n:
+                    info, p, kx = S["INFO"][f], S["PIV"][f], key(E[x])
+                part = bool(info & ACT)
+                inn = part and x > f
+                ge[t], le[t] = inn and kx >= p, inn and kx <= p
+                st[t][k] = dict(part=part, inn=inn)
+            for w in range(WAVES):
+                gm = sum(1 << l for l in range(64) if ge[64 * w + l])
+                lm = sum(1 << l for l in range(64) if le[64 * w + l])
+                cnt[k * WAVES + w] = _popc(gm) | (_popc(lm) << 16)
+                for l in range(64):
+                    t = 64 * w + l
+                    st[t][k].update(ge=ge[t], le=le[t], mg=_popc(gm & ((1 << l) - 1)), ml=_popc(lm & ((1 << l) - 1)))
+        c = [cnt[j] for j in range(PER * WAVES)]     # S2
+        for t in T:
+            w = t // 64
+            for k in range(PER):
+                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
+                base = sum(c[j] for j in range(PER * WAVES) if j < k * WAVES + w)
+                q = st[t][k]
+                gx, lx = (base & 0xFFFF) + q["mg"], (base >> 16) + q["ml"]
+                assert gx < 4096 and lx < 4096
+                if q["part"] and x == f:
+                    S["RLO"][f] = gx | (lx << 16)
+                if q["inn"] and x == e - 1:
+                    S["RLO"][f + 1] = (gx + q["ge"]) | ((lx + q["le"]) << 16)
+                q.update(gx=gx, lx=lx)
+        for t in T:                                  # S3
+            for k in range(PER):
+                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
+                q = st[t][k]
+                if q["part"]:
+                    lo, hi = S["RLO"][f], S["RLO"][f + 1]
+                    gf, lf, gend, lend = lo & 0xFFFF, lo >> 16, hi & 0xFFFF, hi >> 16
+                    nn[t][k] = (gend - gf, lend - lf)
+                    if x == f:
+                        S["CUT"][f] = 0
+                    if q["inn"]:
+                        li, ri = q["gx"] - gf, lend - q["lx"] - 1
+                        if q["ge"]:
+                            S["PL"][f + 1 + li] = x
+                        if q["le"]:
+                            S["PR"][f + 1 + ri] = x
+                        q.update(li=li, ri=ri)
+        val = {}
+        for t in T:                                  # S4
+            for k in range(PER):
+                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
+                q = st[t][k]
+                if q["inn"]:
+                    nL, nR = nn[t][k]
+                    partner = x
+                    if q["ge"] and q["li"] < nR:
+                        j = S["PR"][f + 1 + q["li"]]
+                        if x < j:
+                            partner = j
+                            li = q["li"]
+                            if li + 1 >= min(nL, nR) or not S["PL"][f + 2 + li] < S["PR"][f + 2 + li]:
+                                S["CUT"][f] = li + 1
+                    if q["le"] and q["ri"] < nL:
+                        i = S["PL"][f + 1 + q["ri"]]
+                        if i < x:
+                            assert partner == x, "an element swapped twice"
+                            partner = i
+                    if partner != x:
+                        val[x] = E[partner]
+        for x, v in val.items():
+            E[x] = v
+        anyact = False                               # S5
+        for t in T:
+            for k in range(PER):
+                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
+                if st[t][k]["part"] and x == f:
+                    s, nL = S["CUT"][f], nn[t][k][0]
+                    cut = S["PL"][f + 1] if s == 0 else min(S["PL"][f + 1 + s] if s < nL else 0xFFFFFFFF, S["PR"][f + s])
+                    d = (S["INFO"][f] & BUDGET) - 1
+                    anyact |= _setup(E, S, f, cut, d)
+                    anyact |= _setup(E, S, cut, e, d)
+                    S["CUT"][f] = cut
+        for t in T:                                  # S0
+            for k in range(PER):
+                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
+                if st[t][k]["part"]:
+                    cc = S["CUT"][f]
+                    fe[t][k] = (f | (cc << 16)) if x < cc else (cc | (e << 16))
+    for t in T:
+        for k in range(PER):
+            x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
+            if x < n:
+                r = E[x]
+                if S["INFO"][f] & FINB:
+                    out[x] = r
+                else:
+                    assert e - f <= THRESH
+                    kx = key(r)
+                    rank = sum(1 for j in range(f, e) if key(E[j]) < kx or (key(E[j]) == kx and j < x))
+                    out[f + rank] = r
+    return out.v

@@ -1,0 +1,54 @@
+"""Static ISA checks of the built library (no GPU): every gfx950 code object in
+libcones_gpu.so is disassembled and must contain no out-of-line call (s_swappc_b64).
+
+Two out-of-line device calls in this code base preceded failures that were never explained
+("Lessons"): an exact atan2f called from divergent loops (run-to-run keep-word
+changes) and a non-inlined single-wave sort taking a struct through scratch (a GPU memory
+fault in a probe). Every device function on the path is force-inlined instead; this test keeps
+it that way."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "cones_perception_amd", "lib", "libcones_gpu.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _disassembly(tmp_path):
+    fat = tmp_path / "fat.bin"
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", LIB, str(tmp_path / "x.so")],
+                   check=True)
+    data = fat.read_bytes()
+    offs = []
+    i = data.find(MAGIC)
+    while i >= 0:
+        offs.append(i)
+        i = data.find(MAGIC, i + 1)
+    out = []
+    for k, o in enumerate(offs):   # one bundle per translation unit
+        b = tmp_path / f"b{k}.bin"
+        b.write_bytes(data[o: offs[k + 1] if k + 1 < len(offs) else len(data)])
+        co = tmp_path / f"c{k}.co"
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={b}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        out.append(subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(co)], capture_output=True, text=True,
+                                  check=True).stdout)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_no_out_of_line_calls_in_device_code(tmp_path):
+    units = _disassembly(tmp_path)
+    assert len(units) >= 4, "expected one gfx950 code object per HIP source"
+    kernels = 0
+    for text in units:
+        fn = None
+        for line in text.splitlines():
+            if line.endswith(">:"):
+                fn = line
+                kernels += 1
+            assert "s_swappc_b64" not in line, f"out-of-line call in {fn}: {line.strip()}"
+    assert kernels > 50
