@@ -92,3 +92,13 @@ def test_detector_node_with_gpu_classifier():
         out = node.cloud_handler(cp.frame_cloud(raw[0]))
         assert len(out) == 4
     assert sum(m.width for m in out) > 0
+
+
+def test_reference_csv_crops():
+    """The labelled crops of the reference's cones_clouds/cones.csv through cg_classify_colors:
+    images bit-exact, probabilities within PROB_TOL of the float64 restatement."""
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cones_csv.npz"))
+    o = z["offsets"]
+    clouds = [z["points"][o[i]:o[i + 1]] for i in range(len(o) - 1)]
+    col, _ = _compare(clouds)
+    assert list(col) == [1, 1]   # human labels [1, 2]: see test_colornet.test_reference_csv_crops_through_the_restatement
