@@ -196,6 +196,9 @@ def main():
     if rank == 0 and (args.c5 or (world == 1 and not args.no_c5)):
         try:
             c5 = c5_single_gpu(cp, params, local, order=vorder)
+            if vorder != cp.CG_VOXEL_ORDER_POINT:   # the cost of PCL's exact voxel order on C5
+                c5["point_order_ms_per_frame"] = c5_single_gpu(cp, params, local, reps=20,
+                                                               order=cp.CG_VOXEL_ORDER_POINT)["ms_per_frame"]
         except Exception as e:  # noqa: BLE001
             c5 = {"error": repr(e)}
 
@@ -223,6 +226,11 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu:   # rank 0's own batch, timed on this box's host cores
         cpu = cpu_baseline(cp, params, raw, args.cpu_seconds, engines[0], args.cpu_threads, order=vorder)
+        if isinstance(c5, dict) and "error" not in c5:
+            try:
+                c5["cpu_1core"] = c5_cpu(cp, params, c5.pop("_det"), min(args.cpu_seconds, 8.0))
+            except Exception as e:  # noqa: BLE001
+                c5["cpu_1core"] = {"error": repr(e)}
     if world > 1:   # the other ranks wait for rank 0's CPU leg
         dist.barrier()
 
@@ -265,7 +273,7 @@ def main():
         if pcie is not None:
             line["pcie_inclusive"] = pcie
         if c5 is not None:
-            line["c5_single_gpu"] = c5
+            line["c5_single_gpu"] = {k: v for k, v in c5.items() if not k.startswith("_")}
         if c5t is not None:
             line["c5_tiled"] = c5t
         if scatter is not None:
@@ -490,11 +498,37 @@ def c5_single_gpu(cp, params, device, reps=50, order=None):
     r = eng.fetch(0)
     V, C = int(r.voxels.shape[0]), int(r.centroids.shape[0])
     algo = 16.0 * n + 20.0 * V + 8.0 * C + 64.0
-    return {"ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt, "points": n, "K": r.n_kept,
+    return {"_det": (raw, r), "ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt, "points": n, "K": r.n_kept,
             "M": r.n_filtered, "V": V, "C": C,
             "algorithmic_GBs": algo / dt / 1e9, "hbm_frac": algo / dt / 1e9 / HBM_PEAK_GBS,
             "includes": "device-resident input; one host round trip per frame (survivor count "
                         "and bounds size the backend); backend latency-bound (sorts, union-find)"}
+
+
+def c5_cpu(cp, params, det, budget_s):
+    """C5's frame through the CPU restatement (oracle/, one core, sequential) for about
+    budget_s, and the GPU's result for it (c5_single_gpu) compared bit for bit with the oracle
+    in PCL's voxel order."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    from helpers import assert_same_detection
+    raw, got = det
+    msg = cp.frame_cloud(raw[0])
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ref, _ = O.run(params, msg, O.MODE_PIPELINE)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 50:
+            break
+    try:
+        assert_same_detection(got, ref, "C5")
+        exact = True
+    except AssertionError:
+        exact = False
+    return {"ms_per_frame": el / n * 1e3, "frames_per_s": n / el, "cores": 1, "kind": "port",
+            "sample": f"{n} C5 frames (1,048,576 points, sequential), {el:.1f} s, oracle/cg_oracle.cpp",
+            "gpu_bit_exact_vs_oracle_pcl_order": exact}
 
 
 def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):

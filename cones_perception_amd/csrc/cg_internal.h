@@ -150,11 +150,13 @@ struct LgScratch {
                               // one workgroup (same-address atomics from every chunk serialise)
     uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
     uint32_t pq_cap;          //   entries
+    uint64_t* pqst;           //   the partition levels' look-back words (tickets, finished, per tile)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };
 // Bytes of the large-frame scratch for frames of n points, and its layout at base.
 uint64_t cg_large_bytes(uint32_t n_points);
+uint32_t cg_large_pq_words();   // words of the PCL sort's range lists (diagnostics)
 void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
 // Run n_frames frames of more than CG_MAX_POINTS points, one at a time (synchronises s).
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s);

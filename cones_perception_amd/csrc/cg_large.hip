@@ -771,15 +771,33 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 // ------------------------------------------------------------------------------------------
 // PCL's voxel order for the global backend (cg_pcl.h has the algorithm). index_vector is the
 // finite detector-input points in frame-index order; lg_scan_emit lists them as records
-// (idx << 32 | slot) (PclCompact*), then libstdc++'s introsort runs on them level by level:
-// lg_pcl_level partitions every range of the level longer than LG_PCL_LEAF with one workgroup
-// in HBM (median of three, the parallel Hoare partition: per-wave segment counts, the L and R
-// lists, the swaps), and lg_pcl_leaf finishes each remaining range with pcl_sort, in LDS when
-// it fits, with the depth left on its path, writing (idx, slot) pairs in std::sort's order.
-// Ranges are disjoint, so their order inside a level does not matter; the levels are separate
-// launches (no workgroup waits on another).
-#define LG_PCL_LEAF 2048
-#define LG_PQ_HDR 8            // list counts (four used)
+// (idx << 32 | slot) (PclCompact*), then libstdc++'s introsort runs on them level by level.
+// Each level of ranges longer than LG_PCL_LEAF is two launches, one workgroup per tile of
+// PQ_T elements of a range:
+//   lg_pq_split: every tile of a range computes the range's median of three (the swap with the
+//     first is virtual: V(m) = E[first], V(first) = E[m]), compares its elements with the
+//     pivot, and a decoupled look-back segmented by range (tickets: a tile only waits on tiles
+//     already running) gives each element its index in the range's L list (>= pivot, from the
+//     left) and in the ascending list of <= pivot elements; both lists are written, and each
+//     element's two indices; the range's last tile notes both totals;
+//   lg_pq_swap: the k-th swap pairs L_k with R_k (the k-th <= pivot element from the right)
+//     while L_k < R_k; each element finds its partner with two list reads and writes V of it
+//     (or itself) to the other buffer; the last swap (or L_0 when there is none) computes the
+//     cut and queues both children: longer than LG_PCL_LEAF (budget left) for the next level,
+//     else as leaves (with the buffer they are in).
+// Median-of-three cuts are uneven (C5's index_vector of 49k records takes ~6 levels to reach
+// 4096-element ranges), so the host launches three levels more than an even split needs; a
+// level with no range returns at once. lg_pcl_leaf finishes each leaf with pcl_block_sort in
+// LDS (up to 4096 records, 8 per thread, results straight to the outputs), with the depth
+// budget left on its path; a range still longer (a degenerate split) in HBM.
+#define LG_PCL_LEAF 4096
+#define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR
+#define PQ_LEAFLIST 3
+#define PQ_EW 5                // entry words: first, last, depth, then nL, nR (levels) / buffer (leaves)
+#define PQ_T CG_BLOCK          // elements per tile
+#define PQ_MAXR 2048           // ranges per level (levels <= 11)
+#define LG_PQ_LEVELS_MAX 11
+#define LG_PQ_CAP ((2u << LG_PQ_LEVELS_MAX) + 64)   // entries per list: a level pushes <= 2 per range
 struct PclCompactFlag {   // finite points (non-finite keys carry idx 0xffffffff)
     const uint64_t* key; uint32_t PB;
     __device__ uint32_t operator()(uint32_t j) const { return (uint32_t)(key[j] >> PB) != 0xffffffffu ? 1u : 0u; }
@@ -791,161 +809,271 @@ struct PclCompactEmit {
     }
 };
 
-// Bytes of LDS for a leaf: E and KEY (8 B), seven word arrays (n + 4 each)
-#define LG_PCL_LDS (2 * 8 * LG_PCL_LEAF + 7 * 4 * (LG_PCL_LEAF + 4))
-
 __device__ __forceinline__ uint32_t pq_key(const uint64_t* E, uint32_t x) {
     return ((const uint32_t*)E)[2 * x + 1];
 }
-// One workgroup: __unguarded_partition(first + 1, last, pivot = first) after the median of
-// three, over E in HBM; PL / PR hold the L and R lists. Returns the cut (all threads).
-__device__ uint32_t lg_pcl_partition(uint64_t* E, uint32_t* PL, uint32_t* PR, uint32_t first, uint32_t last) {
-    __shared__ uint32_t sh[4 * WAVES + 4];
-    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
-    if (tid == 0) {
-        cg_move_median_to_first(E, (long)first, (long)first + 1, (long)(first + (last - first) / 2), (long)last - 1,
-                                [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
-        sh[4 * WAVES] = pq_key(E, first);
-        sh[4 * WAVES + 1] = 0u;
+__device__ __forceinline__ uint32_t* pq_list(const LgScratch& S, uint32_t which) {
+    return S.pq + LG_PQ_HDR + (uint64_t)which * PQ_EW * LG_PQ_CAP;
+}
+__device__ __forceinline__ void pq_push(const LgScratch& S, uint32_t which, uint32_t first, uint32_t last, uint32_t depth,
+                                        uint32_t w3) {
+    const uint32_t i = atomicAdd(&S.pq[which], 1u);
+    if (i < LG_PQ_CAP) {
+        uint32_t* e = pq_list(S, which) + PQ_EW * i;
+        e[0] = first; e[1] = last; e[2] = depth; e[3] = w3;
     }
-    __syncthreads();
-    const uint32_t p = sh[4 * WAVES];
-    const uint32_t a = first + 1, m = last - a;
-    const uint32_t seg = ((m + WAVES - 1) / WAVES + 63u) & ~63u;   // each wave: a contiguous segment
-    const uint32_t s0 = min(a + w * seg, last), s1 = min(s0 + seg, last);
-    uint32_t cge = 0, cle = 0;
-    for (uint32_t x0 = s0; x0 < s1; x0 += 256) {   // four strips of 64 in flight
-        uint32_t k[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) { const uint32_t x = x0 + 64 * q + l; k[q] = x < s1 ? pq_key(E, x) : 0u; }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const bool in = x0 + 64 * q + l < s1;
-            cge += (uint32_t)__popcll(__ballot(in && k[q] >= p));
-            cle += (uint32_t)__popcll(__ballot(in && k[q] <= p));
-        }
+}
+// The ranges of a level (level 0: the whole index_vector when it needs partitioning) and the
+// tiles of each: tp[r] = first tile of range r (block-wide, ends with a barrier). Returns the
+// number of tiles.
+__device__ __forceinline__ uint32_t pq_tiles(const LgScratch& S, uint32_t level, uint32_t* tp, uint32_t* red,
+                                             uint32_t& nr) {
+    if (level == 0) {
+        const uint32_t n = S.meta[LG_PCL_N];
+        nr = n > LG_PCL_LEAF ? 1u : 0u;
+        const uint32_t nt = nr ? (n - 1 + PQ_T - 1) / PQ_T : 0u;
+        if (threadIdx.x == 0) { tp[0] = 0; tp[1] = nt; }
+        __syncthreads();
+        return nt;
     }
-    if (l == 0) { sh[w] = cge; sh[WAVES + w] = cle; }
+    nr = min(S.pq[level % 3u], (uint32_t)PQ_MAXR);
+    const uint32_t* L = pq_list(S, level % 3u);
+    const uint32_t nt = block_scan(
+        nr, [&](uint32_t r) -> uint32_t { return (L[PQ_EW * r + 1] - L[PQ_EW * r] - 1 + PQ_T - 1) / PQ_T; },
+        [&](uint32_t r, uint32_t e) { tp[r] = e; }, red);
+    if (threadIdx.x == 0) tp[nr] = nt;
     __syncthreads();
-    uint32_t bge = 0, ble = 0, nL = 0, nR = 0;
-    for (uint32_t v = 0; v < WAVES; v++) {
-        bge += v < w ? sh[v] : 0u;
-        ble += v < w ? sh[WAVES + v] : 0u;
-        nL += sh[v];
-        nR += sh[WAVES + v];
+    return nt;
+}
+__device__ __forceinline__ void pq_range(const LgScratch& S, uint32_t level, uint32_t r, uint32_t& f, uint32_t& e,
+                                         uint32_t& d) {
+    if (level == 0) {
+        f = 0; e = S.meta[LG_PCL_N]; d = (uint32_t)(2 * cg_lg((long)e));
+        return;
     }
-    for (uint32_t x0 = s0; x0 < s1; x0 += 64) {
-        const uint32_t x = x0 + l;
-        const uint32_t k = x < s1 ? pq_key(E, x) : 0u;
-        const uint64_t ge = __ballot(x < s1 && k >= p), le = __ballot(x < s1 && k <= p);
-        if (x < s1 && k >= p) PL[a + bge + mbcnt(ge)] = x;
-        if (x < s1 && k <= p) PR[a + (nR - 1u - (ble + mbcnt(le)))] = x;
-        bge += (uint32_t)__popcll(ge);
-        ble += (uint32_t)__popcll(le);
+    const uint32_t* L = pq_list(S, level % 3u) + PQ_EW * r;
+    f = L[0]; e = L[1]; d = L[2];
+}
+// range of tile t: the last r with tp[r] <= t
+__device__ __forceinline__ uint32_t pq_find(const uint32_t* tp, uint32_t nr, uint32_t t) {
+    uint32_t lo = 0, hi = nr - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (tp[mid] <= t) lo = mid; else hi = mid - 1;
     }
-    __syncthreads();
-    // swaps (L_k, R_k) while L_k < R_k (a prefix of k): count them, swap in parallel
-    const uint32_t m2 = min(nL, nR);
-    uint32_t cnt = 0;
-    for (uint32_t k = tid; k < m2; k += CG_BLOCK) {
-        const uint32_t i = PL[a + k], j = PR[a + k];
-        if (i < j) {
-            const uint64_t t = E[i];
-            E[i] = E[j];
-            E[j] = t;
-            cnt++;
-        }
-    }
-    cnt = wave_sum(cnt);
-    if (l == 0 && cnt) atomicAdd(&sh[4 * WAVES + 1], cnt);
-    __syncthreads();
-    const uint32_t sw = sh[4 * WAVES + 1];
-    const uint32_t cut = sw == 0 ? PL[a] : min(sw < nL ? PL[a + sw] : 0xffffffffu, PR[a + sw - 1]);
-    __syncthreads();
-    return cut;
+    return lo;
+}
+// __move_median_to_first(first, first + 1, mid, last - 1) of [f, e): index and key of the median
+__device__ __forceinline__ void pq_median(const uint64_t* E, uint32_t f, uint32_t e, uint32_t& m, uint32_t& p) {
+    const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
+    const uint32_t ka = pq_key(E, a), kb = pq_key(E, b), kc = pq_key(E, c);
+    m = pb_median(a, b, c, ka, kb, kc);
+    p = m == a ? ka : (m == b ? kb : kc);
+}
+__device__ __forceinline__ uint64_t pq_v(const uint64_t* E, uint32_t f, uint32_t m, uint32_t x) {
+    return E[x == m ? f : (x == f ? m : x)];
 }
 
-// Range lists of the level-synchronous sort (S.pq): four counts, then four lists of
-// (first, last, depth) triples, S.pq_cap entries each. Level lv partitions the ranges of list
-// lv % 3, queues the parts on list (lv + 1) % 3 and clears list (lv + 2) % 3 for the level
-// after it; list 3 collects the leaves.
-#define PQ_LEAF 3
-__device__ __forceinline__ uint32_t* pq_list(const LgScratch& S, uint32_t which) {
-    return S.pq + LG_PQ_HDR + (uint64_t)which * 3 * S.pq_cap;
-}
-__device__ __forceinline__ void pq_push(const LgScratch& S, uint32_t which, uint32_t first, uint32_t last, uint32_t depth) {
-    const uint32_t i = atomicAdd(&S.pq[which], 1u);
-    if (i < S.pq_cap) {
-        uint32_t* e = pq_list(S, which) + 3 * i;
-        e[0] = first; e[1] = last; e[2] = depth;
+// Decoupled look-back over tiles [lo, t) of one range, 64-bit status words: flags in bits
+// 62 / 63, the >= count in bits 32..61, the <= count in bits 0..31 (counts < 2^30).
+#define PQ_ST_A (1ull << 62)
+#define PQ_ST_P (1ull << 63)
+#define PQ_ST_V (~(PQ_ST_A | PQ_ST_P))
+__device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint32_t t, uint64_t count) {
+    const uint32_t l = lane_id();
+    if (t == lo) {
+        if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
     }
-}
-// One level of __introsort_loop: workgroup b partitions range b of the level's list (level 0:
-// the whole index_vector). Parts longer than LG_PCL_LEAF with depth left are queued for the
-// next level (leaves after the last level); the others, and every range whose depth budget
-// is spent (pcl_sort runs the heapsort fallback), are leaves.
-__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_level(LgScratch S, uint64_t* E, uint32_t level, uint32_t last_level) {
-    const uint32_t cur = level % 3u, nxt = (level + 1u) % 3u;
-    uint32_t first, last, depth;
-    if (level == 0) {
-        if (blockIdx.x) return;
-        first = 0; last = S.meta[LG_PCL_N]; depth = (uint32_t)(2 * cg_lg((long)last));
-        if (threadIdx.x == 0) { S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAF] = 0; }
-        if (last <= LG_PCL_LEAF || depth == 0) {
-            if (threadIdx.x == 0) pq_push(S, PQ_LEAF, first, last, depth);
-            return;
+    if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_A | count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t base = 0;
+    int32_t hi = (int32_t)t - 1;
+    for (;;) {
+        const int32_t j = hi - (int32_t)l;
+        const uint64_t w = j >= (int32_t)lo ? __hip_atomic_load(&ts[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                             : PQ_ST_P;
+        const uint64_t pm = __ballot((w & PQ_ST_P) != 0ull);
+        const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
+        if (__ballot(w == 0ull && l < first)) {   // a tile before the nearest prefix not published yet
+            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
-    } else {
-        if (blockIdx.x == 0 && threadIdx.x == 0) S.pq[(level + 2u) % 3u] = 0;
-        const uint32_t n = min(S.pq[cur], S.pq_cap);
-        if (blockIdx.x >= n) return;
-        const uint32_t* e = pq_list(S, cur) + 3 * blockIdx.x;
-        first = e[0]; last = e[1]; depth = e[2];
+        const uint64_t v = l <= first ? (w & PQ_ST_V) : 0ull;
+        base += ((uint64_t)wave_sum((uint32_t)(v >> 32)) << 32) | wave_sum((uint32_t)v);
+        if (first < 64u) break;
+        hi -= 64;
     }
-    const uint32_t cut = lg_pcl_partition(E, S.par, S.cnt, first, last);
-    if (threadIdx.x == 0) {
+    if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | (base + count), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return base;
+}
+
+__global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint64_t* E, uint32_t level) {
+    __shared__ uint32_t tp[PQ_MAXR + 1];
+    __shared__ uint32_t red[8 * WAVES];
+    __shared__ uint32_t tk, cg[WAVES], cl[WAVES], last;
+    __shared__ uint64_t tbase;
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    if (level == 0 && blockIdx.x == 0 && tid == 0) {
+        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0;
+        const uint32_t n = S.meta[LG_PCL_N];
+        if (n <= LG_PCL_LEAF) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
+    }
+    uint32_t nr;
+    const uint32_t active = pq_tiles(S, level, tp, red, nr);
+    if (blockIdx.x >= active) return;
+    uint64_t* st = S.pqst;   // [0] tickets, [1] finished tiles, [2 + t] tile t's status
+    if (tid == 0) tk = (uint32_t)__hip_atomic_fetch_add(&st[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t t = tk, r = pq_find(tp, nr, t), q = t - tp[r];
+    uint32_t f, e, d, m, p;
+    pq_range(S, level, r, f, e, d);
+    pq_median(E, f, e, m, p);
+    const uint32_t x = f + 1 + q * PQ_T + tid;
+    const bool valid = x < e;
+    const uint32_t k = valid ? pcl_key(pq_v(E, f, m, x)) : 0u;
+    const bool ge = valid && k >= p, le = valid && k <= p;
+    const uint64_t gm = __ballot(ge), lm = __ballot(le);
+    if (l == 0) { cg[w] = (uint32_t)__popcll(gm); cl[w] = (uint32_t)__popcll(lm); }
+    __syncthreads();
+    if (w == 0) {
+        uint32_t tg = 0, tl = 0;
+        for (uint32_t v = 0; v < WAVES; v++) { tg += cg[v]; tl += cl[v]; }
+        const uint64_t b = pq_lookback(st + 2, tp[r], t, ((uint64_t)tg << 32) | tl);
+        if (l == 0) {
+            tbase = b;
+            if (t == tp[r + 1] - 1) {   // the range's last tile: both totals
+                uint32_t* tot = level == 0 ? S.pq + 4 : pq_list(S, level % 3u) + PQ_EW * r + 3;
+                tot[0] = (uint32_t)(b >> 32) + tg;
+                tot[1] = (uint32_t)b + tl;
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t gi = (uint32_t)(tbase >> 32) + mbcnt(gm), li = (uint32_t)tbase + mbcnt(lm);
+    for (uint32_t v = 0; v < w; v++) { gi += cg[v]; li += cl[v]; }
+    if (ge) S.par[f + 1 + gi] = x;
+    if (le) S.cnt[f + 1 + li] = x;
+    if (valid) ((uint64_t*)S.vox)[x] = ((uint64_t)gi << 32) | li;
+    // the last tile to finish resets the status words for the next level
+    __syncthreads();
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(&st[1], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
+    __syncthreads();
+    if (last) {
+        __threadfence();
+        for (uint32_t i = tid; i < active + 2; i += CG_BLOCK) st[i] = 0;
+    }
+}
+
+__global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64_t* E, uint64_t* Eo, uint32_t level,
+                                                       uint32_t last_level, uint32_t out_buf) {
+    __shared__ uint32_t tp[PQ_MAXR + 1];
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid == 0 && level > 0) S.pq[(level + 2u) % 3u] = 0;   // the list level + 1 fills
+    uint32_t nr;
+    const uint32_t active = pq_tiles(S, level, tp, red, nr);
+    if (blockIdx.x >= active) return;
+    const uint32_t t = blockIdx.x, r = pq_find(tp, nr, t), q = t - tp[r];
+    uint32_t f, e, d, m, p;
+    pq_range(S, level, r, f, e, d);
+    const uint32_t* tot = level == 0 ? S.pq + 4 : pq_list(S, level % 3u) + PQ_EW * r + 3;
+    const uint32_t nL = tot[0], nR = tot[1];
+    pq_median(E, f, e, m, p);
+    const uint32_t x = f + 1 + q * PQ_T + tid;
+    if (q == 0 && tid == 0) Eo[f] = E[m];
+    if (x >= e) return;
+    const uint64_t vx = pq_v(E, f, m, x);
+    const uint32_t k = pcl_key(vx);
+    const bool ge = k >= p, le = k <= p;
+    const uint64_t rk = ((const uint64_t*)S.vox)[x];
+    const uint32_t gi = (uint32_t)(rk >> 32), li = (uint32_t)rk;
+    uint32_t partner = x;
+    bool cutter = false;
+    uint32_t cut = 0;
+    if (ge && gi < nR) {
+        const uint32_t j = S.cnt[f + 1 + (nR - 1 - gi)];   // R_gi
+        if (x < j) {
+            partner = j;
+            const bool nx = gi + 1 < min(nL, nR);
+            const uint32_t l2 = nx ? S.par[f + 2 + gi] : 0xffffffffu;
+            const uint32_t r2 = nx ? S.cnt[f + 1 + (nR - 2 - gi)] : 0u;
+            if (!nx || !(l2 < r2)) {   // swap gi is the last: s = gi + 1
+                cutter = true;
+                cut = min(gi + 1 < nL ? S.par[f + 2 + gi] : 0xffffffffu, j);
+            }
+        } else if (gi == 0) {   // no swap at all: the left scan stops at L_0
+            cutter = true;
+            cut = x;
+        }
+    }
+    if (le) {
+        const uint32_t ri = nR - 1 - li;
+        if (ri < nL) {
+            const uint32_t i = S.par[f + 1 + ri];   // L_ri
+            if (i < x) partner = i;
+        }
+    }
+    Eo[x] = partner == x ? vx : pq_v(E, f, m, partner);
+    if (cutter) {
+        const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
         for (int c = 0; c < 2; c++) {
-            const uint32_t f = c ? cut : first, l = c ? last : cut, d = depth - 1u;
-            pq_push(S, (l - f > LG_PCL_LEAF && d > 0 && level < last_level) ? nxt : PQ_LEAF, f, l, d);
+            if (hi[c] - lo[c] > LG_PCL_LEAF && d > 1 && level < last_level)
+                pq_push(S, (level + 1u) % 3u, lo[c], hi[c], d - 1u, 0u);
+            else
+                pq_push(S, PQ_LEAFLIST, lo[c], hi[c], d - 1u, out_buf);
         }
     }
 }
-// The rest of each leaf range (cg_pcl.h pcl_sort with the depth left on its path): in LDS
-// when it fits, else in HBM (ranges are disjoint, so each uses its own span of the scratch
-// arrays); out as (idx, slot) pairs in std::sort's order.
-__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E, uint64_t* kout, uint32_t* vout) {
+
+// A leaf's results straight to the outputs: idx in the key array, slot in the value array.
+struct PqLeafOut {
+    uint64_t* k; uint32_t* v; uint32_t base;
+    __device__ __forceinline__ void operator()(uint32_t i, uint64_t r) const {
+        k[base + i] = r >> 32;
+        v[base + i] = (uint32_t)r;
+    }
+};
+#define LG_PCL_LDS (8 * LG_PCL_LEAF + 6 * 4 * (LG_PCL_LEAF + 4))
+// The rest of each leaf range (cg_pcl.h pcl_block_sort with the depth left on its path) from
+// the buffer its last level wrote: in LDS (8 B of record and 24 B of scratch per element),
+// else in HBM (ranges are disjoint, so each uses its own span of the scratch arrays).
+__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
+                                                        uint32_t* vout) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PCL_LDS];
     __shared__ uint32_t red[8 * WAVES];
-    const uint32_t n = min(S.pq[PQ_LEAF], S.pq_cap);
+    const uint32_t n = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
     const uint32_t tid = threadIdx.x;
     for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
-        const uint32_t* e = pq_list(S, PQ_LEAF) + 3 * b;
-        const uint32_t first = e[0], last = e[1], depth = e[2], size = last - first;
-        Work W{};
-        uint64_t* El;
+        const uint32_t* ent = pq_list(S, PQ_LEAFLIST) + PQ_EW * b;
+        const uint32_t first = ent[0], last = ent[1], depth = ent[2], size = last - first;
+        uint64_t* const E = ent[3] ? E1 : E0;
         if (size <= LG_PCL_LEAF) {
-            El = (uint64_t*)smem;
-            uint32_t* w0 = (uint32_t*)(El + 2 * LG_PCL_LEAF);
-            W.KEY = El + LG_PCL_LEAF;
-            W.A = w0; W.PAR = w0 + (LG_PCL_LEAF + 4); W.CNT = w0 + 2 * (LG_PCL_LEAF + 4);
-            W.UK = w0 + 3 * (LG_PCL_LEAF + 4); W.ORD = w0 + 4 * (LG_PCL_LEAF + 4);
-            W.LAB = (int32_t*)(w0 + 5 * (LG_PCL_LEAF + 4)); W.OFF = w0 + 6 * (LG_PCL_LEAF + 4);
+            lds_u64* const El = (lds_u64*)(uint64_t*)smem;
+            lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * LG_PCL_LEAF);
+            const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4),
+                                      w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
+            lds_u32* const Rl = (lds_u32*)red;
+            const PqLeafOut out{kout, vout, first};
             for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
             __syncthreads();
-        } else {   // the range's own span of the HBM arrays (A needs size + 1: first + size <= N)
-            El = E + first;
+            if (size <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, size, depth, PS, Rl);
+            else if (size <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, size, depth, PS, Rl);
+            else if (size <= 4 * CG_BLOCK) pcl_block_sort<4, PbLds>(El, out, size, depth, PS, Rl);
+            else pcl_block_sort<8, PbLds>(El, out, size, depth, PS, Rl);
+        } else {   // the range's own span of the HBM arrays
+            Work W{};
             W.KEY = (uint64_t*)S.vox + 2ull * first;
             W.A = S.lab + first; W.PAR = S.par + first; W.CNT = S.cnt + first; W.UK = S.uk + first;
             W.ORD = S.ord + first; W.LAB = (int32_t*)S.rank + first; W.OFF = S.off + first;
+            pcl_sort<2, false>(W, E + first, size, red, (int)depth);
+            for (uint32_t i = tid; i < size; i += CG_BLOCK) {
+                const uint64_t rr = W.KEY[i];
+                kout[first + i] = rr >> 32;
+                vout[first + i] = (uint32_t)rr;
+            }
+            __syncthreads();
         }
-        if (size <= LG_PCL_LEAF) pcl_sort<4, true>(W, El, size, red, (int)depth);
-        else pcl_sort<4, false>(W, El, size, red, (int)depth);
-        for (uint32_t i = tid; i < size; i += CG_BLOCK) {
-            const uint64_t r = W.KEY[i];
-            kout[first + i] = r >> 32;
-            vout[first + i] = (uint32_t)r;
-        }
-        __syncthreads();
     }
 }
 
@@ -1425,24 +1553,28 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
         buf = radix_sort(S, Mtot, key_bits, s);
     } else {
         // PCL's order: index_vector (finite points in frame-index order) as (idx, slot)
-        // records, then std::sort's permutation of it (lg_pcl_level, lg_pcl_leaf)
+        // records, then std::sort's permutation of it (lg_pq_split, lg_pq_swap, lg_pcl_leaf)
         buf = PB ? radix_sort(S, Mtot, PB, s) : 0;   // unsorted tiles: frame-index order first
         uint64_t* kb[2] = {S.key0, S.key1};
         uint32_t* vb2[2] = {S.val0, S.val1};
         scan_emit(S, Mtot, -1, PclCompactFlag{kb[buf], PB}, PclCompactEmit{kb[buf], vb2[buf], kb[buf ^ 1], PB},
                   LG_PCL_N, s);
-        // levels until every range fits a leaf, then the leaves
-        // (median-of-three cuts are uneven: three levels more than an even split needs keep the
-        // leaves within LG_PCL_LEAF and out of the slow HBM form; levels past the last range
-        // to cut return at once)
-        uint32_t levels = 1;
-        while (((uint64_t)LG_PCL_LEAF << (levels - 1)) < Mtot) levels++;
-        if (levels > 1) levels += 3;
-        for (uint32_t lv = 0; lv < levels; lv++)
-            hipLaunchKernelGGL(lg_pcl_level, dim3(lv ? (1u << lv) : 1u), dim3(CG_BLOCK), 0, s, S, kb[buf ^ 1], lv,
-                               levels - 1);
-        hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (1u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
-                           kb[buf ^ 1], kb[buf], vb2[buf]);
+        // the levels an even split needs until every range fits a leaf, three more for uneven
+        // median-of-three cuts; levels with no range to cut return at once; then the leaves
+        uint32_t levels = 0;
+        while (((uint64_t)LG_PCL_LEAF << levels) < Mtot) levels++;
+        if (levels) levels = std::min<uint32_t>(levels + 3, LG_PQ_LEVELS_MAX);
+        const uint32_t tb = (Mtot + PQ_T - 1) / PQ_T;
+        hipLaunchKernelGGL(lg_pq_split, dim3(std::max<uint32_t>(tb, 1)), dim3(CG_BLOCK), 0, s, S, kb[buf ^ 1], 0u);
+        for (uint32_t lv = 0; lv < levels; lv++) {
+            uint64_t* const Ein = lv % 2 ? kb[buf] : kb[buf ^ 1];
+            uint64_t* const Eout = lv % 2 ? kb[buf ^ 1] : kb[buf];
+            const uint32_t grid = tb + (1u << lv);
+            if (lv) hipLaunchKernelGGL(lg_pq_split, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, lv);
+            hipLaunchKernelGGL(lg_pq_swap, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
+        }
+        hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
+                           kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
         run_pb = 0;   // sorted keys are the idx alone
     }
     const uint64_t* vkey = buf ? S.key1 : S.key0;
@@ -1519,11 +1651,13 @@ uint64_t lg_walk(uint32_t n, F place) {
     for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));
     place(28, take((uint64_t)(LG_DCELLS_MAX + 2) * 4));
     place(29, take(nch * LG_CS_WORDS * 4));
-    place(30, take(LG_PQ_HDR * 4 + (N + 64) * 12 * 4));   // PCL sort range lists: 4 x (first, last, depth)
+    place(30, take((LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP) * 4));   // PCL sort range lists
+    place(31, take((2 + (N + PQ_T - 1) / PQ_T + PQ_MAXR + 2) * 8));   // their look-back words
     return off;
 }
 }  // namespace
 uint64_t cg_large_bytes(uint32_t n) { return lg_walk(n, [](int, uint64_t) {}); }
+uint32_t cg_large_pq_words() { return LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP; }
 void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
     uint32_t** arr[12] = {&S.par, &S.cnt, &S.lab, &S.uk, &S.ca, &S.ord, &S.droot, &S.dsz, &S.rank, &S.fin, &S.off, &S.rk};
     lg_walk(n, [&](int k, uint64_t o) {
@@ -1545,7 +1679,8 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 15: S.run = (uint32_t*)p; break;
             case 28: S.cstart = (uint32_t*)p; break;
             case 29: S.cstat = (uint32_t*)p; break;
-            case 30: S.pq = (uint32_t*)p; S.pq_cap = std::max<uint32_t>(n, 1) + 64; break;
+            case 30: S.pq = (uint32_t*)p; S.pq_cap = LG_PQ_CAP; break;
+            case 31: S.pqst = (uint64_t*)p; break;
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
     });

@@ -192,8 +192,14 @@ __device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K
 
 // Always inlined: an out-of-line call takes its arguments through scratch memory (and
 // tests/test_isa.py asserts that no kernel makes a call).
-template <int PER, class K>
-__device__ __forceinline__ void pcl_block_sort(typename K::P64 E, typename K::P64 out, uint32_t n, uint32_t depth0,
+// The sorted records go through out(position, record): an array store, or straight to the
+// caller's global outputs (lg_pcl_leaf).
+template <class P> struct PbStore {
+    P a;
+    __device__ __forceinline__ void operator()(uint32_t i, uint64_t r) const { a[i] = r; }
+};
+template <int PER, class K, class OUT = PbStore<typename K::P64>>
+__device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint32_t n, uint32_t depth0,
                                                const PbScratch<K> S, typename K::P32 cnt) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     constexpr uint32_t GE = 1u << 24, LE = 1u << 25, IN = 1u << 26, PART = 1u << 27;
@@ -336,14 +342,14 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, typename K::P6
 #pragma unroll
             for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++) kj[j] = f + j < e ? pcl_key(E[f + j]) : 0u;
             if (info & PB_FIN) {
-                out[x] = r;
+                out(x, r);
             } else {
                 const uint32_t kx = pcl_key(r);
                 uint32_t rank = 0;
 #pragma unroll
                 for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++)
                     rank += f + j < e && ((kj[j] < kx) || (kj[j] == kx && f + j < x));
-                out[f + rank] = r;
+                out(f + rank, r);
             }
         }
     }
@@ -380,14 +386,19 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         lds_u64* const El = (lds_u64*)E;
         lds_u64* const Ko = (lds_u64*)W.KEY;
         lds_u32* const Rl = (lds_u32*)red;
-        if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, Ko, n, d0, PS, Rl);
-        else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, Ko, n, d0, PS, Rl);
-        else pcl_block_sort<PMAX, PbLds>(El, Ko, n, d0, PS, Rl);
+        const PbStore<lds_u64*> out{Ko};
+        if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, n, d0, PS, Rl);
+        else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, n, d0, PS, Rl);
+        else pcl_block_sort<PMAX, PbLds>(El, out, n, d0, PS, Rl);
         PCL_STAMP();
         return;
     }
     const PbScratch<PbGen> PS{(uint32_t*)W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD};
-    if (n <= PMAX * CG_BLOCK) { pcl_block_sort<PMAX, PbGen>(E, W.KEY, n, d0, PS, red); PCL_STAMP(); return; }
+    if (n <= PMAX * CG_BLOCK) {
+        pcl_block_sort<PMAX, PbGen>(E, PbStore<uint64_t*>{W.KEY}, n, d0, PS, red);
+        PCL_STAMP();
+        return;
+    }
     const bool big = true;
     for (uint32_t i = tid; i < n; i += CG_BLOCK) {
         RID[i] = big ? 0u : PCL_INACT;
@@ -414,25 +425,28 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
             SC[i] = 0u;
         }
         __syncthreads();
-        // (2) counts of >= pivot (low half) and <= pivot (high half) before each position
-        block_scan(
-            n + 1,
+        // (2) counts of >= pivot (low half) and <= pivot (high half) before each position;
+        // the total (the count before position n) stays on chip: the word after the array is
+        // the next range's first word when leaves of one frame run side by side in HBM
+        const uint32_t ptot = block_scan(
+            n,
             [&](uint32_t i) -> uint32_t {
-                if (i >= n) return 0u;
                 const uint32_t r = RID[i];
                 if (r == PCL_INACT || r == i) return 0u;
                 const uint32_t k = pcl_key(E[i]), p = PIV[r];
                 return (k >= p ? 1u : 0u) | (k <= p ? 0x10000u : 0u);
             },
             [&](uint32_t i, uint32_t e) { PRE[i] = e; }, red);
+        __syncthreads();
+        auto pre = [&](uint32_t i) -> uint32_t { return i < n ? PRE[i] : ptot; };
         // (3) L and R lists of every range, stored from first + 1
         for (uint32_t i = tid; i < n; i += CG_BLOCK) {
             const uint32_t r = RID[i];
             if (r == PCL_INACT || r == i) continue;
-            const uint32_t last = r + (INFO[r] & 0xfffffu), lo = PRE[r + 1];
+            const uint32_t last = r + (INFO[r] & 0xfffffu), lo = pre(r + 1);
             const uint32_t k = pcl_key(E[i]), p = PIV[r];
             if (k >= p) PL[r + 1 + (PRE[i] & 0xffffu) - (lo & 0xffffu)] = i;
-            if (k <= p) PR[r + 1 + (PRE[last] >> 16) - (PRE[i + 1] >> 16)] = i;
+            if (k <= p) PR[r + 1 + (pre(last) >> 16) - (pre(i + 1) >> 16)] = i;
         }
         __syncthreads();
         // (4) swap pairs (L_k, R_k) while L_k < R_k, by the thread at L_k; the last one
@@ -441,8 +455,8 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
             const uint32_t r = RID[i];
             if (r == PCL_INACT || r == i) continue;
             // >= pivot from the counts, not from E: other threads are swapping elements
-            if (((PRE[i + 1] - PRE[i]) & 0xffffu) == 0u) continue;
-            const uint32_t last = r + (INFO[r] & 0xfffffu), lo = PRE[r + 1], hiw = PRE[last];
+            if (((pre(i + 1) - PRE[i]) & 0xffffu) == 0u) continue;
+            const uint32_t last = r + (INFO[r] & 0xfffffu), lo = pre(r + 1), hiw = pre(last);
             const uint32_t nL = (hiw & 0xffffu) - (lo & 0xffffu), nR = (hiw >> 16) - (lo >> 16);
             const uint32_t k = (PRE[i] & 0xffffu) - (lo & 0xffffu);
             const bool c0 = k < nR && i < PR[r + 1 + k];
@@ -460,7 +474,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         for (uint32_t i = tid; i < n; i += CG_BLOCK) {
             if (RID[i] != i) continue;
             const uint32_t size = INFO[i] & 0xfffffu, dep = INFO[i] >> 20, last = i + size;
-            const uint32_t lo = PRE[i + 1], hiw = PRE[last];
+            const uint32_t lo = pre(i + 1), hiw = pre(last);
             const uint32_t nL = (hiw & 0xffffu) - (lo & 0xffffu);
             const uint32_t sw = SC[i];
             uint32_t cut;
@@ -524,7 +538,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         const uint32_t first = CUR[q];
         const uint32_t size = INFO[first] & 0xfffffu, depth = INFO[first] >> 20;
         __syncthreads();   // every thread has the range before pcl_block_sort rewrites INFO[first]
-        pcl_block_sort<PMAX, PbGen>(E + first, KEY + first, size, depth,
+        pcl_block_sort<PMAX, PbGen>(E + first, PbStore<uint64_t*>{KEY + first}, size, depth,
                                     PbScratch<PbGen>{(uint32_t*)W.LAB + first, W.OFF + first, W.A + first,
                                                      W.PAR + first, W.CNT + first, W.ORD + first},
                                     red);

@@ -347,7 +347,8 @@ int cg_debug_route(cg_handle* h, int route);
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */
 int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words);
 /* Diagnostics: raw large-frame scratch of the last frame: 0 = meta words, 1 = z codes
- * ([chunk][group][lane] words of 8 codes), 2 = ground-mode kept bits. */
+ * ([chunk][group][lane] words of 8 codes), 2 = ground-mode kept bits, 3 = the PCL voxel sort's
+ * range lists (8 header words: level counts, leaf count; then 4 lists of 5-word entries). */
 int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes);
 
 /* Exported library version string. */

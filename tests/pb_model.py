@@ -155,7 +155,7 @@ def block_sort(E_in, PER=None, depth0=None):
     """cg_pcl.h pcl_block_sort, thread by thread: element x = tid + 512 k."""
     n = len(E_in)
     if PER is None:
-        PER = 1 if n <= 512 else 2 if n <= 1024 else 4
+        PER = 1 if n <= 512 else 2 if n <= 1024 else 4 if n <= 2048 else 8
     assert n <= BLOCK * PER
     if depth0 is None:
         depth0 = 2 * _lg(n) if n else 0
@@ -274,3 +274,83 @@ def block_sort(E_in, PER=None, depth0=None):
                     rank = sum(1 for j in range(f, e) if key(E[j]) < kx or (key(E[j]) == kx and j < x))
                     out[f + rank] = r
     return out.v
+
+
+# ---- the large path's partition levels (cg_large.hip lg_pq_split / lg_pq_swap / lg_pcl_leaf) ----
+def _pb_median(a, b, c, ka, kb, kc):
+    if ka < kb:
+        return b if kb < kc else (c if ka < kc else a)
+    if ka < kc:
+        return a
+    return c if kb < kc else b
+
+
+def levels_sort(E_in, leaf=4096, levels=None):
+    """cg_large.hip lg_pq_split / lg_pq_swap / lg_pcl_leaf: partition levels over the whole
+    array (tile layout aside: the look-back becomes a prefix over the range), at most `levels`
+    of them (None: until no range longer than `leaf` with budget left remains), then every leaf
+    through block_sort (a longer one through std::sort with its budget); returns the records."""
+    n = len(E_in)
+    if levels is None:
+        levels = 1 << 30
+    bufs = [list(E_in), [None] * n]
+    leaves = []
+    cur = []
+    d0 = 2 * _lg(n) if n else 0
+    if n <= leaf or _lg(n) == 0:
+        leaves.append((0, n, d0, 0))
+    else:
+        cur = [(0, n, d0)]
+    for lv in range(levels):
+        if not cur:
+            break
+        E, Eo = bufs[lv % 2], bufs[(lv + 1) % 2]
+        nxt = []
+        for (f, e, d) in cur:
+            a, b, c = f + 1, f + (e - f) // 2, e - 1
+            m = _pb_median(a, b, c, key(E[a]), key(E[b]), key(E[c]))
+            p = key(E[m])
+
+            def V(x):
+                return E[f if x == m else (m if x == f else x)]
+            PL = [x for x in range(f + 1, e) if key(V(x)) >= p]
+            PRa = [x for x in range(f + 1, e) if key(V(x)) <= p]   # ascending
+            gi = {x: i for i, x in enumerate(PL)}
+            li = {x: i for i, x in enumerate(PRa)}
+            nL, nR = len(PL), len(PRa)
+            Eo[f] = E[m]
+            cuts = []
+            for x in range(f + 1, e):
+                vx = V(x)
+                ge, le = key(vx) >= p, key(vx) <= p
+                partner = x
+                if ge and gi[x] < nR:
+                    g = gi[x]
+                    j = PRa[nR - 1 - g]
+                    if x < j:
+                        partner = j
+                        nxt_ok = g + 1 < min(nL, nR)
+                        if not nxt_ok or not PL[g + 1] < PRa[nR - 2 - g]:
+                            cuts.append(min(PL[g + 1] if g + 1 < nL else 0xFFFFFFFF, j))
+                    elif g == 0:
+                        cuts.append(x)
+                if le:
+                    ri = nR - 1 - li[x]
+                    if ri < nL and PL[ri] < x:
+                        assert partner == x
+                        partner = PL[ri]
+                Eo[x] = vx if partner == x else V(partner)
+            assert len(cuts) == 1, cuts
+            cut = cuts[0]
+            for lo, hi in ((f, cut), (cut, e)):
+                if hi - lo > leaf and d > 1 and lv < levels - 1:
+                    nxt.append((lo, hi, d - 1))
+                else:
+                    leaves.append((lo, hi, d - 1, (lv + 1) % 2))
+        cur = nxt
+    assert not cur
+    out = [None] * n
+    for (f, e, d, b) in leaves:
+        seg = bufs[b][f:e]
+        out[f:e] = block_sort(seg, depth0=d) if e - f <= min(leaf, 4096) else std_sort(seg, depth0=d)
+    return out

@@ -60,7 +60,7 @@ def test_std_sort_restatement_matches_gxx(tmp_path):
         assert [int(x) for x in line.split()] == M.std_sort(a)
 
 
-@pytest.mark.parametrize("seed,nmax", [(1, 512), (2, 1024), (3, 2048)])
+@pytest.mark.parametrize("seed,nmax", [(1, 512), (2, 1024), (3, 2048), (6, 4096)])
 def test_block_sort_model_matches_std_sort(seed, nmax):
     for a in _cases(seed, 40, nmax):
         assert M.block_sort(a) == M.std_sort(a), len(a)
@@ -75,3 +75,19 @@ def test_block_sort_model_heapsort_fallback():
         a = [(rng.randrange(kr) << 32) | i for i in range(n)]
         d = it % 4
         assert M.block_sort(a, depth0=d) == M.std_sort(a, depth0=d), (n, d)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_partition_levels_model_matches_std_sort(seed):
+    """cg_large.hip's split/swap levels (small leaves so that several levels run) with the
+    leaves through the block model, against std::sort's permutation."""
+    rng = random.Random(seed)
+    for it in range(6):
+        n = rng.choice([300, 1000, 2500, 4000])
+        kr = rng.choice([3, 40, 1000, 100000])
+        k = [rng.randrange(kr) for _ in range(n)]
+        if it == 2:
+            k.sort()
+        a = [(k[i] << 32) | i for i in range(n)]
+        assert M.levels_sort(a, leaf=64) == M.std_sort(a), (n, kr)
+        assert M.levels_sort(a, leaf=64, levels=3) == M.std_sort(a), (n, kr)   # long leaves

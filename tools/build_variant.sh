@@ -10,7 +10,7 @@ mkdir -p "$O"
 F="-x hip -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wall -Wno-unused-function -I $R/include"
 C=$R/cones_perception_amd/csrc
 /opt/rocm/bin/hipcc $F "$@" -c $C/cg_kernels.hip -o $O/cg_kernels.o &
-/opt/rocm/bin/hipcc $F "$@" -c $C/cg_large.hip -o $O/cg_large.o &
+/opt/rocm/bin/hipcc $F "$@" -c ${LARGE_SRC:-$C/cg_large.hip} -o $O/cg_large.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_recrop.hip -o $O/cg_recrop.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_colornet.hip -o $O/cg_colornet.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_track.cpp -o $O/cg_track.o &

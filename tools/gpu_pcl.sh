@@ -4,9 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 60 ./tools/pcl_probe 4000 243 || exit $?
-timeout -k 10 60 ./tools/pcl_probe 200 1500 || exit $?
-if [ -x tools/pcl_probe_old ]; then timeout -k 10 60 ./tools/pcl_probe_old 4000 243 || exit $?; fi
-timeout -k 10 400 python -u -m pytest tests/test_gpu_pcl_order.py tests/test_gpu_parity.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_pcl.log 2>&1
+timeout -k 10 60 ./tools/pcl_probe 300 1500 || exit $?
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pcl_order.py tests/test_gpu_large.py tests/test_gpu_parity.py -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_pcl.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_pcl.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --stamps --no-cpu "$@" > gpurun_out/bench.log 2>&1 || exit $?
 python tools/show_bench.py gpurun_out/bench.log | cut -c1-900
