@@ -179,7 +179,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
             pcl_index_vector(W, M, fs->scal[S_MS], E, red, [&](uint32_t j) -> uint32_t { return voxel_idx(W.P[j]); });
             STAMP(7);
             if (flags & CG_F_GLOBAL_SCRATCH) pcl_sort<2, false>(W, E, Mf, red);
-            else pcl_sort<2, true>(W, E, Mf, red);
+            else pcl_sort<2, true>(W, E, Mf, red, -1, E + CG_MMAX);   // VOX's upper half: swaps out of place
         } else {
             // keys (idx << 32 | point index << 16 | slot): unique, so any sort yields PCL's idx
             // order with ties in point order. Non-finite points get idx 0xffffffff (beyond every

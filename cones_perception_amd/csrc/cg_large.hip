@@ -1042,6 +1042,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
                                                         uint32_t* vout) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PCL_LDS];
     __shared__ uint32_t red[8 * WAVES];
+    __shared__ uint64_t ms[2 * WAVES * 8];   // pcl_block_sort's per-wave ballot masks
     const uint32_t n = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
     const uint32_t tid = threadIdx.x;
     for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -1054,13 +1055,14 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
             const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4),
                                       w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
             lds_u32* const Rl = (lds_u32*)red;
+            lds_u64* const Ml = (lds_u64*)(uint64_t*)ms;
             const PqLeafOut out{kout, vout, first};
             for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
             __syncthreads();
-            if (size <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, size, depth, PS, Rl);
-            else if (size <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, size, depth, PS, Rl);
-            else if (size <= 4 * CG_BLOCK) pcl_block_sort<4, PbLds>(El, out, size, depth, PS, Rl);
-            else pcl_block_sort<8, PbLds>(El, out, size, depth, PS, Rl);
+            if (size <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, size, depth, PS, Rl, Ml);
+            else if (size <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, size, depth, PS, Rl, Ml);
+            else if (size <= 4 * CG_BLOCK) pcl_block_sort<4, PbLds>(El, out, size, depth, PS, Rl, Ml);
+            else pcl_block_sort<8, PbLds>(El, out, size, depth, PS, Rl, Ml);
         } else {   // the range's own span of the HBM arrays
             Work W{};
             W.KEY = (uint64_t*)S.vox + 2ull * first;

@@ -198,11 +198,17 @@ template <class P> struct PbStore {
     P a;
     __device__ __forceinline__ void operator()(uint32_t i, uint64_t r) const { a[i] = r; }
 };
-template <int PER, class K, class OUT = PbStore<typename K::P64>>
+// OOP: a second record buffer E2 (n records) takes the swapped records, so a level's swap
+// step reads and writes in one barrier interval (E and E2 trade places every level); without
+// it the records are swapped in place (reads, barrier, writes). MS: 2 * 8 * PER words of
+// 64 bits for the per-wave ballot masks.
+template <int PER, class K, class OUT = PbStore<typename K::P64>, bool OOP = false>
 __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint32_t n, uint32_t depth0,
-                                               const PbScratch<K> S, typename K::P32 cnt) {
+                                               const PbScratch<K> S, typename K::P32 cnt, typename K::P64 MS,
+                                               typename K::P64 E2 = nullptr) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     constexpr uint32_t GE = 1u << 24, LE = 1u << 25, IN = 1u << 26, PART = 1u << 27;
+    constexpr uint32_t NS = PER * WAVES;   // (chunk, wave) slots: position x is in slot x / 64
     uint32_t fe[PER];
 #pragma unroll
     for (int k = 0; k < PER; k++) fe[k] = n << 16;
@@ -213,7 +219,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
     bool any = __syncthreads_or(act);
     while (any) {
         uint32_t st[PER], nn[PER];
-        // S1
+        // S1: compare with the range's pivot; per-slot counts and ballot masks
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
@@ -226,83 +232,114 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
             const bool part = (info & PB_ACT) != 0, in = part && x > f;
             const bool ge = in && kx >= p, le = in && kx <= p;
             const uint64_t gm = __ballot(ge), lm = __ballot(le);
-            if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
+            if (l == 0) {
+                const uint32_t slot = k * WAVES + w;
+                cnt[slot] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
+                MS[2 * slot] = gm;
+                MS[2 * slot + 1] = lm;
+            }
             st[k] = mbcnt(gm) | (mbcnt(lm) << 12) | (ge ? GE : 0u) | (le ? LE : 0u) | (in ? IN : 0u) | (part ? PART : 0u);
         }
         __syncthreads();
         PCL_STEP();
-        // S2: lane j of every wave scans the (chunk, wave) counts; element (k, w) reads entry
-        // k * WAVES + w of the exclusive scan
+        // S2: lane j of every wave scans the slot counts; an element's own counts, and the
+        // counts before its range's f + 1 and e (slot prefix by ds_bpermute plus the slot's
+        // mask below the position), give its L / R list index; the lists are written here
         {
-            const uint32_t cj = l < PER * WAVES ? cnt[l] : 0u;
+            const uint32_t cj = l < NS ? cnt[l] : 0u;
             const uint32_t g = wave_incl_scan(cj & 0xffffu), h = wave_incl_scan(cj >> 16);
             const uint32_t gex = g - (cj & 0xffffu), hex = h - (cj >> 16);
+            const uint32_t totg = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)(NS - 1));
+            const uint32_t totl = (uint32_t)__builtin_amdgcn_readlane((int)h, (int)(NS - 1));
+            uint32_t s1[PER], se[PER];
+            uint64_t m1g[PER], m1l[PER], meg[PER], mel[PER];
+            uint32_t p1g[PER], p1l[PER], peg[PER], pel[PER];
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                const uint32_t f = fe[k] & 0xffffu, e = fe[k] >> 16;
+                s1[k] = min((f + 1) >> 6, NS - 1);
+                se[k] = min(e >> 6, NS - 1);
+                m1g[k] = MS[2 * s1[k]]; m1l[k] = MS[2 * s1[k] + 1];
+                meg[k] = MS[2 * se[k]]; mel[k] = MS[2 * se[k] + 1];
+                p1g[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * s1[k]), (int)gex);
+                p1l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * s1[k]), (int)hex);
+                peg[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * se[k]), (int)gex);
+                pel[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * se[k]), (int)hex);
+            }
 #pragma unroll
             for (int k = 0; k < PER; k++) {
                 const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
                 const uint32_t src = (uint32_t)k * WAVES + w;
                 const uint32_t gx = (uint32_t)__builtin_amdgcn_readlane((int)gex, (int)src) + (st[k] & 0xfffu);
                 const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)hex, (int)src) + ((st[k] >> 12) & 0xfffu);
-                if ((st[k] & PART) && x == f) S.RLO[f] = gx | (lx << 16);
-                if ((st[k] & IN) && x == e - 1)
-                    S.RLO[f + 1] = (gx + ((st[k] & GE) ? 1u : 0u)) | ((lx + ((st[k] & LE) ? 1u : 0u)) << 16);
-                st[k] = gx | (lx << 12) | (st[k] & (GE | LE | IN | PART));
-            }
-        }
-        __syncthreads();
-        PCL_STEP();
-        // S3
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
-            nn[k] = 0;
-            if (st[k] & PART) {
-                const uint32_t lo = S.RLO[f], hi = S.RLO[f + 1];
-                const uint32_t gf = lo & 0xffffu, lf = lo >> 16, gend = hi & 0xffffu, lend = hi >> 16;
-                nn[k] = (gend - gf) | ((lend - lf) << 16);
-                if (x == f) S.CUT[f] = 0u;
-                if (st[k] & IN) {
-                    const uint32_t gx = st[k] & 0xfffu, lx = (st[k] >> 12) & 0xfffu;
-                    const uint32_t li = gx - gf, ri = lend - lx - 1u;
-                    if (st[k] & GE) S.PL[f + 1 + li] = x;
-                    if (st[k] & LE) S.PR[f + 1 + ri] = x;
-                    st[k] = li | ((ri & 0xfffu) << 12) | (st[k] & (GE | LE | IN | PART));
+                nn[k] = 0;
+                if (st[k] & PART) {
+                    const uint64_t b1 = (1ull << ((f + 1) & 63u)) - 1ull;
+                    const uint32_t gf = p1g[k] + (uint32_t)__popcll(m1g[k] & b1);
+                    const uint32_t lf = p1l[k] + (uint32_t)__popcll(m1l[k] & b1);
+                    uint32_t gend = totg, lend = totl;
+                    if ((e >> 6) < NS) {
+                        const uint64_t be = (1ull << (e & 63u)) - 1ull;
+                        gend = peg[k] + (uint32_t)__popcll(meg[k] & be);
+                        lend = pel[k] + (uint32_t)__popcll(mel[k] & be);
+                    }
+                    nn[k] = (gend - gf) | ((lend - lf) << 16);
+                    if (x == f) S.CUT[f] = 0u;
+                    if (st[k] & IN) {
+                        const uint32_t li = gx - gf, ri = lend - lx - 1u;
+                        if (st[k] & GE) S.PL[f + 1 + li] = x;
+                        if (st[k] & LE) S.PR[f + 1 + ri] = x;
+                        st[k] = li | ((ri & 0xfffu) << 12) | (st[k] & (GE | LE | IN | PART));
+                    }
                 }
             }
         }
         __syncthreads();
         PCL_STEP();
-        // S4: the partners and the next pair in one batch, then the partners' elements
+        // S4: the partners and the next pair in one batch, then the partners' records
         uint64_t val[PER];
         uint32_t sw = 0;
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
-            val[k] = 0;
-            if (st[k] & IN) {
-                const uint32_t li = st[k] & 0xfffu, ri = (st[k] >> 12) & 0xfffu;
-                const uint32_t nL = nn[k] & 0xffffu, nR = nn[k] >> 16;
-                const bool hasL = (st[k] & GE) && li < nR, hasR = (st[k] & LE) && ri < nL;
-                const bool nxt = hasL && li + 1 < min(nL, nR);
-                const uint32_t j = hasL ? S.PR[f + 1 + li] : 0u;
-                const uint32_t i = hasR ? S.PL[f + 1 + ri] : 0xffffffffu;
-                const uint32_t pl2 = nxt ? S.PL[f + 2 + li] : 0u, pr2 = nxt ? S.PR[f + 2 + li] : 0u;
-                uint32_t partner = x;
-                if (hasL && x < j) {
-                    partner = j;
-                    if (!nxt || !(pl2 < pr2)) S.CUT[f] = li + 1;
-                }
-                if (hasR && i < x) partner = i;
-                if (partner != x) {
+            const bool in = (st[k] & IN) != 0;
+            const uint32_t li = in ? (st[k] & 0xfffu) : 0u, ri = in ? ((st[k] >> 12) & 0xfffu) : 0u;
+            const uint32_t nL = nn[k] & 0xffffu, nR = nn[k] >> 16;
+            const bool hasL = in && (st[k] & GE) && li < nR, hasR = in && (st[k] & LE) && ri < nL;
+            const bool nxt = hasL && li + 1 < min(nL, nR);
+            const uint32_t top = n ? n - 1 : 0u;
+            const uint32_t j = S.PR[min(f + 1 + (hasL ? li : 0u), top)];
+            const uint32_t i = S.PL[min(f + 1 + (hasR ? ri : 0u), top)];
+            const uint32_t pl2 = S.PL[min(f + 2 + (nxt ? li : 0u), top)];
+            const uint32_t pr2 = S.PR[min(f + 2 + (nxt ? li : 0u), top)];
+            uint32_t partner = x;
+            if (hasL && x < j) {
+                partner = j;
+                if (!nxt || !(pl2 < pr2)) S.CUT[f] = li + 1;
+            }
+            if (hasR && i < x) partner = i;
+            if (x < n) {
+                if (OOP) {
+                    val[k] = E[partner];
+                } else if (partner != x) {
                     val[k] = E[partner];
                     sw |= 1u << k;
                 }
             }
         }
-        __syncthreads();
+        if constexpr (OOP) {
 #pragma unroll
-        for (int k = 0; k < PER; k++)
-            if (sw & (1u << k)) E[tid + CG_BLOCK * k] = val[k];
+            for (int k = 0; k < PER; k++)
+                if (tid + CG_BLOCK * k < n) E2[tid + CG_BLOCK * k] = val[k];
+            const typename K::P64 t = E;
+            E = E2;
+            E2 = t;
+        } else {
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < PER; k++)
+                if (sw & (1u << k)) E[tid + CG_BLOCK * k] = val[k];
+        }
         __syncthreads();
         PCL_STEP();
         // S5: heads
@@ -366,8 +403,11 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
 // barrier.
 // PMAX: the largest pcl_block_sort instantiation (elements per thread) the caller affords;
 // LDS: the arrays of W live in LDS (n <= PMAX * CG_BLOCK then).
+// E2: a second buffer of n records in LDS for the out-of-place swaps (LDS form only), or null.
 template <int PMAX, bool LDS>
-__device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t* red, int depth0 = -1) {
+__device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t* red, int depth0 = -1,
+                                         uint64_t* E2 = nullptr) {
+    __shared__ uint64_t ms[2 * WAVES * PMAX];   // the per-wave ballot masks
     constexpr uint32_t PCL_BLOCK_MAX = PMAX * CG_BLOCK;
     const uint32_t tid = threadIdx.x;
     uint32_t* PRE = W.A;
@@ -387,15 +427,24 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         lds_u64* const Ko = (lds_u64*)W.KEY;
         lds_u32* const Rl = (lds_u32*)red;
         const PbStore<lds_u64*> out{Ko};
-        if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, n, d0, PS, Rl);
-        else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, n, d0, PS, Rl);
-        else pcl_block_sort<PMAX, PbLds>(El, out, n, d0, PS, Rl);
+        lds_u64* const Ml = (lds_u64*)(uint64_t*)ms;
+        if (E2) {
+            lds_u64* const E2l = (lds_u64*)E2;
+            if (n <= CG_BLOCK) pcl_block_sort<1, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, Ml, E2l);
+            else if (PMAX == 2 || n <= 2 * CG_BLOCK)
+                pcl_block_sort<2, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, Ml, E2l);
+            else pcl_block_sort<PMAX, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, Ml, E2l);
+        } else {
+            if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, n, d0, PS, Rl, Ml);
+            else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, n, d0, PS, Rl, Ml);
+            else pcl_block_sort<PMAX, PbLds>(El, out, n, d0, PS, Rl, Ml);
+        }
         PCL_STAMP();
         return;
     }
     const PbScratch<PbGen> PS{(uint32_t*)W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD};
     if (n <= PMAX * CG_BLOCK) {
-        pcl_block_sort<PMAX, PbGen>(E, PbStore<uint64_t*>{W.KEY}, n, d0, PS, red);
+        pcl_block_sort<PMAX, PbGen>(E, PbStore<uint64_t*>{W.KEY}, n, d0, PS, red, (uint64_t*)ms);
         PCL_STAMP();
         return;
     }
@@ -541,7 +590,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         pcl_block_sort<PMAX, PbGen>(E + first, PbStore<uint64_t*>{KEY + first}, size, depth,
                                     PbScratch<PbGen>{(uint32_t*)W.LAB + first, W.OFF + first, W.A + first,
                                                      W.PAR + first, W.CNT + first, W.ORD + first},
-                                    red);
+                                    red, (uint64_t*)ms);
     }
     __syncthreads();
     PCL_STAMP();

@@ -12,7 +12,7 @@
 
 #define NMAX 2048
 __global__ __launch_bounds__(CG_BLOCK) void probe(const uint64_t* in, uint64_t* out, const uint32_t* offs, int stamp) {
-    __shared__ __attribute__((aligned(16))) uint64_t E[NMAX], K[NMAX];
+    __shared__ __attribute__((aligned(16))) uint64_t E[NMAX], K[NMAX], E2[NMAX];
     __shared__ uint32_t w0[7 * (NMAX + 4)];
     __shared__ uint32_t red[8 * WAVES];
     const uint32_t o = offs[blockIdx.x], n = offs[blockIdx.x + 1] - o;
@@ -24,7 +24,7 @@ __global__ __launch_bounds__(CG_BLOCK) void probe(const uint64_t* in, uint64_t* 
     W.A = w0; W.PAR = w0 + (NMAX + 4); W.CNT = w0 + 2 * (NMAX + 4); W.UK = w0 + 3 * (NMAX + 4);
     W.ORD = w0 + 4 * (NMAX + 4); W.LAB = (int32_t*)(w0 + 5 * (NMAX + 4)); W.OFF = w0 + 6 * (NMAX + 4);
     if (stamp) PCL_STAMP();
-    pcl_sort<4, true>(W, E, n, red);
+    pcl_sort<4, true>(W, E, n, red, -1, E2);
     for (uint32_t i = threadIdx.x; i < n; i += CG_BLOCK) out[o + i] = K[i];
 }
 int main(int argc, char** argv) {
