@@ -151,8 +151,9 @@ def _setup(E, S, cf, ce, d):
     return act
 
 
-def block_sort(E_in, PER=None, depth0=None):
-    """cg_pcl.h pcl_block_sort, thread by thread: element x = tid + 512 k."""
+def block_sort(E_in, PER=None, depth0=None, oop=False):
+    """cg_pcl.h pcl_block_sort, thread by thread: element x = tid + 512 k (oop: the swaps go
+    to a second buffer, as in the frame kernel)."""
     n = len(E_in)
     if PER is None:
         PER = 1 if n <= 512 else 2 if n <= 1024 else 4 if n <= 2048 else 8
@@ -164,6 +165,7 @@ def block_sort(E_in, PER=None, depth0=None):
     out = Arr(n)
     S = {k: Arr(n + 1) for k in ("INFO", "PIV", "RLO", "PL", "PR", "CUT")}
     cnt = Arr(8 * PER)
+    MS = Arr(2 * 8 * PER)
     T = range(BLOCK)
     fe = [[n << 16] * PER for _ in T]
     anyact = _setup(E, S, 0, n, depth0) if n else False
@@ -186,35 +188,37 @@ def block_sort(E_in, PER=None, depth0=None):
                 gm = sum(1 << l for l in range(64) if ge[64 * w + l])
                 lm = sum(1 << l for l in range(64) if le[64 * w + l])
                 cnt[k * WAVES + w] = _popc(gm) | (_popc(lm) << 16)
+                MS[2 * (k * WAVES + w)], MS[2 * (k * WAVES + w) + 1] = gm, lm
                 for l in range(64):
                     t = 64 * w + l
                     st[t][k].update(ge=ge[t], le=le[t], mg=_popc(gm & ((1 << l) - 1)), ml=_popc(lm & ((1 << l) - 1)))
-        c = [cnt[j] for j in range(PER * WAVES)]     # S2
+        NS = PER * WAVES                             # S2: counts from the slot masks
+        c = [cnt[j] for j in range(NS)]
+        gex = [sum(c[i] & 0xFFFF for i in range(j)) for j in range(NS)]
+        hex_ = [sum(c[i] >> 16 for i in range(j)) for j in range(NS)]
+        totg, totl = sum(v & 0xFFFF for v in c), sum(v >> 16 for v in c)
+
+        def before(y):   # (>= count, <= count) of the positions before y
+            if (y >> 6) >= NS:
+                return totg, totl
+            sl, b = y >> 6, (1 << (y & 63)) - 1
+            return gex[sl] + _popc(MS[2 * sl] & b), hex_[sl] + _popc(MS[2 * sl + 1] & b)
         for t in T:
             w = t // 64
             for k in range(PER):
                 x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-                base = sum(c[j] for j in range(PER * WAVES) if j < k * WAVES + w)
                 q = st[t][k]
-                gx, lx = (base & 0xFFFF) + q["mg"], (base >> 16) + q["ml"]
+                gx, lx = gex[k * WAVES + w] + q["mg"], hex_[k * WAVES + w] + q["ml"]
                 assert gx < 4096 and lx < 4096
-                if q["part"] and x == f:
-                    S["RLO"][f] = gx | (lx << 16)
-                if q["inn"] and x == e - 1:
-                    S["RLO"][f + 1] = (gx + q["ge"]) | ((lx + q["le"]) << 16)
                 q.update(gx=gx, lx=lx)
-        for t in T:                                  # S3
-            for k in range(PER):
-                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
-                q = st[t][k]
                 if q["part"]:
-                    lo, hi = S["RLO"][f], S["RLO"][f + 1]
-                    gf, lf, gend, lend = lo & 0xFFFF, lo >> 16, hi & 0xFFFF, hi >> 16
+                    gf, lf = before(f + 1)
+                    gend, lend = before(e)
                     nn[t][k] = (gend - gf, lend - lf)
                     if x == f:
                         S["CUT"][f] = 0
                     if q["inn"]:
-                        li, ri = q["gx"] - gf, lend - q["lx"] - 1
+                        li, ri = gx - gf, lend - lx - 1
                         if q["ge"]:
                             S["PL"][f + 1 + li] = x
                         if q["le"]:
@@ -242,8 +246,15 @@ def block_sort(E_in, PER=None, depth0=None):
                             partner = i
                     if partner != x:
                         val[x] = E[partner]
-        for x, v in val.items():
-            E[x] = v
+        if oop:   # every record to the other buffer, then the buffers trade places
+            E2 = Arr(n)
+            E2.v = list(E.v)
+            for x, v in val.items():
+                E2[x] = v
+            E = E2
+        else:
+            for x, v in val.items():
+                E[x] = v
         anyact = False                               # S5
         for t in T:
             for k in range(PER):
