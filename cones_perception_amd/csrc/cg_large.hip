@@ -1509,8 +1509,9 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
 
 // Detector backend over meta[LG_MS] survivors (surv_p / surv_i, frame indices < n_total) and,
 // in pipeline mode with zero_pass, the n_total - K pads; results in frame slot f.
-int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
+int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t N, uint32_t K) {
+    CgDevParams P = P0;
     hipError_t e;
     uint32_t hstack[LG_META_WORDS];
     uint32_t* const hm = S.hmeta ? S.hmeta : hstack;   // pinned when the handle has one
@@ -1520,6 +1521,10 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScrat
     if (K == CG_K_FROM_META) K = hm[LG_K];   // pipeline frames: the ground stage's kept count
     const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
     const uint32_t Mtot = Ms + npad;
+    // PCL's order keeps at most PQ_MAXR ranges per partition level: a detector input beyond
+    // PQ_MAXR * LG_PCL_LEAF / 2 records (4M) is summed in point order instead, and flagged
+    // (CG_F_VOXEL_POINT_ORDER): same voxels and clusters, last bits of some coordinates
+    if ((uint64_t)Mtot > (uint64_t)PQ_MAXR * LG_PCL_LEAF / 2) P.voxel_order = CG_VOXEL_ORDER_POINT;
     CgLaunch Lh = L;
     Lh.n_points = N;   // the header's N is the whole frame's
     if (Mtot <= CG_MMAX && !S.force_global) return cg_launch_lg_back_small(Lh, P, S, f, npad, K, s);
