@@ -371,7 +371,7 @@ int ensure_large(cg_handle* h, uint32_t n) {
 // Frames of <= CG_MAX_POINTS points run as one batch launch of the frame kernel; larger
 // frames (or every frame, under cg_debug_route) go through the multi-workgroup large path.
 int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
-    const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2) && L.n_points > 0);
+    const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2 || h->route == 5) && L.n_points > 0);
     if (!large && L.split) {
         HIPCHK((hipError_t)cg_launch_split(L, h->dp, kmode, s));
         return CG_OK;
@@ -382,7 +382,8 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
     }
     int rc = ensure_large(h, L.n_points);
     if (rc) return rc;
-    h->lg.force_global = h->route == 2 ? 1u : 0u;
+    h->lg.force_global = (h->route == 2 || h->route == 5) ? 1u : 0u;
+    h->lg.pcl_levels_cap = h->route == 5 ? 1u : 0u;
     L.stamps = nullptr;
     HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, h->lg, s));
     return CG_OK;
@@ -1121,7 +1122,7 @@ int cg_debug_launch_span(cg_handle* h, void* d_span) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 4) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 5) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

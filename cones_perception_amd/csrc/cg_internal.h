@@ -152,6 +152,7 @@ struct LgScratch {
     uint32_t pq_cap;          //   entries
     uint64_t* pqst;           //   the partition levels' look-back words (tickets, finished, per tile)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
+    uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };
 // Bytes of the large-frame scratch for frames of n points, and its layout at base.

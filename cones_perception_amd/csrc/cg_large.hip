@@ -1571,6 +1571,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
         uint32_t levels = 0;
         while (((uint64_t)LG_PCL_LEAF << levels) < Mtot) levels++;
         if (levels) levels = std::min<uint32_t>(levels + 3, LG_PQ_LEVELS_MAX);
+        if (S.pcl_levels_cap) levels = std::min(levels, S.pcl_levels_cap);
         const uint32_t tb = (Mtot + PQ_T - 1) / PQ_T;
         hipLaunchKernelGGL(lg_pq_split, dim3(std::max<uint32_t>(tb, 1)), dim3(CG_BLOCK), 0, s, S, kb[buf ^ 1], 0u);
         for (uint32_t lv = 0; lv < levels; lv++) {

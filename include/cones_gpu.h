@@ -341,7 +341,9 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
 /* Diagnostics: route every frame through the large-frame path (1), and also through its
  * global HBM backend even when the detector input fits the LDS backend (2); run single-frame
  * calls in one workgroup instead of the per-chunk split launch (3), or split with the input
- * copied by DMA instead of read by the kernel from pinned memory (4); 0 = automatic. */
+ * copied by DMA instead of read by the kernel from pinned memory (4); the global backend with
+ * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
+ * are finished in HBM side by side (5); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

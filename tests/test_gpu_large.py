@@ -127,3 +127,18 @@ def test_c5_frame_through_detector(params):
     ref, _ = O.run(params, msg, O.MODE_DETECT)
     assert ref.n_filtered > 64 * 4096
     assert_same_detection(got, ref, "C5 detect")
+
+
+@pytest.mark.parametrize("rings,cols,clutter", [(128, 4096, 60), (128, 8192, 60)])
+def test_pcl_sort_leaves_in_hbm(params, rings, cols, clutter):
+    """cg_debug_route 5: the PCL voxel sort stops after one partition level, so both halves of
+    the index_vector (longer than the 4,096-record LDS leaf) are finished in HBM by two
+    workgroups side by side, each in its own span of the scratch arrays (the span boundary is
+    where round 2 found a neighbour's word overwritten)."""
+    msg = _frame(rings, cols, frame=1, clutter=clutter, cpr=12)
+    pipe = cp.ConePipeline(params)
+    pipe.debug_route(5)
+    got = pipe.cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_PIPELINE)
+    assert got.n_filtered > 2 * 4096
+    assert_same_detection(got, ref, f"route 5 {rings}x{cols}")
