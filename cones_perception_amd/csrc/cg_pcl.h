@@ -130,6 +130,8 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 // CUT (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
 #define PB_ACT 0x100u
 #define PB_FIN 0x200u
+#define PB_WAVE 0x400u   // a range of at most PW_MAX records with budget left: one wave sorts it
+#define PW_MAX 64
 #define PB_BUDGET 0xffu
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
@@ -163,7 +165,7 @@ __device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K
     uint64_t v0[2], va[2], vb[2], vc[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
-        med[c] = hi[c] - lo[c] > CG_SORT_THRESHOLD && d > 0;
+        med[c] = hi[c] - lo[c] > PW_MAX && d > 0;
         ia[c] = lo[c] + 1; ib[c] = lo[c] + (hi[c] - lo[c]) / 2; ic[c] = hi[c] - 1;
         if (med[c]) { v0[c] = E[lo[c]]; va[c] = E[ia[c]]; vb[c] = E[ib[c]]; vc[c] = E[ic[c]]; }
     }
@@ -175,6 +177,8 @@ __device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K
             if (d == 0) {   // __partial_sort(first, last, last): final
                 cg_heap_sort_range((uint64_t*)(E + lo[c]), (long)(hi[c] - lo[c]), PwLess{});
                 info |= PB_FIN;
+            } else if (hi[c] - lo[c] <= PW_MAX) {   // the rest of it in one wave (pw_range64)
+                info |= PB_WAVE;
             } else {
                 const uint32_t m = pb_median(ia[c], ib[c], ic[c], pcl_key(va[c]), pcl_key(vb[c]), pcl_key(vc[c]));
                 const uint64_t vm = m == ia[c] ? va[c] : (m == ib[c] ? vb[c] : vc[c]);
@@ -198,6 +202,95 @@ template <class P> struct PbStore {
     P a;
     __device__ __forceinline__ void operator()(uint32_t i, uint64_t r) const { a[i] = r; }
 };
+// ------------------------------------------------------------------------------------------
+// One wave finishes a range of m <= 64 records (__introsort_loop with the budget left on its
+// path, then __final_insertion_sort) in registers: lane i holds record f + i, and every lane
+// knows its sub-range [hd, en) and that sub-range's budget. All sub-ranges longer than 16
+// partition in the same round (segmented): median of three by ds_bpermute, >= / <= ballots,
+// L_k = the k-th set bit of the sub-range's >= mask, R_k the (nR-1-k)-th of its <= mask (read
+// from lane-index tables that one ds_permute per mask builds), the swap count s = a ballot of
+// L_k < R_k counted over the sub-range (a prefix of k), the records moved by ds_bpermute, the
+// cut from s. A spent budget heapsorts its sub-range in the caller's buffer (rare). The final
+// insertion passes are a stable rank inside each sub-range of at most 16 records (sub-ranges
+// are weakly ordered, so insertion never crosses one).
+__device__ __forceinline__ uint32_t pw_b32(uint32_t src, uint32_t x) {   // x of lane src
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)x);
+}
+__device__ __forceinline__ uint64_t pw_low(uint32_t b) {   // bits below b (b <= 64)
+    return b >= 64u ? ~0ull : (1ull << b) - 1ull;
+}
+template <class P64, class OUT>
+__device__ __forceinline__ void pw_range64(P64 E, uint32_t f, uint32_t m, uint32_t depth, OUT out) {
+    const uint32_t l = lane_id();
+    const bool live = l < m;
+    uint64_t v = live ? (uint64_t)E[f + (live ? l : 0u)] : ~0ull;
+    uint32_t hd = live ? 0u : l, en = live ? m : l + 1u, dep = depth;
+    for (;;) {
+        const bool act = live && en - hd > CG_SORT_THRESHOLD && dep > 0;
+        if (!__ballot(act)) break;
+        // __move_median_to_first(hd, hd + 1, mid, en - 1)
+        const uint32_t a = hd + 1, b = hd + (en - hd) / 2, c = en - 1;
+        const uint32_t key = (uint32_t)(v >> 32);
+        const uint32_t ka = pw_b32(a, key), kb = pw_b32(b, key), kc = pw_b32(c, key);
+        const uint32_t mi = pb_median(a, b, c, ka, kb, kc);
+        const uint32_t p = mi == a ? ka : (mi == b ? kb : kc);
+        uint32_t src = l;
+        if (act && l == hd) src = mi;
+        if (act && l == mi) src = hd;
+        v = ((uint64_t)pw_b32(src, (uint32_t)(v >> 32)) << 32) | pw_b32(src, (uint32_t)v);
+        // __unguarded_partition(hd + 1, en, hd), in parallel over the sub-ranges
+        const uint32_t k = (uint32_t)(v >> 32);
+        const bool in = act && l > hd;
+        const uint64_t GE = __ballot(in && k >= p), LE = __ballot(in && k <= p);
+        const uint64_t lo = pw_low(hd + 1), hi = pw_low(en);
+        const uint32_t bG = (uint32_t)__popcll(GE & lo), bL = (uint32_t)__popcll(LE & lo);
+        const uint32_t nL = (uint32_t)__popcll(GE & hi) - bG, nR = (uint32_t)__popcll(LE & hi) - bL;
+        const bool isG = (GE >> l) & 1ull, isL = (LE >> l) & 1ull;
+        const uint32_t gk = mbcnt(GE) - bG, rk = nR - 1u - (mbcnt(LE) - bL);
+        // lane tables: PG[j] = the j-th set bit of GE (j < popc(GE)), PL likewise
+        const uint32_t tG = (uint32_t)__popcll(GE), tL = (uint32_t)__popcll(LE);
+        const uint32_t PG = (uint32_t)__builtin_amdgcn_ds_permute(
+            (int)((isG ? mbcnt(GE) : tG + mbcnt(~GE)) << 2), (int)l);
+        const uint32_t PL = (uint32_t)__builtin_amdgcn_ds_permute(
+            (int)((isL ? mbcnt(LE) : tL + mbcnt(~LE)) << 2), (int)l);
+        const bool pair = isG && gk < nR;
+        const uint32_t Rk = pw_b32(pair ? bL + nR - 1u - gk : 0u, PL);
+        const uint64_t SW = __ballot(pair && l < Rk);
+        const uint32_t s = (uint32_t)__popcll(SW & hi) - (uint32_t)__popcll(SW & lo);
+        const uint32_t Lk = pw_b32(isL && rk < s ? bG + rk : 0u, PG);
+        uint32_t partner = l;
+        if (isG && gk < s) partner = Rk;
+        if (isL && rk < s) partner = Lk;
+        v = ((uint64_t)pw_b32(partner, (uint32_t)(v >> 32)) << 32) | pw_b32(partner, (uint32_t)v);
+        const uint32_t gc = pw_b32(bG + (s < nL ? s : 0u), PG);
+        const uint32_t lc = pw_b32(bL + nR - (s ? s : nR), PL);
+        const uint32_t cut = s == 0 ? gc : min(s < nL ? gc : 64u, lc);
+        if (act) {
+            if (l >= cut) hd = cut; else en = cut;
+            dep -= 1u;
+        }
+    }
+    // spent budgets: __partial_sort(first, last, last) of the sub-range, in the caller's buffer
+    const bool heap = live && en - hd > CG_SORT_THRESHOLD;
+    if (__ballot(heap)) {
+        if (live) E[f + l] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (heap && l == hd) cg_heap_sort_range((uint64_t*)(E + f + hd), (long)(en - hd), PwLess{});
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (live) v = E[f + l];
+    }
+    // the final insertion passes: a stable rank inside each sub-range of at most 16
+    const uint32_t kx = (uint32_t)(v >> 32);
+    uint32_t rank = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++) {
+        const uint32_t kj = pw_b32(hd + j, kx);
+        rank += hd + j < en && ((kj < kx) || (kj == kx && hd + j < l));
+    }
+    if (heap) rank = l - hd;   // already sorted
+    if (live) out(f + hd + rank, v);
+}
+
 // OOP: a second record buffer E2 (n records) takes the swapped records, so a level's swap
 // step reads and writes in one barrier interval (E and E2 trade places every level); without
 // it the records are swapped in place (reads, barrier, writes). MS: 2 * 8 * PER words of
@@ -368,11 +461,35 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
             }
         }
     }
-    // the final insertion passes
+    // ranges of at most PW_MAX records with budget left: one wave each (pw_range64), listed
+    // in PL (first | last << 16) and PR (budget), the count in cnt[0]
+    if (tid == 0) cnt[0] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
+        if (x < n && x == f) {
+            const uint32_t info = S.INFO[f];
+            if (info & PB_WAVE) {
+                const uint32_t q = atomicAdd((uint32_t*)(cnt + 0), 1u);
+                S.PL[q] = fe[k];
+                S.PR[q] = info & PB_BUDGET;
+            }
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t nw = cnt[0];
+        for (uint32_t q = w; q < nw; q += WAVES) {
+            const uint32_t r = S.PL[q];
+            pw_range64(E, r & 0xffffu, (r >> 16) - (r & 0xffffu), S.PR[q], out);
+        }
+    }
+    // the final insertion passes of the other ranges
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
-        if (x < n) {
+        if (x < n && !(S.INFO[f] & PB_WAVE)) {
             const uint64_t r = E[x];
             const uint32_t info = S.INFO[f];
             uint32_t kj[CG_SORT_THRESHOLD];

@@ -365,3 +365,64 @@ def levels_sort(E_in, leaf=4096, levels=None):
         seg = bufs[b][f:e]
         out[f:e] = block_sort(seg, depth0=d) if e - f <= min(leaf, 4096) else std_sort(seg, depth0=d)
     return out
+
+
+# ---- cg_pcl.h pw_range64: one wave sorts a range of at most 64 records in registers ---------
+def _sel(mask, j):
+    """Position of the j-th (0-based) set bit of a 64-bit mask: the popcount binary search."""
+    lo = 0
+    for step in (32, 16, 8, 4, 2, 1):
+        if _popc(mask & ((1 << (lo + step)) - 1)) <= j:
+            lo += step
+    return lo
+
+
+def wave64_sort(recs, depth):
+    """The whole range [0, m) as __introsort_loop + __final_insertion_sort restricted to it
+    (depth: the budget left on its path), lane i holding record i."""
+    m = len(recs)
+    assert m <= 64
+    v = list(recs) + [None] * (64 - m)
+    key_ = lambda i: key(v[i])
+    stack = [(0, m, depth)]
+    while stack:
+        lo, hi, dep = stack.pop()
+        while hi - lo > THRESH:
+            if dep == 0:
+                seg = v[lo:hi]
+                heap_sort_range(seg, 0, hi - lo)
+                v[lo:hi] = seg
+                break
+            dep -= 1
+            a, b, c = lo + 1, lo + (hi - lo) // 2, hi - 1
+            mi = _pb_median(a, b, c, key_(a), key_(b), key_(c))
+            v[lo], v[mi] = v[mi], v[lo]
+            p = key_(lo)
+            GE = sum(1 << i for i in range(lo + 1, hi) if key_(i) >= p)
+            LE = sum(1 << i for i in range(lo + 1, hi) if key_(i) <= p)
+            nL, nR = _popc(GE), _popc(LE)
+            # swap k pairs L_k (k-th set bit of GE) with R_k (the (nR-1-k)-th set bit of LE)
+            s = sum(1 for k in range(min(nL, nR)) if _sel(GE, k) < _sel(LE, nR - 1 - k))
+            nv = list(v)
+            for i in range(lo + 1, hi):
+                partner = i
+                if (GE >> i) & 1:
+                    k = _popc(GE & ((1 << i) - 1))
+                    if k < s:
+                        partner = _sel(LE, nR - 1 - k)
+                if (LE >> i) & 1:
+                    r = nR - 1 - _popc(LE & ((1 << i) - 1))
+                    if r < s:
+                        assert partner == i
+                        partner = _sel(GE, r)
+                nv[i] = v[partner]
+            v = nv
+            cut = _sel(GE, 0) if s == 0 else min(_sel(GE, s) if s < nL else 1 << 30, _sel(LE, nR - s))
+            stack.append((cut, hi, dep))
+            hi = cut
+    # the final insertion passes: a stable rank over the whole (weakly ordered) range
+    out = [None] * m
+    for i in range(m):
+        r = sum(1 for j in range(m) if key_(j) < key_(i) or (key_(j) == key_(i) and j < i))
+        out[r] = v[i]
+    return out

@@ -91,3 +91,18 @@ def test_partition_levels_model_matches_std_sort(seed):
         a = [(k[i] << 32) | i for i in range(n)]
         assert M.levels_sort(a, leaf=64) == M.std_sort(a), (n, kr)
         assert M.levels_sort(a, leaf=64, levels=3) == M.std_sort(a), (n, kr)   # long leaves
+
+
+def test_wave64_model_matches_std_sort():
+    """cg_pcl.h pw_range64's register form (selects by popcount binary search, swaps as lane
+    permutes, the swap count from one ballot) against std::sort on ranges of at most 64, with
+    every depth budget down to the heapsort fallback."""
+    rng = random.Random(9)
+    for it in range(3000):
+        m = rng.randrange(0, 65)
+        kr = rng.choice([1, 2, 3, 5, 20, 1000])
+        a = [(rng.randrange(kr) << 32) | i for i in range(m)]
+        if it % 7 == 0:
+            a.sort()
+        d = (2 * M._lg(m) if m else 0) if it % 4 else rng.randrange(0, 4)
+        assert M.wave64_sort(a, d) == M.std_sort(a, depth0=d), (m, kr, d)
