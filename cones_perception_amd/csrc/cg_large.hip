@@ -391,7 +391,7 @@ __device__ __forceinline__ uint32_t lg_lookback(uint32_t* st, uint32_t t, uint32
     uint32_t* ts = st + 2;
     const uint32_t l = lane_id();
     if (t == 0) {
-        if (l == 0) __hip_atomic_store(&ts[0], LG_ST_P | count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0) __hip_atomic_store(&ts[0], LG_ST_P | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
     if (l == 0) __hip_atomic_store(&ts[t], LG_ST_A | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -410,22 +410,25 @@ __device__ __forceinline__ uint32_t lg_lookback(uint32_t* st, uint32_t t, uint32
         if (first < 64u) break;
         hi -= 64;
     }
-    if (l == 0) __hip_atomic_store(&ts[t], LG_ST_P | (base + count), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (l == 0) __hip_atomic_store(&ts[t], LG_ST_P | (base + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return base;
 }
 // Every thread of the block, after its look-back: the last tile resets the status words.
 __device__ __forceinline__ void lg_tile_done(uint32_t* st, uint32_t active) {
     __shared__ uint32_t last;
     __syncthreads();
-    // release: this tile's status word (published above) is ordered before its count; the
-    // last tile's acquire sees every tile's final word before it zeroes them
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(&st[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
-    __syncthreads();
-    if (last) {
-        __threadfence();
-        for (uint32_t i = threadIdx.x; i < active + 2; i += CG_BLOCK) st[i] = 0;
+    // The status words are the only data the tiles exchange, and they are device-coherent
+    // atomics, so nothing needs a release (an agent-scope release writes back the XCD's whole
+    // L2). Only the zeroing must not overtake a tile's final status store: the thread that
+    // made it (lane 0 of wave 0) waits for its stores to complete (vmcnt(0)) before counting
+    // the tile done.
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
+        last = __hip_atomic_fetch_add(&st[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
     }
+    __syncthreads();
+    if (last)
+        for (uint32_t i = threadIdx.x; i < active + 2; i += CG_BLOCK) st[i] = 0;
 }
 // Block-wide: this tile's eight-per-thread counts c -> each thread's exclusive position;
 // returns through tot_out the device-wide total when this is the last active tile.
@@ -791,7 +794,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 // LDS (up to 4096 records, 8 per thread, results straight to the outputs), with the depth
 // budget left on its path; a range still longer (a degenerate split) in HBM.
 #define LG_PCL_LEAF 4096
-#define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR
+#define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
+                               // [6] wave tasks (lg_pcl_waves)
+#define PQ_WAVES 6
 #define PQ_LEAFLIST 3
 #define PQ_EW 5                // entry words: first, last, depth, then nL, nR (levels) / buffer (leaves)
 #define PQ_T CG_BLOCK          // elements per tile
@@ -882,10 +887,10 @@ __device__ __forceinline__ uint64_t pq_v(const uint64_t* E, uint32_t f, uint32_t
 __device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint32_t t, uint64_t count) {
     const uint32_t l = lane_id();
     if (t == lo) {
-        if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_A | count, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_A | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t base = 0;
     int32_t hi = (int32_t)t - 1;
     for (;;) {
@@ -903,25 +908,25 @@ __device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint3
         if (first < 64u) break;
         hi -= 64;
     }
-    if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | (base + count), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | (base + count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return base;
 }
 
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint64_t* E, uint32_t level) {
     __shared__ uint32_t tp[PQ_MAXR + 1];
     __shared__ uint32_t red[8 * WAVES];
-    __shared__ uint32_t tk, cg[WAVES], cl[WAVES], last;
+    __shared__ uint32_t tk, cg[WAVES], cl[WAVES];
     __shared__ uint64_t tbase;
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     if (level == 0 && blockIdx.x == 0 && tid == 0) {
-        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0;
+        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0;
         const uint32_t n = S.meta[LG_PCL_N];
         if (n <= LG_PCL_LEAF) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
     }
     uint32_t nr;
     const uint32_t active = pq_tiles(S, level, tp, red, nr);
     if (blockIdx.x >= active) return;
-    uint64_t* st = S.pqst;   // [0] tickets, [1] finished tiles, [2 + t] tile t's status
+    uint64_t* st = S.pqst;   // [0] tickets, [2 + t] tile t's status; lg_pq_swap zeroes them
     if (tid == 0) tk = (uint32_t)__hip_atomic_fetch_add(&st[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const uint32_t t = tk, r = pq_find(tp, nr, t), q = t - tp[r];
@@ -954,15 +959,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     if (ge) S.par[f + 1 + gi] = x;
     if (le) S.cnt[f + 1 + li] = x;
     if (valid) ((uint64_t*)S.vox)[x] = ((uint64_t)gi << 32) | li;
-    // the last tile to finish resets the status words for the next level
-    __syncthreads();
-    if (tid == 0)
-        last = __hip_atomic_fetch_add(&st[1], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
-    __syncthreads();
-    if (last) {
-        __threadfence();
-        for (uint32_t i = tid; i < active + 2; i += CG_BLOCK) st[i] = 0;
-    }
 }
 
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64_t* E, uint64_t* Eo, uint32_t level,
@@ -974,6 +970,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64
     uint32_t nr;
     const uint32_t active = pq_tiles(S, level, tp, red, nr);
     if (blockIdx.x >= active) return;
+    // lg_pq_split's ticket and status words of this level, for the next level's split (the
+    // kernel boundary orders these stores after every split tile's look-back, so its status
+    // words need no release)
+    if (tid == 0) {
+        S.pqst[2 + blockIdx.x] = 0;
+        if (blockIdx.x == 0) S.pqst[0] = 0;
+    }
     const uint32_t t = blockIdx.x, r = pq_find(tp, nr, t), q = t - tp[r];
     uint32_t f, e, d, m, p;
     pq_range(S, level, r, f, e, d);
@@ -1034,6 +1037,22 @@ struct PqLeafOut {
         v[base + i] = (uint32_t)r;
     }
 };
+// A leaf's ranges of 17-64 records go back to the leaf's HBM buffer and onto a task list
+// (S.droot: first, size | budget << 8 | buffer << 16; free until the clustering), for
+// lg_pcl_waves: one wave per range over the whole chip instead of the leaf's eight waves.
+struct PwDefer {
+    uint64_t* Eh; uint32_t* list; uint32_t* count; uint32_t base, buf;
+    template <class P64, class OUT>
+    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT) const {
+        const uint32_t l = lane_id();
+        if (l < m) Eh[base + f + l] = E[f + l];
+        if (l == 0) {
+            const uint32_t q = atomicAdd(count, 1u);
+            list[2 * q] = base + f;
+            list[2 * q + 1] = m | (d << 8) | (buf << 16);
+        }
+    }
+};
 #define LG_PCL_LDS (8 * LG_PCL_LEAF + 6 * 4 * (LG_PCL_LEAF + 4))
 // The rest of each leaf range (cg_pcl.h pcl_block_sort with the depth left on its path) from
 // the buffer its last level wrote: in LDS (8 B of record and 24 B of scratch per element),
@@ -1042,7 +1061,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
                                                         uint32_t* vout) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PCL_LDS];
     __shared__ uint32_t red[8 * WAVES];
-    __shared__ uint64_t ms[2 * WAVES * 8];   // pcl_block_sort's per-wave ballot masks
     const uint32_t n = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
     const uint32_t tid = threadIdx.x;
     for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -1055,14 +1073,16 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
             const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4),
                                       w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
             lds_u32* const Rl = (lds_u32*)red;
-            lds_u64* const Ml = (lds_u64*)(uint64_t*)ms;
             const PqLeafOut out{kout, vout, first};
+            const PwDefer wt{E, S.droot, S.pq + PQ_WAVES, first, ent[3]};
             for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
             __syncthreads();
-            if (size <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, size, depth, PS, Rl, Ml);
-            else if (size <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, size, depth, PS, Rl, Ml);
-            else if (size <= 4 * CG_BLOCK) pcl_block_sort<4, PbLds>(El, out, size, depth, PS, Rl, Ml);
-            else pcl_block_sort<8, PbLds>(El, out, size, depth, PS, Rl, Ml);
+            if (size <= CG_BLOCK) pcl_block_sort<1, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
+            else if (size <= 2 * CG_BLOCK)
+                pcl_block_sort<2, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
+            else if (size <= 4 * CG_BLOCK)
+                pcl_block_sort<4, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
+            else pcl_block_sort<8, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
         } else {   // the range's own span of the HBM arrays
             Work W{};
             W.KEY = (uint64_t*)S.vox + 2ull * first;
@@ -1076,6 +1096,18 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
             }
             __syncthreads();
         }
+    }
+}
+
+// The leaves' ranges of 17-64 records (PwDefer's list), one wave each: pw_range64 from the
+// leaf's HBM buffer, results straight to the outputs.
+__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_waves(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
+                                                         uint32_t* vout) {
+    const uint32_t n = S.pq[PQ_WAVES];
+    const PqLeafOut out{kout, vout, 0u};
+    for (uint32_t q = blockIdx.x * WAVES + wave_id(); q < n; q += gridDim.x * WAVES) {
+        const uint32_t first = S.droot[2 * q], w1 = S.droot[2 * q + 1];
+        pw_range64((w1 >> 16) ? E1 : E0, first, w1 & 0xffu, (w1 >> 8) & 0xffu, out);
     }
 }
 
@@ -1583,6 +1615,9 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
         }
         hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
                            kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
+        // ranges of 17-64 records: at most Mtot / 17 of them
+        hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, Mtot / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s,
+                           S, kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
         run_pb = 0;   // sorted keys are the idx alone
     }
     const uint64_t* vkey = buf ? S.key1 : S.key0;

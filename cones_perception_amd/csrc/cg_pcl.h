@@ -113,21 +113,23 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 // The whole workgroup sorts n <= CG_BLOCK * PER elements, every partition of a level of
 // __introsort_loop at once. Element x = tid + CG_BLOCK * k (k < PER); each thread keeps the
 // range [f, e) of its elements in registers and follows the cut after every level. Per level
-// (one LDS round trip and one barrier per step):
+// (a barrier after each step):
 //   S1. >= / <= pivot against the range's pivot; per (chunk, wave) counts;
-//   S2. exclusive counts over positions; the head and the last element of each partitioned
-//       range publish theirs (at f and f + 1: f + 1 is never a head while the range is longer
-//       than 16), so an element's index in its range's L / R list is a difference;
-//   S3. the L and R lists (from first + 1); heads reset the swap count;
+//   S2. the counts scanned: every position's exclusive >= / <= counts over the whole array
+//       (RLO, with the totals at n); the >= elements listed at their count in PL, the <= ones
+//       in PR, so a range's L list is the stretch of PL from RLO[f + 1] and its R list the
+//       stretch of PR below RLO[e], read from the right; heads reset the swap count;
 //   S4. the swaps (L_k, R_k) while L_k < R_k: every partner is read, then every element
-//       written; the last swap of a range records the swap count s;
-//   S5. each head: the cut (header: L_0 if s = 0, else min(L_s, R_{s-1})), then both children
-//       set up as __introsort_loop does (heapsort when the depth budget is spent, else the
-//       median of three moved to first and the pivot), the cut published for S0;
+//       written (or the records go out of place to E2); the last swap of a range records the
+//       swap count s;
+//   S5. each head: the cut (L_0 if s = 0, else min(L_s, R_{s-1})), then both children set up
+//       as __introsort_loop does (heapsort when the depth budget is spent, a wave task when at
+//       most 64 long, else the median of three moved to first and the pivot);
 //   S0. every element follows the cut into its child range.
-// Then the final insertion passes: a stable rank inside each range of at most 16; heapsorted
-// ranges are sorted already. Scratch: INFO (act | final | budget at heads), PIV, RLO, PL, PR,
-// CUT (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
+// Then the ranges of 17-64 records, one wave each (pw_range64), and the final insertion
+// passes of the rest: a stable rank inside each range of at most 16; heapsorted ranges are
+// sorted already. Scratch: INFO (act | final | wave | budget at heads), PIV, RLO, PL, PR, CUT
+// (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
 #define PB_ACT 0x100u
 #define PB_FIN 0x200u
 #define PB_WAVE 0x400u   // a range of at most PW_MAX records with budget left: one wave sorts it
@@ -274,9 +276,9 @@ __device__ __forceinline__ void pw_range64(P64 E, uint32_t f, uint32_t m, uint32
     const bool heap = live && en - hd > CG_SORT_THRESHOLD;
     if (__ballot(heap)) {
         if (live) E[f + l] = v;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");   // E may be in HBM (rare path)
         if (heap && l == hd) cg_heap_sort_range((uint64_t*)(E + f + hd), (long)(en - hd), PwLess{});
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
         if (live) v = E[f + l];
     }
     // the final insertion passes: a stable rank inside each sub-range of at most 16
@@ -291,14 +293,23 @@ __device__ __forceinline__ void pw_range64(P64 E, uint32_t f, uint32_t m, uint32
     if (live) out(f + hd + rank, v);
 }
 
+// The ranges of 17-64 records: by the workgroup's own waves (PwInline), or handed to another
+// launch (a functor of the same shape: the large path's leaves, lg_pcl_leaf).
+struct PwInline {
+    template <class P64, class OUT>
+    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
+        pw_range64(E, f, m, d, out);
+    }
+};
+
 // OOP: a second record buffer E2 (n records) takes the swapped records, so a level's swap
 // step reads and writes in one barrier interval (E and E2 trade places every level); without
-// it the records are swapped in place (reads, barrier, writes). MS: 2 * 8 * PER words of
-// 64 bits for the per-wave ballot masks.
-template <int PER, class K, class OUT = PbStore<typename K::P64>, bool OOP = false>
+// it the records are swapped in place (reads, barrier, writes). cnt: PER * WAVES words (the
+// per-slot counts). S.RLO holds n + 1 words.
+template <int PER, class K, class OUT = PbStore<typename K::P64>, bool OOP = false, class WT = PwInline>
 __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint32_t n, uint32_t depth0,
-                                               const PbScratch<K> S, typename K::P32 cnt, typename K::P64 MS,
-                                               typename K::P64 E2 = nullptr) {
+                                               const PbScratch<K> S, typename K::P32 cnt,
+                                               typename K::P64 E2 = nullptr, WT wt = WT{}) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     constexpr uint32_t GE = 1u << 24, LE = 1u << 25, IN = 1u << 26, PART = 1u << 27;
     constexpr uint32_t NS = PER * WAVES;   // (chunk, wave) slots: position x is in slot x / 64
@@ -312,7 +323,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
     bool any = __syncthreads_or(act);
     while (any) {
         uint32_t st[PER], nn[PER];
-        // S1: compare with the range's pivot; per-slot counts and ballot masks
+        // S1: compare with the range's pivot; per-slot counts
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
@@ -325,86 +336,66 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
             const bool part = (info & PB_ACT) != 0, in = part && x > f;
             const bool ge = in && kx >= p, le = in && kx <= p;
             const uint64_t gm = __ballot(ge), lm = __ballot(le);
-            if (l == 0) {
-                const uint32_t slot = k * WAVES + w;
-                cnt[slot] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
-                MS[2 * slot] = gm;
-                MS[2 * slot + 1] = lm;
-            }
+            if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
             st[k] = mbcnt(gm) | (mbcnt(lm) << 12) | (ge ? GE : 0u) | (le ? LE : 0u) | (in ? IN : 0u) | (part ? PART : 0u);
         }
         __syncthreads();
         PCL_STEP();
-        // S2: lane j of every wave scans the slot counts; an element's own counts, and the
-        // counts before its range's f + 1 and e (slot prefix by ds_bpermute plus the slot's
-        // mask below the position), give its L / R list index; the lists are written here
+        // S2: lane j of every wave scans the slot counts; every position's exclusive >= / <=
+        // counts over the whole array go to RK (RK[n]: the totals), and the >= elements are
+        // listed in position order at their >= count in PL, the <= elements at theirs in PR:
+        // a range's L list is then a contiguous stretch of PL from RK[f + 1], its R list the
+        // stretch of PR below RK[e], read from the right
         {
             const uint32_t cj = l < NS ? cnt[l] : 0u;
             const uint32_t g = wave_incl_scan(cj & 0xffffu), h = wave_incl_scan(cj >> 16);
             const uint32_t gex = g - (cj & 0xffffu), hex = h - (cj >> 16);
-            const uint32_t totg = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)(NS - 1));
-            const uint32_t totl = (uint32_t)__builtin_amdgcn_readlane((int)h, (int)(NS - 1));
-            uint32_t s1[PER], se[PER];
-            uint64_t m1g[PER], m1l[PER], meg[PER], mel[PER];
-            uint32_t p1g[PER], p1l[PER], peg[PER], pel[PER];
-#pragma unroll
-            for (int k = 0; k < PER; k++) {
-                const uint32_t f = fe[k] & 0xffffu, e = fe[k] >> 16;
-                s1[k] = min((f + 1) >> 6, NS - 1);
-                se[k] = min(e >> 6, NS - 1);
-                m1g[k] = MS[2 * s1[k]]; m1l[k] = MS[2 * s1[k] + 1];
-                meg[k] = MS[2 * se[k]]; mel[k] = MS[2 * se[k] + 1];
-                p1g[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * s1[k]), (int)gex);
-                p1l[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * s1[k]), (int)hex);
-                peg[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * se[k]), (int)gex);
-                pel[k] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * se[k]), (int)hex);
+            if (tid == 0) {
+                S.RLO[n] = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)(NS - 1)) |
+                           ((uint32_t)__builtin_amdgcn_readlane((int)h, (int)(NS - 1)) << 16);
             }
 #pragma unroll
             for (int k = 0; k < PER; k++) {
-                const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+                const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
                 const uint32_t src = (uint32_t)k * WAVES + w;
                 const uint32_t gx = (uint32_t)__builtin_amdgcn_readlane((int)gex, (int)src) + (st[k] & 0xfffu);
                 const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)hex, (int)src) + ((st[k] >> 12) & 0xfffu);
-                nn[k] = 0;
-                if (st[k] & PART) {
-                    const uint64_t b1 = (1ull << ((f + 1) & 63u)) - 1ull;
-                    const uint32_t gf = p1g[k] + (uint32_t)__popcll(m1g[k] & b1);
-                    const uint32_t lf = p1l[k] + (uint32_t)__popcll(m1l[k] & b1);
-                    uint32_t gend = totg, lend = totl;
-                    if ((e >> 6) < NS) {
-                        const uint64_t be = (1ull << (e & 63u)) - 1ull;
-                        gend = peg[k] + (uint32_t)__popcll(meg[k] & be);
-                        lend = pel[k] + (uint32_t)__popcll(mel[k] & be);
-                    }
-                    nn[k] = (gend - gf) | ((lend - lf) << 16);
-                    if (x == f) S.CUT[f] = 0u;
-                    if (st[k] & IN) {
-                        const uint32_t li = gx - gf, ri = lend - lx - 1u;
-                        if (st[k] & GE) S.PL[f + 1 + li] = x;
-                        if (st[k] & LE) S.PR[f + 1 + ri] = x;
-                        st[k] = li | ((ri & 0xfffu) << 12) | (st[k] & (GE | LE | IN | PART));
-                    }
-                }
+                if (x < n) S.RLO[x] = gx | (lx << 16);
+                if (st[k] & GE) S.PL[gx] = x;
+                if (st[k] & LE) S.PR[lx] = x;
+                if ((st[k] & PART) && x == f) S.CUT[f] = 0u;
+                st[k] = (gx & 0xfffu) | ((lx & 0xfffu) << 12) | (st[k] & (GE | LE | IN | PART));
             }
         }
         __syncthreads();
         PCL_STEP();
-        // S4: the partners and the next pair in one batch, then the partners' records
+        // S4: the range's list bounds, the partners and the next pair in one batch, then the
+        // partners' records
         uint64_t val[PER];
         uint32_t sw = 0;
+        uint32_t bf[PER], be[PER];
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            const uint32_t f = fe[k] & 0xffffu, e = fe[k] >> 16;
+            const bool part = (st[k] & PART) != 0;
+            bf[k] = part ? S.RLO[f + 1] : 0u;
+            be[k] = part ? S.RLO[e] : 0u;
+        }
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
             const bool in = (st[k] & IN) != 0;
-            const uint32_t li = in ? (st[k] & 0xfffu) : 0u, ri = in ? ((st[k] >> 12) & 0xfffu) : 0u;
-            const uint32_t nL = nn[k] & 0xffffu, nR = nn[k] >> 16;
+            const uint32_t gf = bf[k] & 0xffffu, lend = be[k] >> 16;
+            const uint32_t nL = (be[k] & 0xffffu) - gf, nR = lend - (bf[k] >> 16);
+            nn[k] = nL | (nR << 16);
+            const uint32_t li = in ? (st[k] & 0xfffu) - gf : 0u, ri = in ? lend - 1u - ((st[k] >> 12) & 0xfffu) : 0u;
             const bool hasL = in && (st[k] & GE) && li < nR, hasR = in && (st[k] & LE) && ri < nL;
             const bool nxt = hasL && li + 1 < min(nL, nR);
             const uint32_t top = n ? n - 1 : 0u;
-            const uint32_t j = S.PR[min(f + 1 + (hasL ? li : 0u), top)];
-            const uint32_t i = S.PL[min(f + 1 + (hasR ? ri : 0u), top)];
-            const uint32_t pl2 = S.PL[min(f + 2 + (nxt ? li : 0u), top)];
-            const uint32_t pr2 = S.PR[min(f + 2 + (nxt ? li : 0u), top)];
+            const uint32_t j = S.PR[hasL ? lend - 1u - li : 0u];        // R_li
+            const uint32_t i = S.PL[hasR ? gf + ri : 0u];                // L_ri
+            const uint32_t pl2 = S.PL[min(nxt ? gf + li + 1u : 0u, top)];          // L_li+1
+            const uint32_t pr2 = S.PR[nxt ? lend - 2u - li : 0u];        // R_li+1
             uint32_t partner = x;
             if (hasL && x < j) {
                 partner = j;
@@ -441,9 +432,10 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         for (int k = 0; k < PER; k++) {
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
             if ((st[k] & PART) && x == f) {
-                const uint32_t s = S.CUT[f], info = S.INFO[f], pl1 = S.PL[f + 1];
-                const uint32_t nL = nn[k] & 0xffffu;
-                const uint32_t pls = s < nL ? S.PL[f + 1 + s] : 0xffffffffu, prs = s ? S.PR[f + s] : 0u;
+                const uint32_t s = S.CUT[f], info = S.INFO[f];
+                const uint32_t gf = S.RLO[f + 1] & 0xffffu, lend = S.RLO[e] >> 16, nL = nn[k] & 0xffffu;
+                const uint32_t pl1 = S.PL[gf];
+                const uint32_t pls = s < nL ? S.PL[gf + s] : 0xffffffffu, prs = s ? S.PR[lend - s] : 0u;
                 const uint32_t cut = s == 0 ? pl1 : min(pls, prs);
                 act |= pb_children<K>(E, S, f, cut, e, (info & PB_BUDGET) - 1u);
                 S.CUT[f] = cut;
@@ -482,9 +474,10 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         const uint32_t nw = cnt[0];
         for (uint32_t q = w; q < nw; q += WAVES) {
             const uint32_t r = S.PL[q];
-            pw_range64(E, r & 0xffffu, (r >> 16) - (r & 0xffffu), S.PR[q], out);
+            wt(E, r & 0xffffu, (r >> 16) - (r & 0xffffu), S.PR[q], out);
         }
     }
+    PCL_STEP();
     // the final insertion passes of the other ranges
 #pragma unroll
     for (int k = 0; k < PER; k++) {
@@ -524,7 +517,6 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
 template <int PMAX, bool LDS>
 __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n, uint32_t* red, int depth0 = -1,
                                          uint64_t* E2 = nullptr) {
-    __shared__ uint64_t ms[2 * WAVES * PMAX];   // the per-wave ballot masks
     constexpr uint32_t PCL_BLOCK_MAX = PMAX * CG_BLOCK;
     const uint32_t tid = threadIdx.x;
     uint32_t* PRE = W.A;
@@ -544,24 +536,23 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         lds_u64* const Ko = (lds_u64*)W.KEY;
         lds_u32* const Rl = (lds_u32*)red;
         const PbStore<lds_u64*> out{Ko};
-        lds_u64* const Ml = (lds_u64*)(uint64_t*)ms;
         if (E2) {
             lds_u64* const E2l = (lds_u64*)E2;
-            if (n <= CG_BLOCK) pcl_block_sort<1, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, Ml, E2l);
+            if (n <= CG_BLOCK) pcl_block_sort<1, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, E2l);
             else if (PMAX == 2 || n <= 2 * CG_BLOCK)
-                pcl_block_sort<2, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, Ml, E2l);
-            else pcl_block_sort<PMAX, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, Ml, E2l);
+                pcl_block_sort<2, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, E2l);
+            else pcl_block_sort<PMAX, PbLds, PbStore<lds_u64*>, true>(El, out, n, d0, PS, Rl, E2l);
         } else {
-            if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, n, d0, PS, Rl, Ml);
-            else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, n, d0, PS, Rl, Ml);
-            else pcl_block_sort<PMAX, PbLds>(El, out, n, d0, PS, Rl, Ml);
+            if (n <= CG_BLOCK) pcl_block_sort<1, PbLds>(El, out, n, d0, PS, Rl);
+            else if (PMAX == 2 || n <= 2 * CG_BLOCK) pcl_block_sort<2, PbLds>(El, out, n, d0, PS, Rl);
+            else pcl_block_sort<PMAX, PbLds>(El, out, n, d0, PS, Rl);
         }
         PCL_STAMP();
         return;
     }
     const PbScratch<PbGen> PS{(uint32_t*)W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD};
     if (n <= PMAX * CG_BLOCK) {
-        pcl_block_sort<PMAX, PbGen>(E, PbStore<uint64_t*>{W.KEY}, n, d0, PS, red, (uint64_t*)ms);
+        pcl_block_sort<PMAX, PbGen>(E, PbStore<uint64_t*>{W.KEY}, n, d0, PS, red);
         PCL_STAMP();
         return;
     }
@@ -707,7 +698,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         pcl_block_sort<PMAX, PbGen>(E + first, PbStore<uint64_t*>{KEY + first}, size, depth,
                                     PbScratch<PbGen>{(uint32_t*)W.LAB + first, W.OFF + first, W.A + first,
                                                      W.PAR + first, W.CNT + first, W.ORD + first},
-                                    red, (uint64_t*)ms);
+                                    red);
     }
     __syncthreads();
     PCL_STAMP();
