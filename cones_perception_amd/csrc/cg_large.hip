@@ -795,8 +795,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 // budget left on its path; a range still longer (a degenerate split) in HBM.
 #define LG_PCL_LEAF 4096
 #define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
-                               // [6] wave tasks (lg_pcl_waves)
+                               // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
 #define PQ_WAVES 6
+#define PQ_MIDS 7
 #define PQ_LEAFLIST 3
 #define PQ_EW 5                // entry words: first, last, depth, then nL, nR (levels) / buffer (leaves)
 #define PQ_T CG_BLOCK          // elements per tile
@@ -919,7 +920,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     __shared__ uint64_t tbase;
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     if (level == 0 && blockIdx.x == 0 && tid == 0) {
-        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0;
+        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0; S.pq[PQ_MIDS] = 0;
         const uint32_t n = S.meta[LG_PCL_N];
         if (n <= LG_PCL_LEAF) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
     }
@@ -1037,19 +1038,23 @@ struct PqLeafOut {
         v[base + i] = (uint32_t)r;
     }
 };
-// A leaf's ranges of 17-64 records go back to the leaf's HBM buffer and onto a task list
-// (S.droot: first, size | budget << 8 | buffer << 16; free until the clustering), for
-// lg_pcl_waves: one wave per range over the whole chip instead of the leaf's eight waves.
-struct PwDefer {
+// Ranges handed on to a chip-wide launch: their records go back to the HBM buffer the range
+// was loaded from and onto a task list (first, size | budget << 16 | buffer << 24):
+//   lg_pcl_leaf's ranges of 65-512 records -> S.dsz, for lg_pcl_mid (one workgroup each);
+//   lg_pcl_mid's ranges of 17-64 records  -> S.droot, for lg_pcl_waves (one wave each).
+// (S.dsz and S.droot are free until the clustering.) The leaf and mid workgroups then only
+// run the levels of their longer ranges, on a few CUs; the tasks spread over the chip.
+#define PQ_MID 512
+struct PqDefer {
     uint64_t* Eh; uint32_t* list; uint32_t* count; uint32_t base, buf;
     template <class P64, class OUT>
     __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT) const {
         const uint32_t l = lane_id();
-        if (l < m) Eh[base + f + l] = E[f + l];
+        for (uint32_t i = l; i < m; i += 64) Eh[base + f + i] = E[f + i];
         if (l == 0) {
             const uint32_t q = atomicAdd(count, 1u);
             list[2 * q] = base + f;
-            list[2 * q + 1] = m | (d << 8) | (buf << 16);
+            list[2 * q + 1] = m | (d << 16) | (buf << 24);
         }
     }
 };
@@ -1074,15 +1079,16 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
                                       w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
             lds_u32* const Rl = (lds_u32*)red;
             const PqLeafOut out{kout, vout, first};
-            const PwDefer wt{E, S.droot, S.pq + PQ_WAVES, first, ent[3]};
+            const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ent[3]};
             for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
             __syncthreads();
-            if (size <= CG_BLOCK) pcl_block_sort<1, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
+            if (size <= CG_BLOCK)
+                pcl_block_sort<1, PbLds, PqLeafOut, false, PqDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
             else if (size <= 2 * CG_BLOCK)
-                pcl_block_sort<2, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
+                pcl_block_sort<2, PbLds, PqLeafOut, false, PqDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
             else if (size <= 4 * CG_BLOCK)
-                pcl_block_sort<4, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else pcl_block_sort<8, PbLds, PqLeafOut, false, PwDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
+                pcl_block_sort<4, PbLds, PqLeafOut, false, PqDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
+            else pcl_block_sort<8, PbLds, PqLeafOut, false, PqDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
         } else {   // the range's own span of the HBM arrays
             Work W{};
             W.KEY = (uint64_t*)S.vox + 2ull * first;
@@ -1099,15 +1105,39 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
     }
 }
 
-// The leaves' ranges of 17-64 records (PwDefer's list), one wave each: pw_range64 from the
-// leaf's HBM buffer, results straight to the outputs.
+// The leaves' ranges of 65-512 records (S.dsz), one workgroup each, in LDS; their ranges of
+// 17-64 records go on to lg_pcl_waves.
+#define LG_MID_LDS (8 * PQ_MID + 6 * 4 * (PQ_MID + 4))
+__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
+                                                       uint32_t* vout) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[LG_MID_LDS];
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t n = S.pq[PQ_MIDS];
+    lds_u64* const El = (lds_u64*)(uint64_t*)smem;
+    lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * PQ_MID);
+    const PbScratch<PbLds> PS{w0, w0 + (PQ_MID + 4), w0 + 2 * (PQ_MID + 4), w0 + 3 * (PQ_MID + 4),
+                              w0 + 4 * (PQ_MID + 4), w0 + 5 * (PQ_MID + 4)};
+    lds_u32* const Rl = (lds_u32*)red;
+    for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const uint32_t first = S.dsz[2 * b], w1 = S.dsz[2 * b + 1];
+        const uint32_t size = w1 & 0xffffu, depth = (w1 >> 16) & 0xffu, buf = w1 >> 24;
+        uint64_t* const E = buf ? E1 : E0;
+        for (uint32_t i = threadIdx.x; i < size; i += CG_BLOCK) El[i] = E[first + i];
+        __syncthreads();
+        const PqDefer wt{E, S.droot, S.pq + PQ_WAVES, first, buf};
+        pcl_block_sort<1, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS, Rl,
+                                                            nullptr, wt);
+    }
+}
+// The ranges of 17-64 records (S.droot), one wave each: pw_range64 from the HBM buffer,
+// results straight to the outputs.
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_waves(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
                                                          uint32_t* vout) {
     const uint32_t n = S.pq[PQ_WAVES];
     const PqLeafOut out{kout, vout, 0u};
     for (uint32_t q = blockIdx.x * WAVES + wave_id(); q < n; q += gridDim.x * WAVES) {
         const uint32_t first = S.droot[2 * q], w1 = S.droot[2 * q + 1];
-        pw_range64((w1 >> 16) ? E1 : E0, first, w1 & 0xffu, (w1 >> 8) & 0xffu, out);
+        pw_range64((w1 >> 24) ? E1 : E0, first, w1 & 0xffffu, (w1 >> 16) & 0xffu, out);
     }
 }
 
@@ -1615,7 +1645,9 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
         }
         hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
                            kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
-        // ranges of 17-64 records: at most Mtot / 17 of them
+        // ranges of 65-512 records, then of 17-64 records: at most Mtot / 65 and Mtot / 17
+        hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, Mtot / 65 + 1)), dim3(CG_BLOCK), 0, s, S,
+                           kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
         hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, Mtot / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s,
                            S, kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
         run_pb = 0;   // sorted keys are the idx alone

@@ -158,7 +158,7 @@ __device__ __forceinline__ uint32_t pb_median(uint32_t a, uint32_t b, uint32_t c
 // (final), else its median of three is moved to its first and its pivot noted (partitioned in
 // the next level). The eight elements are read in one batch, then written. Returns whether a
 // child is partitioned next.
-template <class K>
+template <class K, uint32_t WMAX>
 __device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K>& S, uint32_t f, uint32_t cut,
                                             uint32_t e, uint32_t d) {
     const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
@@ -167,7 +167,7 @@ __device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K
     uint64_t v0[2], va[2], vb[2], vc[2];
 #pragma unroll
     for (int c = 0; c < 2; c++) {
-        med[c] = hi[c] - lo[c] > PW_MAX && d > 0;
+        med[c] = hi[c] - lo[c] > WMAX && d > 0;
         ia[c] = lo[c] + 1; ib[c] = lo[c] + (hi[c] - lo[c]) / 2; ic[c] = hi[c] - 1;
         if (med[c]) { v0[c] = E[lo[c]]; va[c] = E[ia[c]]; vb[c] = E[ib[c]]; vc[c] = E[ic[c]]; }
     }
@@ -179,7 +179,7 @@ __device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K
             if (d == 0) {   // __partial_sort(first, last, last): final
                 cg_heap_sort_range((uint64_t*)(E + lo[c]), (long)(hi[c] - lo[c]), PwLess{});
                 info |= PB_FIN;
-            } else if (hi[c] - lo[c] <= PW_MAX) {   // the rest of it in one wave (pw_range64)
+            } else if (hi[c] - lo[c] <= WMAX) {   // the rest of it as a task (one wave: pw_range64)
                 info |= PB_WAVE;
             } else {
                 const uint32_t m = pb_median(ia[c], ib[c], ic[c], pcl_key(va[c]), pcl_key(vb[c]), pcl_key(vc[c]));
@@ -293,8 +293,8 @@ __device__ __forceinline__ void pw_range64(P64 E, uint32_t f, uint32_t m, uint32
     if (live) out(f + hd + rank, v);
 }
 
-// The ranges of 17-64 records: by the workgroup's own waves (PwInline), or handed to another
-// launch (a functor of the same shape: the large path's leaves, lg_pcl_leaf).
+// The ranges of 17-WMAX records: by the workgroup's own waves (PwInline, WMAX = 64), or
+// handed to another launch (a functor of the same shape: the large path, PqDefer).
 struct PwInline {
     template <class P64, class OUT>
     __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
@@ -306,7 +306,10 @@ struct PwInline {
 // step reads and writes in one barrier interval (E and E2 trade places every level); without
 // it the records are swapped in place (reads, barrier, writes). cnt: PER * WAVES words (the
 // per-slot counts). S.RLO holds n + 1 words.
-template <int PER, class K, class OUT = PbStore<typename K::P64>, bool OOP = false, class WT = PwInline>
+// WMAX: ranges of at most WMAX records (with budget left) leave the levels as tasks for wt;
+// PwInline takes at most PW_MAX.
+template <int PER, class K, class OUT = PbStore<typename K::P64>, bool OOP = false, class WT = PwInline,
+          uint32_t WMAX = PW_MAX>
 __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint32_t n, uint32_t depth0,
                                                const PbScratch<K> S, typename K::P32 cnt,
                                                typename K::P64 E2 = nullptr, WT wt = WT{}) {
@@ -318,7 +321,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
     for (int k = 0; k < PER; k++) fe[k] = n << 16;
     bool act = false;
     if (tid == 0 && n) {   // the whole array as the right child of an empty range
-        act = pb_children<K>(E, S, 0, 0, n, depth0);
+        act = pb_children<K, WMAX>(E, S, 0, 0, n, depth0);
     }
     bool any = __syncthreads_or(act);
     while (any) {
@@ -437,7 +440,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
                 const uint32_t pl1 = S.PL[gf];
                 const uint32_t pls = s < nL ? S.PL[gf + s] : 0xffffffffu, prs = s ? S.PR[lend - s] : 0u;
                 const uint32_t cut = s == 0 ? pl1 : min(pls, prs);
-                act |= pb_children<K>(E, S, f, cut, e, (info & PB_BUDGET) - 1u);
+                act |= pb_children<K, WMAX>(E, S, f, cut, e, (info & PB_BUDGET) - 1u);
                 S.CUT[f] = cut;
             }
         }
@@ -453,7 +456,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
             }
         }
     }
-    // ranges of at most PW_MAX records with budget left: one wave each (pw_range64), listed
+    // ranges of at most WMAX records with budget left: one wave each (wt), listed
     // in PL (first | last << 16) and PR (budget), the count in cnt[0]
     if (tid == 0) cnt[0] = 0u;
     __syncthreads();
