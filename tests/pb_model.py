@@ -129,19 +129,22 @@ def std_sort(a, depth0=None):
 
 # ---- the block model ------------------------------------------------------------------------
 BLOCK, WAVES = 512, 8
-ACT, FINB, BUDGET = 0x100, 0x200, 0xFF
+ACT, FINB, WAVEB, BUDGET = 0x100, 0x200, 0x400, 0xFF
+PW_MAX = 64
 
 
 def _popc(m):
     return bin(m).count("1")
 
 
-def _setup(E, S, cf, ce, d):
+def _setup(E, S, cf, ce, d, wmax):
     info, act = d, False
     if ce - cf > THRESH:
         if d == 0:
             heap_sort_range(E, cf, ce - cf)
             info |= FINB
+        elif ce - cf <= wmax:
+            info |= WAVEB
         else:
             move_median_to_first(E, cf, cf + 1, cf + (ce - cf) // 2, ce - 1)
             S["PIV"][cf] = key(E[cf])
@@ -151,9 +154,11 @@ def _setup(E, S, cf, ce, d):
     return act
 
 
-def block_sort(E_in, PER=None, depth0=None, oop=False):
+def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False):
     """cg_pcl.h pcl_block_sort, thread by thread: element x = tid + 512 k (oop: the swaps go
-    to a second buffer, as in the frame kernel)."""
+    to a second buffer, as in the frame kernel). Ranges of 17..wmax records with budget left
+    leave the levels as tasks: sorted by wave_sort (PwInline), or, with defer, returned as
+    (first, size, budget, records) with their output positions left None (PqDefer)."""
     n = len(E_in)
     if PER is None:
         PER = 1 if n <= 512 else 2 if n <= 1024 else 4 if n <= 2048 else 8
@@ -162,13 +167,12 @@ def block_sort(E_in, PER=None, depth0=None, oop=False):
         depth0 = 2 * _lg(n) if n else 0
     E = Arr(n)
     E.v = list(E_in)
-    out = Arr(n)
+    out = Arr(n, None)
     S = {k: Arr(n + 1) for k in ("INFO", "PIV", "RLO", "PL", "PR", "CUT")}
     cnt = Arr(8 * PER)
-    MS = Arr(2 * 8 * PER)
     T = range(BLOCK)
     fe = [[n << 16] * PER for _ in T]
-    anyact = _setup(E, S, 0, n, depth0) if n else False
+    anyact = _setup(E, S, 0, n, depth0, wmax) if n else False
     while anyact:
         st = [[0] * PER for _ in T]
         nn = [[0] * PER for _ in T]
@@ -188,64 +192,58 @@ def block_sort(E_in, PER=None, depth0=None, oop=False):
                 gm = sum(1 << l for l in range(64) if ge[64 * w + l])
                 lm = sum(1 << l for l in range(64) if le[64 * w + l])
                 cnt[k * WAVES + w] = _popc(gm) | (_popc(lm) << 16)
-                MS[2 * (k * WAVES + w)], MS[2 * (k * WAVES + w) + 1] = gm, lm
                 for l in range(64):
                     t = 64 * w + l
                     st[t][k].update(ge=ge[t], le=le[t], mg=_popc(gm & ((1 << l) - 1)), ml=_popc(lm & ((1 << l) - 1)))
-        NS = PER * WAVES                             # S2: counts from the slot masks
+        NS = PER * WAVES                             # S2: global ranks, lists at those ranks
         c = [cnt[j] for j in range(NS)]
         gex = [sum(c[i] & 0xFFFF for i in range(j)) for j in range(NS)]
         hex_ = [sum(c[i] >> 16 for i in range(j)) for j in range(NS)]
-        totg, totl = sum(v & 0xFFFF for v in c), sum(v >> 16 for v in c)
-
-        def before(y):   # (>= count, <= count) of the positions before y
-            if (y >> 6) >= NS:
-                return totg, totl
-            sl, b = y >> 6, (1 << (y & 63)) - 1
-            return gex[sl] + _popc(MS[2 * sl] & b), hex_[sl] + _popc(MS[2 * sl + 1] & b)
+        S["RLO"][n] = sum(v & 0xFFFF for v in c) | (sum(v >> 16 for v in c) << 16)
         for t in T:
             w = t // 64
             for k in range(PER):
-                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
+                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
                 q = st[t][k]
                 gx, lx = gex[k * WAVES + w] + q["mg"], hex_[k * WAVES + w] + q["ml"]
                 assert gx < 4096 and lx < 4096
                 q.update(gx=gx, lx=lx)
-                if q["part"]:
-                    gf, lf = before(f + 1)
-                    gend, lend = before(e)
-                    nn[t][k] = (gend - gf, lend - lf)
-                    if x == f:
-                        S["CUT"][f] = 0
-                    if q["inn"]:
-                        li, ri = gx - gf, lend - lx - 1
-                        if q["ge"]:
-                            S["PL"][f + 1 + li] = x
-                        if q["le"]:
-                            S["PR"][f + 1 + ri] = x
-                        q.update(li=li, ri=ri)
+                if x < n:
+                    S["RLO"][x] = gx | (lx << 16)
+                if q["ge"]:
+                    S["PL"][gx] = x
+                if q["le"]:
+                    S["PR"][lx] = x
+                if q["part"] and x == f:
+                    S["CUT"][f] = 0
         val = {}
-        for t in T:                                  # S4
+        for t in T:                                  # S4: a range's bounds from RLO
             for k in range(PER):
-                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
+                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
                 q = st[t][k]
-                if q["inn"]:
-                    nL, nR = nn[t][k]
-                    partner = x
-                    if q["ge"] and q["li"] < nR:
-                        j = S["PR"][f + 1 + q["li"]]
-                        if x < j:
-                            partner = j
-                            li = q["li"]
-                            if li + 1 >= min(nL, nR) or not S["PL"][f + 2 + li] < S["PR"][f + 2 + li]:
-                                S["CUT"][f] = li + 1
-                    if q["le"] and q["ri"] < nL:
-                        i = S["PL"][f + 1 + q["ri"]]
-                        if i < x:
-                            assert partner == x, "an element swapped twice"
-                            partner = i
-                    if partner != x:
-                        val[x] = E[partner]
+                if not q["part"]:
+                    continue
+                bf, be = S["RLO"][f + 1], S["RLO"][e]
+                gf, lend = bf & 0xFFFF, be >> 16
+                nL, nR = (be & 0xFFFF) - gf, lend - (bf >> 16)
+                nn[t][k] = (nL, nR)
+                if not q["inn"]:
+                    continue
+                li, ri = q["gx"] - gf, lend - 1 - q["lx"]
+                partner = x
+                if q["ge"] and li < nR:
+                    j = S["PR"][lend - 1 - li]            # R_li
+                    if x < j:
+                        partner = j
+                        if li + 1 >= min(nL, nR) or not S["PL"][gf + li + 1] < S["PR"][lend - 2 - li]:
+                            S["CUT"][f] = li + 1
+                if q["le"] and ri < nL:
+                    i = S["PL"][gf + ri]                 # L_ri
+                    if i < x:
+                        assert partner == x, "an element swapped twice"
+                        partner = i
+                if partner != x:
+                    val[x] = E[partner]
         if oop:   # every record to the other buffer, then the buffers trade places
             E2 = Arr(n)
             E2.v = list(E.v)
@@ -261,10 +259,11 @@ def block_sort(E_in, PER=None, depth0=None, oop=False):
                 x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
                 if st[t][k]["part"] and x == f:
                     s, nL = S["CUT"][f], nn[t][k][0]
-                    cut = S["PL"][f + 1] if s == 0 else min(S["PL"][f + 1 + s] if s < nL else 0xFFFFFFFF, S["PR"][f + s])
+                    gf, lend = S["RLO"][f + 1] & 0xFFFF, S["RLO"][e] >> 16
+                    cut = S["PL"][gf] if s == 0 else min(S["PL"][gf + s] if s < nL else 0xFFFFFFFF, S["PR"][lend - s])
                     d = (S["INFO"][f] & BUDGET) - 1
-                    anyact |= _setup(E, S, f, cut, d)
-                    anyact |= _setup(E, S, cut, e, d)
+                    anyact |= _setup(E, S, f, cut, d, wmax)
+                    anyact |= _setup(E, S, cut, e, d, wmax)
                     S["CUT"][f] = cut
         for t in T:                                  # S0
             for k in range(PER):
@@ -272,10 +271,21 @@ def block_sort(E_in, PER=None, depth0=None, oop=False):
                 if st[t][k]["part"]:
                     cc = S["CUT"][f]
                     fe[t][k] = (f | (cc << 16)) if x < cc else (cc | (e << 16))
+    tasks = []                                       # ranges of 17..wmax: tasks
     for t in T:
         for k in range(PER):
             x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-            if x < n:
+            if x < n and x == f and S["INFO"][f] & WAVEB:
+                tasks.append((f, e - f, S["INFO"][f] & BUDGET, [E[j] for j in range(f, e)]))
+    for (f, m, d, recs) in tasks:
+        if not defer:
+            assert m <= PW_MAX
+            for i, r in enumerate(wave_sort(recs, d)):
+                out[f + i] = r
+    for t in T:                                      # final insertion passes of the rest
+        for k in range(PER):
+            x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
+            if x < n and not S["INFO"][f] & WAVEB:
                 r = E[x]
                 if S["INFO"][f] & FINB:
                     out[x] = r
@@ -284,7 +294,7 @@ def block_sort(E_in, PER=None, depth0=None, oop=False):
                     kx = key(r)
                     rank = sum(1 for j in range(f, e) if key(E[j]) < kx or (key(E[j]) == kx and j < x))
                     out[f + rank] = r
-    return out.v
+    return (out.v, tasks) if defer else out.v
 
 
 # ---- the large path's partition levels (cg_large.hip lg_pq_split / lg_pq_swap / lg_pcl_leaf) ----
@@ -361,68 +371,115 @@ def levels_sort(E_in, leaf=4096, levels=None):
         cur = nxt
     assert not cur
     out = [None] * n
-    for (f, e, d, b) in leaves:
+    for (f, e, d, b) in leaves:   # lg_pcl_leaf -> lg_pcl_mid -> lg_pcl_waves
         seg = bufs[b][f:e]
-        out[f:e] = block_sort(seg, depth0=d) if e - f <= min(leaf, 4096) else std_sort(seg, depth0=d)
+        if e - f > min(leaf, 4096):
+            out[f:e] = std_sort(seg, depth0=d)
+            continue
+        lo, mids = block_sort(seg, depth0=d, wmax=512, defer=True)
+        for (mf, mm, md, mrecs) in mids:
+            mo, waves = block_sort(mrecs, depth0=md, defer=True)
+            for (wf, wm, wd, wrecs) in waves:
+                mo[wf:wf + wm] = wave_sort(wrecs, wd)
+            lo[mf:mf + mm] = mo
+        assert None not in lo
+        out[f:e] = lo
     return out
 
 
 # ---- cg_pcl.h pw_range64: one wave sorts a range of at most 64 records in registers ---------
-def _sel(mask, j):
-    """Position of the j-th (0-based) set bit of a 64-bit mask: the popcount binary search."""
-    lo = 0
-    for step in (32, 16, 8, 4, 2, 1):
-        if _popc(mask & ((1 << (lo + step)) - 1)) <= j:
-            lo += step
-    return lo
-
-
-def wave64_sort(recs, depth):
-    """The whole range [0, m) as __introsort_loop + __final_insertion_sort restricted to it
-    (depth: the budget left on its path), lane i holding record i."""
+def wave_sort(recs, depth):
+    """cg_pcl.h pw_range64, lane by lane: lane l holds record l and its sub-range [hd, en) and
+    budget; every sub-range longer than 16 with budget partitions in the same round (lane
+    tables PG / PL as ds_permute builds them, reads as ds_bpermute); spent budgets heapsort;
+    then a stable rank inside each sub-range of at most 16 (heapsorted ones: as they are)."""
     m = len(recs)
-    assert m <= 64
-    v = list(recs) + [None] * (64 - m)
-    key_ = lambda i: key(v[i])
-    stack = [(0, m, depth)]
-    while stack:
-        lo, hi, dep = stack.pop()
-        while hi - lo > THRESH:
-            if dep == 0:
-                seg = v[lo:hi]
-                heap_sort_range(seg, 0, hi - lo)
-                v[lo:hi] = seg
-                break
-            dep -= 1
-            a, b, c = lo + 1, lo + (hi - lo) // 2, hi - 1
-            mi = _pb_median(a, b, c, key_(a), key_(b), key_(c))
-            v[lo], v[mi] = v[mi], v[lo]
-            p = key_(lo)
-            GE = sum(1 << i for i in range(lo + 1, hi) if key_(i) >= p)
-            LE = sum(1 << i for i in range(lo + 1, hi) if key_(i) <= p)
-            nL, nR = _popc(GE), _popc(LE)
-            # swap k pairs L_k (k-th set bit of GE) with R_k (the (nR-1-k)-th set bit of LE)
-            s = sum(1 for k in range(min(nL, nR)) if _sel(GE, k) < _sel(LE, nR - 1 - k))
-            nv = list(v)
-            for i in range(lo + 1, hi):
-                partner = i
-                if (GE >> i) & 1:
-                    k = _popc(GE & ((1 << i) - 1))
-                    if k < s:
-                        partner = _sel(LE, nR - 1 - k)
-                if (LE >> i) & 1:
-                    r = nR - 1 - _popc(LE & ((1 << i) - 1))
-                    if r < s:
-                        assert partner == i
-                        partner = _sel(GE, r)
-                nv[i] = v[partner]
-            v = nv
-            cut = _sel(GE, 0) if s == 0 else min(_sel(GE, s) if s < nL else 1 << 30, _sel(LE, nR - s))
-            stack.append((cut, hi, dep))
-            hi = cut
-    # the final insertion passes: a stable rank over the whole (weakly ordered) range
+    assert 16 < m <= 64
+    L = range(64)
+    v = [recs[l] if l < m else 0xFFFFFFFFFFFFFFFF for l in L]
+    live = [l < m for l in L]
+    hd = [0 if live[l] else l for l in L]
+    en = [m if live[l] else l + 1 for l in L]
+    dep = [depth] * 64
+
+    def bperm(src, x):   # x of lane src (addresses wrap at 64 lanes)
+        return [x[src[l] & 63] for l in L]
+
+    def ballot(pred):
+        return sum(1 << l for l in L if pred[l])
+
+    def mbcnt(mask, l):
+        return _popc(mask & ((1 << l) - 1))
+
+    while True:
+        act = [live[l] and en[l] - hd[l] > THRESH and dep[l] > 0 for l in L]
+        if not any(act):
+            break
+        a = [hd[l] + 1 for l in L]
+        b = [hd[l] + (en[l] - hd[l]) // 2 for l in L]
+        c = [en[l] - 1 for l in L]
+        k0 = [key(x) for x in v]
+        ka, kb, kc = bperm(a, k0), bperm(b, k0), bperm(c, k0)
+        mi = [_pb_median(a[l], b[l], c[l], ka[l], kb[l], kc[l]) for l in L]
+        p = [ka[l] if mi[l] == a[l] else (kb[l] if mi[l] == b[l] else kc[l]) for l in L]
+        src = [mi[l] if act[l] and l == hd[l] else (hd[l] if act[l] and l == mi[l] else l) for l in L]
+        v = bperm(src, v)
+        k = [key(x) for x in v]
+        inn = [act[l] and l > hd[l] for l in L]
+        GE = ballot([inn[l] and k[l] >= p[l] for l in L])
+        LE = ballot([inn[l] and k[l] <= p[l] for l in L])
+        lo = [(1 << (hd[l] + 1)) - 1 if hd[l] + 1 < 64 else (1 << 64) - 1 for l in L]
+        hi = [(1 << en[l]) - 1 if en[l] < 64 else (1 << 64) - 1 for l in L]
+        bG = [_popc(GE & lo[l]) for l in L]
+        bL = [_popc(LE & lo[l]) for l in L]
+        nL = [_popc(GE & hi[l]) - bG[l] for l in L]
+        nR = [_popc(LE & hi[l]) - bL[l] for l in L]
+        isG = [(GE >> l) & 1 == 1 for l in L]
+        isL = [(LE >> l) & 1 == 1 for l in L]
+        gk = [mbcnt(GE, l) - bG[l] for l in L]
+        rk = [nR[l] - 1 - (mbcnt(LE, l) - bL[l]) for l in L]
+        tG, tL = _popc(GE), _popc(LE)
+        PG, PLt = [None] * 64, [None] * 64   # ds_permute: every lane pushes its id
+        for l in L:
+            dg = mbcnt(GE, l) if isG[l] else tG + mbcnt(~GE & ((1 << 64) - 1), l)
+            dl = mbcnt(LE, l) if isL[l] else tL + mbcnt(~LE & ((1 << 64) - 1), l)
+            assert PG[dg] is None and PLt[dl] is None
+            PG[dg], PLt[dl] = l, l
+        pair = [isG[l] and gk[l] < nR[l] for l in L]
+        Rk = bperm([bL[l] + nR[l] - 1 - gk[l] if pair[l] else 0 for l in L], PLt)
+        SW = ballot([pair[l] and l < Rk[l] for l in L])
+        s = [_popc(SW & hi[l]) - _popc(SW & lo[l]) for l in L]
+        Lk = bperm([bG[l] + rk[l] if isL[l] and 0 <= rk[l] < s[l] else 0 for l in L], PG)
+        partner = list(L)
+        for l in L:
+            if isG[l] and gk[l] < s[l]:
+                partner[l] = Rk[l]
+            if isL[l] and rk[l] < s[l]:
+                assert partner[l] == l
+                partner[l] = Lk[l]
+        v = bperm(partner, v)
+        gc = bperm([bG[l] + (s[l] if s[l] < nL[l] else 0) for l in L], PG)
+        lc = bperm([bL[l] + nR[l] - (s[l] if s[l] else nR[l]) for l in L], PLt)
+        for l in L:
+            if act[l]:
+                cut = gc[l] if s[l] == 0 else min(gc[l] if s[l] < nL[l] else 64, lc[l])
+                if l >= cut:
+                    hd[l] = cut
+                else:
+                    en[l] = cut
+                dep[l] -= 1
+    heap = [live[l] and en[l] - hd[l] > THRESH for l in L]
+    for l in L:
+        if heap[l] and l == hd[l]:
+            seg = v[hd[l]:en[l]]
+            heap_sort_range(seg, 0, en[l] - hd[l])
+            v[hd[l]:en[l]] = seg
     out = [None] * m
-    for i in range(m):
-        r = sum(1 for j in range(m) if key_(j) < key_(i) or (key_(j) == key_(i) and j < i))
-        out[r] = v[i]
+    for l in range(m):
+        if heap[l]:
+            rank = l - hd[l]
+        else:
+            kx = key(v[l])
+            rank = sum(1 for j in range(hd[l], en[l]) if key(v[j]) < kx or (key(v[j]) == kx and j < l))
+        out[hd[l] + rank] = v[l]
     return out

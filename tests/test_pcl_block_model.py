@@ -93,16 +93,31 @@ def test_partition_levels_model_matches_std_sort(seed):
         assert M.levels_sort(a, leaf=64, levels=3) == M.std_sort(a), (n, kr)   # long leaves
 
 
-def test_wave64_model_matches_std_sort():
-    """cg_pcl.h pw_range64's register form (selects by popcount binary search, swaps as lane
-    permutes, the swap count from one ballot) against std::sort on ranges of at most 64, with
-    every depth budget down to the heapsort fallback."""
+def test_wave_model_matches_std_sort():
+    """cg_pcl.h pw_range64, lane by lane (tests/pb_model.wave_sort: all sub-ranges of a round
+    partition together; L_k / R_k read from ds_permute lane tables; swaps as lane permutes; the
+    swap count from one ballot counted over the sub-range) against std::sort on ranges of
+    17-64, with every depth budget down to the heapsort fallback."""
     rng = random.Random(9)
-    for it in range(3000):
-        m = rng.randrange(0, 65)
+    for it in range(1500):
+        m = rng.randrange(17, 65)
         kr = rng.choice([1, 2, 3, 5, 20, 1000])
         a = [(rng.randrange(kr) << 32) | i for i in range(m)]
         if it % 7 == 0:
             a.sort()
-        d = (2 * M._lg(m) if m else 0) if it % 4 else rng.randrange(0, 4)
-        assert M.wave64_sort(a, d) == M.std_sort(a, depth0=d), (m, kr, d)
+        if it % 11 == 1:
+            a.sort(reverse=True)
+        d = 2 * M._lg(m) if it % 4 else rng.randrange(0, 4)
+        assert M.wave_sort(a, d) == M.std_sort(a, depth0=d), (m, kr, d)
+
+
+def test_chip_wide_leaf_stages_model():
+    """cg_large.hip's leaf stages: a leaf's levels stop at 512-record ranges (lg_pcl_leaf), those
+    stop at 64 (lg_pcl_mid), the rest one wave each (lg_pcl_waves); against std::sort."""
+    rng = random.Random(12)
+    for it in range(4):
+        n = rng.choice([1500, 3000, 4096])
+        kr = rng.choice([9, 300, 100000])
+        a = [(rng.randrange(kr) << 32) | i for i in range(n)]
+        assert M.levels_sort(a, leaf=4096) == M.std_sort(a), (n, kr)
+        assert M.levels_sort(a, leaf=1024) == M.std_sort(a), (n, kr)
