@@ -793,7 +793,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 // level with no range returns at once. lg_pcl_leaf finishes each leaf with pcl_block_sort in
 // LDS (up to 4096 records, 8 per thread, results straight to the outputs), with the depth
 // budget left on its path; a range still longer (a degenerate split) in HBM.
-#define LG_PCL_LEAF 4096
+#define LG_PCL_LEAF 4096       // the longest leaf sorted in LDS
+#ifndef LG_PCL_CUT
+#define LG_PCL_CUT LG_PCL_LEAF   // the levels cut ranges longer than this
+#endif
 #define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
                                // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
 #define PQ_WAVES 6
@@ -836,7 +839,7 @@ __device__ __forceinline__ uint32_t pq_tiles(const LgScratch& S, uint32_t level,
                                              uint32_t& nr) {
     if (level == 0) {
         const uint32_t n = S.meta[LG_PCL_N];
-        nr = n > LG_PCL_LEAF ? 1u : 0u;
+        nr = n > LG_PCL_CUT ? 1u : 0u;
         const uint32_t nt = nr ? (n - 1 + PQ_T - 1) / PQ_T : 0u;
         if (threadIdx.x == 0) { tp[0] = 0; tp[1] = nt; }
         __syncthreads();
@@ -869,17 +872,6 @@ __device__ __forceinline__ uint32_t pq_find(const uint32_t* tp, uint32_t nr, uin
     }
     return lo;
 }
-// __move_median_to_first(first, first + 1, mid, last - 1) of [f, e): index and key of the median
-__device__ __forceinline__ void pq_median(const uint64_t* E, uint32_t f, uint32_t e, uint32_t& m, uint32_t& p) {
-    const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
-    const uint32_t ka = pq_key(E, a), kb = pq_key(E, b), kc = pq_key(E, c);
-    m = pb_median(a, b, c, ka, kb, kc);
-    p = m == a ? ka : (m == b ? kb : kc);
-}
-__device__ __forceinline__ uint64_t pq_v(const uint64_t* E, uint32_t f, uint32_t m, uint32_t x) {
-    return E[x == m ? f : (x == f ? m : x)];
-}
-
 // Decoupled look-back over tiles [lo, t) of one range, 64-bit status words: flags in bits
 // 62 / 63, the >= count in bits 32..61, the <= count in bits 0..31 (counts < 2^30).
 #define PQ_ST_A (1ull << 62)
@@ -922,7 +914,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     if (level == 0 && blockIdx.x == 0 && tid == 0) {
         S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0; S.pq[PQ_MIDS] = 0;
         const uint32_t n = S.meta[LG_PCL_N];
-        if (n <= LG_PCL_LEAF) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
+        if (n <= LG_PCL_CUT) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
     }
     uint32_t nr;
     const uint32_t active = pq_tiles(S, level, tp, red, nr);
@@ -933,10 +925,16 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     const uint32_t t = tk, r = pq_find(tp, nr, t), q = t - tp[r];
     uint32_t f, e, d, m, p;
     pq_range(S, level, r, f, e, d);
-    pq_median(E, f, e, m, p);
+    // the median of three and this element's key in one batch of loads: x > f, and x's
+    // virtual record is E[f] when x is the median (__move_median_to_first's swap)
     const uint32_t x = f + 1 + q * PQ_T + tid;
     const bool valid = x < e;
-    const uint32_t k = valid ? pcl_key(pq_v(E, f, m, x)) : 0u;
+    const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
+    const uint32_t ka = pq_key(E, a), kb = pq_key(E, b), kc = pq_key(E, c), kf = pq_key(E, f);
+    const uint32_t kx = valid ? pq_key(E, x) : 0u;
+    m = pb_median(a, b, c, ka, kb, kc);
+    p = m == a ? ka : (m == b ? kb : kc);
+    const uint32_t k = valid ? (x == m ? kf : kx) : 0u;
     const bool ge = valid && k >= p, le = valid && k <= p;
     const uint64_t gm = __ballot(ge), lm = __ballot(le);
     if (l == 0) { cg[w] = (uint32_t)__popcll(gm); cl[w] = (uint32_t)__popcll(lm); }
@@ -983,14 +981,20 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64
     pq_range(S, level, r, f, e, d);
     const uint32_t* tot = level == 0 ? S.pq + 4 : pq_list(S, level % 3u) + PQ_EW * r + 3;
     const uint32_t nL = tot[0], nR = tot[1];
-    pq_median(E, f, e, m, p);
+    // one batch of loads: the median of three, E[f], this element and its ranks (x > f)
     const uint32_t x = f + 1 + q * PQ_T + tid;
-    if (q == 0 && tid == 0) Eo[f] = E[m];
+    const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
+    const uint64_t ra = E[a], rb = E[b], rc = E[c], rf = E[f];
+    const uint64_t rx = x < e ? E[x] : 0ull;
+    const uint64_t rk = x < e ? ((const uint64_t*)S.vox)[x] : 0ull;
+    m = pb_median(a, b, c, pcl_key(ra), pcl_key(rb), pcl_key(rc));
+    const uint64_t rm = m == a ? ra : (m == b ? rb : rc);
+    p = pcl_key(rm);
+    if (q == 0 && tid == 0) Eo[f] = rm;
     if (x >= e) return;
-    const uint64_t vx = pq_v(E, f, m, x);
+    const uint64_t vx = x == m ? rf : rx;
     const uint32_t k = pcl_key(vx);
     const bool ge = k >= p, le = k <= p;
-    const uint64_t rk = ((const uint64_t*)S.vox)[x];
     const uint32_t gi = (uint32_t)(rk >> 32), li = (uint32_t)rk;
     uint32_t partner = x;
     bool cutter = false;
@@ -1018,11 +1022,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64
             if (i < x) partner = i;
         }
     }
-    Eo[x] = partner == x ? vx : pq_v(E, f, m, partner);
+    Eo[x] = partner == x ? vx : (partner == m ? rf : E[partner]);
     if (cutter) {
         const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
         for (int c = 0; c < 2; c++) {
-            if (hi[c] - lo[c] > LG_PCL_LEAF && d > 1 && level < last_level)
+            if (hi[c] - lo[c] > LG_PCL_CUT && d > 1 && level < last_level)
                 pq_push(S, (level + 1u) % 3u, lo[c], hi[c], d - 1u, 0u);
             else
                 pq_push(S, PQ_LEAFLIST, lo[c], hi[c], d - 1u, out_buf);
@@ -1044,7 +1048,9 @@ struct PqLeafOut {
 //   lg_pcl_mid's ranges of 17-64 records  -> S.droot, for lg_pcl_waves (one wave each).
 // (S.dsz and S.droot are free until the clustering.) The leaf and mid workgroups then only
 // run the levels of their longer ranges, on a few CUs; the tasks spread over the chip.
+#ifndef PQ_MID
 #define PQ_MID 512
+#endif
 struct PqDefer {
     uint64_t* Eh; uint32_t* list; uint32_t* count; uint32_t base, buf;
     template <class P64, class OUT>
@@ -1125,6 +1131,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
         for (uint32_t i = threadIdx.x; i < size; i += CG_BLOCK) El[i] = E[first + i];
         __syncthreads();
         const PqDefer wt{E, S.droot, S.pq + PQ_WAVES, first, buf};
+        if constexpr (PQ_MID > CG_BLOCK) {
+            if (size > CG_BLOCK) {
+                pcl_block_sort<2, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS,
+                                                                    Rl, nullptr, wt);
+                continue;
+            }
+        }
         pcl_block_sort<1, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS, Rl,
                                                             nullptr, wt);
     }
@@ -1584,9 +1597,9 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
     const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
     const uint32_t Mtot = Ms + npad;
     // PCL's order keeps at most PQ_MAXR ranges per partition level: a detector input beyond
-    // PQ_MAXR * LG_PCL_LEAF / 2 records (4M) is summed in point order instead, and flagged
+    // PQ_MAXR * LG_PCL_CUT / 2 records (4M) is summed in point order instead, and flagged
     // (CG_F_VOXEL_POINT_ORDER): same voxels and clusters, last bits of some coordinates
-    if ((uint64_t)Mtot > (uint64_t)PQ_MAXR * LG_PCL_LEAF / 2) P.voxel_order = CG_VOXEL_ORDER_POINT;
+    if ((uint64_t)Mtot > (uint64_t)PQ_MAXR * LG_PCL_CUT / 2) P.voxel_order = CG_VOXEL_ORDER_POINT;
     CgLaunch Lh = L;
     Lh.n_points = N;   // the header's N is the whole frame's
     if (Mtot <= CG_MMAX && !S.force_global) return cg_launch_lg_back_small(Lh, P, S, f, npad, K, s);
@@ -1631,7 +1644,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
         // the levels an even split needs until every range fits a leaf, three more for uneven
         // median-of-three cuts; levels with no range to cut return at once; then the leaves
         uint32_t levels = 0;
-        while (((uint64_t)LG_PCL_LEAF << levels) < Mtot) levels++;
+        while (((uint64_t)LG_PCL_CUT << levels) < Mtot) levels++;
         if (levels) levels = std::min<uint32_t>(levels + 3, LG_PQ_LEVELS_MAX);
         if (S.pcl_levels_cap) levels = std::min(levels, S.pcl_levels_cap);
         const uint32_t tb = (Mtot + PQ_T - 1) / PQ_T;
