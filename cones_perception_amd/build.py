@@ -71,6 +71,22 @@ def build_host_demo(verbose=False):
     return out
 
 
+def build_probes(verbose=False):
+    """hipcc builds of the sort probes (tools/pcl_probe.hip, tools/pcl_leaf_probe.hip): the
+    device PCL sort against libstdc++'s std::sort, run by tests/test_gpu_pcl_probe.py."""
+    csrc = os.path.join(PKG, "csrc")
+    deps = [os.path.join(csrc, h) for h in os.listdir(csrc) if h.endswith(".h")]
+    outs = []
+    for name in ("pcl_probe", "pcl_leaf_probe"):
+        src = os.path.join(ROOT, "tools", name + ".hip")
+        out = os.path.join(PKG, "lib", name)
+        if _stale(out, [src] + deps):
+            _run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
+                  "-w", "-I", os.path.join(ROOT, "include"), src, "-o", out], verbose)
+        outs.append(out)
+    return outs
+
+
 def build_oracle(verbose=False):
     """Compile the CPU restatement (test infrastructure, oracle/)."""
     _run(["make", "-C", os.path.join(ROOT, "oracle")], verbose)
@@ -81,3 +97,4 @@ if __name__ == "__main__":
     print(build(verbose=True, force="--force" in sys.argv))
     print(build_oracle(verbose=True))
     print(build_host_demo(verbose=True))
+    print(build_probes(verbose=True))
