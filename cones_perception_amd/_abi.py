@@ -139,6 +139,10 @@ _SIGS = {
     "cg_tile_decide": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cg_tile_survivors": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_tile_backend": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
+    "cg_tile_front_async": (C.c_int, [C.c_void_p, C.POINTER(cg_tile), C.c_void_p, C.c_void_p]),
+    "cg_tile_decide_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "cg_tile_survivors_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "cg_tile_backend_own": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "cg_halo_plan_frame": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(cg_halo_plan)]),
     "cg_halo_owner": (C.c_int, [C.c_void_p, C.POINTER(cg_halo_plan), C.c_void_p, C.c_uint32, C.c_void_p]),
     "cg_halo_local": (C.c_int, [C.c_void_p, C.POINTER(cg_halo_plan), C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,

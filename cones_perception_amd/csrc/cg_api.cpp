@@ -921,6 +921,90 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
     return CG_OK;
 }
 
+// ---- the tile protocol with device-side keys and counts (no synchronisation) ----------------
+namespace {
+int tile_check(const cg_tile* t) {
+    if (t->n && !t->d_data) return fail(CG_E_INVALID, "null tile data");
+    if (t->n_total > CG_MAX_FRAME_POINTS || (uint64_t)t->first + t->n > t->n_total)
+        return fail(CG_E_INVALID, "tile [%u, %u + %u) outside a frame of %u points", t->first, t->first, t->n, t->n_total);
+    if (t->point_step == 0 || t->point_step % 4) return fail(CG_E_INVALID, "bad point_step");
+    const int32_t offs[4] = {t->off_x, t->off_y, t->off_z, t->off_intensity};
+    for (int32_t o : offs)
+        if (o >= 0 && (o % 4 || (uint32_t)o + 4 > t->point_step)) return fail(CG_E_INVALID, "bad field offset %d", o);
+    return CG_OK;
+}
+}  // namespace
+
+int cg_tile_front_async(cg_handle* h, const cg_tile* t, uint32_t* d_keys, void* hip_stream) {
+    if (!h || !t || !d_keys) return fail(CG_E_INVALID, "null argument");
+    int rc = tile_check(t);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(h->device));
+    if ((rc = own_stream(h))) return rc;
+    if ((rc = ensure_large(h, std::max<uint32_t>(t->n, 1)))) return rc;
+    const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    h->tile = *t;
+    LgScratch S = h->lg;
+    S.pidx_base = t->first;
+    HIPCHK((hipError_t)cg_large_front(tile_launch(*t), h->dp, CG_KMODE_PIPELINE, S, s, 0, true));
+    HIPCHK(hipMemcpyAsync(d_keys, S.meta + LG_SECKEY, CG_TILE_KEYS * 4, hipMemcpyDeviceToDevice, s));
+    h->tile_ready = true;
+    return CG_OK;
+}
+
+int cg_tile_decide_async(cg_handle* h, const uint32_t* d_merged_keys, uint32_t* d_counts, void* hip_stream) {
+    if (!h || !d_merged_keys || !d_counts) return fail(CG_E_INVALID, "null argument");
+    if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_decide_async before cg_tile_front_async");
+    HIPCHK(hipSetDevice(h->device));
+    const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    LgScratch S = h->lg;
+    S.pidx_base = h->tile.first;
+    HIPCHK(hipMemcpyAsync(S.meta + LG_SECKEY, d_merged_keys, CG_TILE_KEYS * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK((hipError_t)cg_large_decide(tile_launch(h->tile), h->dp, S, s, 0));
+    HIPCHK((hipError_t)cg_large_tile_counts(S, d_counts, s));
+    return CG_OK;
+}
+
+int cg_tile_survivors_async(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t n, void* hip_stream) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_survivors_async before cg_tile_front_async");
+    if (n > std::max<uint32_t>(h->tile.n, 1)) return fail(CG_E_INVALID, "%u survivors in a tile of %u points", n, h->tile.n);
+    if (n && (!d_points || !d_index)) return fail(CG_E_INVALID, "null output buffers");
+    HIPCHK(hipSetDevice(h->device));
+    const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    if (n) {
+        HIPCHK(hipMemcpyAsync(d_points, h->lg.surv_p, (size_t)n * 16, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(d_index, h->lg.surv_i, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    }
+    return CG_OK;
+}
+
+int cg_tile_backend_own(cg_handle* h, uint32_t n_total, void* hip_stream) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_backend_own before cg_tile_decide_async");
+    if (h->tile.first != 0 || h->tile.n != n_total || h->tile.n_total != n_total)
+        return fail(CG_E_INVALID, "cg_tile_backend_own needs the whole frame in the tile ([%u, %u + %u) of %u)",
+                    h->tile.first, h->tile.first, h->tile.n, n_total);
+    HIPCHK(hipSetDevice(h->device));
+    int rc = ensure_batch(h, 1, n_total, false);
+    if (rc) return rc;
+    const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    LgScratch S = h->lg;
+    S.pidx_base = 0;
+    S.force_global = h->route == 2 ? 1u : 0u;
+    CgLaunch L{};
+    L.n_frames = 1;
+    L.n_points = n_total;
+    fill_launch_outputs(h, L);
+    L.stamps = nullptr;
+    // the survivors and the counts (the whole frame's) are where cg_tile_decide_async left them
+    HIPCHK((hipError_t)cg_large_backend(L, h->dp, CG_KMODE_PIPELINE, S, s, 0, n_total, CG_K_FROM_META));
+    h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = s;
+    h->last_single = false;
+    h->batch_valid = false;
+    return CG_OK;
+}
+
 // ---- C5 halo tiling (cg_halo_*): argument checks and the handle's scratch; the work is in
 // cg_large.hip
 namespace {

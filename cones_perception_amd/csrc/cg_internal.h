@@ -172,6 +172,8 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
 int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t n_total, uint32_t K);
 // A tiled frame's gathered survivors and merged counts (K, Ms, nfin, bounds keys) into S.
+// The 9 tile counts (cg_tile_decide's layout) from the meta words to d_counts, on stream s.
+int cg_large_tile_counts(LgScratch S, uint32_t* d_counts, hipStream_t s);
 int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_points, const uint32_t* d_index,
                            uint32_t n, const uint32_t* counts, hipStream_t s);
 // C5 halo tiling (cg_large.hip): a slab's voxels and components -> records; cross-slab

@@ -1515,6 +1515,18 @@ __global__ void lg_set_counts(LgScratch S, uint32_t K, uint32_t Ms, uint32_t nfi
     m[LG_BMIN] = b0; m[LG_BMIN + 1] = b1; m[LG_BMIN + 2] = b2;
     m[LG_BMAX] = b3; m[LG_BMAX + 1] = b4; m[LG_BMAX + 2] = b5;
 }
+// The tile's counts as cg_tile_decide reports them (K, survivors, finite survivors, bounds
+// keys min x3, max x3), written on the device for a device-side merge.
+__global__ void lg_tile_counts(LgScratch S, uint32_t* out) {
+    const uint32_t t = threadIdx.x;
+    if (t >= CG_TILE_COUNTS) return;
+    const uint32_t* m = S.meta;
+    out[t] = t == 0 ? m[LG_K] : t == 1 ? m[LG_MS] : t == 2 ? m[LG_NFIN] : t < 6 ? m[LG_BMIN + t - 3] : m[LG_BMAX + t - 6];
+}
+int cg_large_tile_counts(LgScratch S, uint32_t* d_counts, hipStream_t s) {
+    hipLaunchKernelGGL(lg_tile_counts, dim3(1), dim3(64), 0, s, S, d_counts);
+    return hipGetLastError();
+}
 __global__ __launch_bounds__(CG_BLOCK) void lg_check_sorted(LgScratch S, uint32_t n) {
     const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
     if (j + 1 < n && !(S.surv_i[j] < S.surv_i[j + 1])) S.meta[LG_UNSORTED] = 1;

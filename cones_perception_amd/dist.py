@@ -109,6 +109,41 @@ def merge_tile_counts(counts, device, per_rank: bool = False):
     return (out, [int(x) for x in c[:, 1]]) if per_rank else out
 
 
+def _u32_bits(x):
+    """int64 values in [0, 2^32) -> the same bits as int32 (the C-ABI's uint32 words)."""
+    return (x - ((x >= 2 ** 31).to(torch.int64) << 32)).to(torch.int32)
+
+
+def merge_tile_keys_dev(keys, device):
+    """merge_tile_keys on the device: keys int32[19] (uint32 bits) of this rank, on `device`, ->
+    merged int32[19] on `device`. One MIN all-reduce (on the GPU under RCCL, through the host
+    under gloo); one rank: the keys themselves."""
+    if not _distributed():
+        return keys
+    cd = _coll_device(device)
+    k = keys.to(torch.int64) & 0xFFFFFFFF
+    sh = torch.arange(32, device=keys.device, dtype=torch.int64)
+    v = torch.cat([k[:18], -((k[18] >> sh) & 1)]).to(cd)
+    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    v = v.to(keys.device)
+    word18 = ((v[18:] < 0).to(torch.int64) << sh).sum().view(1)
+    return _u32_bits(torch.cat([v[:18], word18]))
+
+
+def merge_tile_counts_dev(counts, device):
+    """merge_tile_counts for counts int32[9] (uint32 bits) on `device`: one all-gather, then
+    one read to the host (the survivor counts size the survivor gather). Returns (merged
+    uint32[9] numpy, every rank's survivor count)."""
+    import numpy as np
+    cd = _coll_device(device)
+    t = (counts.to(torch.int64) & 0xFFFFFFFF).to(cd)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    c = torch.stack(parts).cpu().numpy()
+    out = np.concatenate([c[:, :3].sum(0), c[:, 3:6].min(0), c[:, 6:9].max(0)]).astype(np.uint32)
+    return out, [int(x) for x in c[:, 1]]
+
+
 def gather_survivors(points, index, device, dst: int = 0, sizes=None):
     """Gather every rank's survivors ((n, 4) float32 and (n,) int32, any n) to dst as one
     concatenation in rank order (the backend does not depend on the order). Others get None.
@@ -167,16 +202,61 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
     fetch=False leaves the result in the handle's device buffers (engine.fetch(0) reads it)
     and returns True on dst."""
     from . import _abi
-    total, sizes, sp, si = _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets)
     if halo:
+        total, sizes, sp, si = _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets)
         det = run_halo_backend(engine, total, sp, si, n_total, device, dst, fetch=fetch)
         if det is not False:
             return det
-    gp, gi = gather_survivors(sp, si, device, dst, sizes=sizes)
-    if _distributed() and dist.get_rank() != dst:
-        return None
-    _abi.check(_abi.lib().cg_tile_backend(engine.handle, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]),
-                                          total.ctypes.data, n_total))
+        gp, gi = gather_survivors(sp, si, device, dst, sizes=sizes)
+        if _distributed() and dist.get_rank() != dst:
+            return None
+        _abi.check(_abi.lib().cg_tile_backend(engine.handle, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]),
+                                              total.ctypes.data, n_total))
+        return engine.fetch(0) if fetch else True
+    return _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets, dst, fetch)
+
+
+def _tile_stream(engine, device):
+    """One torch stream per engine for the gather form: the C-ABI calls, the torch ops and the
+    collectives of a frame all run on it, in order, with no host synchronisation."""
+    st = getattr(engine, "_tile_stream", None)
+    if st is None:
+        st = torch.cuda.Stream(device)
+        engine._tile_stream = st
+    return st
+
+
+def _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets, dst, fetch):
+    """The gather form with the keys and counts on the device (cg_tile_*_async): the keys
+    merge with a MIN all-reduce on the GPU; one rank (its tile the whole frame) runs the
+    backend on its own survivors where they are; several ranks merge the counts with one
+    all-gather, read back once for the survivor counts, and gather the survivors to dst."""
+    import ctypes as C
+    from . import _abi
+    lib, h = _abi.lib(), engine.handle
+    st = _tile_stream(engine, device)
+    st.wait_stream(torch.cuda.current_stream(device))   # the tile's points
+    s = st.cuda_stream
+    with torch.cuda.stream(st):
+        t = _abi.cg_tile(d_tile_ptr, first, n, n_total, point_step, *offsets)
+        keys = torch.empty(_abi.CG_TILE_KEYS, dtype=torch.int32, device=device)
+        _abi.check(lib.cg_tile_front_async(h, C.byref(t), keys.data_ptr(), s))
+        merged = merge_tile_keys_dev(keys, device)
+        counts = torch.empty(_abi.CG_TILE_COUNTS, dtype=torch.int32, device=device)
+        _abi.check(lib.cg_tile_decide_async(h, merged.data_ptr(), counts.data_ptr(), s))
+        if not _distributed():
+            _abi.check(lib.cg_tile_backend_own(h, n_total, s))
+            return engine.fetch(0) if fetch else True
+        total, sizes = merge_tile_counts_dev(counts, device)
+        ns = sizes[dist.get_rank()]
+        sp = torch.empty((max(ns, 1), 4), dtype=torch.float32, device=device)
+        si = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
+        _abi.check(lib.cg_tile_survivors_async(h, sp.data_ptr(), si.data_ptr(), ns, s))
+        gp, gi = gather_survivors(sp[:ns], si[:ns], device, dst, sizes=sizes)
+        if dist.get_rank() != dst:
+            return None
+        st.synchronize()   # cg_tile_backend runs on the handle's own stream
+    _abi.check(lib.cg_tile_backend(h, gp.data_ptr(), gi.data_ptr(), int(gp.shape[0]), total.ctypes.data, n_total))
     return engine.fetch(0) if fetch else True
 
 

@@ -201,6 +201,21 @@ int cg_tile_decide(cg_handle* h, const uint32_t* merged_keys, uint32_t* counts);
 int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t capacity);
 int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index, uint32_t n_survivors,
                     const uint32_t* merged_counts, uint32_t n_total);
+/* The same protocol with the keys and counts left on the device, for device-side merges (RCCL
+ * all-reduce / all-gather on the caller's stream): nothing here synchronises. stream: the
+ * caller's hipStream_t (NULL: the handle's own); every call on the frame passes the same one.
+ *   cg_tile_front_async: step 1; the CG_TILE_KEYS keys to d_keys (device memory);
+ *   cg_tile_decide_async: step 2 from merged keys in device memory; the CG_TILE_COUNTS
+ *     counts to d_counts (device memory);
+ *   cg_tile_survivors_async: step 3 for a survivor count n the caller already holds (its
+ *     own entry of the gathered counts);
+ *   cg_tile_backend_own: step 4 on this rank's own survivors, where they already are, when
+ *     its tile is the whole frame (one rank): the counts are the rank's own. Like the
+ *     single-GPU call it reads the frame's survivor count back once to size the backend. */
+int cg_tile_front_async(cg_handle* h, const cg_tile* t, uint32_t* d_keys, void* hip_stream);
+int cg_tile_decide_async(cg_handle* h, const uint32_t* d_merged_keys, uint32_t* d_counts, void* hip_stream);
+int cg_tile_survivors_async(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t n, void* hip_stream);
+int cg_tile_backend_own(cg_handle* h, uint32_t n_total, void* hip_stream);
 
 /* Spatial tiling with a halo exchange, in place of steps 3-4. The frame's
  * PCL voxel lattice (from the merged bounds) is cut into slabs of voxel columns along x; a
