@@ -1312,7 +1312,9 @@ __device__ __forceinline__ void lg_cross_one(const LgScratch& S, const CgDevPara
         if (o <= v) return;
         const float4 p = S.vox[o];
         const uint32_t po = S.par[o];
-        if (po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, v, o);
+        // pv / po (the flattened parents) lie on v's / o's paths to their roots (unions only
+        // hook roots under roots), so the finds start there
+        if (po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, pv, po);
     });
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P) {
