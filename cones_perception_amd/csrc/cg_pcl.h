@@ -208,11 +208,11 @@ template <class P> struct PbStore {
 // One wave finishes a range of m <= 64 records (__introsort_loop with the budget left on its
 // path, then __final_insertion_sort) in registers: lane i holds record f + i, and every lane
 // knows its sub-range [hd, en) and that sub-range's budget. All sub-ranges longer than 16
-// partition in the same round (segmented): median of three by ds_bpermute, >= / <= ballots,
-// L_k = the k-th set bit of the sub-range's >= mask, R_k the (nR-1-k)-th of its <= mask (read
-// from lane-index tables that one ds_permute per mask builds), the swap count s = a ballot of
-// L_k < R_k counted over the sub-range (a prefix of k), the records moved by ds_bpermute, the
-// cut from s. A spent budget heapsorts its sub-range in the caller's buffer (rare). The final
+// partition in the same round (segmented): median of three by ds_bpermute (the swap with the
+// first virtual), >= / <= ballots, the swap count s = one ballot of the <= lanes with more
+// >= lanes than their reverse rank before them (L_r < R_r), L_k = the k-th set bit of the
+// sub-range's >= mask and R_k the (nR-1-k)-th of its <= mask (read from lane-index tables
+// that one ds_permute per mask builds), the records moved once by ds_bpermute, the cut from s. A spent budget heapsorts its sub-range in the caller's buffer (rare). The final
 // insertion passes are a stable rank inside each sub-range of at most 16 records (sub-ranges
 // are weakly ordered, so insertion never crosses one).
 __device__ __forceinline__ uint32_t pw_b32(uint32_t src, uint32_t x) {   // x of lane src
@@ -233,15 +233,13 @@ __device__ __forceinline__ void pw_range64(P64 E, uint32_t f, uint32_t m, uint32
         // __move_median_to_first(hd, hd + 1, mid, en - 1)
         const uint32_t a = hd + 1, b = hd + (en - hd) / 2, c = en - 1;
         const uint32_t key = (uint32_t)(v >> 32);
-        const uint32_t ka = pw_b32(a, key), kb = pw_b32(b, key), kc = pw_b32(c, key);
+        const uint32_t ka = pw_b32(a, key), kb = pw_b32(b, key), kc = pw_b32(c, key), kh = pw_b32(hd, key);
         const uint32_t mi = pb_median(a, b, c, ka, kb, kc);
         const uint32_t p = mi == a ? ka : (mi == b ? kb : kc);
-        uint32_t src = l;
-        if (act && l == hd) src = mi;
-        if (act && l == mi) src = hd;
-        v = ((uint64_t)pw_b32(src, (uint32_t)(v >> 32)) << 32) | pw_b32(src, (uint32_t)v);
+        // __move_median_to_first, virtually: position mi holds the first's record (key kh),
+        // position hd the median's; the records move once, with the partition's swaps
+        const uint32_t k = act && l == mi ? kh : key;
         // __unguarded_partition(hd + 1, en, hd), in parallel over the sub-ranges
-        const uint32_t k = (uint32_t)(v >> 32);
         const bool in = act && l > hd;
         const uint64_t GE = __ballot(in && k >= p), LE = __ballot(in && k <= p);
         const uint64_t lo = pw_low(hd + 1), hi = pw_low(en);
@@ -255,15 +253,19 @@ __device__ __forceinline__ void pw_range64(P64 E, uint32_t f, uint32_t m, uint32
             (int)((isG ? mbcnt(GE) : tG + mbcnt(~GE)) << 2), (int)l);
         const uint32_t PL = (uint32_t)__builtin_amdgcn_ds_permute(
             (int)((isL ? mbcnt(LE) : tL + mbcnt(~LE)) << 2), (int)l);
-        const bool pair = isG && gk < nR;
-        const uint32_t Rk = pw_b32(pair ? bL + nR - 1u - gk : 0u, PL);
-        const uint64_t SW = __ballot(pair && l < Rk);
+        // R_r (a <= lane, reverse rank r) is swapped iff L_r < R_r, i.e. iff more than r >=
+        // lanes precede it in the sub-range: the swap count s is one ballot, no lane lookup
+        const uint64_t SW = __ballot(isL && mbcnt(GE) - bG > rk);
         const uint32_t s = (uint32_t)__popcll(SW & hi) - (uint32_t)__popcll(SW & lo);
+        const uint32_t Rk = pw_b32(isG && gk < s ? bL + nR - 1u - gk : 0u, PL);
         const uint32_t Lk = pw_b32(isL && rk < s ? bG + rk : 0u, PG);
         uint32_t partner = l;
         if (isG && gk < s) partner = Rk;
         if (isL && rk < s) partner = Lk;
-        v = ((uint64_t)pw_b32(partner, (uint32_t)(v >> 32)) << 32) | pw_b32(partner, (uint32_t)v);
+        // the virtual records: position mi holds v[hd], position hd holds v[mi]
+        uint32_t src = partner;
+        if (act) src = partner == mi ? hd : (partner == hd ? mi : partner);
+        v = ((uint64_t)pw_b32(src, (uint32_t)(v >> 32)) << 32) | pw_b32(src, (uint32_t)v);
         const uint32_t gc = pw_b32(bG + (s < nL ? s : 0u), PG);
         const uint32_t lc = pw_b32(bL + nR - (s ? s : nR), PL);
         const uint32_t cut = s == 0 ? gc : min(s < nL ? gc : 64u, lc);

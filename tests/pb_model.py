@@ -420,11 +420,11 @@ def wave_sort(recs, depth):
         c = [en[l] - 1 for l in L]
         k0 = [key(x) for x in v]
         ka, kb, kc = bperm(a, k0), bperm(b, k0), bperm(c, k0)
+        kh = bperm(hd, k0)
         mi = [_pb_median(a[l], b[l], c[l], ka[l], kb[l], kc[l]) for l in L]
         p = [ka[l] if mi[l] == a[l] else (kb[l] if mi[l] == b[l] else kc[l]) for l in L]
-        src = [mi[l] if act[l] and l == hd[l] else (hd[l] if act[l] and l == mi[l] else l) for l in L]
-        v = bperm(src, v)
-        k = [key(x) for x in v]
+        # __move_median_to_first, virtually: position mi holds the first's record (key kh)
+        k = [kh[l] if act[l] and l == mi[l] else k0[l] for l in L]
         inn = [act[l] and l > hd[l] for l in L]
         GE = ballot([inn[l] and k[l] >= p[l] for l in L])
         LE = ballot([inn[l] and k[l] <= p[l] for l in L])
@@ -445,10 +445,11 @@ def wave_sort(recs, depth):
             dl = mbcnt(LE, l) if isL[l] else tL + mbcnt(~LE & ((1 << 64) - 1), l)
             assert PG[dg] is None and PLt[dl] is None
             PG[dg], PLt[dl] = l, l
-        pair = [isG[l] and gk[l] < nR[l] for l in L]
-        Rk = bperm([bL[l] + nR[l] - 1 - gk[l] if pair[l] else 0 for l in L], PLt)
-        SW = ballot([pair[l] and l < Rk[l] for l in L])
+        # R_r (a <= lane, reverse rank r) is swapped iff L_r < R_r, i.e. more than r >= lanes
+        # precede it in the sub-range: the swap count is one ballot, no lane lookup
+        SW = ballot([isL[l] and mbcnt(GE, l) - bG[l] > rk[l] for l in L])
         s = [_popc(SW & hi[l]) - _popc(SW & lo[l]) for l in L]
+        Rk = bperm([bL[l] + nR[l] - 1 - gk[l] if isG[l] and gk[l] < s[l] else 0 for l in L], PLt)
         Lk = bperm([bG[l] + rk[l] if isL[l] and 0 <= rk[l] < s[l] else 0 for l in L], PG)
         partner = list(L)
         for l in L:
@@ -457,7 +458,10 @@ def wave_sort(recs, depth):
             if isL[l] and rk[l] < s[l]:
                 assert partner[l] == l
                 partner[l] = Lk[l]
-        v = bperm(partner, v)
+        # the virtual records: position mi holds v[hd], position hd holds v[mi]
+        src = [(hd[l] if partner[l] == mi[l] else (mi[l] if partner[l] == hd[l] else partner[l])) if act[l] else l
+               for l in L]
+        v = bperm(src, v)
         gc = bperm([bG[l] + (s[l] if s[l] < nL[l] else 0) for l in L], PG)
         lc = bperm([bL[l] + nR[l] - (s[l] if s[l] else nR[l]) for l in L], PLt)
         for l in L:
