@@ -99,3 +99,42 @@ def test_bench_gpus_flag_launches_ranks():
 def test_bench_refuses_mismatched_world_size():
     rc, line, err = _bench(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0"})
     assert rc != 0 and line is None and "WORLD_SIZE=1" in err
+
+
+def _merge_worker(rank, ws, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from cones_perception_amd import dist as cd
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    dev = torch.device("cpu")
+    rng = np.random.default_rng(100 + rank)
+    ok = True
+    for it in range(20):
+        # sector-minimum keys over the whole uint32 range (bit 31 set in about half), the
+        # used-bin mask, and counts with bounds keys
+        keys = rng.integers(0, 2 ** 32, 19, dtype=np.uint64).astype(np.uint32)
+        keys[18] = rng.integers(0, 2 ** 18, dtype=np.uint64)
+        counts = rng.integers(0, 2 ** 32, 9, dtype=np.uint64).astype(np.uint32)
+        counts[:3] = rng.integers(0, 1 << 20, 3, dtype=np.uint64)
+        host_k = cd.merge_tile_keys(keys, dev)
+        dev_k = cd.merge_tile_keys_dev(torch.from_numpy(keys.view(np.int32).copy()), dev)
+        ok &= np.array_equal(dev_k.numpy().view(np.uint32), host_k)
+        host_c, sizes_h = cd.merge_tile_counts(counts, dev, per_rank=True)
+        dev_c, sizes_d = cd.merge_tile_counts_dev(torch.from_numpy(counts.view(np.int32).copy()), dev)
+        ok &= np.array_equal(dev_c, host_c) and sizes_h == sizes_d
+    res = torch.tensor([int(ok)])
+    dist.all_reduce(res, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        np.save(result_path, res.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_device_side_tile_merges_equal_host_merges(tmp_path):
+    """dist.merge_tile_keys_dev / merge_tile_counts_dev (the tiled C5 gather form's device-side
+    merges, uint32 words carried as int32) against the host merges, world size 2 (gloo)."""
+    out = str(tmp_path / "m.npy")
+    mp.spawn(_merge_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert int(np.load(out)[0]) == 1
