@@ -173,6 +173,7 @@ struct cg_handle {
     bool packed = false;             // the last single-frame launch left its results in d_pack
     uint32_t* d_pack = nullptr;      // fetch_frame: one frame's results packed (CG_PACK_WORDS)
     uint32_t* h_pack = nullptr;      // pinned copy of it; the results handed out point into it
+    uint32_t* h_pack_dev = nullptr;  // h_pack's device address: the split launch packs straight into it
     std::vector<float> h_vox, h_cen;
     std::vector<int32_t> h_lab, h_offs, h_idx;
     uint8_t* h_ground = nullptr;  // pinned
@@ -389,14 +390,22 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
     return CG_OK;
 }
 
-int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
-    const uint64_t cap = h->cap_points;
-    // one packed copy into pinned memory and one synchronisation when the results fit
-    // CG_PACK_MAX entries per array (every frame of the LDS backend: V <= M <= CG_MMAX)
+int ensure_pack(cg_handle* h) {
     if (!h->d_pack) {
         HIPCHK(hipMalloc(&h->d_pack, CG_PACK_WORDS * 4));
         HIPCHK(hipHostMalloc((void**)&h->h_pack, CG_PACK_WORDS * 4, hipHostMallocDefault));
+        HIPCHK(hipHostGetDevicePointer((void**)&h->h_pack_dev, h->h_pack, 0));
     }
+    return CG_OK;
+}
+
+int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
+    const uint64_t cap = h->cap_points;
+    // one packed copy into pinned memory and one synchronisation when the results fit
+    // CG_PACK_MAX entries per array (every frame of the LDS backend: V <= M <= CG_MMAX); the
+    // single-frame split launch packs into the pinned buffer itself (no copy)
+    int rc = ensure_pack(h);
+    if (rc) return rc;
     {
         CgLaunch L{};   // the result arrays only (fill_launch_outputs would reset the stamps)
         L.cap = h->cap_points;
@@ -404,8 +413,10 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
         L.idx = h->d_idx; L.cen = h->d_cen;
         const bool prepacked = h->packed && frame == 0;   // by the single-frame launch just run
         h->packed = false;
-        if (!prepacked) HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
-        HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
+        if (!prepacked) {
+            HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
+            HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
+        }
         HIPCHK(hipStreamSynchronize(s));
         const uint32_t* p = h->h_pack;
         const uint32_t V = p[CG_HDR_V], C = p[CG_HDR_C];
@@ -492,11 +503,9 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
             HIPCHK(hipMemsetAsync(h->d_split + 2, 0xff, (CG_NUM_BINS + 1) * 4, h->stream));
         }
         L.split = h->d_split;
-        if (!h->d_pack) {
-            HIPCHK(hipMalloc(&h->d_pack, CG_PACK_WORDS * 4));
-            HIPCHK(hipHostMalloc((void**)&h->h_pack, CG_PACK_WORDS * 4, hipHostMallocDefault));
-        }
-        L.pack = h->d_pack;   // the kernel packs the results itself
+        rc = ensure_pack(h);
+        if (rc) return rc;
+        L.pack = h->h_pack_dev;   // the kernel packs the results itself, into pinned host memory
     }
     h->packed = L.pack != nullptr;
     rc = launch_frames(h, L, kmode, h->stream);
