@@ -227,6 +227,9 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
     const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
     if (tid < 64) sector_thresholds(S.meta + LG_SECKEY, S.meta[LG_TOUCHED], P, thr, tkey, &band[0], &band[1]);
+    // the frame's sector keys to the caller's per-frame output (the pipeline's re-crop reads them)
+    if (KMODE == CG_KMODE_PIPELINE && c == 0 && tid <= CG_NUM_BINS && L.seckeys)
+        L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = S.meta[LG_SECKEY + tid];
     if (tid == 0) kcount = 0;
     __syncthreads();
     const uint32_t qlo = band[0], qhi = band[1];
@@ -1719,10 +1722,6 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
     for (uint32_t f = 0; f < L.n_frames; f++) {
         if ((e = (hipError_t)cg_large_front(L, P, kmode, S, s, f, true)) != hipSuccess) return e;
         if (kmode == CG_KMODE_GROUND) continue;
-        if (kmode == CG_KMODE_PIPELINE && L.seckeys &&
-            (e = hipMemcpyAsync(L.seckeys + (uint64_t)f * (CG_NUM_BINS + 1), S.meta + LG_SECKEY,
-                                (CG_NUM_BINS + 1) * 4, hipMemcpyDeviceToDevice, s)) != hipSuccess)
-            return e;
         if (kmode == CG_KMODE_PIPELINE && (e = (hipError_t)cg_large_decide(L, P, S, s, f)) != hipSuccess) return e;
         const uint32_t K = kmode == CG_KMODE_PIPELINE ? CG_K_FROM_META : N;
         if ((e = (hipError_t)cg_large_backend(L, P, kmode, S, s, f, N, K)) != hipSuccess) return e;
