@@ -36,8 +36,7 @@
 
 // ------------------------------------------------------------------------------------------
 // Meta words (initialised by lg_init).
-__global__ void lg_init(LgScratch S, CgDevParams P) {
-    const uint32_t t = threadIdx.x;
+__device__ __forceinline__ void lg_init_meta(const LgScratch& S, const CgDevParams& P, uint32_t t) {
     if (t < LG_META_WORDS) {
         uint32_t v = 0;
         if (t <= CG_NUM_BINS) v = cg_fkey(P.default_low);
@@ -45,6 +44,7 @@ __global__ void lg_init(LgScratch S, CgDevParams P) {
         S.meta[t] = v;
     }
 }
+__global__ void lg_init(LgScratch S, CgDevParams P) { lg_init_meta(S, P, threadIdx.x); }
 
 // Bounds of finite points, merged into the frame's meta words (order-preserving keys).
 struct Bounds {
@@ -171,7 +171,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_reduce_chunks(LgScratch S, uint32
 // ------------------------------------------------------------------------------------------
 // Front: pass 1 per chunk.
 template <int LAYOUT, int KMODE>
-__global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+__global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
+                                                       uint32_t init) {
+    // init: workgroup 0 resets the frame's meta words (lg_init's work; nothing here reads them,
+    // lg_reduce_chunks after this launch folds the chunks into them)
+    if (init && blockIdx.x == 0) lg_init_meta(S, P, threadIdx.x);
     constexpr int PPT = LG_CHUNK / CG_BLOCK;
     constexpr int NW = (PPT + 63) / 64;
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
@@ -1556,19 +1560,22 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
     const uint32_t N = L.n_points;
     const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
-    if (init) hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
-    if (nch == 0) return hipGetLastError();
+    if (nch == 0) {
+        if (init) hipLaunchKernelGGL(lg_init, dim3(1), dim3(64), 0, s, S, P);
+        return hipGetLastError();
+    }
+    const uint32_t fi = init ? 1u : 0u;   // lg_front's workgroup 0 resets the meta words
     const dim3 g(nch), b(CG_BLOCK);
 #define LG_FRONT_MODES(LAY)                                                                       \
     if (kmode == CG_KMODE_PIPELINE) {                                                             \
-        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);           \
+        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, fi);           \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u);                      \
     } else if (kmode == CG_KMODE_DETECT) {                                                        \
-        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f);             \
+        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f);                              \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u);                      \
     } else {                                                                                      \
-        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);             \
+        hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u);                      \
         hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);            \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u);                      \
