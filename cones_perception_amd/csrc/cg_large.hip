@@ -1052,7 +1052,8 @@ struct PqLeafOut {
 // Ranges handed on to a chip-wide launch: their records go back to the HBM buffer the range
 // was loaded from and onto a task list (first, size | budget << 16 | buffer << 24):
 //   lg_pcl_leaf's ranges of 65-512 records -> S.dsz, for lg_pcl_mid (one workgroup each);
-//   lg_pcl_mid's ranges of 17-64 records  -> S.droot, for lg_pcl_waves (one wave each).
+//   ranges of 17-64 records (of the leaves and of lg_pcl_mid) -> S.droot, for lg_pcl_waves
+//   (one wave each).
 // (S.dsz and S.droot are free until the clustering.) The leaf and mid workgroups then only
 // run the levels of their longer ranges, on a few CUs; the tasks spread over the chip.
 #ifndef PQ_MID
@@ -1060,14 +1061,17 @@ struct PqLeafOut {
 #endif
 struct PqDefer {
     uint64_t* Eh; uint32_t* list; uint32_t* count; uint32_t base, buf;
+    uint32_t* wlist = nullptr; uint32_t* wcount = nullptr;   // ranges of <= 64 straight to the waves
     template <class P64, class OUT>
     __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT) const {
         const uint32_t l = lane_id();
         for (uint32_t i = l; i < m; i += 64) Eh[base + f + i] = E[f + i];
         if (l == 0) {
-            const uint32_t q = atomicAdd(count, 1u);
-            list[2 * q] = base + f;
-            list[2 * q + 1] = m | (d << 16) | (buf << 24);
+            const bool w = wlist && m <= PW_MAX;
+            const uint32_t q = atomicAdd(w ? wcount : count, 1u);
+            uint32_t* const e = (w ? wlist : list) + 2 * q;
+            e[0] = base + f;
+            e[1] = m | (d << 16) | (buf << 24);
         }
     }
 };
@@ -1092,7 +1096,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
                                       w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
             lds_u32* const Rl = (lds_u32*)red;
             const PqLeafOut out{kout, vout, first};
-            const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ent[3]};
+            const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ent[3], S.droot, S.pq + PQ_WAVES};
             for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
             __syncthreads();
             if (size <= CG_BLOCK)
