@@ -115,10 +115,10 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 // range [f, e) of its elements in registers and follows the cut after every level. Per level
 // (a barrier after each step):
 //   S1. >= / <= pivot against the range's pivot; per (chunk, wave) counts;
-//   S2. the counts scanned: every position's exclusive >= / <= counts over the whole array
-//       (RLO, with the totals at n); the >= elements listed at their count in PL, the <= ones
-//       in PR, so a range's L list is the stretch of PL from RLO[f + 1] and its R list the
-//       stretch of PR below RLO[e], read from the right; heads reset the swap count;
+//   S2. the counts scanned: every position's inclusive >= / <= counts over the whole array
+//       (RLO); the >= elements listed at their exclusive count in PL, the <= ones in PR, so
+//       a range's L list is the stretch of PL from RLO[f] and its R list the stretch of PR
+//       below RLO[e - 1], read from the right; heads reset the swap count;
 //   S4. the swaps (L_k, R_k) while L_k < R_k: every partner is read, then every element
 //       written (or the records go out of place to E2); the last swap of a range records the
 //       swap count s;
@@ -128,8 +128,9 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 //   S0. every element follows the cut into its child range.
 // Then the ranges of 17-64 records, one wave each (pw_range64), and the final insertion
 // passes of the rest: a stable rank inside each range of at most 16; heapsorted ranges are
-// sorted already. Scratch: INFO (act | final | wave | budget at heads), PIV, RLO, PL, PR, CUT
-// (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
+// sorted already. A (wave, k) slot whose elements are all in final ranges skips every step
+// of the later levels. Scratch: INFO (act | final | wave | budget at heads), PIV, RLO, PL,
+// PR, CUT (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
 #define PB_ACT 0x100u
 #define PB_FIN 0x200u
 #define PB_WAVE 0x400u   // a range of at most PW_MAX records with budget left: one wave sorts it
@@ -326,11 +327,19 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         act = pb_children<K, WMAX>(E, S, 0, 0, n, depth0);
     }
     bool any = __syncthreads_or(act);
+    // (wave, k) slots with an element in a partitioned range; a slot without one has nothing
+    // to do in any later level (ranges only shrink, and a final range stays final)
+    uint32_t live = (1u << PER) - 1u;
     while (any) {
         uint32_t st[PER], nn[PER];
         // S1: compare with the range's pivot; per-slot counts
 #pragma unroll
         for (int k = 0; k < PER; k++) {
+            if (!((live >> k) & 1u)) {
+                if (l == 0) cnt[k * WAVES + w] = 0u;
+                st[k] = 0u;
+                continue;
+            }
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
             uint32_t info = 0, p = 0, kx = 0;
             if (x < n) {
@@ -343,29 +352,28 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
             const uint64_t gm = __ballot(ge), lm = __ballot(le);
             if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
             st[k] = mbcnt(gm) | (mbcnt(lm) << 12) | (ge ? GE : 0u) | (le ? LE : 0u) | (in ? IN : 0u) | (part ? PART : 0u);
+            if (!__ballot(part)) live &= ~(1u << k);
         }
         __syncthreads();
         PCL_STEP();
-        // S2: lane j of every wave scans the slot counts; every position's exclusive >= / <=
-        // counts over the whole array go to RK (RK[n]: the totals), and the >= elements are
-        // listed in position order at their >= count in PL, the <= elements at theirs in PR:
-        // a range's L list is then a contiguous stretch of PL from RK[f + 1], its R list the
-        // stretch of PR below RK[e], read from the right
+        // S2: lane j of every wave scans the slot counts; every position's >= / <= counts over
+        // the whole array, inclusive, go to RLO, and the >= elements are listed in position
+        // order at their exclusive >= count in PL, the <= elements at theirs in PR: a range's
+        // L list is then a contiguous stretch of PL from RLO[f] (the head counts for nothing),
+        // its R list the stretch of PR below RLO[e - 1], read from the right. Both words lie
+        // in live slots.
         {
             const uint32_t cj = l < NS ? cnt[l] : 0u;
             const uint32_t g = wave_incl_scan(cj & 0xffffu), h = wave_incl_scan(cj >> 16);
             const uint32_t gex = g - (cj & 0xffffu), hex = h - (cj >> 16);
-            if (tid == 0) {
-                S.RLO[n] = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)(NS - 1)) |
-                           ((uint32_t)__builtin_amdgcn_readlane((int)h, (int)(NS - 1)) << 16);
-            }
 #pragma unroll
             for (int k = 0; k < PER; k++) {
+                if (!((live >> k) & 1u)) continue;
                 const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
                 const uint32_t src = (uint32_t)k * WAVES + w;
                 const uint32_t gx = (uint32_t)__builtin_amdgcn_readlane((int)gex, (int)src) + (st[k] & 0xfffu);
                 const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)hex, (int)src) + ((st[k] >> 12) & 0xfffu);
-                if (x < n) S.RLO[x] = gx | (lx << 16);
+                if (x < n) S.RLO[x] = (gx + ((st[k] & GE) ? 1u : 0u)) | ((lx + ((st[k] & LE) ? 1u : 0u)) << 16);
                 if (st[k] & GE) S.PL[gx] = x;
                 if (st[k] & LE) S.PR[lx] = x;
                 if ((st[k] & PART) && x == f) S.CUT[f] = 0u;
@@ -383,11 +391,12 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         for (int k = 0; k < PER; k++) {
             const uint32_t f = fe[k] & 0xffffu, e = fe[k] >> 16;
             const bool part = (st[k] & PART) != 0;
-            bf[k] = part ? S.RLO[f + 1] : 0u;
-            be[k] = part ? S.RLO[e] : 0u;
+            bf[k] = part ? S.RLO[f] : 0u;
+            be[k] = part ? S.RLO[e - 1] : 0u;
         }
 #pragma unroll
         for (int k = 0; k < PER; k++) {
+            if (!OOP && !((live >> k) & 1u)) continue;   // out of place, every record moves
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
             const bool in = (st[k] & IN) != 0;
             const uint32_t gf = bf[k] & 0xffffu, lend = be[k] >> 16;
@@ -438,7 +447,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
             if ((st[k] & PART) && x == f) {
                 const uint32_t s = S.CUT[f], info = S.INFO[f];
-                const uint32_t gf = S.RLO[f + 1] & 0xffffu, lend = S.RLO[e] >> 16, nL = nn[k] & 0xffffu;
+                const uint32_t gf = S.RLO[f] & 0xffffu, lend = S.RLO[e - 1] >> 16, nL = nn[k] & 0xffffu;
                 const uint32_t pl1 = S.PL[gf];
                 const uint32_t pls = s < nL ? S.PL[gf + s] : 0xffffffffu, prs = s ? S.PR[lend - s] : 0u;
                 const uint32_t cut = s == 0 ? pl1 : min(pls, prs);

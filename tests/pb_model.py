@@ -173,13 +173,19 @@ def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False)
     T = range(BLOCK)
     fe = [[n << 16] * PER for _ in T]
     anyact = _setup(E, S, 0, n, depth0, wmax) if n else False
+    live = [[True] * PER for _ in range(WAVES)]       # (wave, k) slots with a partitioned range
     while anyact:
         st = [[0] * PER for _ in T]
         nn = [[0] * PER for _ in T]
+        S["RLO"] = Arr(n + 1, None)                  # a read of a word not written this level fails
         for k in range(PER):                         # S1
             ge = [False] * BLOCK
             le = [False] * BLOCK
+            dead = [not live[w][k] for w in range(WAVES)]
             for t in T:
+                if dead[t // 64]:                    # a dead slot: nothing to do in any step
+                    st[t][k] = dict(part=False, inn=False)
+                    continue
                 x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
                 info = p = kx = 0
                 if x < n:
@@ -189,9 +195,14 @@ def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False)
                 ge[t], le[t] = inn and kx >= p, inn and kx <= p
                 st[t][k] = dict(part=part, inn=inn)
             for w in range(WAVES):
+                if dead[w]:
+                    cnt[k * WAVES + w] = 0
+                    continue
                 gm = sum(1 << l for l in range(64) if ge[64 * w + l])
                 lm = sum(1 << l for l in range(64) if le[64 * w + l])
                 cnt[k * WAVES + w] = _popc(gm) | (_popc(lm) << 16)
+                if not any(st[64 * w + l][k]["part"] for l in range(64)):
+                    live[w][k] = False               # ranges only shrink: dead for good
                 for l in range(64):
                     t = 64 * w + l
                     st[t][k].update(ge=ge[t], le=le[t], mg=_popc(gm & ((1 << l) - 1)), ml=_popc(lm & ((1 << l) - 1)))
@@ -199,17 +210,18 @@ def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False)
         c = [cnt[j] for j in range(NS)]
         gex = [sum(c[i] & 0xFFFF for i in range(j)) for j in range(NS)]
         hex_ = [sum(c[i] >> 16 for i in range(j)) for j in range(NS)]
-        S["RLO"][n] = sum(v & 0xFFFF for v in c) | (sum(v >> 16 for v in c) << 16)
         for t in T:
             w = t // 64
             for k in range(PER):
                 x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
                 q = st[t][k]
+                if "ge" not in q:                    # dead slot (it was dead in S1 already)
+                    continue
                 gx, lx = gex[k * WAVES + w] + q["mg"], hex_[k * WAVES + w] + q["ml"]
                 assert gx < 4096 and lx < 4096
                 q.update(gx=gx, lx=lx)
-                if x < n:
-                    S["RLO"][x] = gx | (lx << 16)
+                if x < n:   # inclusive counts: a range's words are at its first and last position
+                    S["RLO"][x] = (gx + q["ge"]) | ((lx + q["le"]) << 16)
                 if q["ge"]:
                     S["PL"][gx] = x
                 if q["le"]:
@@ -223,7 +235,7 @@ def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False)
                 q = st[t][k]
                 if not q["part"]:
                     continue
-                bf, be = S["RLO"][f + 1], S["RLO"][e]
+                bf, be = S["RLO"][f], S["RLO"][e - 1]
                 gf, lend = bf & 0xFFFF, be >> 16
                 nL, nR = (be & 0xFFFF) - gf, lend - (bf >> 16)
                 nn[t][k] = (nL, nR)
@@ -259,7 +271,7 @@ def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False)
                 x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
                 if st[t][k]["part"] and x == f:
                     s, nL = S["CUT"][f], nn[t][k][0]
-                    gf, lend = S["RLO"][f + 1] & 0xFFFF, S["RLO"][e] >> 16
+                    gf, lend = S["RLO"][f] & 0xFFFF, S["RLO"][e - 1] >> 16
                     cut = S["PL"][gf] if s == 0 else min(S["PL"][gf + s] if s < nL else 0xFFFFFFFF, S["PR"][lend - s])
                     d = (S["INFO"][f] & BUDGET) - 1
                     anyact |= _setup(E, S, f, cut, d, wmax)
