@@ -923,13 +923,16 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
         const uint32_t n = S.meta[LG_PCL_N];
         if (n <= LG_PCL_CUT) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
     }
-    uint32_t nr;
-    const uint32_t active = pq_tiles(S, level, tp, red, nr);
-    if (blockIdx.x >= active) return;
     uint64_t* st = S.pqst;   // [0] tickets, [2 + t] tile t's status; lg_pq_swap zeroes them
+    // the ticket first (its latency overlaps the range lists' loads): tickets are handed out
+    // in start order to every workgroup, and the one holding ticket t runs tile t, so a tile
+    // still waits only on tiles already running; tickets past the tiles return
     if (tid == 0) tk = (uint32_t)__hip_atomic_fetch_add(&st[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t t = tk, r = pq_find(tp, nr, t), q = t - tp[r];
+    uint32_t nr;
+    const uint32_t active = pq_tiles(S, level, tp, red, nr);   // ends with a barrier
+    const uint32_t t = tk;
+    if (t >= active) return;
+    const uint32_t r = pq_find(tp, nr, t), q = t - tp[r];
     uint32_t f, e, d, m, p;
     pq_range(S, level, r, f, e, d);
     // the median of three and this element's key in one batch of loads: x > f, and x's
@@ -973,16 +976,14 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64
     __shared__ uint32_t red[8 * WAVES];
     const uint32_t tid = threadIdx.x;
     if (blockIdx.x == 0 && tid == 0 && level > 0) S.pq[(level + 2u) % 3u] = 0;   // the list level + 1 fills
+    // lg_pq_split's ticket counter (every split workgroup takes a ticket) and status words of
+    // this level, for the next level's split (the kernel boundary orders these stores after
+    // every split tile's look-back, so its status words need no release)
+    if (blockIdx.x == 0 && tid == 0) S.pqst[0] = 0;
     uint32_t nr;
     const uint32_t active = pq_tiles(S, level, tp, red, nr);
     if (blockIdx.x >= active) return;
-    // lg_pq_split's ticket and status words of this level, for the next level's split (the
-    // kernel boundary orders these stores after every split tile's look-back, so its status
-    // words need no release)
-    if (tid == 0) {
-        S.pqst[2 + blockIdx.x] = 0;
-        if (blockIdx.x == 0) S.pqst[0] = 0;
-    }
+    if (tid == 0) S.pqst[2 + blockIdx.x] = 0;
     const uint32_t t = blockIdx.x, r = pq_find(tp, nr, t), q = t - tp[r];
     uint32_t f, e, d, m, p;
     pq_range(S, level, r, f, e, d);
@@ -1085,6 +1086,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
     __shared__ uint32_t red[8 * WAVES];
     const uint32_t n = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
     const uint32_t tid = threadIdx.x;
+    // the split's ticket counter, also when no level followed the level-0 split (no swap)
+    if (blockIdx.x == 0 && tid == 0) S.pqst[0] = 0;
     for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
         const uint32_t* ent = pq_list(S, PQ_LEAFLIST) + PQ_EW * b;
         const uint32_t first = ent[0], last = ent[1], depth = ent[2], size = last - first;
