@@ -808,6 +808,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
                                // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
 #define PQ_WAVES 6
 #define PQ_MIDS 7
+#define PQ_TILES 8             // S.ca: [0] a level's tile count; from word 8, eight words per tile
+                               // (range, median, pivot, budget, range index, tile in range):
+                               // lg_pq_split -> lg_pq_swap (<= 8 (N / 512 + 2048) + 8 words)
 #define PQ_LEAFLIST 3
 #define PQ_EW 5                // entry words: first, last, depth, then nL, nR (levels) / buffer (leaves)
 #define PQ_T CG_BLOCK          // elements per tile
@@ -931,6 +934,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     uint32_t nr;
     const uint32_t active = pq_tiles(S, level, tp, red, nr);   // ends with a barrier
     const uint32_t t = tk;
+    if (t == 0 && tid == 0) S.ca[0] = active;   // for lg_pq_swap (PQ_TILES)
     if (t >= active) return;
     const uint32_t r = pq_find(tp, nr, t), q = t - tp[r];
     uint32_t f, e, d, m, p;
@@ -944,6 +948,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     const uint32_t kx = valid ? pq_key(E, x) : 0u;
     m = pb_median(a, b, c, ka, kb, kc);
     p = m == a ? ka : (m == b ? kb : kc);
+    if (tid == 0) {   // the tile's range, median and pivot for lg_pq_swap: one load there
+        uint32_t* tt = S.ca + PQ_TILES + 8u * t;
+        tt[0] = f; tt[1] = e; tt[2] = m; tt[3] = p;
+        tt[4] = d; tt[5] = r; tt[6] = q; tt[7] = 0u;
+    }
     const uint32_t k = valid ? (x == m ? kf : kx) : 0u;
     const bool ge = valid && k >= p, le = valid && k <= p;
     const uint64_t gm = __ballot(ge), lm = __ballot(le);
@@ -972,33 +981,27 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
 
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64_t* E, uint64_t* Eo, uint32_t level,
                                                        uint32_t last_level, uint32_t out_buf) {
-    __shared__ uint32_t tp[PQ_MAXR + 1];
-    __shared__ uint32_t red[8 * WAVES];
     const uint32_t tid = threadIdx.x;
     if (blockIdx.x == 0 && tid == 0 && level > 0) S.pq[(level + 2u) % 3u] = 0;   // the list level + 1 fills
     // lg_pq_split's ticket counter (every split workgroup takes a ticket) and status words of
     // this level, for the next level's split (the kernel boundary orders these stores after
     // every split tile's look-back, so its status words need no release)
     if (blockIdx.x == 0 && tid == 0) S.pqst[0] = 0;
-    uint32_t nr;
-    const uint32_t active = pq_tiles(S, level, tp, red, nr);
+    const uint32_t active = S.ca[0];   // the split's tile count
     if (blockIdx.x >= active) return;
     if (tid == 0) S.pqst[2 + blockIdx.x] = 0;
-    const uint32_t t = blockIdx.x, r = pq_find(tp, nr, t), q = t - tp[r];
-    uint32_t f, e, d, m, p;
-    pq_range(S, level, r, f, e, d);
+    // the tile's range, median and pivot as the split left them, then one batch of loads:
+    // E[f], this element and its ranks (x > f), the range's totals
+    const uint32_t t = blockIdx.x;
+    const uint4 t0 = ((const uint4*)(S.ca + PQ_TILES))[2 * t], t1 = ((const uint4*)(S.ca + PQ_TILES))[2 * t + 1];
+    const uint32_t f = t0.x, e = t0.y, m = t0.z, p = t0.w, d = t1.x, r = t1.y, q = t1.z;
     const uint32_t* tot = level == 0 ? S.pq + 4 : pq_list(S, level % 3u) + PQ_EW * r + 3;
     const uint32_t nL = tot[0], nR = tot[1];
-    // one batch of loads: the median of three, E[f], this element and its ranks (x > f)
     const uint32_t x = f + 1 + q * PQ_T + tid;
-    const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
-    const uint64_t ra = E[a], rb = E[b], rc = E[c], rf = E[f];
+    const uint64_t rf = E[f];
     const uint64_t rx = x < e ? E[x] : 0ull;
     const uint64_t rk = x < e ? ((const uint64_t*)S.vox)[x] : 0ull;
-    m = pb_median(a, b, c, pcl_key(ra), pcl_key(rb), pcl_key(rc));
-    const uint64_t rm = m == a ? ra : (m == b ? rb : rc);
-    p = pcl_key(rm);
-    if (q == 0 && tid == 0) Eo[f] = rm;
+    if (q == 0 && tid == 0) Eo[f] = E[m];
     if (x >= e) return;
     const uint64_t vx = x == m ? rf : rx;
     const uint32_t k = pcl_key(vx);
