@@ -691,7 +691,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevPara
         }
     }
     __syncthreads();
-    {   // the dense neighbour grid's cell counts (lg_dgrid_count), ncell from lg_grid_setup
+    {   // the dense neighbour grid's cell counts (lg_voxel_centroids), ncell from lg_grid_setup
         const uint32_t nc = m[LG_NCELL] + 1;
         for (uint32_t i = j; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
     }
@@ -730,6 +730,40 @@ struct VoxelEmit {
     __device__ void operator()(uint32_t r, uint32_t v) const { run[v] = r; }
 };
 
+// The dense neighbour grid of the clustering (its words from lg_grid_setup, in meta).
+__device__ __forceinline__ uint32_t lg_dcell(float c, float o, float inv, uint32_t n) {
+    const float q = floorf((c - o) * inv);
+    if (!(q >= 0.f)) return 0u;                      // NaN or below the origin
+    return q >= (float)(n - 1) ? n - 1 : (uint32_t)q;   // clamped: a superset of neighbours
+}
+struct LgGrid {
+    float o[3], inv[3];
+    uint32_t n[3];
+    __device__ explicit LgGrid(const uint32_t* m) {
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            o[a] = __uint_as_float(m[LG_ORG + a]);
+            inv[a] = __uint_as_float(m[LG_DGINV + a]);
+            n[a] = m[LG_DGN + a];
+        }
+    }
+    __device__ void cell(const float4& q, uint32_t& cx, uint32_t& cy, uint32_t& cz) const {
+        cx = lg_dcell(q.x, o[0], inv[0], n[0]);
+        cy = lg_dcell(q.y, o[1], inv[1], n[1]);
+        cz = lg_dcell(q.z, o[2], inv[2], n[2]);
+    }
+    __device__ uint32_t id(uint32_t cx, uint32_t cy, uint32_t cz) const { return cx + n[0] * (cy + n[1] * cz); }
+};
+// A voxel's neighbour-grid cell and its slot there (the cell counts; lg_voxel_keys zeroed
+// them): written with the voxel's centroid, by the lane that computed it.
+__device__ __forceinline__ void lg_dgrid_count_one(const LgScratch& S, uint32_t v, const float4& c) {
+    const LgGrid g(S.meta);
+    uint32_t cx, cy, cz;
+    g.cell(c, cx, cy, cz);
+    const uint32_t k = g.id(cx, cy, cz);
+    S.uk[v] = k;
+    S.ca[v] = atomicAdd(&S.cstart[k], 1u);
+}
 // CentroidPoint: float sums in ascending frame index / float(n); passthrough copies the point.
 // One wave per voxel: the lanes fetch 64 members at a time, the sums run through them in
 // member order.
@@ -750,6 +784,7 @@ __device__ __forceinline__ void lg_voxel_centroids_one(const CgLaunch& L, const 
             const float4 p = lg_point(S, val[v], Ms);
             S.vox[v] = p;
             vox_out[v] = p;
+            lg_dgrid_count_one(S, v, p);
         }
         return;
     }
@@ -771,6 +806,7 @@ __device__ __forceinline__ void lg_voxel_centroids_one(const CgLaunch& L, const 
     const float4 c = make_float4(sx / nn, sy / nn, sz / nn, si / nn);
     S.vox[v] = c;
     vox_out[v] = c;
+    lg_dgrid_count_one(S, v, c);
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScratch S, uint32_t f, uint32_t Mtot,
                                                                int buf) {
@@ -1181,39 +1217,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_waves(LgScratch S, uint64_t* 
 //   flatten: pointer jumping;
 //   cross: only edges between different trees are united (uf_union hooks the larger root
 //   under the smaller, so roots stay the components' lowest indices).
-__device__ __forceinline__ uint32_t lg_dcell(float c, float o, float inv, uint32_t n) {
-    const float q = floorf((c - o) * inv);
-    if (!(q >= 0.f)) return 0u;                      // NaN or below the origin
-    return q >= (float)(n - 1) ? n - 1 : (uint32_t)q;   // clamped: a superset of neighbours
-}
-struct LgGrid {
-    float o[3], inv[3];
-    uint32_t n[3];
-    __device__ explicit LgGrid(const uint32_t* m) {
-#pragma unroll
-        for (int a = 0; a < 3; a++) {
-            o[a] = __uint_as_float(m[LG_ORG + a]);
-            inv[a] = __uint_as_float(m[LG_DGINV + a]);
-            n[a] = m[LG_DGN + a];
-        }
-    }
-    __device__ void cell(const float4& q, uint32_t& cx, uint32_t& cy, uint32_t& cz) const {
-        cx = lg_dcell(q.x, o[0], inv[0], n[0]);
-        cy = lg_dcell(q.y, o[1], inv[1], n[1]);
-        cz = lg_dcell(q.z, o[2], inv[2], n[2]);
-    }
-    __device__ uint32_t id(uint32_t cx, uint32_t cy, uint32_t cz) const { return cx + n[0] * (cy + n[1] * cz); }
-};
-__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_count(LgScratch S) {
-    const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
-    if (v >= V) return;
-    const LgGrid g(S.meta);
-    uint32_t cx, cy, cz;
-    g.cell(S.vox[v], cx, cy, cz);
-    const uint32_t c = g.id(cx, cy, cz);
-    S.uk[v] = c;
-    S.ca[v] = atomicAdd(&S.cstart[c], 1u);
-}
 // exclusive scan of cstart[0, ncell] in place (single pass, lg_tile_scan)
 __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_scan(LgScratch S) {
     const uint32_t n = S.meta[LG_NCELL] + 1;
@@ -1709,7 +1712,6 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
     const uint32_t VB = bits_of(Mtot);
     const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = lg_wave_blocks(Mtot);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;   // tiles past ncell return at once
-    hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
@@ -1869,7 +1871,6 @@ int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
                        L, S, 0u, Mtot, buf);
     const uint32_t vb = std::max<uint32_t>(1, blocks_of(Mtot)), wb = lg_wave_blocks(Mtot);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
-    hipLaunchKernelGGL(lg_dgrid_count, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
