@@ -363,9 +363,11 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         // its R list the stretch of PR below RLO[e - 1], read from the right. Both words lie
         // in live slots.
         {
+            // both counts in one scan of the packed word (totals <= n <= 4,096: no carry
+            // between the halves)
             const uint32_t cj = l < NS ? cnt[l] : 0u;
-            const uint32_t g = wave_incl_scan(cj & 0xffffu), h = wave_incl_scan(cj >> 16);
-            const uint32_t gex = g - (cj & 0xffffu), hex = h - (cj >> 16);
+            const uint32_t ex = wave_incl_scan(cj) - cj;
+            const uint32_t gex = ex & 0xffffu, hex = ex >> 16;
 #pragma unroll
             for (int k = 0; k < PER; k++) {
                 if (!((live >> k) & 1u)) continue;
