@@ -3,7 +3,8 @@ no oracle in between: tools/pcl_probe.hip (the frame kernel's LDS form: 4,000 ra
 sorted, reversed and organ-pipe cases of up to 2,048 records; every seventh case starts with a
 depth budget of 0-3, checked against libstdc++'s __introsort_loop + __final_insertion_sort with
 that budget, so the heapsort fallbacks run) and tools/pcl_leaf_probe.hip (the large path's leaf
-configuration: up to 4,096 records, 8 per thread). Built by build() into the package's lib/."""
+configuration: up to 4,096 records, 8 per thread; every seventh case with a spent budget too).
+Built by build() into the package's lib/."""
 import os
 import subprocess
 
