@@ -28,12 +28,16 @@ struct Work {
 //     min(L_s, R_{s-1}). Depth budget and heapsort fallback per range as in the sequential
 //     code (cg_sort.h);
 //  3. up to PMAX * CG_BLOCK elements (pcl_block_sort) each thread keeps its elements' ranges in
-//     registers; longer arrays (HBM scratch) run block levels until every range fits, then
-//     pcl_block_sort on each range;
+//     registers; the workgroup levels stop at ranges of at most 64, which one wave each
+//     finishes in registers (pw_range64); longer arrays (HBM scratch) run block levels until
+//     every range fits, then pcl_block_sort on each range. The large path (cg_large.hip) runs
+//     the first levels across workgroups and hands the leaves to pcl_block_sort in LDS;
 //  4. the final insertion passes: a stable sort inside each range of at most 16 (the ranges
 //     are weakly ordered, so this is the stable sort of the whole array).
-// The permutation is checked against std::sort on the host (tests/test_math_host.py, the
-// level model) and on the device against the oracle's ORDER_PCL (tests/test_gpu_pcl_order.py).
+// The permutation is checked against std::sort on the host (tests/test_math_host.py and the
+// thread-level model tests/pb_model.py), on the device directly against libstdc++
+// (tools/pcl_probe.hip, tools/pcl_leaf_probe.hip: tests/test_gpu_pcl_probe.py) and against the
+// oracle's ORDER_PCL (tests/test_gpu_pcl_order.py).
 #ifdef CG_PCL_PROBE
 __device__ unsigned long long g_pcl_probe[64];
 __device__ unsigned int g_pcl_probe_n;
