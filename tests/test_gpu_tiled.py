@@ -119,3 +119,47 @@ def test_tiled_single_rank_matches_oracle(halo):
                              halo=halo)
     ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_STABLE if halo else O.ORDER_PCL)
     assert_same_detection(got, ref, "tiled x1")
+
+
+def test_tile_async_argument_checks():
+    """The async tile entry points refuse calls out of order and tiles that do not fit the
+    call: no kernel is launched for a refused call, and the handle stays usable."""
+    import ctypes as C
+    import torch
+    from cones_perception_amd import _abi
+    lib = _abi.lib()
+    dev = torch.device("cuda", 0)
+    eng = cp.BatchEngine(cp.load_params("simulation"), device=0)
+    h = eng.handle
+    raw = cp.synth_frames(1, first_frame=3, rings=16, cols=1024, clutter=10, cones_per_row=4)
+    n = raw.shape[1] // 16
+    d = torch.from_numpy(raw[0].copy()).to(dev)
+    keys = torch.empty(_abi.CG_TILE_KEYS, dtype=torch.int32, device=dev)
+    counts = torch.empty(_abi.CG_TILE_COUNTS, dtype=torch.int32, device=dev)
+    sp = torch.empty(n * 4, dtype=torch.float32, device=dev)
+    si = torch.empty(n, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    # before any cg_tile_front_async
+    assert lib.cg_tile_decide_async(h, keys.data_ptr(), counts.data_ptr(), s) == _abi.CG_E_INVALID
+    assert lib.cg_tile_survivors_async(h, sp.data_ptr(), si.data_ptr(), 0, s) == _abi.CG_E_INVALID
+    assert lib.cg_tile_backend_own(h, n, s) == _abi.CG_E_INVALID
+    # a tile running past the end of its frame, a null tile pointer
+    bad = _abi.cg_tile(d.data_ptr(), n // 2, n, n, 16, 0, 4, 8, 12)
+    assert lib.cg_tile_front_async(h, C.byref(bad), keys.data_ptr(), s) == _abi.CG_E_INVALID
+    assert lib.cg_tile_front_async(h, C.byref(_abi.cg_tile(0, 0, n, n, 16, 0, 4, 8, 12)), keys.data_ptr(),
+                                   s) == _abi.CG_E_INVALID
+    # the first half of a frame: the backend needs the whole frame in the tile
+    half = n // 2
+    t = _abi.cg_tile(d.data_ptr(), 0, half, n, 16, 0, 4, 8, 12)
+    _abi.check(lib.cg_tile_front_async(h, C.byref(t), keys.data_ptr(), s))
+    _abi.check(lib.cg_tile_decide_async(h, keys.data_ptr(), counts.data_ptr(), s))
+    assert lib.cg_tile_backend_own(h, n, s) == _abi.CG_E_INVALID
+    assert lib.cg_tile_survivors_async(h, sp.data_ptr(), si.data_ptr(), half + 1, s) == _abi.CG_E_INVALID
+    assert lib.cg_tile_survivors_async(h, 0, 0, 1, s) == _abi.CG_E_INVALID
+    torch.cuda.synchronize(dev)
+    # the handle still runs a whole frame through the tile protocol, bit-exact
+    from cones_perception_amd import dist as cd
+    params = cp.load_params("simulation")
+    got = cd.run_tiled_frame(eng, d.data_ptr(), 0, n, n, dev)
+    ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_PCL)
+    assert_same_detection(got, ref, "tiled after refused calls")
