@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_COPY_GBS = 6290.0   # the same guide's measured float4 copy rate (79% of spec), for context only
 XGMI_LINK_GBS = 153.0   # one xGMI link, one direction (7 links x ~153 GB/s per GPU)
 METRIC = "LiDAR frames/sec @64k pts/frame, 1/2/4/8 MI355X; cluster-set match vs PCL"
 
@@ -262,7 +263,10 @@ def main():
                          # launches on S streams overlap, so per-launch duration counts shared
                          # time S-fold; the aggregate rate is bytes of all launches / wall time
                          "aggregate_achieved": bytes_per_launch * args.steps * world / elapsed / 1e9 / world,
-                         "aggregate_frac": bytes_per_launch * args.steps / elapsed / 1e9 / HBM_PEAK_GBS},
+                         "aggregate_frac": bytes_per_launch * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
+                         # the guide's measured streaming rate; frac stays against the spec peak
+                         "aggregate_frac_of_measured_copy": bytes_per_launch * args.steps / elapsed / 1e9
+                         / HBM_COPY_GBS},
             "cpu_baseline": cpu,
             "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
         }
