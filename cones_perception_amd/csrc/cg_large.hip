@@ -1621,6 +1621,9 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
 
 // Detector backend over meta[LG_MS] survivors (surv_p / surv_i, frame indices < n_total) and,
 // in pipeline mode with zero_pass, the n_total - K pads; results in frame slot f.
+#ifndef LG_PQ_SPARE
+#define LG_PQ_SPARE 3   // partition levels beyond an even split's, for uneven median-of-three cuts
+#endif
 int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t N, uint32_t K) {
     CgDevParams P = P0;
@@ -1682,7 +1685,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
         // median-of-three cuts; levels with no range to cut return at once; then the leaves
         uint32_t levels = 0;
         while (((uint64_t)LG_PCL_CUT << levels) < Mtot) levels++;
-        if (levels) levels = std::min<uint32_t>(levels + 3, LG_PQ_LEVELS_MAX);
+        if (levels) levels = std::min<uint32_t>(levels + LG_PQ_SPARE, LG_PQ_LEVELS_MAX);
         if (S.pcl_levels_cap) levels = std::min(levels, S.pcl_levels_cap);
         const uint32_t tb = (Mtot + PQ_T - 1) / PQ_T;
         hipLaunchKernelGGL(lg_pq_split, dim3(std::max<uint32_t>(tb, 1)), dim3(CG_BLOCK), 0, s, S, kb[buf ^ 1], 0u);
