@@ -78,6 +78,9 @@ def _worker(rank, world, port, out, rings, cols, over, halo=False, mutate=None):
     (3, 64, 2048, {"distance_treshold_max": 1e5}, True, "passthrough"),   # no lattice: falls back to the gather
     (3, 64, 2048, {}, True, "narrow"),
     (2, 64, 2048, {}, True, "nonfinite"),
+    # C5's own frame size: 1,048,576 points over 2 ranks, both forms
+    (2, 128, 8192, {}, False, None),
+    (2, 128, 8192, {}, True, None),
 ])
 def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over, halo, mutate):
     out = str(tmp_path / "r0.npz")
