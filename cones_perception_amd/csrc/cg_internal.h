@@ -95,7 +95,7 @@ struct CgLaunch {
 // finished chunks, [1] used sector bins, [2, 20) sector-minimum keys (all reset by the last
 // workgroup), then the z codes (one uint2 per chunk and lane) and filter bits (one byte per
 // chunk and lane).
-#define CG_SPLIT_CHUNK 4096
+#define CG_SPLIT_CHUNK (8 * CG_BLOCK)   // 8 points per lane: one uint2 of codes, one byte of bits
 #define CG_SPLIT_CODES 64
 #define CG_SPLIT_POSM (CG_SPLIT_CODES + 2 * (CG_MAX_POINTS / 8))
 #define CG_SPLIT_WORDS (CG_SPLIT_POSM + CG_MAX_POINTS / 8 / 4)

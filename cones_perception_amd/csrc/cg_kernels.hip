@@ -631,6 +631,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     uint2* const sp_codes = SPLIT ? (uint2*)(L.split + CG_SPLIT_CODES) : nullptr;
     if constexpr (SPLIT) {
         static_assert(PPT * CG_BLOCK == CG_MAX_POINTS, "split frames use the 64k tail");
+        static_assert(CG_SPLIT_CHUNK == 8 * CG_BLOCK, "a chunk's codes are one uint2 and its bits one byte per lane");
         const uint32_t c = blockIdx.x, c0 = c * CG_SPLIT_CHUNK;
         const uint32_t Nc = N > c0 ? min((uint32_t)CG_SPLIT_CHUNK, N - c0) : 0u;
         if (L.in_host) {   // the chunk over PCIe from pinned host memory into the device copy
