@@ -104,7 +104,9 @@ int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 #ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
 #endif
+#ifndef CG_MMAX
 #define CG_MMAX 1024           // LDS-path capacity (points surviving the filter)
+#endif
 #define CG_MAX_POINTS 65536    // frame kernel: 128 points per lane; larger frames: cg_large.hip
 #define CG_MAX_FRAME_POINTS (1u << 28)
 

@@ -66,7 +66,11 @@ struct BackLds {
 };
 #define SMEM_BYTES (FRONT_BYTES + sizeof(BackLds))
 static_assert(SMEM_BYTES <= 163840, "LDS budget");
+#ifndef CG_CODES_HBM
 static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overlay must fit");
+#endif
+// (experiment, -DCG_CODES_HBM: the z codes in the frame's HBM scratch instead of LDS, so that a
+// smaller CG_MMAX lets more workgroups share a CU)
 
 #ifndef CG_PREFETCH
 #define CG_PREFETCH 2   // filter survivors per lane loaded right after pass 1
@@ -85,7 +89,12 @@ enum {
 uint64_t cg_scratch_bytes(uint32_t n) {
     uint64_t n2 = 1; while (n2 < n) n2 <<= 1;
     uint64_t c = (uint64_t)n + 4;
-    return 16 * c + 8 * n2 + 16 * c + 4 * c * 8 + 256;
+    const uint64_t b = 16 * c + 8 * n2 + 16 * c + 4 * c * 8 + 256;
+#ifdef CG_CODES_HBM
+    return b > CG_MAX_POINTS ? b : (uint64_t)CG_MAX_POINTS;   // the codes overlay it until compaction
+#else
+    return b;
+#endif
 }
 
 __device__ __forceinline__ Work global_work(uint8_t* base, uint32_t n) {
@@ -689,7 +698,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             if ((uint32_t)cc < nch) posm.set_byte(cc, pb[cc * CG_BLOCK + tid]);
         __syncthreads();
     } else {
+#ifdef CG_CODES_HBM
+        uint2* const zc = (uint2*)(L.scratch + (uint64_t)f * L.scratch_stride);
+        auto store = [&](int g, uint2 c) { zc[g * CG_BLOCK + tid] = c; };
+#else
         auto store = [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; };
+#endif
         if (LAYOUT == CG_LAYOUT_XYZI16 && N == (uint32_t)(PPT * CG_BLOCK))   // whole groups only
             stream_pass1<PPT, LAYOUT, GROUND, FILTER, decltype(store), true>(fb, N, L, P, fs->sec_key, fs->rays,
                                                                           posm, touched, store);
@@ -741,7 +755,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
     if (GROUND) {
         pass2_keep<PPT, LAYOUT>(fb, N, L, P, fs->scal[S_TKMIN], fs->scal[S_TKMAX], fs->tkey,
                                 [&](int g) {
+#ifdef CG_CODES_HBM
+                                    return SPLIT ? sp_codes[g * CG_BLOCK + tid]
+                                                 : ((const uint2*)(L.scratch + (uint64_t)f * L.scratch_stride))[g * CG_BLOCK + tid];
+#else
                                     return SPLIT ? sp_codes[g * CG_BLOCK + tid] : ((const uint2*)zq)[g * CG_BLOCK + tid];
+#endif
                                 }, keepgm);
         const uint32_t kc = wave_sum(keepgm.count());
         if (l == 0) atomicAdd(&fs->scal[S_K], kc);
