@@ -1,28 +1,31 @@
 // cg_kernels.hip — gfx950 kernels for the LiDAR cone-detection hot path.
 //
-// One 1024-lane workgroup (16 waves) owns one frame end to end; a batch launch is a grid of
-// n_frames workgroups. Per frame:
+// One 512-lane workgroup (8 waves) owns one frame end to end, two workgroups per CU; a batch
+// launch is a grid of n_frames workgroups (a single frame: cg_launch_split, below). Per frame:
 //
 //  frontend (HBM-streaming, ~all of the frame's bytes)
-//    pass 1  coalesced point loads (lane t handles points k*1024 + t), glibc-exact atan2f,
-//            22-degree sector, position-filter bit; z kept on chip (32 points per lane in VGPRs,
-//            the rest in LDS); running per-lane sector minimum flushed into 17 LDS bins with
-//            ds_min_u32 on order-preserving keys        (src/ground_removal.cpp:58-68)
-//    pass 2  ground threshold per sector, keep bits, ballot counts per (k, wave)
+//    pass 1  coalesced point loads (lane t handles points k*512 + t, up to 128 per lane),
+//            certified 22-degree sector (glibc-exact atan2f only near an edge), position-filter
+//            bits in registers, z kept as an 8-bit monotone code in LDS (64 KiB, overlaying the
+//            backend arrays); per-lane sector minimum flushed into 17 LDS bins with ds_min_u32
+//            on order-preserving keys                 (src/ground_removal.cpp:58-68)
+//    pass 2  sector thresholds; ground decisions from the codes against the band of used
+//            thresholds, exact re-read of x, y, z for band codes only
 //                                                       (src/ground_removal.cpp:70-77, and
 //                                                        src/cone_detection.cpp:189-204)
-//    scan    one exclusive scan over the 1024 (k, wave) counts = stable compaction offsets
-//    pass 3  re-gather the few survivors (x, y, z, intensity) into LDS (or HBM scratch)
-//  backend (LDS-resident, latency-bound; M ~ 1e3 points)
-//    voxel   min/max, PCL idx key, bitonic sort of (idx, position), run heads, centroid sums
-//            in ascending position order             (pcl::VoxelGrid, src/cone_detection.cpp:240-249)
-//    cluster neighbour grid (cell >= tolerance), binary-searched cell rows, exact float
+//    gather  per-wave atomic append of the survivors (x, y, z, intensity, point index) into LDS
+//            (M <= CG_MMAX) or the frame's HBM scratch
+//  backend (latency-bound; M ~ 1e2-1e3 points)
+//    voxel   bounds, PCL idx key, std::sort's permutation of PCL's index_vector (cg_pcl.h; or a
+//            rank sort in point order), run heads, centroid sums in that order
+//                                                       (pcl::VoxelGrid, src/cone_detection.cpp:240-249)
+//    cluster all pairs (V <= CG_BRUTE_V) or a neighbour grid (cell >= tolerance), exact float
 //            L2_Simple predicate, lock-free union-find hooking larger roots under smaller
 //            ones so a component's root is its lowest voxel index = PCL's seed
-//                                                    (KdTree + ECE, src/cone_detection.cpp:206-220)
+//                                                       (KdTree + ECE, src/cone_detection.cpp:206-220)
 //    order   size filter, PCL's std::sort(rbegin, rend) order (restated, cg_sort.h),
-//            stable counting sort into CSR, per-cluster centroid + radial push
-//                                                    (src/cone_detection.cpp:261-279)
+//            counting sort into CSR, per-cluster centroid + radial push
+//                                                       (src/cone_detection.cpp:261-279)
 //
 // Compiled with -ffp-contract=off: every float/double expression must round like the
 // reference's non-FMA x86-64 build.
