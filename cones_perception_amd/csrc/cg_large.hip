@@ -12,16 +12,18 @@
 //               with their VoxelGrid bounds
 //   lg_ground_* ground-only mode: stable per-chunk output offsets, kept points then zero pads
 //   backend     M <= CG_MMAX: one workgroup from LDS (cg_kernels.hip, cg_launch_lg_back_small);
-//               otherwise the global backend below: PCL idx keys sorted by a stable LSD radix
-//               sort (the survivors are already in frame-index order), voxel runs + centroids
-//               in frame-index order, a dense neighbour grid, a lowest-neighbour forest, pointer
-//               jumping and cross-tree unions (roots = lowest voxel index = PCL's seed), size
-//               filter, PCL's cluster order, CSR by a sort of the rank bits, per-cluster
-//               centroids.
-//   cg_halo_*   C5 spatial tiling: the backend per voxel slab, cross-slab edges, merge.
+//               otherwise the global backend below: PCL's index_vector as (idx, slot) records
+//               and std::sort's permutation of it (partition levels lg_pq_split / lg_pq_swap,
+//               then lg_pcl_leaf, lg_pcl_mid, lg_pcl_waves; point order instead: a stable LSD
+//               radix sort), voxel runs + centroids in that order, a dense neighbour grid, a
+//               lowest-neighbour forest, pointer jumping and cross-tree unions (roots = lowest
+//               voxel index = PCL's seed), size filter, PCL's cluster order, CSR by a sort of
+//               the rank bits, per-cluster centroids.
+//   cg_halo_*   C5 spatial tiling: the backend per voxel slab, cross-slab edges, merge (voxel
+//               sums in point order there).
 //
-// Every sum keeps the reference's order (PCL sorts by idx; ties in point order here, as in
-// the frame kernel), so results are bit-identical to the frame kernel's on the same input.
+// Every sum keeps the order of the frame kernel's on the same input (PCL's std::sort order by
+// default), so the results are bit-identical to it.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
