@@ -357,11 +357,14 @@ def dry_run(args, world, rank):
 
 
 def traffic_per_launch(F):
-    """HBM bytes per launch from the committed PMC summary (profiles/r1_traffic.json:
+    """HBM bytes per launch from the newest committed PMC summary (profiles/rNN_traffic.json:
     FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction), scaled to this launch's frames."""
-    p = os.path.join(ROOT, "profiles", "r1_traffic.json")
-    if not os.path.exists(p):
+    import glob
+    got = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*_traffic.json")),
+                 key=lambda q: int(os.path.basename(q)[1:].split("_")[0]))
+    if not got:
         return None
+    p = got[-1]
     with open(p) as fh:
         t = json.load(fh)
     return t["hbm_bytes_per_frame"] * F
