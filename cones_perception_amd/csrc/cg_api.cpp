@@ -417,7 +417,7 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
             HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
             HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
         }
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(cg_stream_wait(s));
         const uint32_t* p = h->h_pack;
         const uint32_t V = p[CG_HDR_V], C = p[CG_HDR_C];
         if (V <= CG_PACK_MAX && C <= CG_PACK_MAX && (C == 0 || p[CG_PACK_OFFS + C] <= CG_PACK_MAX)) {
@@ -438,7 +438,7 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
     }
     HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, CG_HDR_WORDS * 4,
                           hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(cg_stream_wait(s));
     const uint32_t V = h->h_hdr[CG_HDR_V], C = h->h_hdr[CG_HDR_C];
     h->h_vox.resize((size_t)V * 4 + 4);
     h->h_lab.resize((size_t)V + 1);
@@ -454,11 +454,11 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
     if (C) {
         HIPCHK(hipMemcpyAsync(h->h_cen.data(), h->d_cen + frame * cap, (size_t)C * 8, hipMemcpyDeviceToHost, s));
     }
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(cg_stream_wait(s));
     const uint32_t nidx = C ? (uint32_t)h->h_offs[C] : 0u;
     if (nidx) {
         HIPCHK(hipMemcpyAsync(h->h_idx.data(), h->d_idx + frame * cap, (size_t)nidx * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(cg_stream_wait(s));
     }
     out->n_points = h->h_hdr[CG_HDR_N];
     out->n_kept = h->h_hdr[CG_HDR_K];
@@ -522,7 +522,7 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         }
         if (n) HIPCHK(hipMemcpyAsync(h->h_ground, h->d_ground, (size_t)n * 32, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr, CG_HDR_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
+        HIPCHK(cg_stream_wait(h->stream));
         gres->n_points = n;
         gres->n_kept = h->h_hdr[CG_HDR_K];
         gres->width = in->width;
@@ -602,7 +602,7 @@ int cg_create(const cg_params* params, int device, cg_handle** out) {
 int cg_destroy(cg_handle* h) {
     if (!h) return CG_OK;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->stream) (void)cg_stream_wait(h->stream);
     free_batch(h);
     if (h->d_stamps) (void)hipFree(h->d_stamps);
     if (h->d_in) (void)hipFree(h->d_in);
@@ -683,7 +683,7 @@ static int recrop_frame(cg_handle* h, const CgLaunch& L, bool pipe, const uint32
             HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, d_seckeys, h->d_boxes, nb, h->d_rc_cnt, nullptr,
                                                 nullptr, false, h->stream));
             HIPCHK(hipMemcpyAsync(h->h_rc_cnt.data(), h->d_rc_cnt, ncnt * 4, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
+            HIPCHK(cg_stream_wait(h->stream));
         }
         // device slots: box-major, blocks in order
         std::vector<uint32_t> off(ncnt), box_lo(nb), box_n(nb, 0u);
@@ -708,7 +708,7 @@ static int recrop_frame(cg_handle* h, const CgLaunch& L, bool pipe, const uint32
             HIPCHK((hipError_t)cg_launch_recrop(L, h->dp, pipe, d_seckeys, h->d_boxes, nb, nullptr,
                                                 h->d_rc_cnt + ncnt, h->d_rc_out, true, h->stream));
             HIPCHK(hipMemcpyAsync(h->h_rc_dev.data(), h->d_rc_out, total * 16, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
+            HIPCHK(cg_stream_wait(h->stream));
         }
         // each box: its device points in cloud order, then the zero pads if the box holds the origin
         for (uint32_t b = 0; b < nb; b++) {
@@ -749,7 +749,7 @@ int cg_batch_recrop(cg_handle* h, uint32_t frame, const float* centers_xy, uint3
     uint32_t hdr[CG_HDR_WORDS];
     HIPCHK(hipMemcpyAsync(hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, sizeof(hdr), hipMemcpyDeviceToHost,
                           h->last_stream));
-    HIPCHK(hipStreamSynchronize(h->last_stream));
+    HIPCHK(cg_stream_wait(h->last_stream));
     CgLaunch L = h->last_batch;
     L.in += (uint64_t)frame * L.frame_stride;
     L.n_frames = 1;
@@ -858,7 +858,7 @@ int cg_tile_front(cg_handle* h, const cg_tile* t, uint32_t* keys) {
     S.pidx_base = t->first;
     HIPCHK((hipError_t)cg_large_front(L, h->dp, CG_KMODE_PIPELINE, S, h->stream, 0, true));
     HIPCHK(hipMemcpyAsync(keys, S.meta + LG_SECKEY, CG_TILE_KEYS * 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     h->tile_ready = true;
     return CG_OK;
 }
@@ -874,7 +874,7 @@ int cg_tile_decide(cg_handle* h, const uint32_t* merged_keys, uint32_t* counts) 
     HIPCHK((hipError_t)cg_large_decide(L, h->dp, S, h->stream, 0));
     uint32_t m[LG_META_WORDS];
     HIPCHK(hipMemcpyAsync(m, S.meta, sizeof(m), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     counts[0] = m[LG_K];
     counts[1] = m[LG_MS];
     counts[2] = m[LG_NFIN];
@@ -888,14 +888,14 @@ int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t
     HIPCHK(hipSetDevice(h->device));
     uint32_t n = 0;
     HIPCHK(hipMemcpyAsync(&n, h->lg.meta + LG_MS, 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     if (n > capacity) return fail(CG_E_INVALID, "%u survivors do not fit %u", n, capacity);
     if (n && (!d_points || !d_index)) return fail(CG_E_INVALID, "null output buffers");
     if (n) {
         HIPCHK(hipMemcpyAsync(d_points, h->lg.surv_p, (size_t)n * 16, hipMemcpyDeviceToDevice, h->stream));
         HIPCHK(hipMemcpyAsync(d_index, h->lg.surv_i, (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
     }
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     return CG_OK;
 }
 
@@ -924,7 +924,7 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
     fill_launch_outputs(h, L);
     L.stamps = nullptr;
     HIPCHK((hipError_t)cg_large_backend(L, h->dp, CG_KMODE_PIPELINE, S, h->stream, 0, n_total, merged_counts[0]));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
     h->last_single = false;
     return CG_OK;
@@ -1051,7 +1051,7 @@ int cg_halo_owner(cg_handle* h, const cg_halo_plan* plan, const float* d_points,
     if (rc) return rc;
     HIPCHK((hipError_t)cg_launch_halo_owner(d_points, n, h->dp.inv_leaf[0], plan->min_b[0], plan->slab_w, plan->slabs,
                                             d_slab, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     return CG_OK;
 }
 
@@ -1096,7 +1096,7 @@ int cg_halo_edges(cg_handle* h, const uint32_t* d_own, uint32_t n_own, const uin
     HIPCHK((hipError_t)cg_halo_edges_run(d_own, n_own, d_halo, n_halo, h->dp.r2, d_pairs, capacity, d_count,
                                          h->stream));
     HIPCHK(hipMemcpyAsync(n_pairs, d_count, 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     return CG_OK;
 }
 
@@ -1124,7 +1124,7 @@ int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec,
     L.stamps = nullptr;
     HIPCHK((hipError_t)cg_halo_merge_run(L, h->dp, S, h->stream, d_rec, n_rec, d_pairs, n_pairs, plan->key_bits,
                                          (uint32_t)Mtot, merged_counts[0]));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
     h->last_single = false;
     return CG_OK;
@@ -1140,7 +1140,7 @@ int cg_colornet_set(cg_handle* h, const float* weights, uint32_t n_weights) {
     if (rc) return rc;
     if (!h->d_cn_w) HIPCHK(hipMalloc(&h->d_cn_w, CG_COLORNET_WEIGHTS * sizeof(float)));
     HIPCHK(hipMemcpyAsync(h->d_cn_w, weights, CG_COLORNET_WEIGHTS * sizeof(float), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     return CG_OK;
 }
 
@@ -1182,7 +1182,7 @@ int cg_classify_colors(cg_handle* h, const float* points, const uint32_t* offset
     HIPCHK(hipMemcpyAsync(colors, d_col, (size_t)n_cones * 4, hipMemcpyDeviceToHost, h->stream));
     if (probs) HIPCHK(hipMemcpyAsync(probs, d_prob, (size_t)n_cones * 12, hipMemcpyDeviceToHost, h->stream));
     if (images) HIPCHK(hipMemcpyAsync(images, d_img, (size_t)n_cones * 180, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     return CG_OK;
 }
 
@@ -1236,7 +1236,7 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames) {
     if (!h || !out) return fail(CG_E_INVALID, "null argument");
     if (!h->d_stamps || n_frames > h->stamps_frames) return fail(CG_E_INVALID, "stamps not enabled");
     HIPCHK(hipSetDevice(h->device));
-    if (h->last_stream) HIPCHK(hipStreamSynchronize(h->last_stream));
+    if (h->last_stream) HIPCHK(cg_stream_wait(h->last_stream));
     HIPCHK(hipMemcpy(out, h->d_stamps, (size_t)n_frames * 32 * 8, hipMemcpyDeviceToHost));
     return CG_OK;
 }
@@ -1254,7 +1254,7 @@ int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out,
     HIPCHK(hipMemcpy(dy, y, (size_t)n * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dx, x, (size_t)n * 4, hipMemcpyHostToDevice));
     HIPCHK((hipError_t)cg_launch_selftest_atan2f(dy, dx, dout, n, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
     (void)hipFree(dy); (void)hipFree(dx); (void)hipFree(dout);
     return CG_OK;
@@ -1271,7 +1271,7 @@ int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n) {
     HIPCHK(hipMalloc(&dout, (size_t)n * 8));
     HIPCHK(hipMemcpy(din, s, (size_t)n * 8, hipMemcpyHostToDevice));
     HIPCHK((hipError_t)cg_launch_selftest_sqrt(din, dout, n, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(cg_stream_wait(h->stream));
     HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
     (void)hipFree(din); (void)hipFree(dout);
     return CG_OK;

@@ -101,6 +101,21 @@ struct CgLaunch {
 #define CG_SPLIT_WORDS (CG_SPLIT_POSM + CG_MAX_POINTS / 8 / 4)
 int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
 
+// Host wait for a stream's queued work. Default: hipStreamSynchronize. CG_SPIN_SYNC (a variant
+// build, tools/build_variant.sh): busy-poll hipStreamQuery on the calling thread, trading a
+// host core for the wake-up latency of the blocking wait.
+static inline hipError_t cg_stream_wait(hipStream_t s) {
+#ifdef CG_SPIN_SYNC
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    (void)hipGetLastError();   // the polls' not-ready status is not an error
+    return e;
+#else
+    return hipStreamSynchronize(s);
+#endif
+}
+
 #ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
 #endif

@@ -1633,7 +1633,7 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
     uint32_t hstack[LG_META_WORDS];
     uint32_t* const hm = S.hmeta ? S.hmeta : hstack;   // pinned when the handle has one
     if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if ((e = cg_stream_wait(s)) != hipSuccess) return e;
     const uint32_t Ms = hm[LG_MS];
     if (K == CG_K_FROM_META) K = hm[LG_K];   // pipeline frames: the ground stage's kept count
     const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
@@ -1861,7 +1861,7 @@ int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     uint32_t hstack[LG_META_WORDS];
     uint32_t* const hm = S.hmeta ? S.hmeta : hstack;
     if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if ((e = cg_stream_wait(s)) != hipSuccess) return e;
     const uint32_t Mtot = n + npad_local;
     *n_vox = 0;
     if (Mtot == 0) return hipSuccess;
@@ -1884,7 +1884,7 @@ int cg_halo_local_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_halo_records, dim3(vb), dim3(CG_BLOCK), 0, s, S, buf, PB, d_rec, cap);
     if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if ((e = cg_stream_wait(s)) != hipSuccess) return e;
     *n_vox = hm[LG_V];
     return hipGetLastError();
 }
