@@ -96,7 +96,15 @@ def main():
     backend = os.environ.get("CG_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # --scatter at one rank: a world-size-1 RCCL group with collectives forced on, so the C4
+    # scatter/gather runs under RCCL on a one-GPU box too
+    solo_pg = world == 1 and args.scatter
+    if solo_pg:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or solo_pg:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -105,6 +113,9 @@ def main():
     dev = torch.device("cuda", local)
 
     import cones_perception_amd as cp
+    if solo_pg:
+        from cones_perception_amd import dist as cd0
+        cd0.force_collectives(True)
     params = cp.load_params("simulation")
     F, N = args.frames, args.rings * args.cols
     # each rank owns frames [rank*F, (rank+1)*F): distinct synthetic scenes per rank
@@ -188,7 +199,7 @@ def main():
                          around=lambda: [step(i) for i in range(1, S)], tag="loaded")
 
     scatter = None
-    if world > 1 and (args.scatter or not args.no_scatter):
+    if args.scatter or (world > 1 and not args.no_scatter):
         scatter = scatter_composition(cp, cd, engines[0], streams[0], raw, F, N, dev, rank, world, args.steps)
 
     # C5's frame shape on this GPU: by default at N=1 (no collective involved; a failure is
@@ -283,19 +294,24 @@ def main():
         if scatter is not None:
             line["c4_scatter_gather"] = scatter
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or solo_pg:
         dist.destroy_process_group()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def launch_ranks(n, dry_run):
     """Start `n` rank processes of this script under torch.distributed.run on this node
     (rendezvous on 127.0.0.1) and return their exit code. Called before any GPU call."""
-    import socket
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = free_port()
     env = dict(os.environ)
     if dry_run:
         env["CG_DIST_BACKEND"] = "gloo"
@@ -474,13 +490,19 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
     el = cd.max_over_ranks(time.perf_counter() - t0, dev)
     # the root's egress: every peer's share of the batch leaves over that peer's direct link
     egress = float(F * (world - 1) * raw.shape[1])
-    ach = egress / (el / steps) / 1e9
-    peak = XGMI_LINK_GBS * min(world - 1, 7)
-    return {"frames_per_s": F * world * steps / el, "ms_per_step": el / steps * 1e3,
-            "roofline": {"bound": "xgmi", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
-                         "bytes_per_step": egress,
-                         "peak_basis": f"root egress over {min(world - 1, 7)} direct xGMI links x {XGMI_LINK_GBS} GB/s"},
-            "includes": "RCCL scatter of the batch from rank 0, processing, gather of headers"}
+    out = {"frames_per_s": F * world * steps / el, "ms_per_step": el / steps * 1e3,
+           "backend": dist.get_backend(), "ranks": world,
+           "includes": "RCCL scatter of the batch from rank 0, processing, gather of headers"}
+    if world > 1:
+        ach = egress / (el / steps) / 1e9
+        peak = XGMI_LINK_GBS * min(world - 1, 7)
+        out["roofline"] = {"bound": "xgmi", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
+                           "bytes_per_step": egress,
+                           "peak_basis": f"root egress over {min(world - 1, 7)} direct xGMI links x {XGMI_LINK_GBS} GB/s"}
+    else:   # one rank: the scatter is the root's own share, a device-local copy through RCCL
+        out["roofline"] = None
+        out["note"] = "world size 1 with collectives forced on: RCCL scatter/gather executed, no xGMI traffic"
+    return out
 
 
 def c5_single_gpu(cp, params, device, reps=50, order=None):

@@ -48,12 +48,17 @@ def build(verbose=False, force=False):
     if force or _stale(o, [src] + HEADERS):
         _run(["gcc", "-O2", "-fPIC", "-ffp-contract=off", "-std=c11", "-Wall", "-c", src, "-o", o], verbose)
     objs.append(o)
+    jobs = []
     for name in ("cg_kernels.hip", "cg_large.hip", "cg_recrop.hip", "cg_colornet.hip", "cg_api.cpp", "cg_track.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(OBJ, name.rsplit(".", 1)[0] + ".o")
         if force or _stale(o, [src] + HEADERS):
-            _run([HIPCC, "-x", "hip", *HIP_FLAGS, "-c", src, "-o", o], verbose)
+            jobs.append([HIPCC, "-x", "hip", *HIP_FLAGS, "-c", src, "-o", o])
         objs.append(o)
+    if jobs:   # the translation units compile independently (hipcc is single-threaded)
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(min(len(jobs), max(1, (os.cpu_count() or 1)))) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or _stale(LIB, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB, *objs, "-lpthread"], verbose)
     return LIB

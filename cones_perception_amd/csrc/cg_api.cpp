@@ -355,6 +355,16 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
     }
 }
 
+// The large-path scratch with the diagnostic route's settings applied: every entry point
+// that runs the large backend takes its copy from here, so a route set (or cleared) by
+// cg_debug_route reaches the tile and halo protocols too, whatever ran last.
+LgScratch route_scratch(cg_handle* h) {
+    LgScratch S = h->lg;
+    S.force_global = (h->route == 2 || h->route == 5) ? 1u : 0u;
+    S.pcl_levels_cap = h->route == 5 ? 1u : 0u;
+    return S;
+}
+
 int ensure_large(cg_handle* h, uint32_t n) {
     if (n <= h->large_points && h->d_large) return CG_OK;
     if (h->d_large) (void)hipFree(h->d_large);
@@ -383,10 +393,8 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
     }
     int rc = ensure_large(h, L.n_points);
     if (rc) return rc;
-    h->lg.force_global = (h->route == 2 || h->route == 5) ? 1u : 0u;
-    h->lg.pcl_levels_cap = h->route == 5 ? 1u : 0u;
     L.stamps = nullptr;
-    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, h->lg, s));
+    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s));
     return CG_OK;
 }
 
@@ -854,7 +862,7 @@ int cg_tile_front(cg_handle* h, const cg_tile* t, uint32_t* keys) {
     if (rc) return rc;
     h->tile = *t;
     CgLaunch L = tile_launch(*t);
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = t->first;
     HIPCHK((hipError_t)cg_large_front(L, h->dp, CG_KMODE_PIPELINE, S, h->stream, 0, true));
     HIPCHK(hipMemcpyAsync(keys, S.meta + LG_SECKEY, CG_TILE_KEYS * 4, hipMemcpyDeviceToHost, h->stream));
@@ -867,7 +875,7 @@ int cg_tile_decide(cg_handle* h, const uint32_t* merged_keys, uint32_t* counts) 
     if (!h || !merged_keys || !counts) return fail(CG_E_INVALID, "null argument");
     if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_decide before cg_tile_front");
     HIPCHK(hipSetDevice(h->device));
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = h->tile.first;
     HIPCHK(hipMemcpyAsync(S.meta + LG_SECKEY, merged_keys, CG_TILE_KEYS * 4, hipMemcpyHostToDevice, h->stream));
     CgLaunch L = tile_launch(h->tile);
@@ -914,7 +922,7 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
     if (rc) return rc;
     rc = ensure_batch(h, 1, n_total, false);
     if (rc) return rc;
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = 0;
     S.force_global = h->route == 2 ? 1u : 0u;
     HIPCHK((hipError_t)cg_large_set_survivors(S, h->dp, d_points, d_index, n_survivors, merged_counts, h->stream));
@@ -953,7 +961,7 @@ int cg_tile_front_async(cg_handle* h, const cg_tile* t, uint32_t* d_keys, void* 
     if ((rc = ensure_large(h, std::max<uint32_t>(t->n, 1)))) return rc;
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     h->tile = *t;
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = t->first;
     HIPCHK((hipError_t)cg_large_front(tile_launch(*t), h->dp, CG_KMODE_PIPELINE, S, s, 0, true));
     HIPCHK(hipMemcpyAsync(d_keys, S.meta + LG_SECKEY, CG_TILE_KEYS * 4, hipMemcpyDeviceToDevice, s));
@@ -966,7 +974,7 @@ int cg_tile_decide_async(cg_handle* h, const uint32_t* d_merged_keys, uint32_t* 
     if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_decide_async before cg_tile_front_async");
     HIPCHK(hipSetDevice(h->device));
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = h->tile.first;
     HIPCHK(hipMemcpyAsync(S.meta + LG_SECKEY, d_merged_keys, CG_TILE_KEYS * 4, hipMemcpyDeviceToDevice, s));
     HIPCHK((hipError_t)cg_large_decide(tile_launch(h->tile), h->dp, S, s, 0));
@@ -998,7 +1006,7 @@ int cg_tile_backend_own(cg_handle* h, uint32_t n_total, void* hip_stream) {
     int rc = ensure_batch(h, 1, n_total, false);
     if (rc) return rc;
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = 0;
     S.force_global = h->route == 2 ? 1u : 0u;
     CgLaunch L{};
@@ -1072,7 +1080,7 @@ int cg_halo_local(cg_handle* h, const cg_halo_plan* plan, const float* d_points,
     if (!rc) rc = ensure_large(h, n_total);
     if (!rc) rc = ensure_batch(h, 1, n_total, false);
     if (rc) return rc;
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = 0;
     CgLaunch L{};
     L.n_frames = 1;
@@ -1115,7 +1123,7 @@ int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec,
     if (!rc) rc = ensure_large(h, n_total);
     if (!rc) rc = ensure_batch(h, 1, n_total, false);
     if (rc) return rc;
-    LgScratch S = h->lg;
+    LgScratch S = route_scratch(h);
     S.pidx_base = 0;
     CgLaunch L{};
     L.n_frames = 1;

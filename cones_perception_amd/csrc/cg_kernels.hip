@@ -69,6 +69,10 @@ struct BackLds {
 };
 #define SMEM_BYTES (FRONT_BYTES + sizeof(BackLds))
 static_assert(SMEM_BYTES <= 163840, "LDS budget");
+// pcl_index_vector keeps a 2,048-word point bitmap and its 2,048-word prefix in VOX
+static_assert(sizeof(((BackLds*)nullptr)->VOX) >= 4096 * sizeof(uint32_t), "VOX holds the index_vector bitmap");
+// the LDS PCL sort (pcl_sort<2, true>) covers at most two records per thread
+static_assert(CG_MMAX <= 2 * CG_BLOCK, "LDS backend capacity within pcl_block_sort<2>");
 #ifndef CG_CODES_HBM
 static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overlay must fit");
 #endif
@@ -651,14 +655,20 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
             uint8_t* dst = (uint8_t*)L.in + b0;
             const uint8_t* src = L.in_host + b0;
             const uint64_t n16 = nb / 16;
+            // four 16-byte reads in flight per lane; named registers (an array with
+            // conditional elements was kept in scratch)
+            const uint4* s4 = (const uint4*)src;
+            uint4* d4 = (uint4*)dst;
             for (uint64_t i = tid; i < n16; i += CG_BLOCK * 4) {
-                uint4 v[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (i + (uint64_t)u * CG_BLOCK < n16) v[u] = ((const uint4*)src)[i + (uint64_t)u * CG_BLOCK];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (i + (uint64_t)u * CG_BLOCK < n16) ((uint4*)dst)[i + (uint64_t)u * CG_BLOCK] = v[u];
+                const uint64_t i1 = i + CG_BLOCK, i2 = i + 2 * CG_BLOCK, i3 = i + 3 * CG_BLOCK;
+                const uint4 v0 = s4[i];
+                const uint4 v1 = s4[i1 < n16 ? i1 : i];
+                const uint4 v2 = s4[i2 < n16 ? i2 : i];
+                const uint4 v3 = s4[i3 < n16 ? i3 : i];
+                d4[i] = v0;
+                if (i1 < n16) d4[i1] = v1;
+                if (i2 < n16) d4[i2] = v2;
+                if (i3 < n16) d4[i3] = v3;
             }
             for (uint64_t i = n16 * 16 + 4 * (uint64_t)tid; i < nb; i += 4 * CG_BLOCK)
                 *(uint32_t*)(dst + i) = *(const uint32_t*)(src + i);

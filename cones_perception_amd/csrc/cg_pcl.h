@@ -527,7 +527,7 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
 // PCL_BLOCK_MAX elements: pcl_block_sort (scratch W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD; red
 // for the counts). Longer arrays (the HBM-scratch backend, large-frame leaves in HBM): block
 // levels over W.A (prefix, n + 1), W.PAR / W.CNT (L and R lists), W.UK (range of each
-// position), W.ORD (flags), W.LAB (size | depth << 20 at each range's first), W.OFF (pivot,
+// position), W.ORD (flags), W.LAB (size | depth << 26 at each range's first), W.OFF (pivot,
 // later last), KEY as words (s, later cut), until every range is at most PCL_BLOCK_MAX; those
 // are then sorted one after another by pcl_block_sort. Every thread calls it; ends with a
 // barrier.
@@ -576,19 +576,26 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         PCL_STAMP();
         return;
     }
-    const bool big = true;
+    // INFO at a range's first: size (26 bits) | depth budget << 26 (2 lg n <= 62)
+    constexpr uint32_t ISZ = (1u << 26) - 1u;
+    // per position, the exclusive counts of >= pivot and of <= pivot elements before it: two
+    // 16-bit halves of one scan word while n < 65,536 (no carry between the halves); longer
+    // arrays (a large frame's leaf in HBM) scan them separately, the <= counts in KEY's words
+    // [n, 2n), which are free until the sorted records land in KEY after the levels
+    const bool wide = n > 0xffffu;
+    uint32_t* const PRL = SC + n;
     for (uint32_t i = tid; i < n; i += CG_BLOCK) {
-        RID[i] = big ? 0u : PCL_INACT;
+        RID[i] = 0u;
         FLG[i] = i == 0 ? PCL_HEAD : 0u;
     }
-    if (tid == 0 && n) INFO[0] = n | (d0 << 20);
+    if (tid == 0 && n) INFO[0] = n | (d0 << 26);
     __syncthreads();
-    bool any = big;
+    bool any = n > 0;
     while (any) {
         // (1) per range: depth budget, heapsort fallback or median of three to first
         for (uint32_t i = tid; i < n; i += CG_BLOCK) {
             if (RID[i] != i) continue;
-            const uint32_t size = INFO[i] & 0xfffffu, depth = INFO[i] >> 20, last = i + size;
+            const uint32_t size = INFO[i] & ISZ, depth = INFO[i] >> 26, last = i + size;
             if (depth == 0) {
                 cg_heap_sort_range(E + i, (long)size, [](uint64_t a, uint64_t b) { return pcl_key(a) < pcl_key(b); });
                 for (uint32_t j = i; j < last; j++) { FLG[j] |= PCL_HEAP; RID[j] = PCL_INACT; }
@@ -598,32 +605,45 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
             cg_move_median_to_first(E, (long)i, (long)i + 1, (long)mid, (long)last - 1,
                                     [](uint64_t a, uint64_t b) { return pcl_key(a) < pcl_key(b); });
             PIV[i] = pcl_key(E[i]);
-            INFO[i] = size | ((depth - 1u) << 20);
+            INFO[i] = size | ((depth - 1u) << 26);
             SC[i] = 0u;
         }
         __syncthreads();
-        // (2) counts of >= pivot (low half) and <= pivot (high half) before each position;
-        // the total (the count before position n) stays on chip: the word after the array is
-        // the next range's first word when leaves of one frame run side by side in HBM
-        const uint32_t ptot = block_scan(
-            n,
-            [&](uint32_t i) -> uint32_t {
-                const uint32_t r = RID[i];
-                if (r == PCL_INACT || r == i) return 0u;
-                const uint32_t k = pcl_key(E[i]), p = PIV[r];
-                return (k >= p ? 1u : 0u) | (k <= p ? 0x10000u : 0u);
-            },
-            [&](uint32_t i, uint32_t e) { PRE[i] = e; }, red);
+        // (2) counts of >= pivot and <= pivot before each position; the totals (the counts
+        // before position n) stay on chip: the word after the array is the next range's first
+        // word when leaves of one frame run side by side in HBM
+        auto is_ge = [&](uint32_t i) -> bool {
+            const uint32_t r = RID[i];
+            return r != PCL_INACT && r != i && pcl_key(E[i]) >= PIV[r];
+        };
+        auto is_le = [&](uint32_t i) -> bool {
+            const uint32_t r = RID[i];
+            return r != PCL_INACT && r != i && pcl_key(E[i]) <= PIV[r];
+        };
+        uint32_t totg, totl;
+        if (!wide) {
+            const uint32_t ptot = block_scan(
+                n, [&](uint32_t i) -> uint32_t { return (is_ge(i) ? 1u : 0u) | (is_le(i) ? 0x10000u : 0u); },
+                [&](uint32_t i, uint32_t e) { PRE[i] = e; }, red);
+            totg = ptot & 0xffffu;
+            totl = ptot >> 16;
+        } else {
+            totg = block_scan(n, [&](uint32_t i) -> uint32_t { return is_ge(i) ? 1u : 0u; },
+                              [&](uint32_t i, uint32_t e) { PRE[i] = e; }, red);
+            totl = block_scan(n, [&](uint32_t i) -> uint32_t { return is_le(i) ? 1u : 0u; },
+                              [&](uint32_t i, uint32_t e) { PRL[i] = e; }, red);
+        }
         __syncthreads();
-        auto pre = [&](uint32_t i) -> uint32_t { return i < n ? PRE[i] : ptot; };
+        auto preg = [&](uint32_t i) -> uint32_t { return i < n ? (wide ? PRE[i] : PRE[i] & 0xffffu) : totg; };
+        auto prel = [&](uint32_t i) -> uint32_t { return i < n ? (wide ? PRL[i] : PRE[i] >> 16) : totl; };
         // (3) L and R lists of every range, stored from first + 1
         for (uint32_t i = tid; i < n; i += CG_BLOCK) {
             const uint32_t r = RID[i];
             if (r == PCL_INACT || r == i) continue;
-            const uint32_t last = r + (INFO[r] & 0xfffffu), lo = pre(r + 1);
+            const uint32_t last = r + (INFO[r] & ISZ);
             const uint32_t k = pcl_key(E[i]), p = PIV[r];
-            if (k >= p) PL[r + 1 + (PRE[i] & 0xffffu) - (lo & 0xffffu)] = i;
-            if (k <= p) PR[r + 1 + (pre(last) >> 16) - (pre(i + 1) >> 16)] = i;
+            if (k >= p) PL[r + 1 + preg(i) - preg(r + 1)] = i;
+            if (k <= p) PR[r + 1 + prel(last) - prel(i + 1)] = i;
         }
         __syncthreads();
         // (4) swap pairs (L_k, R_k) while L_k < R_k, by the thread at L_k; the last one
@@ -632,10 +652,10 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
             const uint32_t r = RID[i];
             if (r == PCL_INACT || r == i) continue;
             // >= pivot from the counts, not from E: other threads are swapping elements
-            if (((pre(i + 1) - PRE[i]) & 0xffffu) == 0u) continue;
-            const uint32_t last = r + (INFO[r] & 0xfffffu), lo = pre(r + 1), hiw = pre(last);
-            const uint32_t nL = (hiw & 0xffffu) - (lo & 0xffffu), nR = (hiw >> 16) - (lo >> 16);
-            const uint32_t k = (PRE[i] & 0xffffu) - (lo & 0xffffu);
+            if (preg(i + 1) == preg(i)) continue;
+            const uint32_t last = r + (INFO[r] & ISZ);
+            const uint32_t nL = preg(last) - preg(r + 1), nR = prel(last) - prel(r + 1);
+            const uint32_t k = preg(i) - preg(r + 1);
             const bool c0 = k < nR && i < PR[r + 1 + k];
             const bool c1 = k + 1 < nL && k + 1 < nR && PL[r + 2 + k] < PR[r + 2 + k];
             if (c0) {
@@ -650,16 +670,15 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         // (5) per range: the cut, the two children (active while longer than 64)
         for (uint32_t i = tid; i < n; i += CG_BLOCK) {
             if (RID[i] != i) continue;
-            const uint32_t size = INFO[i] & 0xfffffu, dep = INFO[i] >> 20, last = i + size;
-            const uint32_t lo = pre(i + 1), hiw = pre(last);
-            const uint32_t nL = (hiw & 0xffffu) - (lo & 0xffffu);
+            const uint32_t size = INFO[i] & ISZ, dep = INFO[i] >> 26, last = i + size;
+            const uint32_t nL = preg(last) - preg(i + 1);
             const uint32_t sw = SC[i];
             uint32_t cut;
             if (sw == 0) cut = PL[i + 1];
             else cut = min(sw < nL ? PL[i + 1 + sw] : 0xffffffffu, PR[i + sw]);
             FLG[cut] |= PCL_HEAD;
-            INFO[i] = (cut - i) | (dep << 20);
-            INFO[cut] = (last - cut) | (dep << 20);
+            INFO[i] = (cut - i) | (dep << 26);
+            INFO[cut] = (last - cut) | (dep << 26);
             PIV[i] = last;
             SC[i] = cut;
         }
@@ -686,10 +705,10 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
     const uint32_t ncur = block_scan(
         n,
         [&](uint32_t i) -> uint32_t {
-            return (FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD && (INFO[i] & 0xfffffu) > CG_SORT_THRESHOLD ? 1u : 0u;
+            return (FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD && (INFO[i] & ISZ) > CG_SORT_THRESHOLD ? 1u : 0u;
         },
         [&](uint32_t i, uint32_t e) {
-            if ((FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD && (INFO[i] & 0xfffffu) > CG_SORT_THRESHOLD) CUR[e] = i;
+            if ((FLG[i] & (PCL_HEAD | PCL_HEAP)) == PCL_HEAD && (INFO[i] & ISZ) > CG_SORT_THRESHOLD) CUR[e] = i;
         },
         red);
     for (uint32_t i = tid; i < n; i += CG_BLOCK) {
@@ -698,7 +717,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         uint32_t s0 = i;   // the range's first, if within 16 positions
         while (!(FLG[s0] & PCL_HEAD) && s0 + CG_SORT_THRESHOLD > i) s0--;
         if (!(FLG[s0] & PCL_HEAD)) continue;
-        const uint32_t size = INFO[s0] & 0xfffffu;
+        const uint32_t size = INFO[s0] & ISZ;
         if (size > CG_SORT_THRESHOLD) continue;   // a task
         const uint32_t ki = pcl_key(ri);
         uint32_t rank = 0;
@@ -713,7 +732,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
     // tasks, one after another: each range by the whole workgroup, scratch at its own positions
     for (uint32_t q = 0; q < ncur; q++) {
         const uint32_t first = CUR[q];
-        const uint32_t size = INFO[first] & 0xfffffu, depth = INFO[first] >> 20;
+        const uint32_t size = INFO[first] & ISZ, depth = INFO[first] >> 26;
         __syncthreads();   // every thread has the range before pcl_block_sort rewrites INFO[first]
         pcl_block_sort<PMAX, PbGen>(E + first, PbStore<uint64_t*>{KEY + first}, size, depth,
                                     PbScratch<PbGen>{(uint32_t*)W.LAB + first, W.OFF + first, W.A + first,

@@ -13,6 +13,17 @@ import torch
 import torch.distributed as dist
 
 
+# Collectives run even at world size 1 when forced (CG_FORCE_COLLECTIVES=1 or
+# force_collectives()): one rank under RCCL then exercises every device-tensor collective of
+# the multi-GPU paths on a one-GPU box (tests/test_gpu_rccl.py, bench.py --scatter).
+_FORCE = os.environ.get("CG_FORCE_COLLECTIVES", "0") == "1"
+
+
+def force_collectives(on: bool = True) -> None:
+    global _FORCE
+    _FORCE = bool(on)
+
+
 def world():
     return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), \
         int(os.environ.get("LOCAL_RANK", "0"))
@@ -24,7 +35,7 @@ def frame_range(rank: int, frames_per_rank: int) -> range:
 
 
 def max_over_ranks(value: float, device) -> float:
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _distributed():
         return value
     t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -63,7 +74,7 @@ def tile_range(n_total: int, rank: int, world_size: int):
 
 
 def _distributed() -> bool:
-    return dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_initialized() and (dist.get_world_size() > 1 or _FORCE)
 
 
 def _coll_device(device):
@@ -235,7 +246,8 @@ def _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step,
     from . import _abi
     lib, h = _abi.lib(), engine.handle
     st = _tile_stream(engine, device)
-    st.wait_stream(torch.cuda.current_stream(device))   # the tile's points
+    caller = torch.cuda.current_stream(device)
+    st.wait_stream(caller)   # the tile's points
     s = st.cuda_stream
     with torch.cuda.stream(st):
         t = _abi.cg_tile(d_tile_ptr, first, n, n_total, point_step, *offsets)
@@ -246,6 +258,9 @@ def _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step,
         _abi.check(lib.cg_tile_decide_async(h, merged.data_ptr(), counts.data_ptr(), s))
         if not _distributed():
             _abi.check(lib.cg_tile_backend_own(h, n_total, s))
+            # the caller's stream waits for the frame: its tile buffer and the handle's
+            # outputs are safe to reuse or read there once this returns (fetch=False)
+            caller.wait_stream(st)
             return engine.fetch(0) if fetch else True
         total, sizes = merge_tile_counts_dev(counts, device)
         ns = sizes[dist.get_rank()]
@@ -313,7 +328,7 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     slab = slab[:ns]
     # survivors to their slab's rank; sources hold ascending frame-index ranges, so every rank
     # receives its slab's survivors in frame-index order
-    if ws > 1:
+    if _distributed():
         rows = torch.cat([sp, si.view(torch.float32).unsqueeze(1)], 1)
         got = _split_exchange(rows, slab, ws, device)
         mp_, mi = got[:, :4].contiguous(), got[:, 4].contiguous().view(torch.int32)
@@ -333,7 +348,7 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     top = rec[col >= lo + plan.slab_w - plan.band].contiguous()    # own side of the upper edge
     low = rec[col < lo + plan.band].contiguous()                   # halo for the slab below
     halo = torch.empty((0, _abi.CG_HALO_REC_WORDS), dtype=torch.int32, device=device)
-    if ws > 1:
+    if _distributed():
         counts = _all_gather_ints([int(rec.shape[0]), int(low.shape[0])], device)
         cd = _coll_device(device)
         ops = []
@@ -361,7 +376,7 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     last_halo_stats.update(slabs=int(plan.slabs), slab_w=int(plan.slab_w), band=int(plan.band), survivors=n,
                            voxels=int(rec.shape[0]), halo_sent=int(low.shape[0]) if 0 < rank < plan.slabs else 0,
                            halo_received=int(halo.shape[0]), pairs=int(pairs.shape[0]))
-    if ws > 1:
+    if _distributed():
         sizes = _all_gather_ints([int(rec.shape[0]), int(pairs.shape[0])], device)
         vmax = max(1, max(s[0] for s in sizes))
         pmax = max(1, max(s[1] for s in sizes))

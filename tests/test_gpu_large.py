@@ -142,3 +142,20 @@ def test_pcl_sort_leaves_in_hbm(params, rings, cols, clutter):
     ref, _ = O.run(params, msg, O.MODE_PIPELINE)
     assert got.n_filtered > 2 * 4096
     assert_same_detection(got, ref, f"route 5 {rings}x{cols}")
+
+
+def test_pcl_sort_hbm_leaves_beyond_16_bit_counts(params):
+    """cg_debug_route 5 on the detector's C5 frame (~550k filtered points): one partition level
+    leaves two halves of ~275k records, each finished in HBM by one workgroup. Past 65,535
+    records the >= / <= pivot counts no longer fit two 16-bit halves of one scan word; the HBM
+    form scans them separately there (cg_pcl.h pcl_sort), so the order stays std::sort's."""
+    msg = _frame(128, 8192, frame=0, clutter=60, cpr=12)
+    det = cp.ConeDetector(params)
+    det.debug_route(5)
+    got = det.cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_DETECT)
+    assert ref.n_filtered > 2 * 65536 + 4096
+    assert_same_detection(got, ref, "C5 detect route 5")
+    det.debug_route(0)    # the route cleared: the next frame takes every partition level again
+    got = det.cloud_handler(msg)
+    assert_same_detection(got, ref, "C5 detect after route 5")

@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 import cones_perception_amd as cp
 import oracle_py as O
 from cones_perception_amd import Detection
-from helpers import assert_same_detection
+from helpers import assert_same_detection, assert_same_cluster_sets
 
 pytestmark = pytest.mark.gpu
 
@@ -94,6 +94,9 @@ def test_tiled_frame_matches_oracle(tmp_path, world, rings, cols, over, halo, mu
     ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_STABLE if halo else O.ORDER_PCL)
     assert got.n_points == rings * cols
     assert_same_detection(got, ref, f"tiled x{world} halo={halo}")
+    if halo:   # the north star's bar against PCL's own voxel order: same cluster sets, centroids within 1e-5 m
+        pcl, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_PCL)
+        assert_same_cluster_sets(got, pcl, f"tiled x{world} halo vs ORDER_PCL")
     if mutate == "passthrough":
         assert got.flags & 1                                    # PCL's guard: voxel cloud = input
     if halo and mutate != "passthrough":
@@ -122,6 +125,9 @@ def test_tiled_single_rank_matches_oracle(halo):
                              halo=halo)
     ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_STABLE if halo else O.ORDER_PCL)
     assert_same_detection(got, ref, "tiled x1")
+    if halo:
+        pcl, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE, O.ORDER_PCL)
+        assert_same_cluster_sets(got, pcl, "tiled x1 halo vs ORDER_PCL")
 
 
 def test_tile_async_argument_checks():

@@ -5,7 +5,14 @@ Two out-of-line device calls in this code base preceded failures that were never
 ("Lessons"): an exact atan2f called from divergent loops (run-to-run keep-word
 changes) and a non-inlined single-wave sort taking a struct through scratch (a GPU memory
 fault in a probe). Every device function on the path is force-inlined instead; this test keeps
-it that way."""
+it that way.
+
+The metadata check goes further: no kernel of the library may use scratch at all (private
+segment size 0, no dynamic stack), so no dispatch of ours depends on the runtime provisioning
+per-lane scratch. DESIGN.md ("Lessons") records what a rebuilt out-of-line probe shows: a
+VGPR value passed by reference lives in the private segment and the callee reaches it with
+flat loads through the private aperture.
+"""
 import os
 import subprocess
 
@@ -17,7 +24,8 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
-def _disassembly(tmp_path):
+def _code_objects(tmp_path):
+    """The gfx950 code objects of the library's fat binary, one per HIP translation unit."""
     fat = tmp_path / "fat.bin"
     subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", LIB, str(tmp_path / "x.so")],
                    check=True)
@@ -34,9 +42,35 @@ def _disassembly(tmp_path):
         co = tmp_path / f"c{k}.co"
         subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={b}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-        out.append(subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(co)], capture_output=True, text=True,
-                                  check=True).stdout)
+        out.append(co)
     return out
+
+
+def _disassembly(tmp_path):
+    return [subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(co)], capture_output=True, text=True,
+                           check=True).stdout for co in _code_objects(tmp_path)]
+
+
+def _kernel_metadata(tmp_path):
+    """(name, {key: value}) per kernel, from each code object's AMDGPU metadata note."""
+    kernels = []
+    for co in _code_objects(tmp_path):
+        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], capture_output=True, text=True,
+                               check=True).stdout
+        cur = None
+        for line in notes.splitlines():
+            t = line.strip()
+            if t.startswith("- .agpr_count:"):       # first key of each kernel's map
+                cur = {}
+                kernels.append(cur)
+            if cur is not None and t.startswith(".") and ":" in t:
+                k, v = t.split(":", 1)
+                if v.strip():
+                    cur[k.strip()] = v.strip()
+            elif cur is not None and t.startswith("- .") and ":" in t:
+                k, v = t[2:].split(":", 1)
+                cur.setdefault(k.strip(), v.strip())
+    return [(k.get(".name"), k) for k in kernels]
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
@@ -52,3 +86,14 @@ def test_no_out_of_line_calls_in_device_code(tmp_path):
                 kernels += 1
             assert "s_swappc_b64" not in line, f"out-of-line call in {fn}: {line.strip()}"
     assert kernels > 50
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_no_kernel_uses_scratch(tmp_path):
+    kernels = _kernel_metadata(tmp_path)
+    assert len(kernels) > 50
+    bad = [(n, m.get(".private_segment_fixed_size"), m.get(".uses_dynamic_stack"), m.get(".vgpr_spill_count"))
+           for n, m in kernels
+           if m.get(".private_segment_fixed_size") != "0" or m.get(".uses_dynamic_stack") != "false"
+           or m.get(".vgpr_spill_count", "0") != "0"]
+    assert not bad, f"kernels with scratch (private segment, dynamic stack, VGPR spills): {bad}"
