@@ -18,7 +18,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
-HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h", "cg_device.h", "cg_pcl.h")] + \
+HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h", "cg_device.h", "cg_pcl.h",
+                                            "cg_backend.h")] + \
           [os.path.join(ROOT, "include", "cones_gpu.h")]
 
 
@@ -55,6 +56,12 @@ def build(verbose=False, force=False):
         if force or _stale(o, [src] + HEADERS):
             jobs.append([HIPCC, "-x", "hip", *HIP_FLAGS, "-c", src, "-o", o])
         objs.append(o)
+    # the backend launch of batch frames: the same device code at 256 threads per workgroup
+    src = os.path.join(CSRC, "cg_back.hip")
+    o = os.path.join(OBJ, "cg_back.o")
+    if force or _stale(o, [src, os.path.join(CSRC, "cg_backend.h")] + HEADERS):
+        jobs.append([HIPCC, "-x", "hip", *HIP_FLAGS, "-DCG_BLOCK=256", "-c", src, "-o", o])
+    objs.append(o)
     if jobs:   # the translation units compile independently (hipcc is single-threaded)
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(min(len(jobs), max(1, (os.cpu_count() or 1)))) as ex:

@@ -388,7 +388,7 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
         return CG_OK;
     }
     if (!large) {
-        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s));
+        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s, h->route == 6));
         return CG_OK;
     }
     int rc = ensure_large(h, L.n_points);
@@ -1223,7 +1223,7 @@ int cg_debug_launch_span(cg_handle* h, void* d_span) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 5) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 6) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

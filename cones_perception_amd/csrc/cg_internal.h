@@ -215,7 +215,10 @@ int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScr
 // Bytes of HBM scratch one frame of n points needs for the global (non-LDS) path.
 uint64_t cg_scratch_bytes(uint32_t n_points);
 // Enqueue the batch kernel. Returns a hipError_t.
-int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
+// Batch frames of <= CG_MAX_POINTS points. Detector batches run as a front launch plus the
+// backend launch (cg_launch_back, cg_back.hip); `fused` keeps each frame in one workgroup.
+int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused = false);
+int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 // Cone re-crop (cg_recrop.hip): exact float form of the reference's double box compares.
 struct RcBox { float lox, hix, loy, hiy; };
 #define CG_RECROP_MAX_BOXES 256   // boxes per launch (more: several launches)

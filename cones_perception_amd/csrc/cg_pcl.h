@@ -60,15 +60,16 @@ __device__ unsigned int g_pcl_probe_n;
 __device__ __forceinline__ uint32_t pcl_key(uint64_t r) { return (uint32_t)(r >> 32); }
 
 // Records (idx << 32 | slot) of the Mf finite points of W.P in index_vector order -> E.
-// Kept survivors are slots [0, Ms) with point index W.IDX[slot] < 65536; zero pads are slots
-// [Ms, M). Uses W.VOX (bitmap, word prefix; then E) and W.ORD. Ends with a barrier.
+// Kept survivors are slots [0, Ms) with W.IDX[slot] < 32 * nbw (point indices of a 64k frame:
+// nbw = 2048; ranks in point order: fewer); zero pads are slots [Ms, M). Uses W.VOX (bitmap,
+// word prefix: 2 * nbw words; then E) and W.ORD. Ends with a barrier.
 template <class KF>
 __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint32_t Ms, uint64_t* E,
-                                                 uint32_t* red, KF voxel_idx) {
+                                                 uint32_t* red, uint32_t nbw, KF voxel_idx) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
-    uint32_t* BM = (uint32_t*)W.VOX;       // 2048 words: one bit per point index
-    uint32_t* WP = BM + 2048;              // exclusive popcount prefix per word
-    for (uint32_t i = tid; i < 2048; i += CG_BLOCK) BM[i] = 0u;
+    uint32_t* BM = (uint32_t*)W.VOX;       // nbw words: one bit per point index (or rank)
+    uint32_t* WP = BM + nbw;               // exclusive popcount prefix per word
+    for (uint32_t i = tid; i < nbw; i += CG_BLOCK) BM[i] = 0u;
     __syncthreads();
     for (uint32_t j = tid; j < Ms; j += CG_BLOCK) {
         const float4 p = W.P[j];
@@ -78,17 +79,21 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
         }
     }
     __syncthreads();
-    constexpr uint32_t PER = 2048 / CG_BLOCK;   // words per lane
-    uint32_t c[PER], sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) { c[k] = __popc(BM[tid * PER + k]); sum += c[k]; }
+    const uint32_t per = (nbw + CG_BLOCK - 1) / CG_BLOCK;   // consecutive words per lane
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t i = tid * per + k;
+        sum += i < nbw ? (uint32_t)__popc(BM[i]) : 0u;
+    }
     const uint32_t inc = wave_incl_scan(sum);
     if (l == 63) red[w] = inc;
     __syncthreads();
     uint32_t base = inc - sum;
     for (uint32_t v = 0; v < w; v++) base += red[v];
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) { WP[tid * PER + k] = base; base += c[k]; }
+    for (uint32_t k = 0; k < per; k++) {
+        const uint32_t i = tid * per + k;
+        if (i < nbw) { WP[i] = base; base += (uint32_t)__popc(BM[i]); }
+    }
     __syncthreads();
     uint32_t total = 0;
     for (uint32_t v = 0; v < WAVES; v++) total += red[v];   // finite kept survivors

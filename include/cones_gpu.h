@@ -358,7 +358,8 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * calls in one workgroup instead of the per-chunk split launch (3), or split with the input
  * copied by DMA instead of read by the kernel from pinned memory (4); the global backend with
  * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
- * are finished in HBM side by side (5); 0 = automatic. */
+ * are finished in HBM side by side (5); batch frames of <= 65,536 points in one fused
+ * workgroup per frame instead of the front launch + backend launch (6); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

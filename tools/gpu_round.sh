@@ -1,12 +1,16 @@
 #!/bin/bash
-# GPU: the round's evidence at HEAD: full -m gpu suite, smoke(), the default bench line (with the
-# CPU baseline), then tools/profile.sh (rocprofv3 kernel stats and PMC passes). Stops at the
-# first failing step.
-set -o pipefail
+# One GPU call: the -m gpu suite, then (unless the suite ended in a fault, abort, timeout or
+# hang) the default bench line and extra bench legs given as arguments.
+#   tools/gpu_round.sh TAG [bench args for an extra leg ...]
+# Outputs under gpurun_out/: TAG_gpu.log, TAG_bench.json/.err, TAG_extra.json/.err
+tag=${1:-r3}; shift
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 400 python bench.py > gpurun_out/bench_default.log 2>&1 || exit $?
-grep '^{' gpurun_out/bench_default.log | cut -c1-400
-bash tools/profile.sh
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/${tag}_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/${tag}_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "suite ended with rc=$rc: no further GPU steps"; exit $rc; fi
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || exit $?
+if [ $# -gt 0 ]; then
+  timeout -k 10 300 python bench.py "$@" > gpurun_out/${tag}_extra.json 2> gpurun_out/${tag}_extra.err || exit $?
+fi
+exit $rc
