@@ -8,9 +8,12 @@ batch. Frames are independent units: each rank processes its own batch (weak sca
 data-path collective); the timed region is bracketed by barrier + synchronize and the max
 over ranks is reported.
 
-The roofline object prices the dominant (only) kernel, cg_frame_kernel, by its algorithmic
-bytes B = 16 N + 20 V + 8 C + 64 per frame over its average duration from
-HIP events recorded on the launch stream. cpu_baseline times the CPU restatement
+The roofline object prices the dominant kernel by the algorithmic bytes B = 16 N + 20 V + 8 C
++ 64 per frame over its average execution span, which the kernel stamps itself
+(s_memrealtime: first workgroup start to last workgroup end, cg_debug_front_span). A batch is
+two launches on one stream: cg_front_kernel (pass 1, thresholds, pass 2, the survivors: every
+input byte) and cg_back_kernel (voxel grid, clustering, centroids on ~240 points per frame);
+the front is the dominant kernel, and the pair's span is reported beside it (step_span_ms). cpu_baseline times the CPU restatement
 (oracle/, single core, same frames) on a bounded sample on rank 0 (any N).
 
 `--gpus N` without a launcher environment starts N ranks itself (torch.distributed.run on
@@ -43,8 +46,8 @@ def main():
     ap.add_argument("--cols", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="threads of the frame-parallel CPU leg (the box's CPU share is 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the frame-parallel CPU leg (0: the process's CPU share, see cpu_share())")
     ap.add_argument("--single-frame", action="store_true",
                     help="also time C2 single-frame latency at N>1 (always at N=1)")
     ap.add_argument("--colornet", action="store_true",
@@ -153,14 +156,18 @@ def main():
     # each timed launch also stamps its own execution span (first workgroup start, last
     # workgroup end: what rocprofv3's kernel trace reports); events on a stream with queued
     # work also count the wait for CU slots behind the other streams' launches
-    spans = torch.zeros((args.steps, 2), dtype=torch.int64, device=dev)
+    # [step start, step end, front start, front end]: a detector batch is a front launch (all the
+    # frame streaming) and a backend launch on the same stream
+    spans = torch.zeros((args.steps, 4), dtype=torch.int64, device=dev)
     spans[:, 0] = 2 ** 63 - 1
+    spans[:, 2] = 2 ** 63 - 1
     torch.cuda.synchronize(dev)
     lib = cp.lib()
     t0 = time.perf_counter()
     for s in range(args.steps):
         st = streams[(counter[0]) % S]
         lib.cg_debug_launch_span(engines[counter[0] % S].handle, spans[s].data_ptr())
+        lib.cg_debug_front_span(engines[counter[0] % S].handle, spans[s, 2:].data_ptr())
         if not args.no_events:
             evs[s][0].record(st)
         step()
@@ -176,7 +183,10 @@ def main():
     avg_event_ms = sum(kern_ms) / len(kern_ms)
     sp = spans.cpu().numpy()
     spans_ok = bool((sp[:, 0] < 2 ** 63 - 1).all() and (sp[:, 1] > sp[:, 0]).all())
-    avg_kernel_ms = float((sp[:, 1] - sp[:, 0]).mean()) * 1e-5 if spans_ok else avg_event_ms   # 100 MHz ticks
+    step_span_ms = float((sp[:, 1] - sp[:, 0]).mean()) * 1e-5 if spans_ok else avg_event_ms   # 100 MHz ticks
+    front_ok = bool((sp[:, 2] < 2 ** 63 - 1).all() and (sp[:, 3] > sp[:, 2]).all())
+    split = front_ok   # front launch + backend launch (cg_debug_route 6: one fused kernel)
+    avg_kernel_ms = float((sp[:, 3] - sp[:, 2]).mean()) * 1e-5 if split else step_span_ms
 
     # algorithmic bytes of one launch, from the frames' own V and C
     res = engines[(counter[0] - 1) % S].results()
@@ -267,8 +277,12 @@ def main():
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),
-                         "kernel": "cg_frame_kernel", "avg_kernel_ms": avg_kernel_ms,
+                         "kernel": "cg_front_kernel" if split else "cg_frame_kernel",
+                         "avg_kernel_ms": avg_kernel_ms,
                          "avg_kernel_ms_source": "in-kernel span (s_memrealtime)" if spans_ok else "HIP events",
+                         # the step's device work: front launch start to backend launch end
+                         "step_span_ms": step_span_ms,
+                         "step_span_frac": bytes_per_launch / (step_span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "avg_launch_ms_events": avg_event_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          # launches on S streams overlap, so per-launch duration counts shared
@@ -318,6 +332,19 @@ def launch_ranks(n, dry_run):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
     return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_share():
+    """Threads for the all-core CPU leg and where the number comes from: OMP_NUM_THREADS when the
+    environment sets it (the GPU box exports its per-GPU CPU share there, 16, while nproc and the
+    affinity mask show every CPU of the machine), else the affinity mask."""
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return int(omp), "OMP_NUM_THREADS"
+    try:
+        return len(os.sched_getaffinity(0)), "sched_getaffinity"
+    except AttributeError:
+        return os.cpu_count() or 1, "os.cpu_count"
 
 
 def host_info():
@@ -679,8 +706,9 @@ def single_frame_latency(cp, params, raw, device, reps=200, order=None):
     dt = (time.perf_counter() - t0) / reps
     return {"latency_ms": dt * 1e3, "frames_per_s": 1.0 / dt,
             "includes": "C2: one 64k-point PointCloud2 in pageable host memory through the synchronous "
-                        "ConePipeline.cloud_handler (staging + PCIe H2D of 1 MiB, frame kernel, packed D2H "
-                        "of the results, Python result objects)"}
+                        "ConePipeline.cloud_handler (staging copy into pinned memory, the split kernel reading "
+                        "it over PCIe, its last workgroup writing the packed results into pinned host memory, "
+                        "one synchronisation, Python result objects)"}
 
 
 def cpu_baseline(cp, params, raw, budget_s, eng, threads, order=None):
@@ -712,6 +740,11 @@ def cpu_baseline(cp, params, raw, budget_s, eng, threads, order=None):
                      f"first {min(n, F)}), sequential, {el:.1f} s, oracle/cg_oracle.cpp "
                      "(g++ -O2 -ffp-contract=off)"}
     # frame-parallel: ctypes releases the GIL inside the oracle call
+    share, share_src = cpu_share()
+    if threads <= 0:
+        threads = share
+    else:
+        share_src = "--cpu-threads"
     nt = max(1, threads)
     cnt = [0]
     stop = time.perf_counter() + budget_s / 2
@@ -727,7 +760,7 @@ def cpu_baseline(cp, params, raw, budget_s, eng, threads, order=None):
     with ThreadPoolExecutor(nt) as ex:
         done = sum(ex.map(worker, range(nt)))
     el2 = time.perf_counter() - t1
-    out["all_cores"] = {"value": done / el2, "unit": "frames/s", "cores": nt,
+    out["all_cores"] = {"value": done / el2, "unit": "frames/s", "cores": nt, "cores_source": share_src,
                         "sample": f"{done} frames, {nt} threads, {el2:.1f} s"}
     # parity of the GPU batch against the same sample: bit for bit against the oracle in the
     # engine's voxel order; cluster index sets and centroids against PCL's order (ORDER_PCL)

@@ -161,6 +161,7 @@ _SIGS = {
     "cg_debug_stamps": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_debug_route": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_debug_launch_span": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "cg_debug_front_span": (C.c_int, [C.c_void_p, C.c_void_p]),
     "cg_debug_large_meta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_debug_large_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "cg_debug_stamps_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),

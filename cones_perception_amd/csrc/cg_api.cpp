@@ -185,6 +185,7 @@ struct cg_handle {
     LgScratch lg{};
     int route = 0;                // cg_debug_route
     unsigned long long* next_span = nullptr;   // cg_debug_launch_span
+    unsigned long long* next_front_span = nullptr;   // cg_debug_front_span
     cg_tile tile{};               // the rank's tile (cg_tile_front .. cg_tile_decide)
     bool tile_ready = false;
     // the last single-frame call, for cg_recrop
@@ -799,6 +800,8 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
     L.span = h->next_span;
     h->next_span = nullptr;
+    L.span_front = h->next_front_span;
+    h->next_front_span = nullptr;
     const int kmode = mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT;
     if (kmode == CG_KMODE_PIPELINE) L.seckeys = h->d_seckeys;   // per frame, for cg_batch_recrop
     rc = launch_frames(h, L, kmode, s);
@@ -1218,6 +1221,12 @@ int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
 int cg_debug_launch_span(cg_handle* h, void* d_span) {
     if (!h) return fail(CG_E_INVALID, "null handle");
     h->next_span = (unsigned long long*)d_span;
+    return CG_OK;
+}
+
+int cg_debug_front_span(cg_handle* h, void* d_span) {
+    if (!h) return fail(CG_E_INVALID, "null handle");
+    h->next_front_span = (unsigned long long*)d_span;
     return CG_OK;
 }
 

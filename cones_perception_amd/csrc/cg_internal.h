@@ -82,6 +82,9 @@ struct CgLaunch {
     // timing: [first workgroup start, last workgroup end] of the launch (s_memrealtime,
     // 100 MHz), or null (cg_debug_launch_span)
     unsigned long long* span;
+    // timing: [first front workgroup start, last front workgroup end] of a split batch's front
+    // launch (cg_debug_front_span), or null
+    unsigned long long* span_front;
     // split single-frame launch (cg_launch_split): CG_SPLIT_WORDS of state, or null
     uint32_t* split;
     // split launch: the frame's results also packed here (CG_PACK_WORDS) at the end, or null

@@ -112,6 +112,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     const uint32_t N = L.n_points;
     STAMP(0);
     if (L.span && tid == 0) atomicMin(&L.span[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (FRONT && L.span_front && tid == 0) atomicMin(&L.span_front[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
     init_rays<FILTER>(P, fs->rays, tid);
@@ -426,6 +427,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
                 rec[CG_FREC_BMIN + a] = fs->scal[S_BMIN0 + a];
                 rec[CG_FREC_BMAX + a] = fs->scal[S_BMAX0 + a];
             }
+            if (L.span_front) atomicMax(&L.span_front[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
         }
         return;
     }

@@ -351,6 +351,10 @@ int cg_debug_stamps(cg_handle* h, int enable);
  * start and the last workgroup's end, s_memrealtime ticks (100 MHz). One atomic per workgroup
  * at each end; frames of more than 65,536 points (large-frame path) do not record. */
 int cg_debug_launch_span(cg_handle* h, void* d_span);
+/* Timing: the next cg_run_batch call that runs as a front launch plus a backend launch (detector
+ * batches of <= 65,536-point frames) records the front launch's own span in d_span (2 x uint64,
+ * as above); cg_debug_launch_span then spans both launches (front start to backend end). */
+int cg_debug_front_span(cg_handle* h, void* d_span);
 int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
 
 /* Diagnostics: route every frame through the large-frame path (1), and also through its
