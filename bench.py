@@ -70,6 +70,9 @@ def main():
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
     ap.add_argument("--no-scatter", action="store_true", help="at N>1, skip the C4 scatter/gather leg")
+    ap.add_argument("--fused", action="store_true",
+                    help="experiment: each frame in one fused workgroup (cg_debug_route 6) instead of the front "
+                         "launch + backend launches")
     ap.add_argument("--voxel-order", choices=["pcl", "point"], default="pcl",
                     help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
                          "every voxel bit as the reference) or ascending point order")
@@ -132,6 +135,9 @@ def main():
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
     vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
     engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
+    if args.fused:
+        for e in engines:
+            e.debug_route(6)
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
     assert all(st.cuda_stream != 0 for st in streams)
     eng, stream = engines[0], streams[0]
@@ -274,6 +280,7 @@ def main():
                                    "simulation params), ground_removal + cone_detection fused",
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
+                       "launches": "fused frame kernel" if args.fused else "front + backend",
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),

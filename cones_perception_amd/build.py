@@ -19,7 +19,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
              "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include")]
 HEADERS = [os.path.join(CSRC, h) for h in ("cg_math.h", "cg_sort.h", "cg_internal.h", "cg_device.h", "cg_pcl.h",
-                                            "cg_backend.h")] + \
+                                            "cg_backend.h", "cg_grid.h", "cg_host.h")] + \
           [os.path.join(ROOT, "include", "cones_gpu.h")]
 
 
@@ -50,7 +50,8 @@ def build(verbose=False, force=False):
         _run(["gcc", "-O2", "-fPIC", "-ffp-contract=off", "-std=c11", "-Wall", "-c", src, "-o", o], verbose)
     objs.append(o)
     jobs = []
-    for name in ("cg_kernels.hip", "cg_large.hip", "cg_recrop.hip", "cg_colornet.hip", "cg_api.cpp", "cg_track.cpp"):
+    for name in ("cg_kernels.hip", "cg_large.hip", "cg_recrop.hip", "cg_colornet.hip", "cg_api.cpp", "cg_host.cpp",
+                 "cg_track.cpp"):
         src = os.path.join(CSRC, name)
         o = os.path.join(OBJ, name.rsplit(".", 1)[0] + ".o")
         if force or _stale(o, [src] + HEADERS):

@@ -14,27 +14,18 @@
 #include "../../include/cones_gpu.h"
 #include "cg_internal.h"
 #include "cg_math.h"
+#include "cg_host.h"
 
 namespace {
-
-thread_local std::string g_err;
 
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char* fmt, ...) {
-    char buf[512];
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
+    const int rc = cg_vfail(code, fmt, ap);
     va_end(ap);
-    g_err = buf;
-    return code;
+    return rc;
 }
-}  // namespace
-
-// shared with the host-only translation units (cg_track.cpp)
-int cg_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
-
-namespace {
 
 #define HIPCHK(expr)                                                                     \
     do {                                                                                 \
@@ -44,101 +35,7 @@ namespace {
                         #expr, hipGetErrorString(e_), __FILE__, __LINE__);               \
     } while (0)
 
-// Smallest S >= 0 (a double) with pred(S) true; pred must be monotone in S. Returns
-// `none` if pred(+inf) is false.
-template <class F>
-double min_double_where(F pred, double none) {
-    const uint64_t inf_bits = cg_dbits(INFINITY);
-    if (!pred(INFINITY)) return none;
-    if (pred(0.0)) return 0.0;
-    uint64_t lo = 0, hi = inf_bits;   // pred(lo) false, pred(hi) true
-    while (hi - lo > 1) {
-        const uint64_t mid = lo + (hi - lo) / 2;
-        if (pred(cg_bitsd(mid))) hi = mid; else lo = mid;
-    }
-    return cg_bitsd(hi);
-}
-
-// euclidan_dist(p, 0) as a function of S = (x^2 + y^2) + z^2 (src/perception_handling/utils.cpp:33)
-float dist_of_sumsq(double S) { return (float)std::sqrt(S); }
-
-int prepare(const cg_params& p, CgDevParams& d) {
-    if (!(p.voxel_filter_leaf_size_x > 0) || !(p.voxel_filter_leaf_size_y > 0) ||
-        !(p.voxel_filter_leaf_size_z > 0))
-        return fail(CG_E_INVALID, "voxel_filter_leaf_size_* must be > 0");
-    std::memset(&d, 0, sizeof(d));
-    d.default_low = p.default_lowest_point;
-    // (double)z < level_threshold
-    d.level_f = cg_ceil_to_float(p.level_threshold);
-    // euclidan_dist(...) > distance_treshold_max  <=>  S >= s_far
-    const double dmax = p.distance_treshold_max, dmin = p.distance_treshold_min;
-    d.s_far = (dmax != dmax) ? NAN
-                             : min_double_where([&](double S) { return (double)dist_of_sumsq(S) > dmax; }, NAN);
-    // euclidan_dist(...) < distance_treshold_min  <=>  S < s_near
-    d.s_near = (dmin != dmin) ? 0.0
-                              : min_double_where([&](double S) { return (double)dist_of_sumsq(S) >= dmin; },
-                                                 INFINITY);
-    // -angle*pi/180 >= atan2f  <=>  a <= ang_lo ;  atan2f >= angle*pi/180  <=>  a >= ang_hi
-    const double theta = p.angle_threshold * M_PI / 180;
-    const double ntheta = -p.angle_threshold * M_PI / 180;
-    d.ang_lo = cg_floor_to_float(ntheta);
-    d.ang_hi = cg_ceil_to_float(theta);
-    d.ang_cert_hi = cg_ceil_to_float((double)d.ang_hi + (double)CG_ANG_MARGIN);
-    d.ang_cert_lo = cg_floor_to_float((double)d.ang_hi - (double)CG_ANG_MARGIN);
-    // sector rays and the angle-filter class of each sector's wedge (cg_device.h ray_inside)
-    for (int sct = 0; sct < CG_NUM_BINS; sct++) {
-        const double lo = sct * (double)CG_SECTOR_ANGLE_RAD;             // exact product
-        const double hi = sct + 1 < CG_NUM_BINS ? (sct + 1) * (double)CG_SECTOR_ANGLE_RAD : 2.0 * M_PI;
-        d.ray[sct] = make_float4((float)std::cos(lo), (float)std::sin(lo), (float)std::cos(hi), (float)std::sin(hi));
-        // unwrapped angles a in (-pi, pi] of the padded wedge: one or two intervals
-        const double wl = lo - CG_RAY_WEDGE_PAD, wh = hi + CG_RAY_WEDGE_PAD;
-        double iv[2][2];
-        int niv = 0;
-        if (wh <= M_PI) { iv[0][0] = wl; iv[0][1] = wh; niv = 1; }
-        else if (wl >= M_PI) { iv[0][0] = wl - 2 * M_PI; iv[0][1] = wh - 2 * M_PI; niv = 1; }
-        else { iv[0][0] = wl; iv[0][1] = M_PI; iv[1][0] = -M_PI; iv[1][1] = wh - 2 * M_PI; niv = 2; }
-        bool keep = true, rm = true;
-        for (int k = 0; k < niv; k++) {
-            // keep: ang_lo < a < ang_hi on the whole interval; remove: a <= ang_lo or a >= ang_hi
-            keep = keep && iv[k][0] > (double)d.ang_lo && iv[k][1] < (double)d.ang_hi;
-            rm = rm && (iv[k][1] <= (double)d.ang_lo || iv[k][0] >= (double)d.ang_hi);
-        }
-        if (keep || rm) d.ray_filter_ok |= 1u << sct;
-        if (rm) d.ray_arm |= 1u << sct;
-    }
-    // pcl::VoxelGrid::setLeafSize(float, float, float): inverse = 1.0f / leaf
-    d.inv_leaf[0] = 1.0f / (float)p.voxel_filter_leaf_size_x;
-    d.inv_leaf[1] = 1.0f / (float)p.voxel_filter_leaf_size_y;
-    d.inv_leaf[2] = 1.0f / (float)p.voxel_filter_leaf_size_z;
-    // tolerance (src/cone_detection.cpp:22-23,212): const float members promoted by pow
-    const float cone_width = 0.228, cone_height = 0.325;
-    const double tol = std::sqrt(std::pow(cone_height, 2) + std::pow(cone_width, 2));
-    const float tol_f = (float)tol;                               // extract(): float tolerance
-    d.r2 = (float)((double)tol_f * (double)tol_f);                 // KdTreeFLANN::radiusSearch
-    d.cell_inv = 1.0f / (tol_f * 1.0625f);
-    d.min_cl = (uint32_t)p.min_cluster_size;
-    d.max_cl = (uint32_t)p.max_cluster_size;
-    d.ext = p.cone_position_extension_length;
-    // float certificates for the distance compares: the device's fma(x,x,fma(y,y,z*z)) is
-    // within 3 roundings (2e-7 relative) of S, far inside the 1e-6 slack
-    d.sfar_lo = cg_floor_to_float(d.s_far * (1.0 - 1e-6));
-    d.sfar_hi = cg_ceil_to_float(d.s_far * (1.0 + 1e-6));
-    d.snear_lo = cg_floor_to_float(d.s_near * (1.0 - 1e-6));
-    d.snear_hi = cg_ceil_to_float(d.s_near * (1.0 + 1e-6));
-    // z-code window: every sector threshold is ceil(low + 0.1) with low <= default_lowest_point,
-    // so thresholds lie at or below T_max; codes resolve 1/64 m over ~4 m below it
-    const float tmax = cg_ceil_to_float((double)p.default_lowest_point + 0.1);
-    // (descending code: T_max codes 1, so a NaN z, coded 0, is below qlo whenever it can be)
-    d.zq_z0 = (tmax == tmax && std::isfinite(tmax)) ? tmax : 0.0f;
-    d.zq_bias = 64.0f * d.zq_z0 + 1.0f;
-    // does PointXYZI() (0,0,0) survive filter_points_position?
-    const float a0 = cg_atan2f(0.0f, 0.0f);
-    const double S0 = 0.0;
-    const bool rm = (0.0f < d.level_f) || (S0 >= d.s_far) || (S0 < d.s_near) || (a0 <= d.ang_lo) ||
-                    (a0 >= d.ang_hi);
-    d.zero_pass = rm ? 0 : 1;
-    return CG_OK;
-}
+int prepare(const cg_params& p, CgDevParams& d) { return cg_prepare_params(p, d); }
 
 }  // namespace
 
@@ -197,6 +94,7 @@ struct cg_handle {
     bool batch_valid = false;
     uint32_t last_k = 0;
     uint32_t* d_seckeys = nullptr;   // 18 words per frame inside d_hdr (not owned)
+    uint32_t* d_biglist = nullptr;   // split batches' large-capacity frame list inside d_hdr (not owned)
     RcBox* d_boxes = nullptr;
     uint32_t* d_rc_cnt = nullptr;    // boxes x blocks, twice (counts, offsets)
     size_t rc_cnt_cap = 0;
@@ -232,6 +130,7 @@ void free_batch(cg_handle* h) {
     h->d_hdr = nullptr; h->d_vox = nullptr; h->d_lab = nullptr; h->d_offs = nullptr;
     h->d_idx = nullptr; h->d_cen = nullptr; h->d_ground = nullptr; h->d_scratch = nullptr;
     h->d_seckeys = nullptr;
+    h->d_biglist = nullptr;
     h->cap_frames = h->cap_points = 0;
 }
 
@@ -247,8 +146,12 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     free_batch(h);
     const uint64_t F = nf, C = np;
     // headers, then each frame's 18 final sector-minimum keys (cg_recrop of a pipeline frame)
-    HIPCHK(hipMalloc(&h->d_hdr, F * (CG_HDR_WORDS + CG_NUM_BINS + 1) * 4));
+    // headers, sector keys, then the split batch's list of large-capacity frames (F + 2 words,
+    // zeroed here; each batch's cg_back_big clears it again)
+    HIPCHK(hipMalloc(&h->d_hdr, (F * (CG_HDR_WORDS + CG_NUM_BINS + 1) + F + 2) * 4));
     h->d_seckeys = h->d_hdr + F * CG_HDR_WORDS;
+    h->d_biglist = h->d_seckeys + F * (CG_NUM_BINS + 1);
+    HIPCHK(hipMemset(h->d_biglist, 0, (F + 2) * 4));
     HIPCHK(hipMalloc(&h->d_vox, F * C * 16));
     HIPCHK(hipMalloc(&h->d_lab, F * C * 4));
     HIPCHK(hipMalloc(&h->d_offs, F * (C + 1) * 4));
@@ -263,23 +166,7 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     return CG_OK;
 }
 
-int check_view(const cg_cloud_view* v) {
-    if (!v) return fail(CG_E_INVALID, "null cloud view");
-    const uint64_t n = (uint64_t)v->width * v->height;
-    if (n > CG_MAX_FRAME_POINTS)
-        return fail(CG_E_CAPACITY, "cloud has %llu points; the engine supports <= %u",
-                    (unsigned long long)n, (unsigned)CG_MAX_FRAME_POINTS);
-    if (n == 0) return CG_OK;
-    if (!v->data) return fail(CG_E_INVALID, "null cloud data");
-    if (v->point_step == 0) return fail(CG_E_INVALID, "point_step is 0");
-    if ((uint64_t)v->row_step < (uint64_t)v->width * v->point_step)
-        return fail(CG_E_INVALID, "row_step < width * point_step");
-    const int32_t offs[4] = {v->off_x, v->off_y, v->off_z, v->off_intensity};
-    for (int32_t o : offs)
-        if (o >= 0 && (uint64_t)o + 4 > v->point_step)
-            return fail(CG_E_INVALID, "field offset %d outside point_step %u", o, v->point_step);
-    return CG_OK;
-}
+int check_view(const cg_cloud_view* v) { return cg_check_view(v); }
 
 // Stage a PointCloud2 data block as one contiguous device frame. Aligned, unpadded rows are
 // uploaded verbatim; padded rows or unaligned fields are re-packed (pure byte moves, the
@@ -341,6 +228,7 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
     L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
     L.idx = h->d_idx; L.cen = h->d_cen; L.ground = h->d_ground;
     L.scratch = h->d_scratch; L.scratch_stride = h->scratch_stride;
+    L.biglist = h->d_biglist;
     L.stamps = nullptr;
     if (h->stamps_on) {
         if (h->stamps_frames < h->cap_frames) {
@@ -562,7 +450,6 @@ RcBox crop_box(float cx, float cy) {
 
 extern "C" {
 
-const char* cg_last_error(void) { return g_err.c_str(); }
 const char* cg_version(void) { return "cones_gpu 0.1.0 (gfx950)"; }
 
 void cg_params_init(cg_params* p) {
@@ -943,16 +830,7 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
 
 // ---- the tile protocol with device-side keys and counts (no synchronisation) ----------------
 namespace {
-int tile_check(const cg_tile* t) {
-    if (t->n && !t->d_data) return fail(CG_E_INVALID, "null tile data");
-    if (t->n_total > CG_MAX_FRAME_POINTS || (uint64_t)t->first + t->n > t->n_total)
-        return fail(CG_E_INVALID, "tile [%u, %u + %u) outside a frame of %u points", t->first, t->first, t->n, t->n_total);
-    if (t->point_step == 0 || t->point_step % 4) return fail(CG_E_INVALID, "bad point_step");
-    const int32_t offs[4] = {t->off_x, t->off_y, t->off_z, t->off_intensity};
-    for (int32_t o : offs)
-        if (o >= 0 && (o % 4 || (uint32_t)o + 4 > t->point_step)) return fail(CG_E_INVALID, "bad field offset %d", o);
-    return CG_OK;
-}
+int tile_check(const cg_tile* t) { return cg_check_tile(t); }
 }  // namespace
 
 int cg_tile_front_async(cg_handle* h, const cg_tile* t, uint32_t* d_keys, void* hip_stream) {
@@ -1028,19 +906,8 @@ int cg_tile_backend_own(cg_handle* h, uint32_t n_total, void* hip_stream) {
 // ---- C5 halo tiling (cg_halo_*): argument checks and the handle's scratch; the work is in
 // cg_large.hip
 namespace {
-int halo_counts_ok(const uint32_t* c, uint32_t n_total) {
-    if (!c) return fail(CG_E_INVALID, "null merged counts");
-    if (n_total == 0 || n_total > CG_MAX_FRAME_POINTS || c[0] > n_total || c[1] > n_total || c[2] > c[1])
-        return fail(CG_E_INVALID, "inconsistent tile counts (K %u, survivors %u, finite %u, N %u)", c[0], c[1], c[2],
-                    n_total);
-    return CG_OK;
-}
-int halo_plan_ok(const cg_halo_plan* p) {
-    if (!p) return fail(CG_E_INVALID, "null plan");
-    if (p->passthrough) return fail(CG_E_INVALID, "passthrough frame: no voxel lattice to tile");
-    if (p->slabs == 0 || p->slab_w == 0) return fail(CG_E_INVALID, "empty slab plan");
-    return CG_OK;
-}
+int halo_counts_ok(const uint32_t* c, uint32_t n_total) { return cg_halo_counts_check(c, n_total); }
+int halo_plan_ok(const cg_halo_plan* p) { return cg_halo_plan_check(p); }
 }  // namespace
 
 int cg_halo_plan_frame(cg_handle* h, const uint32_t* merged_counts, uint32_t n_total, uint32_t n_ranks,

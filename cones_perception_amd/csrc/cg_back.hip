@@ -13,12 +13,9 @@
 #define CG_BRUTE_V 128
 #include "cg_backend.h"
 
-#ifndef CG_BACK_CAP
-#define CG_BACK_CAP 392   // C3's synthetic frames: M <= 413, 97.7% of them <= 384
-#endif
+// CG_BACK_CAP (cg_internal.h): C3's synthetic frames have M <= 413, 97.7% of them <= 384
 static_assert(CG_BLOCK == 256, "cg_back.hip is built with CG_BLOCK=256 (build.py)");
 static_assert(CG_BACK_CAP <= 2 * CG_BLOCK, "LDS backend capacity within pcl_block_sort<2>");
-static_assert(CG_BACK_CAP <= CG_RANK_SORT_MAX, "survivors ranked by one rank sort (no bitonic sort over KEY)");
 static_assert(backend_lds_fits<CG_BACK_CAP, (CG_BACK_CAP + 32) / 32>(), "backend overlays fit the LDS arrays");
 typedef BackLdsT<CG_BACK_CAP> BackLdsB;
 #define BACK_SMEM (FRONT_BYTES + sizeof(BackLdsB))
@@ -27,45 +24,15 @@ static_assert(2 * (FRONT_BYTES + CG_MAX_POINTS) + BACK_SMEM <= 163840, "LDS: two
 
 __global__ __launch_bounds__(CG_BLOCK, 4) void cg_back_kernel(CgLaunch L, CgDevParams P) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[BACK_SMEM];
-    FrontShared* fs = (FrontShared*)smem;
-    BackLdsB* bl = (BackLdsB*)(smem + FRONT_BYTES);
-    const uint32_t f = blockIdx.x, tid = threadIdx.x, N = L.n_points;
-    uint8_t* const slot = L.scratch + (uint64_t)f * L.scratch_stride;
-    const uint32_t* const rec = (const uint32_t*)(slot + cg_work_bytes(N));
-    const Work Wg = global_work(slot, N);
-    const uint32_t Ms = rec[CG_FREC_MS], M = rec[CG_FREC_M];
-    if (tid < 64) {
-        uint32_t v = 0;
-        if (tid == S_MS) v = Ms;
-        else if (tid == S_MF) v = rec[CG_FREC_NFIN];
-        else if (tid >= S_BMIN0 && tid <= S_BMIN2) v = rec[CG_FREC_BMIN + (tid - S_BMIN0)];
-        else if (tid >= S_BMAX0 && tid <= S_BMAX2) v = rec[CG_FREC_BMAX + (tid - S_BMAX0)];
-        fs->scal[tid] = v;
-    }
-    if (M <= CG_BACK_CAP) {
-        // the front appended survivors in wave order; ranked by point index they take their
-        // rank as point index, so index_vector (cloud order) and the point-order ties are the
-        // frame kernel's, and pcl_index_vector's bitmap spans Ms bits
-        const Work W = lds_work(bl);
-        uint64_t* const tmp = (uint64_t*)W.VOX;   // free until pcl_index_vector
-        for (uint32_t j = tid; j < Ms; j += CG_BLOCK) tmp[j] = ((uint64_t)Wg.IDX[j] << 16) | j;
-        __syncthreads();
-        rank_sort(tmp, W.KEY, Ms);
-        for (uint32_t r = tid; r < Ms; r += CG_BLOCK) {
-            W.P[r] = Wg.P[(uint32_t)(W.KEY[r] & 0xffffu)];
-            W.IDX[r] = r;
-        }
-        for (uint32_t j = Ms + tid; j < M; j += CG_BLOCK) {   // PointXYZI() pads after every kept point
-            W.P[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            W.IDX[j] = 0xffffu;
-        }
-        __syncthreads();
-        backend(W, M, fs, L, P, f, 0u, (Ms + 32) / 32, CG_BACK_CAP);
-    } else {
-        __syncthreads();
-        backend(Wg, M, fs, L, P, f, 0x2u, CG_MAX_POINTS / 32, 0);
-    }
-    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    const uint32_t f = blockIdx.x;
+    const uint32_t* const rec = (const uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(L.n_points));
+    // up to CG_BACK_CAP detector points in LDS here; up to CG_MMAX the front listed the frame
+    // for cg_back_big (the frame kernel's LDS capacity); beyond, the backend on the frame's HBM
+    // slot here (dense scenes only)
+    const uint32_t M = rec[CG_FREC_M];
+    if (M <= CG_BACK_CAP) back_frame<CG_BACK_CAP>(L, P, f, (FrontShared*)smem, (BackLdsB*)(smem + FRONT_BYTES));
+    else if (M > CG_MMAX) back_frame<0>(L, P, f, (FrontShared*)smem, nullptr);
+    if (L.span && threadIdx.x == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {

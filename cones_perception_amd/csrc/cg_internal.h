@@ -85,6 +85,9 @@ struct CgLaunch {
     // timing: [first front workgroup start, last front workgroup end] of a split batch's front
     // launch (cg_debug_front_span), or null
     unsigned long long* span_front;
+    // split batches: frames whose detector points exceed CG_BACK_CAP, listed by the front for
+    // the large-capacity backend launch: [0] count, [1] finished workgroups, then frame indices
+    uint32_t* biglist;
     // split single-frame launch (cg_launch_split): CG_SPLIT_WORDS of state, or null
     uint32_t* split;
     // split launch: the frame's results also packed here (CG_PACK_WORDS) at the end, or null
@@ -121,6 +124,9 @@ static inline hipError_t cg_stream_wait(hipStream_t s) {
 
 #ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
+#endif
+#ifndef CG_BACK_CAP
+#define CG_BACK_CAP 392        // the backend launch's LDS capacity (cg_back.hip); more: cg_back_big
 #endif
 #ifndef CG_MMAX
 #define CG_MMAX 1024           // LDS-path capacity (points surviving the filter)

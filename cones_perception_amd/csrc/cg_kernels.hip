@@ -427,6 +427,10 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
                 rec[CG_FREC_BMIN + a] = fs->scal[S_BMIN0 + a];
                 rec[CG_FREC_BMAX + a] = fs->scal[S_BMAX0 + a];
             }
+            if (M > CG_BACK_CAP && M <= CG_MMAX) {   // beyond the backend launch's LDS: cg_back_big
+                const uint32_t q = atomicAdd(&L.biglist[0], 1u);
+                L.biglist[2 + q] = f;
+            }
             if (L.span_front) atomicMax(&L.span_front[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
         }
         return;
@@ -463,6 +467,33 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, CG_BLOCK), amdgpu_num_v
 template <int PPT, int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 2) void cg_split_kernel(CgLaunch L, CgDevParams P) {
     frame_body<PPT, LAYOUT, KMODE, true>(L, P);
+}
+
+// Split batches: the frames the front listed (CG_BACK_CAP < M <= CG_MMAX, a few per C3 batch)
+// in the frame kernel's LDS capacity, after the backend launch on the same stream. The last workgroup to finish clears the list for the next batch.
+#define BACK_BIG_GRID 32
+__global__ __launch_bounds__(CG_BLOCK, 2) void cg_back_big_kernel(CgLaunch L, CgDevParams P) {
+    // one workgroup per CU (LDS past half a CU): registers for 2 waves per SIMD, no spills
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES <= 81920 ? 81920 + 256 : SMEM_BYTES];
+    uint32_t* const list = L.biglist;
+    const uint32_t n = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma clang loop unroll(disable)
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        back_frame<CG_MMAX>(L, P, list[2 + i], (FrontShared*)smem, (BackLds*)(smem + FRONT_BYTES));
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (L.span) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        // every workgroup read the count before it counts itself done
+        if (__hip_atomic_fetch_add(&list[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            __hip_atomic_store(&list[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&list[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+static hipError_t launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
+    hipLaunchKernelGGL(cg_back_big_kernel, dim3(BACK_BIG_GRID), dim3(CG_BLOCK), 0, s, L, P);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -537,7 +568,8 @@ static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hi
                 hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
             } else {
                 hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
-                return (hipError_t)cg_launch_back(L, P, s);
+                if (hipError_t e = (hipError_t)cg_launch_back(L, P, s)) return e;
+                return launch_back_big(L, P, s);
             }
             break;
         case CG_KMODE_DETECT:
@@ -545,7 +577,8 @@ static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hi
                 hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
             } else {
                 hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
-                return (hipError_t)cg_launch_back(L, P, s);
+                if (hipError_t e = (hipError_t)cg_launch_back(L, P, s)) return e;
+                return launch_back_big(L, P, s);
             }
             break;
         default:

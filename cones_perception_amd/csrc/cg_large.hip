@@ -594,7 +594,7 @@ uint32_t lg_wave_blocks(uint64_t n) {
     return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + WAVES - 1) / WAVES, 1024));
 }
 uint32_t blocks_of(uint64_t n) { return (uint32_t)((n + CG_BLOCK - 1) / CG_BLOCK); }
-uint32_t bits_of(uint64_t v) { uint32_t b = 0; while (b < 64 && (1ull << b) <= v) b++; return b ? b : 1; }
+uint32_t bits_of(uint64_t v) { return cg_bits_of(v); }
 
 // Stable sort of n pairs in (k[0], v[0]) by key bits [lo, bits); returns the buffer index (0 or
 // 1) that holds the result. The pairs are already in order of the bits below lo. With n_dev,
@@ -2019,40 +2019,4 @@ int cg_launch_halo_owner(const float* pts, uint32_t n, float inv0, int32_t min_b
     if (n) hipLaunchKernelGGL(lg_halo_owner, dim3(blocks_of(n)), dim3(CG_BLOCK), 0, s, (const float4*)pts, n, inv0,
                               min_b0, slab_w, slabs, out);
     return hipGetLastError();
-}
-// The plan (cg_halo_plan_frame): the whole frame's lattice from the merged counts, as
-// cg_large_backend computes it, cut into slabs at least `band` columns wide.
-void cg_halo_plan_compute(const CgDevParams& P, const uint32_t* c, uint32_t N, uint32_t n_ranks, struct cg_halo_plan* out) {
-    const uint32_t K = c[0];
-    const uint32_t npad = P.zero_pass ? N - K : 0u;
-    float bmn[3], bmx[3];
-    uint32_t nfin = c[2];
-    for (int a = 0; a < 3; a++) {
-        bmn[a] = nfin ? cg_fkey_inv(c[3 + a]) : INFINITY;
-        bmx[a] = nfin ? cg_fkey_inv(c[6 + a]) : -INFINITY;
-        if (npad) { bmn[a] = std::min(bmn[a], 0.f); bmx[a] = std::max(bmx[a], 0.f); }
-    }
-    nfin += npad;
-    uint32_t pass = 0;
-    int min_b[3], div_b[3];
-    voxel_grid_setup(nfin, bmn, bmx, P, pass, min_b, div_b);
-    *out = cg_halo_plan{};
-    out->passthrough = pass;
-    for (int a = 0; a < 3; a++) { out->min_b[a] = min_b[a]; out->div_b[a] = (uint32_t)div_b[a]; }
-    // |x1 - x2| < tol between centroids of columns i1 < i2 needs i2 - i1 <= tol / leaf + 1;
-    // one column more covers a centroid rounded across its cell edge
-    out->band = (uint32_t)std::ceil((double)std::sqrt(P.r2) * (double)P.inv_leaf[0]) + 2u;
-    const uint32_t dx = (uint32_t)div_b[0];
-    out->slabs = std::max<uint32_t>(1, std::min<uint32_t>(std::max<uint32_t>(n_ranks, 1), dx / out->band));
-    out->slab_w = (dx + out->slabs - 1) / out->slabs;
-    out->n_pads = npad;
-    out->pad_slab = -1;
-    if (npad && !pass) {
-        const int i0 = (int)(floorf(0.f * P.inv_leaf[0]) - (float)min_b[0]);
-        out->pad_slab = (int32_t)std::min<uint32_t>((uint32_t)i0 / out->slab_w, out->slabs - 1);
-    }
-    out->key_bits = pass ? 0u
-                         : 1u + bits_of((uint64_t)(uint32_t)div_b[0] * (uint64_t)(uint32_t)div_b[1] *
-                                        (uint64_t)(uint32_t)div_b[2]);
-    out->key_bits = std::min<uint32_t>(out->key_bits, 32u);
 }

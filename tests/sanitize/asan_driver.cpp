@@ -1,6 +1,6 @@
 // Host sanitizer driver (AddressSanitizer + UndefinedBehaviorSanitizer, -fno-sanitize-recover):
 // the CPU restatement (oracle/cg_oracle.cpp) and the host-only parts of the C-ABI library
-// (csrc/cg_track.cpp, csrc/cg_synth.c) built with the sanitizers and driven over synthetic
+// (csrc/cg_track.cpp, csrc/cg_synth.c, csrc/cg_host.cpp) built with the sanitizers and driven over synthetic
 // frames of every size class, edge clouds (empty, non-finite, all pads, the voxel overflow
 // guard), the three parameter profiles, both voxel orders, the re-crop, the node's tracking
 // with full / short / failed colour responses, and the tracker's own C-ABI. Test
@@ -27,9 +27,114 @@ void oracle_node_destroy(void* node);
 int oracle_node_step(void* node, const void* params, const void* view, int mode, const float* centroids,
                      uint32_t n, ServiceFn service, void* ctx, uint32_t* counts, float* xy, uint32_t cap);
 }
-// cg_track.cpp reports errors through the library's thread-local message (cg_api.cpp, a HIP
-// translation unit): a stand-in that keeps the code
-int cg_set_error(int code, const char*) { return code; }
+#include "cg_math.h"
+#include "cg_host.h"   // the C-ABI's host-only logic (csrc/cg_host.cpp): checks, parameters, halo plan
+
+// The C-ABI's host-only logic under the sanitizers: parameter preparation over the profiles and
+// random / degenerate values, the cloud-view and tile argument checks, and the halo tiling plan
+// of a tiled frame over random merged counts and bounds, with the plan's invariants checked.
+static int host_api(const std::vector<cg_params>& profiles) {
+    std::mt19937 rng(17);
+    auto unif = [&](double lo, double hi) { return lo + (hi - lo) * (double)(rng() % 1000001) / 1e6; };
+    const double specials[] = {NAN, INFINITY, -INFINITY, 0.0, -0.0, 1e-300, 1e300, -1.0, 0.04, 25.0};
+    for (const cg_params& p0 : profiles) {
+        CgDevParams d;
+        if (cg_prepare_params(p0, d) != CG_OK) return 20;
+        for (int k = 0; k < 3000; k++) {
+            cg_params p = p0;
+            double* dbl[] = {&p.distance_treshold_max, &p.distance_treshold_min, &p.angle_threshold,
+                             &p.level_threshold, &p.cone_position_extension_length};
+            for (double* x : dbl) if (rng() % 3 == 0) *x = rng() % 2 ? specials[rng() % 10] : unif(-400.0, 400.0);
+            if (rng() % 3 == 0) p.default_lowest_point = rng() % 2 ? (float)specials[rng() % 10] : (float)unif(-10, 10);
+            double* leaf[] = {&p.voxel_filter_leaf_size_x, &p.voxel_filter_leaf_size_y, &p.voxel_filter_leaf_size_z};
+            for (double* x : leaf) if (rng() % 4 == 0) *x = rng() % 2 ? specials[rng() % 10] : unif(1e-4, 2.0);
+            if (rng() % 4 == 0) p.min_cluster_size = (int)(rng() % 200) - 20;
+            if (rng() % 4 == 0) p.max_cluster_size = (int)(rng() % 100000) - 20;
+            const bool leaf_ok = p.voxel_filter_leaf_size_x > 0 && p.voxel_filter_leaf_size_y > 0 && p.voxel_filter_leaf_size_z > 0;
+            const int rc = cg_prepare_params(p, d);
+            if ((rc == CG_OK) != leaf_ok) return 21;
+            if (rc != CG_OK && !*cg_last_error()) return 22;
+            if (rc == CG_OK && d.s_far == d.s_far && !(d.sfar_lo <= d.sfar_hi)) return 23;
+        }
+    }
+    // cloud views
+    std::vector<uint8_t> buf(64 * 32);
+    if (cg_check_view(nullptr) == CG_OK) return 30;
+    for (int k = 0; k < 20000; k++) {
+        cg_cloud_view v;
+        std::memset(&v, 0, sizeof(v));
+        v.data = rng() % 8 ? buf.data() : nullptr;
+        v.width = rng() % 4 ? rng() % 70 : rng();
+        v.height = rng() % 4 ? 1 + rng() % 3 : rng();
+        v.point_step = rng() % 6 ? 4 * (rng() % 9) : rng() % 40;
+        v.row_step = rng() % 3 ? v.width * v.point_step : rng();
+        int32_t* offs[] = {&v.off_x, &v.off_y, &v.off_z, &v.off_intensity};
+        for (int32_t* o : offs) *o = rng() % 5 ? 4 * (int32_t)(rng() % 8) : (int32_t)(rng() % 64) - 8;
+        const int rc = cg_check_view(&v);
+        const uint64_t n = (uint64_t)v.width * v.height;
+        if (rc == CG_OK && n && (!v.data || !v.point_step || (uint64_t)v.row_step < (uint64_t)v.width * v.point_step))
+            return 31;
+        if (rc == CG_OK) {
+            for (int32_t* o : offs) if (*o >= 0 && (uint64_t)*o + 4 > v.point_step && n) return 32;
+        }
+    }
+    // tiles
+    for (int k = 0; k < 20000; k++) {
+        cg_tile t;
+        std::memset(&t, 0, sizeof(t));
+        t.d_data = rng() % 8 ? buf.data() : nullptr;
+        t.n_total = rng() % 4 ? rng() % 5000 : rng();
+        t.first = rng() % 3000;
+        t.n = rng() % 3000;
+        t.point_step = rng() % 6 ? 4 * (rng() % 9) : rng() % 40;
+        int32_t* offs[] = {&t.off_x, &t.off_y, &t.off_z, &t.off_intensity};
+        for (int32_t* o : offs) *o = rng() % 5 ? 4 * (int32_t)(rng() % 8) : (int32_t)(rng() % 64) - 8;
+        const int rc = cg_check_tile(&t);
+        if (rc == CG_OK && ((uint64_t)t.first + t.n > t.n_total || !t.point_step || t.point_step % 4)) return 33;
+    }
+    // halo plans of tiled frames: merged counts (K, survivors, finite survivors, bounds keys)
+    if (cg_halo_counts_check(nullptr, 10) == CG_OK || cg_halo_plan_check(nullptr) == CG_OK) return 40;
+    long plans = 0;
+    for (const cg_params& p0 : profiles) {
+        for (int zp = 0; zp < 2; zp++) {
+            cg_params p = p0;
+            if (zp) p.distance_treshold_min = 0.0;   // zero pads survive: they join the lattice
+            CgDevParams d;
+            if (cg_prepare_params(p, d) != CG_OK) return 41;
+            for (int k = 0; k < 5000; k++) {
+                const uint32_t N = rng() % 5 ? 1 + rng() % (1u << 20) : 1 + rng() % (1u << 28);
+                uint32_t c[9];
+                c[0] = rng() % 4 ? rng() % (N + 1) : rng();
+                c[1] = rng() % 4 ? rng() % (N + 1) : rng();
+                c[2] = rng() % 4 ? (c[1] ? rng() % (c[1] + 1) : 0u) : rng();
+                const double span = rng() % 8 ? unif(0.0, 60.0) : unif(0.0, 2e5);   // wide spans trip PCL's guard
+                for (int a = 0; a < 3; a++) {
+                    const float lo = (float)unif(-1e5, 1e5);
+                    c[3 + a] = cg_fkey(lo);
+                    c[6 + a] = cg_fkey((float)((double)lo + (a == 2 ? span / 20 : span)));
+                }
+                const uint32_t ranks = rng() % 10;
+                const int ok = cg_halo_counts_check(c, N);
+                if (ok == CG_OK && (c[0] > N || c[1] > N || c[2] > c[1])) return 42;
+                if (ok != CG_OK) continue;
+                cg_halo_plan plan;
+                cg_halo_plan_compute(d, c, N, ranks, &plan);
+                plans++;
+                if (plan.slabs < 1 || plan.slabs > (ranks > 1 ? ranks : 1u) || plan.key_bits > 32) return 43;
+                if (!plan.passthrough) {
+                    if ((uint64_t)plan.slab_w * plan.slabs < plan.div_b[0]) return 44;
+                    if (plan.slabs > 1 && plan.slab_w < plan.band) return 45;
+                    if (plan.n_pads && (plan.pad_slab < 0 || (uint32_t)plan.pad_slab >= plan.slabs)) return 46;
+                    if (cg_halo_plan_check(&plan) != CG_OK) return 47;
+                } else if (cg_halo_plan_check(&plan) == CG_OK) {
+                    return 48;
+                }
+            }
+        }
+    }
+    std::printf("host C-ABI checks: %ld halo plans\n", plans);
+    return 0;
+}
 
 static cg_cloud_view view_of(const std::vector<uint8_t>& d, uint32_t n, uint32_t step) {
     cg_cloud_view v;
@@ -187,6 +292,7 @@ int main(int argc, char** argv) {
         }
         cg_tracker_destroy(t);
     }
-    std::printf("sanitizers clean: %ld clouds, 4 tracker variants\n", frames);
+    if (int rc = host_api(profiles)) { std::printf("host C-ABI check %d failed\n", rc); return rc; }
+    std::printf("sanitizers clean: %ld clouds, 4 tracker variants, the C-ABI's host logic\n", frames);
     return 0;
 }
