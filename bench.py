@@ -241,6 +241,11 @@ def main():
             single = single_frame_latency(cp, params, raw, local, order=vorder)
         except Exception as e:  # noqa: BLE001
             single = {"error": repr(e)}
+    if single is not None and "error" not in single:
+        try:
+            single["cpp_node"] = single_frame_cpp()
+        except Exception as e:  # noqa: BLE001
+            single["cpp_node"] = {"error": repr(e)}
     pcie = None
     if rank == 0 and world == 1:   # the same batch from pinned host memory: PCIe-inclusive rate
         try:
@@ -716,6 +721,21 @@ def single_frame_latency(cp, params, raw, device, reps=200, order=None):
                         "ConePipeline.cloud_handler (staging copy into pinned memory, the split kernel reading "
                         "it over PCIe, its last workgroup writing the packed results into pinned host memory, "
                         "one synchronisation, Python result objects)"}
+
+
+def single_frame_cpp(reps=500):
+    """C2 through the C++ node mirror (cones_perception_amd/host/cones_nodes.hpp, the reference
+    nodes' own language): nodes_demo --latency, a child process with its own GPU context."""
+    import subprocess
+    exe = os.path.join(ROOT, "cones_perception_amd", "lib", "nodes_demo")
+    r = subprocess.run([exe, "--latency", str(reps)], capture_output=True, text=True, timeout=120)
+    if r.returncode != 0:
+        return {"error": (r.stderr or r.stdout)[-500:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["includes"] = ("C2 in C++: ConePipeline::cloud_handler (cones_nodes.hpp) on one 64k-point PointCloud2 in "
+                       "pageable memory: cg_pipeline (staging into pinned memory, split kernel reading it over "
+                       "PCIe, results written to pinned host memory, one synchronisation), result vectors")
+    return out
 
 
 def cpu_baseline(cp, params, raw, budget_s, eng, threads, order=None):

@@ -1,6 +1,7 @@
 // nodes_demo.cpp — runs the two-node composition of launch/cones_perception.launch
 // (GroundRemover -> groundless_cloud -> ConeDetector) through the C++ mirror and checks that
 // it equals the fused cg_pipeline on the same frames, bit for bit. Exit 0 on success.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -35,7 +36,37 @@ static bool same(const std::vector<float>& a, const std::vector<float>& b) {
     return true;
 }
 
+// `nodes_demo --latency R`: the C2 regime of the reference (one 64k-point frame per ROS
+// callback, in C++): R synchronous ConePipeline::cloud_handler calls on the first synthetic
+// frame with the simulation profile; prints one JSON line with the mean latency.
+static int latency(int reps) {
+    cg_params p;
+    cg_params_init(&p);
+    p.num_of_sectors = 16; p.default_lowest_point = -0.1;   // config/ground_removal_params.yaml
+    p.distance_treshold_max = 10.0; p.distance_treshold_min = 1.0; p.level_threshold = -5.0;
+    p.angle_threshold = 160.0; p.min_cluster_size = 2; p.max_cluster_size = 500;
+    p.cone_position_extension_length = 0.05;
+    ConePipeline fused(p);
+    const PointCloud2 msg = synth_cloud(0);
+    uint32_t c = 0;
+    for (int i = 0; i < 20; i++) c += (uint32_t)fused.cloud_handler(msg).clusters.size();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; i++) c += (uint32_t)fused.cloud_handler(msg).clusters.size();
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("{\"latency_ms\": %.6f, \"frames_per_s\": %.3f, \"calls\": %d, \"clusters\": %u}\n",
+                s / reps * 1e3, reps / s, reps, c / (uint32_t)(reps + 20));
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 2 && std::strcmp(argv[1], "--latency") == 0) {
+        try {
+            return latency(std::atoi(argv[2]));
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "%s\n", e.what());
+            return 2;
+        }
+    }
     const int frames = argc > 1 ? std::atoi(argv[1]) : 4;
     cg_params p;
     cg_params_init(&p);   // reference defaults, then the simulation profile
