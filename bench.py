@@ -70,6 +70,9 @@ def main():
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
     ap.add_argument("--no-scatter", action="store_true", help="at N>1, skip the C4 scatter/gather leg")
+    ap.add_argument("--split-streams", default="",
+                    help="F,B: each batch's front launch on one of F front streams and its backend launches on "
+                         "one of B back streams (cg_run_batch_split); --streams engines rotate over them")
     ap.add_argument("--fused", action="store_true",
                     help="experiment: each frame in one fused workgroup (cg_debug_route 6) instead of the front "
                          "launch + backend launches")
@@ -138,16 +141,23 @@ def main():
     if args.fused:
         for e in engines:
             e.debug_route(6)
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
-    assert all(st.cuda_stream != 0 for st in streams)
+    split_fb = [int(x) for x in args.split_streams.split(",")] if args.split_streams else None
+    if split_fb:   # F front streams, B back streams
+        streams = [torch.cuda.Stream(dev) for _ in range(split_fb[0])]
+        backs = [torch.cuda.Stream(dev) for _ in range(split_fb[1])]
+    else:
+        streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        backs = []
+    assert all(st.cuda_stream != 0 for st in streams + backs)
     eng, stream = engines[0], streams[0]
     counter = [0]
 
     def step(idx=None):
         i = counter[0] if idx is None else idx
         counter[0] += 1
-        e, st = engines[i % S], streams[i % S]
-        e.run(d_ins[i % S].data_ptr(), F, N, 16, stream=st.cuda_stream)
+        e, st = engines[i % S], streams[i % len(streams)]
+        bs = backs[i % len(backs)].cuda_stream if backs else 0
+        e.run(d_ins[i % S].data_ptr(), F, N, 16, stream=st.cuda_stream, back_stream=bs)
         return st
 
     torch.cuda.synchronize(dev)
@@ -171,7 +181,7 @@ def main():
     lib = cp.lib()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        st = streams[(counter[0]) % S]
+        st = streams[(counter[0]) % len(streams)]
         lib.cg_debug_launch_span(engines[counter[0] % S].handle, spans[s].data_ptr())
         lib.cg_debug_front_span(engines[counter[0] % S].handle, spans[s, 2:].data_ptr())
         if not args.no_events:
@@ -286,6 +296,7 @@ def main():
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
                        "launches": "fused frame kernel" if args.fused else "front + backend",
+                       "split_streams": args.split_streams or None,
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),

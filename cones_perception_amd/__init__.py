@@ -440,14 +440,21 @@ class BatchEngine(_Handle):
 
     def run(self, d_ptr: int, n_frames: int, n_points: int, point_step: int = 16,
             frame_stride: Optional[int] = None, mode: int = CG_MODE_PIPELINE, stream: int = 0,
-            offsets=(0, 4, 8, 12), is_dense: bool = True):
+            offsets=(0, 4, 8, 12), is_dense: bool = True, back_stream: int = 0):
+        """back_stream (with stream): the backend launches of a split batch on their own stream
+        (cg_run_batch_split); the results are complete once back_stream has run them."""
         b = _abi.cg_batch()
         b.d_data = d_ptr
         b.frame_stride = frame_stride if frame_stride is not None else n_points * point_step
         b.n_frames, b.n_points, b.point_step = n_frames, n_points, point_step
         b.off_x, b.off_y, b.off_z, b.off_intensity = offsets
         b.is_dense = 1 if is_dense else 0
-        check(lib().cg_run_batch(self._h, C.byref(b), mode, C.c_void_p(stream) if stream else None))
+        if back_stream:
+            if not stream:
+                raise ValueError("back_stream needs an explicit front stream")
+            check(lib().cg_run_batch_split(self._h, C.byref(b), mode, C.c_void_p(stream), C.c_void_p(back_stream)))
+        else:
+            check(lib().cg_run_batch(self._h, C.byref(b), mode, C.c_void_p(stream) if stream else None))
 
     def results(self) -> _abi.cg_batch_results:
         r = _abi.cg_batch_results()

@@ -135,6 +135,7 @@ _SIGS = {
     "cg_detect": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_detect_result)]),
     "cg_pipeline": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_detect_result)]),
     "cg_run_batch": (C.c_int, [C.c_void_p, C.POINTER(cg_batch), C.c_int, C.c_void_p]),
+    "cg_run_batch_split": (C.c_int, [C.c_void_p, C.POINTER(cg_batch), C.c_int, C.c_void_p, C.c_void_p]),
     "cg_tile_front": (C.c_int, [C.c_void_p, C.POINTER(cg_tile), C.c_void_p]),
     "cg_tile_decide": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cg_tile_survivors": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),

@@ -64,6 +64,10 @@ struct cg_handle {
     uint32_t last_frames = 0, last_points = 0;
     int last_mode = -1;
     hipStream_t last_stream = nullptr;
+    // split batches on two streams (cg_run_batch_split): the front launch's completion, and the
+    // last backend launch's (the next front on this handle reuses the survivor slots)
+    hipEvent_t ev_front = nullptr, ev_back = nullptr;
+    hipStream_t back_stream_pending = nullptr;   // stream of the backend launches not yet waited on
     // host results
     uint32_t h_hdr[CG_HDR_WORDS] = {};
     uint32_t* d_split = nullptr;     // split single-frame launch state (CG_SPLIT_WORDS)
@@ -125,6 +129,10 @@ int own_stream(cg_handle* h) {
 }
 
 void free_batch(cg_handle* h) {
+    if (h->back_stream_pending && h->ev_back) {   // a split batch's backends still read the slots
+        (void)hipEventSynchronize(h->ev_back);
+        h->back_stream_pending = nullptr;
+    }
     (void)hipFree(h->d_hdr); (void)hipFree(h->d_vox); (void)hipFree(h->d_lab); (void)hipFree(h->d_offs);
     (void)hipFree(h->d_idx); (void)hipFree(h->d_cen); (void)hipFree(h->d_ground); (void)hipFree(h->d_scratch);
     h->d_hdr = nullptr; h->d_vox = nullptr; h->d_lab = nullptr; h->d_offs = nullptr;
@@ -270,13 +278,31 @@ int ensure_large(cg_handle* h, uint32_t n) {
 
 // Frames of <= CG_MAX_POINTS points run as one batch launch of the frame kernel; larger
 // frames (or every frame, under cg_debug_route) go through the multi-workgroup large path.
-int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
+int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream_t s_back = nullptr) {
     const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2 || h->route == 5) && L.n_points > 0);
     if (!large && L.split) {
         HIPCHK((hipError_t)cg_launch_split(L, h->dp, kmode, s));
         return CG_OK;
     }
     if (!large) {
+        if (s_back && s_back != s && h->route != 6) {
+            // the front on s; the backend launches on s_back once the front is done; the next
+            // front of this handle waits for them (cg_run_batch_split)
+            if (!h->ev_front) HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
+            if (!h->ev_back) HIPCHK(hipEventCreateWithFlags(&h->ev_back, hipEventDisableTiming));
+            if (h->back_stream_pending) HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
+            HIPCHK((hipError_t)cg_launch_front(L, h->dp, kmode, s));
+            HIPCHK(hipEventRecord(h->ev_front, s));
+            HIPCHK(hipStreamWaitEvent(s_back, h->ev_front, 0));
+            HIPCHK((hipError_t)cg_launch_backends(L, h->dp, s_back));
+            HIPCHK(hipEventRecord(h->ev_back, s_back));
+            h->back_stream_pending = s_back;
+            return CG_OK;
+        }
+        if (h->back_stream_pending) {   // a split batch's backend may still read the survivor slots
+            HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
+            h->back_stream_pending = nullptr;
+        }
         HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s, h->route == 6));
         return CG_OK;
     }
@@ -500,6 +526,8 @@ int cg_destroy(cg_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)cg_stream_wait(h->stream);
     free_batch(h);
+    if (h->ev_front) (void)hipEventDestroy(h->ev_front);
+    if (h->ev_back) (void)hipEventDestroy(h->ev_back);
     if (h->d_stamps) (void)hipFree(h->d_stamps);
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->h_meta) (void)hipHostFree(h->h_meta);
@@ -654,7 +682,21 @@ int cg_batch_recrop(cg_handle* h, uint32_t frame, const float* centers_xy, uint3
                         n_centers, out);
 }
 
+namespace {
+int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream, void* back_stream);
+}  // namespace
+
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
+    return run_batch(h, b, mode, hip_stream, nullptr);
+}
+
+int cg_run_batch_split(cg_handle* h, const cg_batch* b, int mode, void* front_stream, void* back_stream) {
+    if (!front_stream || !back_stream) return fail(CG_E_INVALID, "cg_run_batch_split needs two streams");
+    return run_batch(h, b, mode, front_stream, back_stream);
+}
+
+namespace {
+int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream, void* back_stream) {
     if (!h || !b) return fail(CG_E_INVALID, "null argument");
     if (mode != CG_MODE_PIPELINE && mode != CG_MODE_DETECT) return fail(CG_E_INVALID, "bad mode %d", mode);
     if (b->n_points > CG_MAX_FRAME_POINTS)
@@ -691,15 +733,18 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     h->next_front_span = nullptr;
     const int kmode = mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT;
     if (kmode == CG_KMODE_PIPELINE) L.seckeys = h->d_seckeys;   // per frame, for cg_batch_recrop
-    rc = launch_frames(h, L, kmode, s);
+    rc = launch_frames(h, L, kmode, s, (hipStream_t)back_stream);
     if (rc) return rc;
     h->last_batch = L;
     h->batch_kmode = kmode;
     h->batch_valid = true;
-    h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode; h->last_stream = s;
+    h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode;
+    // the results are complete where the last launch of the batch ran
+    h->last_stream = h->back_stream_pending ? h->back_stream_pending : s;
     h->last_single = false;
     return CG_OK;
 }
+}  // namespace
 
 int cg_batch_results_get(cg_handle* h, cg_batch_results* out) {
     if (!h || !out) return fail(CG_E_INVALID, "null argument");

@@ -228,6 +228,9 @@ uint64_t cg_scratch_bytes(uint32_t n_points);
 // backend launch (cg_launch_back, cg_back.hip); `fused` keeps each frame in one workgroup.
 int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused = false);
 int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
+// the halves of a split detector batch (frames of <= CG_MAX_POINTS points)
+int cg_launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
+int cg_launch_backends(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 // Cone re-crop (cg_recrop.hip): exact float form of the reference's double box compares.
 struct RcBox { float lox, hix, loy, hiy; };
 #define CG_RECROP_MAX_BOXES 256   // boxes per launch (more: several launches)

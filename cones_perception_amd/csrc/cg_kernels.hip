@@ -603,6 +603,33 @@ int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
     return hipGetLastError();
 }
 
+// The two halves of a split batch, for callers that run them on different streams.
+template <int PPT, int LAYOUT>
+static void launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
+    const dim3 grid(L.n_frames), block(CG_BLOCK);
+    if (kmode == CG_KMODE_PIPELINE)
+        hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
+    else
+        hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
+}
+int cg_launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
+    if (L.n_frames == 0) return hipSuccess;
+    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
+    if (L.n_points <= 32 * CG_BLOCK) {
+        if (xyzi16) launch_front<32, CG_LAYOUT_XYZI16>(L, P, kmode, s);
+        else launch_front<32, CG_LAYOUT_GENERIC>(L, P, kmode, s);
+    } else {
+        if (xyzi16) launch_front<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_XYZI16>(L, P, kmode, s);
+        else launch_front<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_GENERIC>(L, P, kmode, s);
+    }
+    return hipGetLastError();
+}
+int cg_launch_backends(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
+    if (L.n_frames == 0) return hipSuccess;
+    if (hipError_t e = (hipError_t)cg_launch_back(L, P, s)) return e;
+    return launch_back_big(L, P, s);
+}
+
 int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused) {
     if (L.n_frames == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 &&

@@ -153,6 +153,16 @@ typedef struct cg_batch {
  * and the call synchronises the stream (it sizes each frame's backend from its counts). */
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream);
 
+/* cg_run_batch over two streams. A detector batch of frames of <= 65,536 points is a front
+ * launch (the frame streaming: ground decisions, position filter, survivors) and backend
+ * launches (voxel grid, clustering, centroids); here the front runs on front_stream and the
+ * backends on back_stream once it is done, so the backends of one batch overlap the next
+ * batch's front (another handle's, on another front stream). The results are complete when
+ * back_stream reaches this call's work (cg_batch_fetch waits there); this handle's next batch
+ * waits for these backends before its front reuses their inputs. Other batches run as in
+ * cg_run_batch on front_stream. */
+int cg_run_batch_split(cg_handle* h, const cg_batch* b, int mode, void* front_stream, void* back_stream);
+
 /* Per-frame header words in the device result buffer. */
 #define CG_HDR_N      0
 #define CG_HDR_K      1
