@@ -97,3 +97,20 @@ def test_no_kernel_uses_scratch(tmp_path):
            if m.get(".private_segment_fixed_size") != "0" or m.get(".uses_dynamic_stack") != "false"
            or m.get(".vgpr_spill_count", "0") != "0"]
     assert not bad, f"kernels with scratch (private segment, dynamic stack, VGPR spills): {bad}"
+
+
+def test_out_of_line_probe_needs_scratch(tmp_path):
+    """The mechanism behind the round-2 probe fault, read from a rebuilt probe (tools/
+    scratch_probe.hip): a VGPR value passed by reference to an out-of-line device function
+    lives in the private segment, which the callee reaches with flat accesses; the stack is
+    static (no dynamic stack)."""
+    co = tmp_path / "probe.co"
+    src = os.path.join(ROOT, "tools", "scratch_probe.hip")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "--no-gpu-bundle-output",
+                    "-c", src, "-o", str(co)], check=True, capture_output=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", str(co)], capture_output=True, text=True,
+                           check=True).stdout
+    meta = dict(l.strip().split(":", 1) for l in notes.splitlines() if l.strip().startswith((".private_segment", ".uses_dyn")))
+    assert int(meta[".private_segment_fixed_size"]) > 0 and meta[".uses_dynamic_stack"].strip() == "false", meta
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(co)], capture_output=True, text=True, check=True).stdout
+    assert "s_swappc_b64" in dis and "scratch_store_dword" in dis and "flat_load_dword" in dis
