@@ -83,6 +83,11 @@ struct cg_handle {
     uint8_t* d_large = nullptr;
     uint32_t* h_meta = nullptr;      // pinned: the large path's per-frame meta read
     uint32_t large_points = 0;
+    // a second large-frame scratch set: batches of several large frames pipeline over two
+    LgScratch lg2{};
+    uint8_t* d_large2 = nullptr;
+    uint32_t* h_meta2 = nullptr;
+    uint32_t large2_points = 0;
     LgScratch lg{};
     int route = 0;                // cg_debug_route
     unsigned long long* next_span = nullptr;   // cg_debug_launch_span
@@ -255,8 +260,8 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
 // The large-path scratch with the diagnostic route's settings applied: every entry point
 // that runs the large backend takes its copy from here, so a route set (or cleared) by
 // cg_debug_route reaches the tile and halo protocols too, whatever ran last.
-LgScratch route_scratch(cg_handle* h) {
-    LgScratch S = h->lg;
+LgScratch route_scratch(cg_handle* h, bool second = false) {
+    LgScratch S = second ? h->lg2 : h->lg;
     S.force_global = (h->route == 2 || h->route == 5) ? 1u : 0u;
     S.pcl_levels_cap = h->route == 5 ? 1u : 0u;
     return S;
@@ -278,6 +283,20 @@ int ensure_large(cg_handle* h, uint32_t n) {
 
 // Frames of <= CG_MAX_POINTS points run as one batch launch of the frame kernel; larger
 // frames (or every frame, under cg_debug_route) go through the multi-workgroup large path.
+int ensure_large2(cg_handle* h, uint32_t n) {
+    if (n <= h->large2_points && h->d_large2) return CG_OK;
+    if (h->d_large2) (void)hipFree(h->d_large2);
+    h->d_large2 = nullptr;
+    h->large2_points = 0;
+    HIPCHK(hipMalloc(&h->d_large2, cg_large_bytes(n)));
+    HIPCHK(hipMemset(h->d_large2, 0, cg_large_bytes(n)));
+    cg_large_layout(h->d_large2, n, h->lg2);
+    if (!h->h_meta2) HIPCHK(hipHostMalloc((void**)&h->h_meta2, LG_META_WORDS * 4, hipHostMallocDefault));
+    h->lg2.hmeta = h->h_meta2;
+    h->large2_points = n;
+    return CG_OK;
+}
+
 int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream_t s_back = nullptr) {
     const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2 || h->route == 5) && L.n_points > 0);
     if (!large && L.split) {
@@ -309,6 +328,13 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream
     int rc = ensure_large(h, L.n_points);
     if (rc) return rc;
     L.stamps = nullptr;
+    if (L.n_frames > 1 && kmode != CG_KMODE_GROUND) {   // two scratch sets: frames pipelined
+        rc = ensure_large2(h, L.n_points);
+        if (rc) return rc;
+        const LgScratch S2 = route_scratch(h, true);
+        HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, &S2));
+        return CG_OK;
+    }
     HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s));
     return CG_OK;
 }
@@ -532,6 +558,8 @@ int cg_destroy(cg_handle* h) {
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->h_meta) (void)hipHostFree(h->h_meta);
     if (h->d_large) (void)hipFree(h->d_large);
+    if (h->h_meta2) (void)hipHostFree(h->h_meta2);
+    if (h->d_large2) (void)hipFree(h->d_large2);
     if (h->d_cn_w) (void)hipFree(h->d_cn_w);
     if (h->d_cn_pts) (void)hipFree(h->d_cn_pts);
     if (h->d_cn_offs) (void)hipFree(h->d_cn_offs);

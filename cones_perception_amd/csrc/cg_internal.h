@@ -186,7 +186,8 @@ uint64_t cg_large_bytes(uint32_t n_points);
 uint32_t cg_large_pq_words();   // words of the PCL sort's range lists (diagnostics)
 void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
 // Run n_frames frames of more than CG_MAX_POINTS points, one at a time (synchronises s).
-int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s);
+int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
+                 const LgScratch* S2 = nullptr);
 // The phases of cg_run_large for one frame f (also the tiles of cg_tile_*):
 //   front: meta init + pass 1 (ground-only mode: the whole ground output);
 //   decide: thresholds from meta, pass 2, candidates -> survivors (pipeline mode);

@@ -1626,14 +1626,21 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
 #ifndef LG_PQ_SPARE
 #define LG_PQ_SPARE 3   // partition levels beyond an even split's, for uneven median-of-three cuts
 #endif
+static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScratch S, hipStream_t s,
+                              uint32_t f, uint32_t N, uint32_t K, const uint32_t* hm);
 int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t N, uint32_t K) {
-    CgDevParams P = P0;
     hipError_t e;
     uint32_t hstack[LG_META_WORDS];
     uint32_t* const hm = S.hmeta ? S.hmeta : hstack;   // pinned when the handle has one
     if ((e = hipMemcpyAsync(hm, S.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = cg_stream_wait(s)) != hipSuccess) return e;
+    return large_backend_from(L, P0, kmode, S, s, f, N, K, hm);
+}
+// The backend's launches, sized from the frame's meta words already on the host (hm).
+static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScratch S, hipStream_t s,
+                              uint32_t f, uint32_t N, uint32_t K, const uint32_t* hm) {
+    CgDevParams P = P0;
     const uint32_t Ms = hm[LG_MS];
     if (K == CG_K_FROM_META) K = hm[LG_K];   // pipeline frames: the ground stage's kept count
     const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
@@ -1739,10 +1746,42 @@ int cg_large_backend(const CgLaunch& L, const CgDevParams& P0, int kmode, LgScra
 // ------------------------------------------------------------------------------------------
 // Host driver: one frame at a time on stream s. Synchronises once per frame: the survivor
 // count and bounds size the backend launches.
-int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s) {
+//
+// With a second scratch set (S2, several detector frames) the frames are software-pipelined:
+// frame f + 1's front and decide are enqueued before frame f's backend, on the other set, so
+// the stream holds work while the host reads frame f's counts and sizes its backend. The
+// stream order keeps every set's reads before its next writes (frame f + 2's front follows
+// frame f's backend).
+int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, const LgScratch* S2) {
     const uint32_t N = L.n_points;
     hipError_t e;
     S.pidx_base = 0;
+    if (S2 && L.n_frames > 1 && kmode != CG_KMODE_GROUND && S.hmeta && S2->hmeta) {
+        LgScratch set[2] = {S, *S2};
+        set[1].pidx_base = 0;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        for (int k = 0; k < 2; k++)
+            if ((e = hipEventCreateWithFlags(&ev[k], hipEventDisableTiming)) != hipSuccess) return e;
+        auto fetch = [&](uint32_t f) -> hipError_t {
+            LgScratch& Q = set[f & 1];
+            hipError_t r;
+            if ((r = (hipError_t)cg_large_front(L, P, kmode, Q, s, f, true)) != hipSuccess) return r;
+            if (kmode == CG_KMODE_PIPELINE && (r = (hipError_t)cg_large_decide(L, P, Q, s, f)) != hipSuccess) return r;
+            if ((r = hipMemcpyAsync(Q.hmeta, Q.meta, LG_META_WORDS * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return r;
+            return hipEventRecord(ev[f & 1], s);
+        };
+        e = fetch(0);
+        for (uint32_t f = 0; f < L.n_frames && e == hipSuccess; f++) {
+            if (f + 1 < L.n_frames && (e = fetch(f + 1)) != hipSuccess) break;
+            if ((e = hipEventSynchronize(ev[f & 1])) != hipSuccess) break;
+            uint32_t hm[LG_META_WORDS];   // frame f + 2's copy lands in this buffer after the backend below
+            std::memcpy(hm, set[f & 1].hmeta, sizeof(hm));
+            const uint32_t K = kmode == CG_KMODE_PIPELINE ? CG_K_FROM_META : N;
+            e = (hipError_t)large_backend_from(L, P, kmode, set[f & 1], s, f, N, K, hm);
+        }
+        for (int k = 0; k < 2; k++) (void)hipEventDestroy(ev[k]);
+        return e;
+    }
     for (uint32_t f = 0; f < L.n_frames; f++) {
         if ((e = (hipError_t)cg_large_front(L, P, kmode, S, s, f, true)) != hipSuccess) return e;
         if (kmode == CG_KMODE_GROUND) continue;

@@ -159,3 +159,21 @@ def test_pcl_sort_hbm_leaves_beyond_16_bit_counts(params):
     det.debug_route(0)    # the route cleared: the next frame takes every partition level again
     got = det.cloud_handler(msg)
     assert_same_detection(got, ref, "C5 detect after route 5")
+
+
+@pytest.mark.parametrize("mode", ["pipeline", "detect"])
+def test_large_batch_pipelined_over_two_scratch_sets(params, mode):
+    """Several large frames in one batch: frame f + 1's front runs on the second scratch set
+    while the host sizes frame f's backend (cg_run_large); every frame bit-exact, in both the
+    LDS and the global backend."""
+    import torch
+    raw = np.concatenate([cp.synth_frames(1, first_frame=20 + f, rings=128, cols=1024, clutter=c, cones_per_row=8)
+                          for f, c in enumerate((0, 60, 0, 200, 20))])
+    eng = cp.BatchEngine(params)
+    d = torch.from_numpy(raw).cuda()
+    m = cp.CG_MODE_PIPELINE if mode == "pipeline" else cp.CG_MODE_DETECT
+    for rep in range(2):   # the sets are reused by the next batch
+        eng.run(d.data_ptr(), raw.shape[0], 128 * 1024, 16, mode=m)
+        for f in range(raw.shape[0]):
+            ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE if mode == "pipeline" else O.MODE_DETECT)
+            assert_same_detection(eng.fetch(f), ref, f"pipelined batch {rep} frame {f}")
