@@ -203,6 +203,39 @@ def _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step
     return total, sizes, sp[:ns], si[:ns]
 
 
+def _tile_front_decide_dev(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets):
+    """_tile_front_decide with the keys and counts on the device (cg_tile_*_async on the
+    engine's tile stream, as the gather form): one host read, of the merged counts (every
+    rank's survivor count sizes its survivor buffer), and the survivors complete on return
+    (the cg_halo_* calls run on the handle's own stream)."""
+    import ctypes as C
+    import numpy as np
+    from . import _abi
+    lib, h = _abi.lib(), engine.handle
+    st = _tile_stream(engine, device)
+    st.wait_stream(torch.cuda.current_stream(device))   # the tile's points
+    s = st.cuda_stream
+    with torch.cuda.stream(st):
+        t = _abi.cg_tile(d_tile_ptr, first, n, n_total, point_step, *offsets)
+        keys = torch.empty(_abi.CG_TILE_KEYS, dtype=torch.int32, device=device)
+        _abi.check(lib.cg_tile_front_async(h, C.byref(t), keys.data_ptr(), s))
+        merged = merge_tile_keys_dev(keys, device)
+        counts = torch.empty(_abi.CG_TILE_COUNTS, dtype=torch.int32, device=device)
+        _abi.check(lib.cg_tile_decide_async(h, merged.data_ptr(), counts.data_ptr(), s))
+        if _distributed():
+            total, sizes = merge_tile_counts_dev(counts, device)
+            ns = sizes[dist.get_rank()]
+        else:
+            total = counts.cpu().numpy().view(np.uint32).copy()
+            sizes = [int(total[1])]
+            ns = sizes[0]
+        sp = torch.empty((max(ns, 1), 4), dtype=torch.float32, device=device)
+        si = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
+        _abi.check(lib.cg_tile_survivors_async(h, sp.data_ptr(), si.data_ptr(), ns, s))
+    st.synchronize()
+    return total, sizes, sp[:ns], si[:ns]
+
+
 def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, device, point_step: int = 16,
                     offsets=(0, 4, 8, 12), dst: int = 0, halo: bool = False, fetch: bool = True):
     """Pipeline one frame of n_total points whose points [first, first + n) are at d_tile_ptr
@@ -214,7 +247,8 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
     and returns True on dst."""
     from . import _abi
     if halo:
-        total, sizes, sp, si = _tile_front_decide(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets)
+        total, sizes, sp, si = _tile_front_decide_dev(engine, d_tile_ptr, first, n, n_total, device, point_step,
+                                                      offsets)
         det = run_halo_backend(engine, total, sp, si, n_total, device, dst, fetch=fetch)
         if det is not False:
             return det
@@ -365,10 +399,10 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
             halo = hbuf.to(device)
     pairs = torch.empty((max(4 * halo.shape[0], 64), 2), dtype=torch.int32, device=device)
     npairs = C.c_uint32(0)
-    for _ in range(2):   # once more with room for every pair when the first guess was short
+    for _ in range(2 if halo.shape[0] and top.shape[0] else 0):   # no halo rows (the top slab, one rank): no edges
         _abi.check(lib.cg_halo_edges(h, top.data_ptr(), top.shape[0], halo.data_ptr(), halo.shape[0],
                                      pairs.data_ptr(), pairs.shape[0], C.byref(npairs)))
-        if npairs.value <= pairs.shape[0]:
+        if npairs.value <= pairs.shape[0]:   # once more with room for every pair when the first guess was short
             break
         pairs = torch.empty((npairs.value, 2), dtype=torch.int32, device=device)
     pairs = pairs[: npairs.value]
