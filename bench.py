@@ -73,9 +73,9 @@ def main():
     ap.add_argument("--split-streams", default="",
                     help="F,B: each batch's front launch on one of F front streams and its backend launches on "
                          "one of B back streams (cg_run_batch_split); --streams engines rotate over them")
-    ap.add_argument("--fused", action="store_true",
-                    help="experiment: each frame in one fused workgroup (cg_debug_route 6) instead of the front "
-                         "launch + backend launches")
+    ap.add_argument("--split", action="store_true",
+                    help="experiment: each batch as a front launch + backend launches (cg_debug_route 6) instead "
+                         "of one fused workgroup per frame")
     ap.add_argument("--voxel-order", choices=["pcl", "point"], default="pcl",
                     help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
                          "every voxel bit as the reference) or ascending point order")
@@ -138,7 +138,7 @@ def main():
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
     vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
     engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
-    if args.fused:
+    if args.split:
         for e in engines:
             e.debug_route(6)
     split_fb = [int(x) for x in args.split_streams.split(",")] if args.split_streams else None
@@ -201,7 +201,7 @@ def main():
     spans_ok = bool((sp[:, 0] < 2 ** 63 - 1).all() and (sp[:, 1] > sp[:, 0]).all())
     step_span_ms = float((sp[:, 1] - sp[:, 0]).mean()) * 1e-5 if spans_ok else avg_event_ms   # 100 MHz ticks
     front_ok = bool((sp[:, 2] < 2 ** 63 - 1).all() and (sp[:, 3] > sp[:, 2]).all())
-    split = front_ok   # front launch + backend launch (cg_debug_route 6: one fused kernel)
+    split = front_ok   # front launch + backend launches (--split / --split-streams; default: one fused kernel)
     avg_kernel_ms = float((sp[:, 3] - sp[:, 2]).mean()) * 1e-5 if split else step_span_ms
 
     # algorithmic bytes of one launch, from the frames' own V and C
@@ -295,7 +295,7 @@ def main():
                                    "simulation params), ground_removal + cone_detection fused",
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
-                       "launches": "fused frame kernel" if args.fused else "front + backend",
+                       "launches": "front + backend" if (args.split or args.split_streams) else "fused frame kernel",
                        "split_streams": args.split_streams or None,
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -501,6 +501,17 @@ def phase_stamps(eng, step, F, around=None, tag="alone"):
         out["gatherC barrier (wave0)"] = round(float(np.median((t[sub, 5] - t[sub, 26]) / 100.0)), 2)
     life = (t[:, 20] - t[:, 0]) / 100.0
     out["wg_lifetime_us_p10_p50_p90"] = [round(float(np.percentile(life, q)), 1) for q in (10, 50, 90)]
+    pct = lambda x: [round(float(np.percentile(x, q)), 1) for q in (0, 10, 50, 90, 100)]
+    both = (t[:, 6] > 0) & (t[:, 5] > 0) & (t[:, 20] > 0)
+    if both.sum() > 1:   # split batches: front (0-5) and backend (6-20) workgroups
+        t = t[both]
+        out["split_frames_stamped"] = int(both.sum())
+        base = t[:, 0].min()
+        out["front_start_us_pcts"] = pct((t[:, 0] - base) / 100.0)
+        out["front_us_pcts"] = pct((t[:, 5] - t[:, 0]) / 100.0)
+        out["back_start_us_pcts"] = pct((t[:, 6] - base) / 100.0)
+        out["back_us_pcts"] = pct((t[:, 20] - t[:, 6]) / 100.0)
+        out["back_end_us_pcts"] = pct((t[:, 20] - base) / 100.0)
     print("STAMPS " + json.dumps(out), flush=True)
 
 
@@ -558,6 +569,7 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
 def c5_single_gpu(cp, params, device, reps=50, order=None, batch=8, breps=6):
     """C5's frame shape on one GPU, device-resident: one 1M-point dense frame per call of the
     batch engine (large-frame path; the call synchronises once the frame is done)."""
+    import numpy as np
     import torch
     raw = cp.synth_frames(1, first_frame=0, rings=128, cols=8192, clutter=60, cones_per_row=12)
     d = torch.from_numpy(raw).to(torch.device("cuda", device))
@@ -583,8 +595,8 @@ def c5_single_gpu(cp, params, device, reps=50, order=None, batch=8, breps=6):
            "includes": "device-resident input; one frame per call: one host round trip per frame (survivor "
                        "count and bounds size the backend); backend latency-bound (sorts, union-find)"}
     if batch > 1:   # a stream of C5 frames: batches of distinct frames, pipelined over two scratch sets
-        fr = cp.synth_frames(batch, first_frame=0, rings=128, cols=8192, clutter=60, cones_per_row=12)
-        db = torch.from_numpy(fr).to(torch.device("cuda", device))
+        # the same frame in `batch` distinct buffers: per-frame cost comparable with the leg above
+        db = torch.from_numpy(np.repeat(raw, batch, axis=0)).to(torch.device("cuda", device))
         for _ in range(2):
             eng.run(db.data_ptr(), batch, n, 16, stream=st.cuda_stream)
         st.synchronize()
@@ -594,8 +606,9 @@ def c5_single_gpu(cp, params, device, reps=50, order=None, batch=8, breps=6):
         st.synchronize()
         bt = (time.perf_counter() - t0) / (breps * batch)
         out["stream_of_frames"] = {"ms_per_frame": bt * 1e3, "frames_per_s": 1.0 / bt, "frames_per_call": batch,
-                                   "includes": f"{breps} calls of {batch} distinct 1M-point frames each; frame f+1's "
-                                               "front overlaps the host sizing frame f's backend"}
+                                   "includes": f"{breps} calls of {batch} 1M-point frames each (copies of the frame above "
+                                               "in distinct buffers); frame f+1's front overlaps the host "
+                                               "sizing frame f's backend"}
     return out
 
 

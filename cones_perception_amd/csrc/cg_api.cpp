@@ -304,7 +304,7 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream
         return CG_OK;
     }
     if (!large) {
-        if (s_back && s_back != s && h->route != 6) {
+        if (s_back && s_back != s) {
             // the front on s; the backend launches on s_back once the front is done; the next
             // front of this handle waits for them (cg_run_batch_split)
             if (!h->ev_front) HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
@@ -322,7 +322,8 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream
             HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
             h->back_stream_pending = nullptr;
         }
-        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s, h->route == 6));
+        // one fused workgroup per frame; cg_debug_route 6: the front launch + backend launches
+        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s, h->route != 6));
         return CG_OK;
     }
     int rc = ensure_large(h, L.n_points);

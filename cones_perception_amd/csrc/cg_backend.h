@@ -113,9 +113,11 @@ __device__ __forceinline__ Work global_work(uint8_t* base, uint32_t n) {
 // for point indices of a 64k frame; fewer when W.IDX holds ranks).
 // lds_cap: the LDS capacity when W is in LDS (the out-of-place sort buffer starts at VOX's
 // second half, E + lds_cap).
+// bail_v: a frame with more voxels than this stops after its voxel centroids and joins the
+// split batch's large-capacity list (L.biglist) instead (0: never); uniform per workgroup.
 __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* fs, const CgLaunch& L,
                                         const CgDevParams& P, uint32_t f, uint32_t flags, uint32_t nbw,
-                                        uint32_t lds_cap) {
+                                        uint32_t lds_cap, uint32_t bail_v = 0) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     uint32_t* red = fs->red;
     // ---- voxel grid: getMinMax3D (finite points; bounds gathered by the frontend) ----
@@ -238,6 +240,13 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         __syncthreads();
     }
     STAMP(10);
+    if (bail_v && V > bail_v) {   // all-pairs clustering here stops at bail_v voxels: cg_back_big
+        if (tid == 0) {
+            const uint32_t q = atomicAdd(&L.biglist[0], 1u);
+            L.biglist[2 + q] = f;
+        }
+        return;
+    }
     // ---- Euclidean clustering over the V voxel points ----
     uint32_t C = 0;
     if (V > 0) {
@@ -641,6 +650,8 @@ __device__ __forceinline__ void back_frame(const CgLaunch& L, const CgDevParams&
             W.IDX[j] = 0xffffu;
         }
         __syncthreads();
-        backend(W, M, fs, L, P, f, 0u, RANK ? (Ms + 32) / 32 : CG_MAX_POINTS / 32, CAP);
+        // the 256-lane launch's all-pairs clustering covers CG_BRUTE_V voxels (its adjacency rows
+        // overlay KEY); a frame with more goes on to cg_back_big
+        backend(W, M, fs, L, P, f, 0u, RANK ? (Ms + 32) / 32 : CG_MAX_POINTS / 32, CAP, RANK ? CG_BRUTE_V : 0u);
     }
 }

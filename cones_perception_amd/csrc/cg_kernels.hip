@@ -557,8 +557,8 @@ int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScr
 
 // ------------------------------------------------------------------------------------------
 // Launchers.
-// Detector batches (pipeline, detect) run as the front launch plus the backend launch
-// (cg_back.hip) unless `fused` (cg_debug_route 6: the whole frame in one workgroup).
+// Detector batches (pipeline, detect): one fused workgroup per frame, or (not `fused`,
+// cg_debug_route 6 / cg_run_batch_split) the front launch plus the backend launches.
 template <int PPT, int LAYOUT>
 static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused) {
     const dim3 grid(L.n_frames), block(CG_BLOCK);

@@ -160,7 +160,8 @@ int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream);
  * batch's front (another handle's, on another front stream). The results are complete when
  * back_stream reaches this call's work (cg_batch_fetch waits there); this handle's next batch
  * waits for these backends before its front reuses their inputs. Other batches run as in
- * cg_run_batch on front_stream. */
+ * cg_run_batch on front_stream. (Measured slower than cg_run_batch's fused frames on C3:
+ * DESIGN.md (d); kept for callers whose frames carry heavier backends.) */
 int cg_run_batch_split(cg_handle* h, const cg_batch* b, int mode, void* front_stream, void* back_stream);
 
 /* Per-frame header words in the device result buffer. */
@@ -372,8 +373,8 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * calls in one workgroup instead of the per-chunk split launch (3), or split with the input
  * copied by DMA instead of read by the kernel from pinned memory (4); the global backend with
  * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
- * are finished in HBM side by side (5); batch frames of <= 65,536 points in one fused
- * workgroup per frame instead of the front launch + backend launch (6); 0 = automatic. */
+ * are finished in HBM side by side (5); detector batches of <= 65,536-point frames as a front
+ * launch plus backend launches instead of one fused workgroup per frame (6); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

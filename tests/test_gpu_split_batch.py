@@ -1,7 +1,8 @@
-"""Batch frames as two launches (cg_launch_batch): the streaming front (pass 1, thresholds,
-pass 2, survivors to the frame's HBM slot) and the 256-lane backend launch (cg_back.hip).
-Every frame bit-exact against the oracle in PCL's voxel order, and identical to the fused
-one-workgroup-per-frame kernel (cg_debug_route 6), across the backend launch's branches:
+"""Batch frames as a front launch plus backend launches (cg_debug_route 6, cg_run_batch_split):
+the streaming front (pass 1, thresholds, pass 2, survivors to the frame's HBM slot), the
+256-lane backend launch (cg_back.hip) and the 512-lane one for the frames it hands on.
+Every frame bit-exact against the oracle in PCL's voxel order, and identical to the default
+fused one-workgroup-per-frame kernel, across the backend launches' branches:
 LDS (M <= 392) with all-pairs (V <= 128) or neighbour-grid clustering, the HBM slot (M > 392),
 zero pads, C1-sized frames (32 points per lane), the detector-only mode and the known-answer
 clouds as one-frame batches."""
@@ -39,8 +40,8 @@ def test_split_batch_matches_oracle_and_fused(over, rings):
     params = cp.load_params("simulation", over)
     raw = _mixed(rings)
     n = rings * 1024
-    split = _run(params, raw, n)
-    fused = _run(params, raw, n, route=6)
+    split = _run(params, raw, n, route=6)
+    fused = _run(params, raw, n)
     ms, vs = [], []
     for f in range(raw.shape[0]):
         ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE, O.ORDER_PCL)
@@ -56,7 +57,7 @@ def test_split_batch_matches_oracle_and_fused(over, rings):
 def test_split_batch_detector_mode():
     params = cp.load_params("simulation")
     raw = _mixed()
-    got = _run(params, raw, 65536, mode=cp.CG_MODE_DETECT)
+    got = _run(params, raw, 65536, mode=cp.CG_MODE_DETECT, route=6)
     for f in range(raw.shape[0]):
         ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_DETECT, O.ORDER_PCL)
         assert_same_detection(got[f], ref, f"detect batch frame {f}")
@@ -67,7 +68,7 @@ def test_split_batch_point_order():
     raw = _mixed()
     import torch
     d = torch.from_numpy(raw).cuda()
-    eng = cp.BatchEngine(params).set_voxel_order(cp.CG_VOXEL_ORDER_POINT)
+    eng = cp.BatchEngine(params).set_voxel_order(cp.CG_VOXEL_ORDER_POINT).debug_route(6)
     eng.run(d.data_ptr(), raw.shape[0], 65536, 16)
     torch.cuda.synchronize()
     for f in range(raw.shape[0]):
@@ -84,7 +85,7 @@ def test_kats_as_one_frame_batches(kat):
     n = raw.shape[1] // 16
     if n == 0 or n > 65536:
         pytest.skip("batch frames hold 1-65,536 points")
-    got = _run(params, raw, n)[0]
+    got = _run(params, raw, n, route=6)[0]
     ref, _ = O.run(params, msg, O.MODE_PIPELINE, O.ORDER_PCL)
     assert_same_detection(got, ref, f"{name} as a batch")
 
