@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "gpurun_out", "prof")
 RND = sys.argv[1] if len(sys.argv) > 1 else "r1"
 DST = os.path.join(ROOT, "profiles")
-KERNEL = "cg_frame_kernel<128, 1, 0, false>"   # the batch instantiation (SPLIT = false)
+KERNEL = "cg_frame_kernel<128, 1, 0>("   # the batch instantiation (pipeline, xyzi16)
 
 
 def one(pattern):
