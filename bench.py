@@ -76,6 +76,9 @@ def main():
     ap.add_argument("--split", action="store_true",
                     help="experiment: each batch as a front launch + backend launches (cg_debug_route 6) instead "
                          "of one fused workgroup per frame")
+    ap.add_argument("--pair", action="store_true",
+                    help="experiment: each frame as two half-frame workgroups (cg_debug_route 7, cg_pair.hip) "
+                         "instead of one fused workgroup per frame")
     ap.add_argument("--voxel-order", choices=["pcl", "point"], default="pcl",
                     help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
                          "every voxel bit as the reference) or ascending point order")
@@ -138,9 +141,9 @@ def main():
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
     vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
     engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
-    if args.split:
+    if args.split or args.pair:
         for e in engines:
-            e.debug_route(6)
+            e.debug_route(6 if args.split else 7)
     split_fb = [int(x) for x in args.split_streams.split(",")] if args.split_streams else None
     if split_fb:   # F front streams, B back streams
         streams = [torch.cuda.Stream(dev) for _ in range(split_fb[0])]
@@ -295,16 +298,18 @@ def main():
                                    "simulation params), ground_removal + cone_detection fused",
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
-                       "launches": "front + backend" if (args.split or args.split_streams) else "fused frame kernel",
+                       "launches": "front + backend" if (args.split or args.split_streams) else
+                       ("half-frame pair kernel" if args.pair else "fused frame kernel"),
                        "split_streams": args.split_streams or None,
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),
-                         "kernel": "cg_front_kernel" if split else "cg_frame_kernel",
+                         "kernel": "cg_front_kernel" if split else ("cg_pair_kernel" if args.pair else "cg_frame_kernel"),
                          "avg_kernel_ms": avg_kernel_ms,
                          "avg_kernel_ms_source": "in-kernel span (s_memrealtime)" if spans_ok else "HIP events",
                          # the step's device work: front launch start to backend launch end
                          "step_span_ms": step_span_ms,
+                         "step_span_ms_max": float((sp[:, 1] - sp[:, 0]).max()) * 1e-5 if spans_ok else None,
                          "step_span_frac": bytes_per_launch / (step_span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "avg_launch_ms_events": avg_event_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch,
@@ -317,6 +322,8 @@ def main():
                          / HBM_COPY_GBS},
             "cpu_baseline": cpu,
             "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+            # the pair launch's never-expected wait timeouts, in the last batch's frame flags
+            "pair_timeouts": int(((hdr_np[:, 5] & 0x10) != 0).sum()) if args.pair else None,
         }
         if single is not None:
             line["single_frame"] = single

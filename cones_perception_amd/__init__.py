@@ -19,7 +19,7 @@ import numpy as np
 from . import _abi
 from ._abi import (CG_VOXEL_ORDER_PCL, CG_VOXEL_ORDER_POINT, CG_F_VOXEL_POINT_ORDER,  # noqa: F401
                    CG_MODE_DETECT, CG_MODE_PIPELINE, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL,
-                   CG_F_VOXEL_PASSTHROUGH, CgError, check, lib)
+                   CG_F_VOXEL_PASSTHROUGH, CG_F_PAIR_TIMEOUT, CgError, check, lib)
 
 lib()   # fail loudly at import if the gfx950 library is missing
 

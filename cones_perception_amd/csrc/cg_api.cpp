@@ -90,6 +90,7 @@ struct cg_handle {
     uint32_t large2_points = 0;
     LgScratch lg{};
     int route = 0;                // cg_debug_route
+    uint32_t pair_epoch = 0;      // pair launches so far (cg_pair.hip ready words)
     unsigned long long* next_span = nullptr;   // cg_debug_launch_span
     unsigned long long* next_front_span = nullptr;   // cg_debug_front_span
     cg_tile tile{};               // the rank's tile (cg_tile_front .. cg_tile_decide)
@@ -173,6 +174,10 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     // the frame kernel's HBM fallback (M > CG_MMAX) serves frames of <= CG_MAX_POINTS points
     h->scratch_stride = (cg_scratch_bytes(std::min<uint32_t>(np, CG_MAX_POINTS)) + 255) & ~255ull;
     HIPCHK(hipMalloc(&h->d_scratch, F * h->scratch_stride));
+    HIPCHK(hipMemset(h->d_scratch, 0, F * h->scratch_stride));   // the pair launch's exchange words
+    // the zeroed words before any launch on the caller's (non-blocking) streams
+    HIPCHK(hipStreamSynchronize(nullptr));
+    h->pair_epoch = 0;
     if (had_ground) HIPCHK(hipMalloc(&h->d_ground, F * C * 32));
     h->cap_frames = nf;
     h->cap_points = np;
@@ -321,6 +326,14 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream
         if (h->back_stream_pending) {   // a split batch's backend may still read the survivor slots
             HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
             h->back_stream_pending = nullptr;
+        }
+        if (h->route == 7 && kmode == CG_KMODE_PIPELINE && L.n_points > CG_MAX_POINTS / 2) {
+            // two half-frame workgroups per frame (cg_pair.hip); no phase stamps (they are
+            // indexed by workgroup, and this grid has twice as many as the buffer has frames)
+            L.epoch = ++h->pair_epoch;
+            L.stamps = nullptr;
+            HIPCHK((hipError_t)cg_launch_pair(L, h->dp, s));
+            return CG_OK;
         }
         // one fused workgroup per frame; cg_debug_route 6: the front launch + backend launches
         HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s, h->route != 6));
@@ -1173,7 +1186,7 @@ int cg_debug_front_span(cg_handle* h, void* d_span) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 6) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 7) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

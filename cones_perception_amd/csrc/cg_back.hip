@@ -39,3 +39,28 @@ int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
     hipLaunchKernelGGL(cg_back_kernel, dim3(L.n_frames), dim3(CG_BLOCK), 0, s, L, P);
     return hipGetLastError();
 }
+
+// Pair batches (cg_pair.hip): the listed frames of more than CG_MMAX detector points, the
+// backend on their HBM slots (cg_back_big then takes the listed frames up to CG_MMAX and clears
+// the list).
+#define BACK_LIST_GRID 32
+// 32 workgroups: registers for 2 waves per SIMD, no spills
+__global__ __launch_bounds__(CG_BLOCK, 2) void cg_back_list_kernel(CgLaunch L, CgDevParams P) {
+    __shared__ FrontShared fs;
+    const uint32_t* const list = L.biglist;
+    const uint32_t n = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma clang loop unroll(disable)
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t f = list[2 + i];
+        const uint32_t* const rec = (const uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(L.n_points));
+        if (rec[CG_FREC_M] <= CG_MMAX) continue;
+        back_frame<0>(L, P, f, &fs, nullptr);
+        __syncthreads();
+    }
+    if (L.span && threadIdx.x == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+int cg_launch_back_list(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
+    hipLaunchKernelGGL(cg_back_list_kernel, dim3(BACK_LIST_GRID), dim3(CG_BLOCK), 0, s, L, P);
+    return hipGetLastError();
+}

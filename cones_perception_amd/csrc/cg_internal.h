@@ -95,7 +95,13 @@ struct CgLaunch {
     // split launch: the frame in pinned host memory; each chunk workgroup copies its chunk to
     // `in` (the device copy) before pass 1, or null (`in` already holds the frame)
     const uint8_t* in_host;
+    // pair launch (cg_pair.hip): this batch's number, the value of a frame's ready word once
+    // its first half has published (the words start zeroed; a handle's batches count from 1)
+    uint32_t epoch;
 };
+// The pair launch's exchange area: the last CG_PAIR_X_BYTES of each frame's scratch slot
+// (header words, a half's z codes, its filter bits), zeroed when the slots are allocated.
+#define CG_PAIR_X_BYTES (128 + CG_MAX_POINTS / 2 + 2 * 256 * 8 + 128)
 // A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
 // for pass 1; the last chunk to finish runs the rest of the frame kernel. State words: [0]
 // finished chunks, [1] used sector bins, [2, 20) sector-minimum keys (all reset by the last
@@ -232,6 +238,13 @@ int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 // the halves of a split detector batch (frames of <= CG_MAX_POINTS points)
 int cg_launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
 int cg_launch_backends(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
+// Pipeline batches of frames of CG_MAX_POINTS / 2 < n <= CG_MAX_POINTS points as two half-frame
+// workgroups per frame (cg_pair.hip, cg_debug_route 7); frames of more detector points than
+// the pair kernel's LDS backend holds are listed (L.biglist) for cg_launch_back_list (HBM
+// slot, > CG_MMAX) and cg_launch_back_big (LDS, <= CG_MMAX; clears the list), launched after it.
+int cg_launch_pair(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
+int cg_launch_back_list(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
+int cg_launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 // Cone re-crop (cg_recrop.hip): exact float form of the reference's double box compares.
 struct RcBox { float lox, hix, loy, hiy; };
 #define CG_RECROP_MAX_BOXES 256   // boxes per launch (more: several launches)

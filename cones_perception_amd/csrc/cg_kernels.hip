@@ -56,7 +56,8 @@ static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overla
 static_assert(CG_MAX_POINTS / 64 * sizeof(uint32_t) <= CG_MAX_POINTS, "ground counts fit the code area");
 
 uint64_t cg_scratch_bytes(uint32_t n) {
-    const uint64_t b = cg_work_bytes(n) + 256;   // the work arrays, then the front record
+    // the work arrays, the front record, then the pair launch's exchange area at the slot's end
+    const uint64_t b = cg_work_bytes(n) + 256 + CG_PAIR_X_BYTES;
 #ifdef CG_CODES_HBM
     return b > CG_MAX_POINTS ? b : (uint64_t)CG_MAX_POINTS;   // the codes overlay it until compaction
 #else
@@ -479,7 +480,11 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void cg_back_big_kernel(CgLaunch L, Cg
     const uint32_t n = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma clang loop unroll(disable)
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        back_frame<CG_MMAX>(L, P, list[2 + i], (FrontShared*)smem, (BackLds*)(smem + FRONT_BYTES));
+        const uint32_t f = list[2 + i];
+        // the pair launch also lists frames past CG_MMAX: cg_back_list_kernel ran them on the slot
+        const uint32_t* const rec = (const uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(L.n_points));
+        if (rec[CG_FREC_M] > CG_MMAX) continue;
+        back_frame<CG_MMAX>(L, P, f, (FrontShared*)smem, (BackLds*)(smem + FRONT_BYTES));
         __syncthreads();
     }
     if (threadIdx.x == 0) {
@@ -495,6 +500,7 @@ static hipError_t launch_back_big(const CgLaunch& L, const CgDevParams& P, hipSt
     hipLaunchKernelGGL(cg_back_big_kernel, dim3(BACK_BIG_GRID), dim3(CG_BLOCK), 0, s, L, P);
     return hipGetLastError();
 }
+int cg_launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s) { return launch_back_big(L, P, s); }
 
 // ------------------------------------------------------------------------------------------
 // Large frames whose detector input fits the LDS path (M <= CG_MMAX): the survivors come from

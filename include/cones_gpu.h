@@ -39,6 +39,10 @@ extern "C" {
                                         std::sort may order equal-size clusters differently */
 #define CG_F_VOXEL_POINT_ORDER 0x8u  /* voxel sums ran in ascending point order, not in PCL's
                                         std::sort order (cg_set_voxel_order, the halo form) */
+#define CG_F_PAIR_TIMEOUT      0x10u /* diagnostic (cg_debug_route 7): the frame's second half
+                                        gave up waiting for the first's data after 100 ms; the
+                                        result is invalid. Never expected: the first half is
+                                        running whenever the second waits */
 
 /* ---- parameters --------------------------------------------------------------------- */
 /* Field names are the YAML keys, misspellings kept (config/ *.yaml). */
@@ -374,7 +378,8 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * copied by DMA instead of read by the kernel from pinned memory (4); the global backend with
  * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
  * are finished in HBM side by side (5); detector batches of <= 65,536-point frames as a front
- * launch plus backend launches instead of one fused workgroup per frame (6); 0 = automatic. */
+ * launch plus backend launches instead of one fused workgroup per frame (6); pipeline batches
+ * of 32,769-65,536-point frames as two half-frame workgroups per frame (7); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */
