@@ -10,11 +10,12 @@ over ranks is reported.
 
 The roofline object prices the dominant kernel by the algorithmic bytes B = 16 N + 20 V + 8 C
 + 64 per frame over its average execution span, which the kernel stamps itself
-(s_memrealtime: first workgroup start to last workgroup end, cg_debug_front_span). A batch is
-two launches on one stream: cg_front_kernel (pass 1, thresholds, pass 2, the survivors: every
-input byte) and cg_back_kernel (voxel grid, clustering, centroids on ~240 points per frame);
-the front is the dominant kernel, and the pair's span is reported beside it (step_span_ms). cpu_baseline times the CPU restatement
-(oracle/, single core, same frames) on a bounded sample on rank 0 (any N).
+(s_memrealtime: first workgroup start to last workgroup end, cg_debug_launch_span). A batch is
+one launch of the fused frame kernel, cg_frame_kernel: one workgroup per frame. The
+diagnostic structures --split (front launch + backend launches; the front is then the priced
+kernel, cg_debug_front_span) and --pair (two half-frame workgroups per frame) are measured
+slower. cpu_baseline times the CPU restatement (oracle/, one core and the job's CPU share,
+same frames) on a bounded sample on rank 0.
 
 `--gpus N` without a launcher environment starts N ranks itself (torch.distributed.run on
 127.0.0.1, before any GPU call); under a launcher WORLD_SIZE must equal N. At N > 1 the C4
