@@ -458,8 +458,8 @@ def fetch_headers(res, F):
     return out
 
 
-STAMP_NAMES = ["start", "pass1 stream", "thresholds", "pass2 keep bits", "compaction scan",
-               "pass3 gather", "voxel minmax", "voxel keys", "voxel sort", "voxel runs",
+STAMP_NAMES = ["start", "pass1 stream", "thresholds", "pass2 codes", "survivor loads + ambiguous",
+               "pads + bounds", "voxel minmax", "voxel keys", "voxel sort", "voxel runs",
                "voxel centroids", "cluster adjacency", "cluster forest", "cluster roots", "cluster sizes",
                "cluster keep scan", "cluster order", "csr offsets", "labels", "csr indices",
                "centroids+header"]
@@ -503,10 +503,10 @@ def phase_stamps(eng, step, F, around=None, tag="alone"):
         out["clusterC flatten"] = round(float(np.median((t[sub, 24] - t[sub, 23]) / 100.0)), 2)
         out["clusterD cross unions"] = round(float(np.median((t[sub, 12] - t[sub, 24]) / 100.0)), 2)
     sub = (t[:, 25] > 0) & (t[:, 26] > 0)
-    if sub.any():   # gather (wave 0): survivor loads, pads + bounds, barrier wait
-        out["gatherA loads (wave0)"] = round(float(np.median((t[sub, 25] - t[sub, 4]) / 100.0)), 2)
-        out["gatherB bounds (wave0)"] = round(float(np.median((t[sub, 26] - t[sub, 25]) / 100.0)), 2)
-        out["gatherC barrier (wave0)"] = round(float(np.median((t[sub, 5] - t[sub, 26]) / 100.0)), 2)
+    if sub.any():   # survivors (wave 0): its loads and appends, the barrier wait, pads + bounds
+        out["gatherA loads (wave0)"] = round(float(np.median((t[sub, 25] - t[sub, 3]) / 100.0)), 2)
+        out["gatherB barrier (wave0)"] = round(float(np.median((t[sub, 4] - t[sub, 25]) / 100.0)), 2)
+        out["gatherC pads+bounds (wave0)"] = round(float(np.median((t[sub, 26] - t[sub, 4]) / 100.0)), 2)
     life = (t[:, 20] - t[:, 0]) / 100.0
     out["wg_lifetime_us_p10_p50_p90"] = [round(float(np.percentile(life, q)), 1) for q in (10, 50, 90)]
     pct = lambda x: [round(float(np.percentile(x, q)), 1) for q in (0, 10, 50, 90, 100)]

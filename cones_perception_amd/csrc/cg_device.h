@@ -593,17 +593,18 @@ __device__ __forceinline__ void sector_thresholds(const uint32_t* sec_key, uint3
 
 // Pass 2 over the lane's PPT points: codes(g) returns the lane's code word of group g (8
 // points). Two compares per code (zc_kept, zc_not_ground): c < qlo keeps, qlo <= c <= qhi is
-// ambiguous, c > qhi is ground. Ambiguous points re-read x, y, z and compare exactly against their own sector's
-// threshold key. keep returns the lane's kept points (points past N excluded).
-template <int PPT, int LAYOUT, class CODES>
-__device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const CgLaunch& L,
-                                           const CgDevParams& P, uint32_t qlo, uint32_t qhi,
-                                           const uint32_t* tkey, CODES codes,
-                                           LaneBits<(PPT + 63) / 64>& keep) {
+// ambiguous, c > qhi is ground. Ambiguous points re-read x, y, z and compare exactly against
+// their own sector's threshold key. keep returns the lane's kept points (points past N
+// excluded).
+// pass2_codes is the part the codes settle: keep, and the ambiguous points in amb, with no
+// memory traffic past the codes. The caller resolves amb: pass2_keep below, or the frame
+// kernel's survivor loads, which load most of those points anyway.
+template <int PPT, class CODES>
+__device__ __forceinline__ void pass2_codes(uint32_t N, uint32_t qlo, uint32_t qhi, CODES codes,
+                                            LaneBits<(PPT + 63) / 64>& keep, LaneBits<(PPT + 63) / 64>& amb) {
     constexpr int NG = PPT / 8;
     constexpr int NW = (PPT + 63) / 64;
     const uint32_t tid = threadIdx.x;
-    LaneBits<NW> amb;
     keep.clear();
     amb.clear();
     // all of the lane's code words first, then the compares; bits accumulate as v = 2v + bit
@@ -634,6 +635,24 @@ __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const 
             amb.w[wi] &= vm;
         }
     }
+}
+// An ambiguous point's exact decision (src/ground_removal.cpp:75): its own sector's threshold key.
+__device__ __forceinline__ bool pass2_exact(const CgDevParams& P, const uint32_t* tkey, float x, float y, float z) {
+    int sx = 0;
+    bool unused = false;
+    classify_angle<true, false>(P, x, y, sx, unused);
+    return !(cg_zkey(z) < tkey[sx]);
+}
+template <int PPT, int LAYOUT, class CODES>
+__device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const CgLaunch& L,
+                                           const CgDevParams& P, uint32_t qlo, uint32_t qhi,
+                                           const uint32_t* tkey, CODES codes,
+                                           LaneBits<(PPT + 63) / 64>& keep) {
+    constexpr int NW = (PPT + 63) / 64;
+    const uint32_t tid = threadIdx.x;
+    LaneBits<NW> amb;
+    pass2_codes<PPT>(N, qlo, qhi, codes, keep, amb);
+    STAMP(21);
     // ambiguous: exact z and sector from HBM (rare: tens per frame), four loads in flight
 #pragma unroll
     for (int wi = 0; wi < NW; wi++) {
@@ -650,13 +669,8 @@ __device__ __forceinline__ void pass2_keep(const uint8_t* fb, uint32_t N, const 
             for (int q = 0; q < 4; q++)
                 if (ks[q] >= 0) pt[q] = load_xyz3<LAYOUT>(fb, (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid, L);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ks[q] < 0) continue;
-                int sx = 0;
-                bool unused = false;
-                classify_angle<true, false>(P, pt[q].x, pt[q].y, sx, unused);
-                if (!(cg_zkey(pt[q].z) < tkey[sx])) keep.w[wi] |= 1ull << ks[q];
-            }
+            for (int q = 0; q < 4; q++)
+                if (ks[q] >= 0 && pass2_exact(P, tkey, pt[q].x, pt[q].y, pt[q].z)) keep.w[wi] |= 1ull << ks[q];
         }
     }
 }

@@ -241,21 +241,25 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     __syncthreads();
     STAMP(2);
 
-    // ---- pass 2: ground decisions from the LDS codes ----
-    LaneBits<NW> keepgm;
-    keepgm.clear();
-    if (GROUND) {
-        pass2_keep<PPT, LAYOUT>(fb, N, L, P, fs->scal[S_TKMIN], fs->scal[S_TKMAX], fs->tkey,
-                                [&](int g) {
+    // ---- pass 2: ground decisions from the codes ----
+    auto codes_of = [&](int g) {
 #ifdef CG_CODES_HBM
-                                    return SPLIT ? sp_codes[g * CG_BLOCK + tid]
-                                                 : ((const uint2*)(L.scratch + (uint64_t)f * L.scratch_stride))[g * CG_BLOCK + tid];
+        return SPLIT ? sp_codes[g * CG_BLOCK + tid]
+                     : ((const uint2*)(L.scratch + (uint64_t)f * L.scratch_stride))[g * CG_BLOCK + tid];
 #else
-                                    return SPLIT ? sp_codes[g * CG_BLOCK + tid] : ((const uint2*)zq)[g * CG_BLOCK + tid];
+        return SPLIT ? sp_codes[g * CG_BLOCK + tid] : ((const uint2*)zq)[g * CG_BLOCK + tid];
 #endif
-                                }, keepgm);
+    };
+    LaneBits<NW> keepgm, amb;
+    keepgm.clear();
+    amb.clear();
+    if (KMODE == CG_KMODE_GROUND) {
+        pass2_keep<PPT, LAYOUT>(fb, N, L, P, fs->scal[S_TKMIN], fs->scal[S_TKMAX], fs->tkey, codes_of, keepgm);
         const uint32_t kc = wave_sum(keepgm.count());
         if (l == 0) atomicAdd(&fs->scal[S_K], kc);
+    } else if (GROUND) {
+        // the ambiguous points are decided below, in the same round of loads as the survivors
+        pass2_codes<PPT>(N, fs->scal[S_TKMIN], fs->scal[S_TKMAX], codes_of, keepgm, amb);
     } else {
 #pragma unroll
         for (int k = 0; k < PPT; k++)
@@ -304,19 +308,93 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         return;
     }
 
-    // ---- compaction: per-wave atomic append; each survivor carries its point index, and
-    // the voxel sort orders by (voxel idx, point index), so append order does not matter ----
-    LaneBits<NW> keepm;
-#pragma unroll
-    for (int i = 0; i < NW; i++) keepm.w[i] = FILTER ? (keepgm.w[i] & posm.w[i]) : keepgm.w[i];
-    const uint32_t nsv = keepm.count();
-    const uint32_t incl = wave_incl_scan(nsv);
-    uint32_t wbase = 0;
-    if (l == 63) wbase = atomicAdd(&fs->scal[S_MS], incl);
-    wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
-    uint32_t pos = wbase + incl - nsv;
-    __syncthreads();   // counts complete; z-code overlay in LDS is dead from here on
+    // ---- survivors: one round of loads per lane gathers the kept filter survivors and
+    // decides the ambiguous points (exactly, from the loaded x, y, z); each wave appends its
+    // survivors per round. Every survivor carries its point index and the voxel sort orders by
+    // (voxel idx, point index), so append order does not matter. Slots below the LDS capacity
+    // go to LDS, the rest to the frame's HBM slot (moved whole below when M does not fit) ----
+    __syncthreads();   // every wave is past the codes: LDS survivor slots overlay them from here
     STAMP(3);
+    const uint32_t lcap = FRONT ? 0u : (uint32_t)CG_MMAX;
+    const Work Wl = lds_work(bl);
+    const Work Wg = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t nfin = 0;
+    auto bound = [&](const float4& p) {
+        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+            nfin++;
+        }
+    };
+    // the points to load: kept filter survivors, and every ambiguous point (an ambiguous point
+    // outside the filter only counts toward K)
+    LaneBits<NW> todo;
+#pragma unroll
+    for (int i = 0; i < NW; i++) todo.w[i] = (FILTER ? (keepgm.w[i] & posm.w[i]) : keepgm.w[i]) | amb.w[i];
+    uint32_t kamb = 0;   // ambiguous points the exact test keeps
+    for (;;) {
+        bool more = false;
+#pragma unroll
+        for (int wi = 0; wi < NW; wi++) more |= todo.w[wi] != 0ull;
+        if (!__ballot(more)) break;   // wave-uniform: every lane takes part in the appends
+        int ks[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            ks[q] = -1;
+#pragma unroll
+            for (int wi = 0; wi < NW; wi++)
+                if (ks[q] < 0 && todo.w[wi]) {
+                    ks[q] = 64 * wi + __builtin_ctzll(todo.w[wi]);
+                    todo.w[wi] &= todo.w[wi] - 1;
+                }
+        }
+        float4 pt[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (ks[q] < 0) continue;
+            bool pre = false;
+#pragma unroll
+            for (int p = 0; p < CG_PREFETCH; p++)
+                if (FILTER && pk[p] == ks[q]) { pt[q] = pv[p]; pre = true; }
+            if (!pre) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
+        }
+        bool sv[4];
+        uint32_t ns = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            sv[q] = false;
+            if (ks[q] < 0) continue;
+            bool kept = true;
+            if (GROUND && amb.get(ks[q])) {
+                kept = pass2_exact(P, fs->tkey, pt[q].x, pt[q].y, pt[q].z);
+                kamb += kept ? 1u : 0u;
+            }
+            sv[q] = kept && (!FILTER || posm.get(ks[q]));
+            ns += sv[q] ? 1u : 0u;
+        }
+        const uint32_t incl = wave_incl_scan(ns);
+        uint32_t wbase = 0;
+        if (l == 63 && incl) wbase = atomicAdd(&fs->scal[S_MS], incl);
+        wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
+        uint32_t pos = wbase + incl - ns;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (!sv[q]) continue;
+            const uint32_t idx = (uint32_t)ks[q] * CG_BLOCK + tid;   // point index
+            if (pos < lcap) { Wl.P[pos] = pt[q]; Wl.IDX[pos] = idx; }
+            else { Wg.P[pos] = pt[q]; Wg.IDX[pos] = idx; }
+            bound(pt[q]);
+            pos++;
+        }
+    }
+    if (GROUND) {
+        const uint32_t kc = wave_sum(keepgm.count() + kamb);
+        if (l == 0) atomicAdd(&fs->scal[S_K], kc);
+    }
+    STAMP(25);
+    __syncthreads();   // counts complete
+    STAMP(4);
 
 #if defined(CG_EXP_STOP) && CG_EXP_STOP == 2
     if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
@@ -336,58 +414,14 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         h[0] = N;
         h[1] = K;
     }
-    STAMP(4);
-    Work W;
-    if (use_lds) {
-        W = lds_work(bl);
-    } else {
-        W = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
-    }
-    // ---- gather survivors (4 loads in flight per lane) and the VoxelGrid bounds ----
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    uint32_t nfin = 0;
-    auto bound = [&](const float4& p) {
-        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
-            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-            nfin++;
-        }
-    };
-#pragma unroll
-    for (int q = 0; q < CG_PREFETCH; q++) {
-        if (pk[q] >= 0 && keepm.get(pk[q])) {
-            keepm.clear_bit(pk[q]);
-            W.P[pos] = pv[q];
-            W.IDX[pos] = (uint32_t)pk[q] * CG_BLOCK + tid;
-            bound(pv[q]);
-            pos++;
+    const Work W = use_lds ? Wl : Wg;
+    if (!use_lds) {   // the slots below the LDS capacity to the frame's HBM slot
+        const uint32_t nl = min(Ms, lcap);
+        for (uint32_t j = tid; j < nl; j += CG_BLOCK) {
+            Wg.P[j] = Wl.P[j];
+            Wg.IDX[j] = Wl.IDX[j];
         }
     }
-#pragma unroll
-    for (int wi = 0; wi < NW; wi++) {
-        uint64_t m = keepm.w[wi];
-        while (m) {
-            int ks[4];
-            float4 pt[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                ks[q] = m ? __builtin_ctzll(m) : -1;
-                if (m) m &= m - 1;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (ks[q] >= 0) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid, L);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ks[q] < 0) continue;
-                W.P[pos] = pt[q];
-                W.IDX[pos] = (uint32_t)(64 * wi + ks[q]) * CG_BLOCK + tid;   // point index
-                bound(pt[q]);
-                pos++;
-            }
-        }
-    }
-    STAMP(25);
     for (uint32_t j = tid; j < npad; j += CG_BLOCK) {
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         W.P[Ms + j] = z4;
