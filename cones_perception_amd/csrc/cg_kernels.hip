@@ -10,11 +10,11 @@
 //            backend arrays); per-lane sector minimum flushed into 17 LDS bins with ds_min_u32
 //            on order-preserving keys                 (src/ground_removal.cpp:58-68)
 //    pass 2  sector thresholds; ground decisions from the codes against the band of used
-//            thresholds, exact re-read of x, y, z for band codes only
-//                                                       (src/ground_removal.cpp:70-77, and
+//            thresholds (band codes are ambiguous)  (src/ground_removal.cpp:70-77, and
 //                                                        src/cone_detection.cpp:189-204)
-//    gather  per-wave atomic append of the survivors (x, y, z, intensity, point index) into LDS
-//            (M <= CG_MMAX) or the frame's HBM scratch
+//    gather  one round of loads: the kept filter survivors and the ambiguous points (decided
+//            exactly from the loaded x, y, z); per-wave atomic append of the survivors (x, y,
+//            z, intensity, point index) into LDS (M <= CG_MMAX) or the frame's HBM scratch
 //  backend (latency-bound; M ~ 1e2-1e3 points)
 //    voxel   bounds, PCL idx key, std::sort's permutation of PCL's index_vector (cg_pcl.h; or a
 //            rank sort in point order), run heads, centroid sums in that order
