@@ -77,6 +77,10 @@ def main():
     ap.add_argument("--split", action="store_true",
                     help="experiment: each batch as a front launch + backend launches (cg_debug_route 6) instead "
                          "of one fused workgroup per frame")
+    ap.add_argument("--serve", action="store_true",
+                    help="experiment: each batch's backend launch beside its front launch, taking each frame as "
+                         "its front publishes it (cg_debug_route 8; backends on --split-streams' back streams, "
+                         "default 3,1)")
     ap.add_argument("--pair", action="store_true",
                     help="experiment: each frame as two half-frame workgroups (cg_debug_route 7, cg_pair.hip) "
                          "instead of one fused workgroup per frame")
@@ -142,9 +146,11 @@ def main():
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
     vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
     engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
-    if args.split or args.pair:
+    if args.split or args.pair or args.serve:
         for e in engines:
-            e.debug_route(6 if args.split else 7)
+            e.debug_route(6 if args.split else (7 if args.pair else 8))
+    if args.serve and not args.split_streams:
+        args.split_streams = "3,1"
     split_fb = [int(x) for x in args.split_streams.split(",")] if args.split_streams else None
     if split_fb:   # F front streams, B back streams
         streams = [torch.cuda.Stream(dev) for _ in range(split_fb[0])]
@@ -299,8 +305,9 @@ def main():
                                    "simulation params), ground_removal + cone_detection fused",
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
-                       "launches": "front + backend" if (args.split or args.split_streams) else
-                       ("half-frame pair kernel" if args.pair else "fused frame kernel"),
+                       "launches": "front + served backend" if args.serve else
+                       ("front + backend" if (args.split or args.split_streams) else
+                        ("half-frame pair kernel" if args.pair else "fused frame kernel")),
                        "split_streams": args.split_streams or None,
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -105,6 +105,8 @@ struct cg_handle {
     uint32_t last_k = 0;
     uint32_t* d_seckeys = nullptr;   // 18 words per frame inside d_hdr (not owned)
     uint32_t* d_biglist = nullptr;   // split batches' large-capacity frame list inside d_hdr (not owned)
+    uint32_t* d_serve = nullptr;     // served batches' publish words inside d_hdr (not owned)
+    uint32_t serve_epoch = 0;        // served batches so far
     RcBox* d_boxes = nullptr;
     uint32_t* d_rc_cnt = nullptr;    // boxes x blocks, twice (counts, offsets)
     size_t rc_cnt_cap = 0;
@@ -145,6 +147,7 @@ void free_batch(cg_handle* h) {
     h->d_idx = nullptr; h->d_cen = nullptr; h->d_ground = nullptr; h->d_scratch = nullptr;
     h->d_seckeys = nullptr;
     h->d_biglist = nullptr;
+    h->d_serve = nullptr;
     h->cap_frames = h->cap_points = 0;
 }
 
@@ -161,11 +164,14 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     const uint64_t F = nf, C = np;
     // headers, then each frame's 18 final sector-minimum keys (cg_recrop of a pipeline frame)
     // headers, sector keys, then the split batch's list of large-capacity frames (F + 2 words,
-    // zeroed here; each batch's cg_back_big clears it again)
-    HIPCHK(hipMalloc(&h->d_hdr, (F * (CG_HDR_WORDS + CG_NUM_BINS + 1) + F + 2) * 4));
+    // zeroed here; each batch's cg_back_big clears it again), then the served batch's words
+    // (zeroed here; the publish words hold the batch's epoch)
+    HIPCHK(hipMalloc(&h->d_hdr, (F * (CG_HDR_WORDS + CG_NUM_BINS + 1) + F + 2 + CG_SERVE_WORDS(F)) * 4));
     h->d_seckeys = h->d_hdr + F * CG_HDR_WORDS;
     h->d_biglist = h->d_seckeys + F * (CG_NUM_BINS + 1);
-    HIPCHK(hipMemset(h->d_biglist, 0, (F + 2) * 4));
+    h->d_serve = h->d_biglist + F + 2;
+    HIPCHK(hipMemset(h->d_biglist, 0, (F + 2 + CG_SERVE_WORDS(F)) * 4));
+    h->serve_epoch = 0;
     HIPCHK(hipMalloc(&h->d_vox, F * C * 16));
     HIPCHK(hipMalloc(&h->d_lab, F * C * 4));
     HIPCHK(hipMalloc(&h->d_offs, F * (C + 1) * 4));
@@ -309,6 +315,22 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream
         return CG_OK;
     }
     if (!large) {
+        if (h->route == 8 && kmode != CG_KMODE_GROUND) {
+            // served batch: the front on s publishes each frame; the backend launch on s_back
+            // (s when none) takes each as it comes, with no dependency on the front's end. The
+            // next front of this handle waits for it (the slots are read until then).
+            hipStream_t sb = s_back ? s_back : s;
+            if (!h->ev_back) HIPCHK(hipEventCreateWithFlags(&h->ev_back, hipEventDisableTiming));
+            if (h->back_stream_pending) HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
+            L.serve = h->d_serve;
+            L.epoch = ++h->serve_epoch;
+            L.stamps = nullptr;
+            HIPCHK((hipError_t)cg_launch_front(L, h->dp, kmode, s));
+            HIPCHK((hipError_t)cg_launch_serve(L, h->dp, sb));
+            HIPCHK(hipEventRecord(h->ev_back, sb));
+            h->back_stream_pending = sb;
+            return CG_OK;
+        }
         if (s_back && s_back != s) {
             // the front on s; the backend launches on s_back once the front is done; the next
             // front of this handle waits for them (cg_run_batch_split)
@@ -1186,7 +1208,7 @@ int cg_debug_front_span(cg_handle* h, void* d_span) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 7) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 8) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

@@ -40,6 +40,52 @@ int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Served batches (cg_debug_route 8): the batch's backend launch runs beside its front launch
+// (another stream) instead of after it: workgroup f waits for frame f's publish word (the
+// front's survivors and record are in the slot, written device-coherently), then runs
+// back_frame on it: in LDS up to CG_BACK_CAP detector points, else on the frame's slot. So a
+// frame's backend starts as soon as its own front ends, with no launch boundary in between,
+// and no launch follows (a large-LDS follow-up launch would wait for CU room behind the fronts).
+// Workgroups start in frame order, as the fronts do; the fronts never wait on them, and a
+// waiting workgroup leaves room for two fronts on its CU (BACK_SMEM beside two front
+// workgroups, like cg_back_kernel). Every wait is bounded (SERVE_TIMEOUT: then L.serve[2] is
+// set and the frame skipped).
+#define SERVE_TIMEOUT 100000000ull   // s_memrealtime ticks (100 MHz): 1 s
+__global__ __launch_bounds__(CG_BLOCK, 4) void cg_serve_kernel(CgLaunch L, CgDevParams P) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[BACK_SMEM];
+    __shared__ uint32_t late_s;
+    uint32_t* const sv = L.serve;
+    const uint32_t f = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t late = 0;
+        while (ld_rlx(&sv[4 + f]) != L.epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > SERVE_TIMEOUT) {
+                late = 1;
+                st_rlx(&sv[2], 1u);
+                break;
+            }
+        }
+        late_s = late;
+    }
+    __syncthreads();
+    if (late_s) return;
+    const uint32_t* const rec =
+        (const uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(L.n_points));
+    if (ld_rlx((uint32_t*)&rec[CG_FREC_M]) <= CG_BACK_CAP)
+        back_frame<CG_BACK_CAP, true>(L, P, f, (FrontShared*)smem, (BackLdsB*)(smem + FRONT_BYTES));
+    else   // more detector points: the backend on the frame's slot
+        back_frame<0, true>(L, P, f, (FrontShared*)smem, nullptr);
+    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+int cg_launch_serve(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
+    if (L.n_frames == 0 || !L.serve) return hipSuccess;
+    hipLaunchKernelGGL(cg_serve_kernel, dim3(L.n_frames), dim3(CG_BLOCK), 0, s, L, P);
+    return hipGetLastError();
+}
+
 // Pair batches (cg_pair.hip): the listed frames of more than CG_MMAX detector points, the
 // backend on their HBM slots (cg_back_big then takes the listed frames up to CG_MMAX and clears
 // the list).

@@ -606,7 +606,10 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
 // pcl_index_vector's 2,048-word point bitmap in VOX they keep their point indices; otherwise
 // (the 256-lane launch) they are ranked by point index and take the rank as point index, so
 // index_vector (cloud order) and the point-order ties are the frame kernel's either way.
-template <uint32_t CAP>
+// COH (served batches, cg_serve_kernel): the front ran concurrently on any XCD, so the record
+// and the survivors are read with device-coherent loads, and the slot-resident backend starts
+// with an agent-scope acquire (this XCD's caches invalidated).
+template <uint32_t CAP, bool COH = false>
 __device__ __forceinline__ void back_frame(const CgLaunch& L, const CgDevParams& P, uint32_t f, FrontShared* fs,
                                            BackLdsT<(CAP ? CAP : 1)>* bl) {
     constexpr uint32_t C = CAP ? CAP : 1;
@@ -614,35 +617,38 @@ __device__ __forceinline__ void back_frame(const CgLaunch& L, const CgDevParams&
     static_assert(!CAP || !RANK || CAP <= CG_RANK_SORT_MAX, "survivors ranked by one rank sort");
     const uint32_t tid = threadIdx.x, N = L.n_points;
     uint8_t* const slot = L.scratch + (uint64_t)f * L.scratch_stride;
-    const uint32_t* const rec = (const uint32_t*)(slot + cg_work_bytes(N));
+    uint32_t* const rec = (uint32_t*)(slot + cg_work_bytes(N));
     const Work Wg = global_work(slot, N);
-    const uint32_t Ms = rec[CG_FREC_MS], M = rec[CG_FREC_M];
+    auto rd = [&](uint32_t* p) -> uint32_t { return COH ? ld_rlx(p) : *p; };
+    auto rd4 = [&](const float4* p) -> float4 { return COH ? ld_f4(p) : *p; };
+    const uint32_t Ms = rd(&rec[CG_FREC_MS]), M = rd(&rec[CG_FREC_M]);
     if (tid < 64) {
         uint32_t v = 0;
         if (tid == S_MS) v = Ms;
-        else if (tid == S_MF) v = rec[CG_FREC_NFIN];
-        else if (tid >= S_BMIN0 && tid <= S_BMIN2) v = rec[CG_FREC_BMIN + (tid - S_BMIN0)];
-        else if (tid >= S_BMAX0 && tid <= S_BMAX2) v = rec[CG_FREC_BMAX + (tid - S_BMAX0)];
+        else if (tid == S_MF) v = rd(&rec[CG_FREC_NFIN]);
+        else if (tid >= S_BMIN0 && tid <= S_BMIN2) v = rd(&rec[CG_FREC_BMIN + (tid - S_BMIN0)]);
+        else if (tid >= S_BMAX0 && tid <= S_BMAX2) v = rd(&rec[CG_FREC_BMAX + (tid - S_BMAX0)]);
         fs->scal[tid] = v;
     }
     if constexpr (CAP == 0) {
+        if (COH) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         __syncthreads();
         backend(Wg, M, fs, L, P, f, 0x2u, CG_MAX_POINTS / 32, 0);
     } else {
         const Work W = lds_work(bl);
         if constexpr (RANK) {
             uint64_t* const tmp = (uint64_t*)W.VOX;   // free until pcl_index_vector
-            for (uint32_t j = tid; j < Ms; j += CG_BLOCK) tmp[j] = ((uint64_t)Wg.IDX[j] << 16) | j;
+            for (uint32_t j = tid; j < Ms; j += CG_BLOCK) tmp[j] = ((uint64_t)rd(&Wg.IDX[j]) << 16) | j;
             __syncthreads();
             rank_sort(tmp, W.KEY, Ms);
             for (uint32_t r = tid; r < Ms; r += CG_BLOCK) {
-                W.P[r] = Wg.P[(uint32_t)(W.KEY[r] & 0xffffu)];
+                W.P[r] = rd4(&Wg.P[(uint32_t)(W.KEY[r] & 0xffffu)]);
                 W.IDX[r] = r;
             }
         } else {
             for (uint32_t j = tid; j < Ms; j += CG_BLOCK) {
-                W.P[j] = Wg.P[j];
-                W.IDX[j] = Wg.IDX[j];
+                W.P[j] = rd4(&Wg.P[j]);
+                W.IDX[j] = rd(&Wg.IDX[j]);
             }
         }
         for (uint32_t j = Ms + tid; j < M; j += CG_BLOCK) {   // PointXYZI() pads after every kept point
@@ -652,6 +658,8 @@ __device__ __forceinline__ void back_frame(const CgLaunch& L, const CgDevParams&
         __syncthreads();
         // the 256-lane launch's all-pairs clustering covers CG_BRUTE_V voxels (its adjacency rows
         // overlay KEY); a frame with more goes on to cg_back_big
-        backend(W, M, fs, L, P, f, 0u, RANK ? (Ms + 32) / 32 : CG_MAX_POINTS / 32, CAP, RANK ? CG_BRUTE_V : 0u);
+        // (a served frame has no later launch: it clusters more voxels on the neighbour grid here)
+        backend(W, M, fs, L, P, f, 0u, RANK ? (Ms + 32) / 32 : CG_MAX_POINTS / 32, CAP,
+                RANK && !COH ? CG_BRUTE_V : 0u);
     }
 }

@@ -160,6 +160,23 @@ __device__ __forceinline__ uint32_t ld_rlx(uint32_t* p) {
 __device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld64(uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// float4 records through device-coherent 64-bit halves (visible to workgroups on other XCDs
+// without an L2 writeback)
+__device__ __forceinline__ void st_f4(float4* p, float4 v) {
+    st64((uint64_t*)p, ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x));
+    st64((uint64_t*)p + 1, ((uint64_t)__float_as_uint(v.w) << 32) | __float_as_uint(v.z));
+}
+__device__ __forceinline__ float4 ld_f4(const float4* p) {
+    const uint64_t a = ld64((uint64_t*)p), b = ld64((uint64_t*)p + 1);
+    return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)),
+                       __uint_as_float((uint32_t)b), __uint_as_float((uint32_t)(b >> 32)));
+}
 // Union-find with path halving; roots only ever point to smaller indices.
 __device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
     while (true) {

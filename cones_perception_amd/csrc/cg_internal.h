@@ -96,9 +96,14 @@ struct CgLaunch {
     // `in` (the device copy) before pass 1, or null (`in` already holds the frame)
     const uint8_t* in_host;
     // pair launch (cg_pair.hip): this batch's number, the value of a frame's ready word once
-    // its first half has published (the words start zeroed; a handle's batches count from 1)
+    // its first half has published (the words start zeroed; a handle's batches count from 1);
+    // served batches (cg_debug_route 8): the same for the front's publish words
     uint32_t epoch;
+    // served batches: [2] a backend workgroup's wait timed out, [4 + f] frame f's survivors
+    // are in its slot (= epoch); or null
+    uint32_t* serve;
 };
+#define CG_SERVE_WORDS(F) ((F) + 4)
 // The pair launch's exchange area: the last CG_PAIR_X_BYTES of each frame's scratch slot
 // (header words, a half's z codes, its filter bits), zeroed when the slots are allocated.
 #define CG_PAIR_X_BYTES (128 + CG_MAX_POINTS / 2 + 2 * 256 * 8 + 128)
@@ -244,6 +249,9 @@ int cg_launch_backends(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 // slot, > CG_MMAX) and cg_launch_back_big (LDS, <= CG_MMAX; clears the list), launched after it.
 int cg_launch_pair(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 int cg_launch_back_list(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
+// Served batches (cg_debug_route 8): the front launch publishes each frame (L.serve) and the
+// backend launch beside it (cg_back.hip) takes each frame as soon as it is published.
+int cg_launch_serve(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 int cg_launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
 // Cone re-crop (cg_recrop.hip): exact float form of the reference's double box compares.
 struct RcBox { float lox, hix, loy, hiy; };

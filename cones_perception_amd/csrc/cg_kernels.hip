@@ -382,8 +382,16 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         for (int q = 0; q < 4; q++) {
             if (!sv[q]) continue;
             const uint32_t idx = (uint32_t)ks[q] * CG_BLOCK + tid;   // point index
-            if (pos < lcap) { Wl.P[pos] = pt[q]; Wl.IDX[pos] = idx; }
-            else { Wg.P[pos] = pt[q]; Wg.IDX[pos] = idx; }
+            if (pos < lcap) {
+                Wl.P[pos] = pt[q];
+                Wl.IDX[pos] = idx;
+            } else if (FRONT) {   // device-coherent: a backend workgroup on any XCD reads them
+                st_f4(&Wg.P[pos], pt[q]);
+                st_rlx(&Wg.IDX[pos], idx);
+            } else {
+                Wg.P[pos] = pt[q];
+                Wg.IDX[pos] = idx;
+            }
             bound(pt[q]);
             pos++;
         }
@@ -424,8 +432,13 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     }
     for (uint32_t j = tid; j < npad; j += CG_BLOCK) {
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        W.P[Ms + j] = z4;
-        W.IDX[Ms + j] = 0xffffu;   // after every kept point; exact-zero terms are order-free
+        if (FRONT) {
+            st_f4(&W.P[Ms + j], z4);
+            st_rlx(&W.IDX[Ms + j], 0xffffu);
+        } else {
+            W.P[Ms + j] = z4;
+            W.IDX[Ms + j] = 0xffffu;   // after every kept point; exact-zero terms are order-free
+        }
         bound(z4);
     }
     {
@@ -454,19 +467,24 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     if constexpr (FRONT) {   // the front record for the backend launch (cg_back.hip)
         if (tid == 0) {
             uint32_t* rec = (uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(N));
-            rec[CG_FREC_MS] = Ms;
-            rec[CG_FREC_M] = M;
-            rec[CG_FREC_NFIN] = fs->scal[S_MF];
+            st_rlx(&rec[CG_FREC_MS], Ms);
+            st_rlx(&rec[CG_FREC_M], M);
+            st_rlx(&rec[CG_FREC_NFIN], fs->scal[S_MF]);
 #pragma unroll
             for (int a = 0; a < 3; a++) {
-                rec[CG_FREC_BMIN + a] = fs->scal[S_BMIN0 + a];
-                rec[CG_FREC_BMAX + a] = fs->scal[S_BMAX0 + a];
+                st_rlx(&rec[CG_FREC_BMIN + a], fs->scal[S_BMIN0 + a]);
+                st_rlx(&rec[CG_FREC_BMAX + a], fs->scal[S_BMAX0 + a]);
             }
-            if (M > CG_BACK_CAP && M <= CG_MMAX) {   // beyond the backend launch's LDS: cg_back_big
+            if (!L.serve && M > CG_BACK_CAP && M <= CG_MMAX) {   // beyond the backend launch's LDS: cg_back_big
                 const uint32_t q = atomicAdd(&L.biglist[0], 1u);
                 L.biglist[2 + q] = f;
             }
             if (L.span_front) atomicMax(&L.span_front[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        }
+        if (L.serve) {   // served batch: the frame published once every lane's stores are complete
+            __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
+            __syncthreads();
+            if (tid == 0) st_rlx(&L.serve[4 + f], L.epoch);
         }
         return;
     }

@@ -37,13 +37,6 @@ static_assert(4 * PAIR_SMEM <= 163840, "four pair workgroups per CU");
 // the exchange area: the last CG_PAIR_X_BYTES of the frame's scratch slot
 static_assert(CG_PAIR_X_BYTES >= 128 + PAIR_HALF + 2 * CG_BLOCK * 8 && CG_PAIR_X_BYTES % 256 == 0, "exchange area");
 
-__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld64(uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int LAYOUT>
 __global__ __launch_bounds__(CG_BLOCK, 4) void cg_pair_kernel(CgLaunch L, CgDevParams P) {
     constexpr int PPT = PAIR_PPT, NW = PPT / 64;
@@ -283,6 +276,9 @@ int cg_launch_pair(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
     if (xyzi16) hipLaunchKernelGGL(cg_pair_kernel<CG_LAYOUT_XYZI16>, grid, block, 0, s, L, P);
     else hipLaunchKernelGGL(cg_pair_kernel<CG_LAYOUT_GENERIC>, grid, block, 0, s, L, P);
     if (hipError_t e = hipGetLastError()) return e;
+#ifdef CG_PAIR_NO_FOLLOWUP   // (experiment: what the two listed-frame launches cost; C3 lists none)
+    return hipSuccess;
+#endif
     if (int e = cg_launch_back_list(L, P, s)) return e;
     return cg_launch_back_big(L, P, s);
 }
