@@ -379,7 +379,9 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
  * are finished in HBM side by side (5); detector batches of <= 65,536-point frames as a front
  * launch plus backend launches instead of one fused workgroup per frame (6); pipeline batches
- * of 32,769-65,536-point frames as two half-frame workgroups per frame (7); 0 = automatic. */
+ * of 32,769-65,536-point frames as two half-frame workgroups per frame (7); detector batches
+ * whose backend launch runs beside the front launch, on cg_run_batch_split's back stream, taking
+ * each frame as its front publishes it (8); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */
