@@ -114,3 +114,37 @@ def test_out_of_line_probe_needs_scratch(tmp_path):
     assert int(meta[".private_segment_fixed_size"]) > 0 and meta[".uses_dynamic_stack"].strip() == "false", meta
     dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(co)], capture_output=True, text=True, check=True).stdout
     assert "s_swappc_b64" in dis and "scratch_store_dword" in dis and "flat_load_dword" in dis
+
+
+def _find(kernels, prefix):
+    out = [(n, m) for n, m in kernels if n and n.startswith(prefix)]
+    assert out, f"no kernel named {prefix}*"
+    return out
+
+
+def _vgprs(m):   # allocated: gfx950 hands out VGPRs in blocks of 8
+    return (int(m[".vgpr_count"]) + 7) // 8 * 8
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_occupancy_contracts(tmp_path):
+    """The residency each launch structure is designed around, from the code-object metadata
+    (160 KiB of LDS and 512 VGPRs per SIMD lane on a gfx950 CU; a 512-lane workgroup puts two
+    waves on each SIMD, a 256-lane one one wave):
+      - the fused frame kernel: two workgroups per CU (LDS <= 80 KiB, <= 128 VGPRs);
+      - the batch front + backend launches (routes 6 and 8): two fronts and one backend
+        workgroup per CU;
+      - the half-frame pair kernel: four workgroups per CU."""
+    k = _kernel_metadata(tmp_path)
+    lds = lambda m: int(m[".group_segment_fixed_size"])
+    for n, m in _find(k, "_Z15cg_frame_kernelILi128E"):
+        assert 2 * lds(m) <= 163840 and 4 * _vgprs(m) <= 512, (n, lds(m), m[".vgpr_count"])
+    fronts = _find(k, "_Z15cg_front_kernelILi128E")
+    front_lds = max(lds(m) for _, m in fronts)
+    front_vgpr = max(_vgprs(m) for n, m in fronts if "ELi0EE" in n)   # the pipeline fronts
+    for name in ("_Z14cg_back_kernel", "_Z15cg_serve_kernel"):
+        for n, m in _find(k, name):
+            assert 2 * front_lds + lds(m) <= 163840, (n, front_lds, lds(m))
+            assert 4 * front_vgpr + _vgprs(m) <= 512, (n, front_vgpr, m[".vgpr_count"])
+    for n, m in _find(k, "_Z14cg_pair_kernel"):
+        assert 4 * lds(m) <= 163840 and 4 * _vgprs(m) <= 512, (n, lds(m), m[".vgpr_count"])
