@@ -66,9 +66,6 @@ __device__ __forceinline__ Work lds_work(BackLdsT<CAP>* bl) {
     return W;
 }
 
-#ifndef CG_PREFETCH
-#define CG_PREFETCH 2   // filter survivors per lane loaded right after pass 1
-#endif
 
 // Scalar slots in FrontShared::scal
 enum {

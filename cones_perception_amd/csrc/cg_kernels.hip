@@ -202,29 +202,9 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         else
             stream_pass1<PPT, LAYOUT, GROUND, FILTER>(fb, N, L, P, fs->sec_key, fs->rays, posm, touched, store);
     }
-    const uint32_t nlast = N ? N - 1 : 0u;
     if (GROUND && !SPLIT) {
         touched = wave_or(touched);
         if (l == 0) atomicOr(&fs->scal[S_TOUCHED], touched);
-    }
-    // the lane's first CG_PREFETCH filter survivors are the likely first gather loads: issue them now,
-    // they land while the thresholds and pass 2 run (a survivor that turns out to be ground
-    // costs one wasted load)
-    int pk[CG_PREFETCH];
-    float4 pv[CG_PREFETCH];
-#pragma unroll
-    for (int q = 0; q < CG_PREFETCH; q++) pk[q] = -1;
-    if (FILTER) {
-#pragma unroll
-        for (int wi = 0; wi < NW; wi++) {
-            uint64_t m = posm.w[wi];
-#pragma unroll
-            for (int q = 0; q < CG_PREFETCH; q++)
-                if (pk[q] < 0 && m) { pk[q] = 64 * wi + __builtin_ctzll(m); m &= m - 1; }
-        }
-#pragma unroll
-        for (int q = 0; q < CG_PREFETCH; q++)
-            pv[q] = load_xyzi<LAYOUT>(fb, min((uint32_t)(pk[q] < 0 ? 0 : pk[q]) * CG_BLOCK + tid, nlast), L);
     }
     __syncthreads();
     STAMP(1);
@@ -308,11 +288,13 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         return;
     }
 
-    // ---- survivors: one round of loads per lane gathers the kept filter survivors and
-    // decides the ambiguous points (exactly, from the loaded x, y, z); each wave appends its
-    // survivors per round. Every survivor carries its point index and the voxel sort orders by
-    // (voxel idx, point index), so append order does not matter. Slots below the LDS capacity
-    // go to LDS, the rest to the frame's HBM slot (moved whole below when M does not fit) ----
+    // ---- survivors: one round of loads gathers the kept filter survivors and decides the
+    // ambiguous points (exactly, from the loaded x, y, z). The points are spread over the
+    // wave's lanes: a lane with many (a near cone's column) would otherwise take one round of
+    // loads per four of them while its wave waits. Each wave appends its survivors per round;
+    // every survivor carries its point index and the voxel sort orders by (voxel idx, point
+    // index), so append order does not matter. Slots below the LDS capacity go to LDS, the rest
+    // to the frame's HBM slot (moved whole below when M does not fit) ----
     __syncthreads();   // every wave is past the codes: LDS survivor slots overlay them from here
     STAMP(3);
     const uint32_t lcap = FRONT ? 0u : (uint32_t)CG_MMAX;
@@ -327,50 +309,70 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
             nfin++;
         }
     };
+    auto put = [&](uint32_t pos, const float4& pt, uint32_t idx) {
+        if (pos < lcap) {
+            Wl.P[pos] = pt;
+            Wl.IDX[pos] = idx;
+        } else if (FRONT) {   // device-coherent: a backend workgroup on any XCD reads them
+            st_f4(&Wg.P[pos], pt);
+            st_rlx(&Wg.IDX[pos], idx);
+        } else {
+            Wg.P[pos] = pt;
+            Wg.IDX[pos] = idx;
+        }
+        bound(pt);
+    };
     // the points to load: kept filter survivors, and every ambiguous point (an ambiguous point
     // outside the filter only counts toward K)
     LaneBits<NW> todo;
 #pragma unroll
     for (int i = 0; i < NW; i++) todo.w[i] = (FILTER ? (keepgm.w[i] & posm.w[i]) : keepgm.w[i]) | amb.w[i];
+    // the rest listed in wave order, 256 per round, in the wave's stage (KEY: free until the
+    // backend): k << 8 | lane << 2 | ambiguous << 1 | filter survivor (never 0)
+    uint32_t* const stage = (uint32_t*)Wl.KEY + w * 256;
+    const uint32_t cnt = todo.count();
+    const uint32_t lincl = wave_incl_scan(cnt);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)lincl, 63), lex = lincl - cnt;
     uint32_t kamb = 0;   // ambiguous points the exact test keeps
-    for (;;) {
-        bool more = false;
+    uint32_t r0 = 0;
+    do {   // wave-uniform rounds
+        {
+            uint32_t idx = lex;
 #pragma unroll
-        for (int wi = 0; wi < NW; wi++) more |= todo.w[wi] != 0ull;
-        if (!__ballot(more)) break;   // wave-uniform: every lane takes part in the appends
-        int ks[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            ks[q] = -1;
-#pragma unroll
-            for (int wi = 0; wi < NW; wi++)
-                if (ks[q] < 0 && todo.w[wi]) {
-                    ks[q] = 64 * wi + __builtin_ctzll(todo.w[wi]);
-                    todo.w[wi] &= todo.w[wi] - 1;
+            for (int wi = 0; wi < NW; wi++) {
+                uint64_t m = todo.w[wi];
+                while (m && idx < r0 + 256u) {
+                    const uint32_t k = 64 * wi + (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1;
+                    if (idx >= r0)
+                        stage[idx - r0] = (k << 8) | (l << 2) | (amb.get(k) ? 2u : 0u) |
+                                          ((!FILTER || posm.get(k)) ? 1u : 0u);
+                    idx++;
                 }
+            }
         }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t n = T > r0 ? min(256u, T - r0) : 0u;
+        uint32_t e[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) e[q] = (uint32_t)(l + 64 * q) < n ? stage[l + 64 * q] : 0u;
+        __builtin_amdgcn_wave_barrier();   // the stage read before the next round writes it
         float4 pt[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (ks[q] < 0) continue;
-            bool pre = false;
-#pragma unroll
-            for (int p = 0; p < CG_PREFETCH; p++)
-                if (FILTER && pk[p] == ks[q]) { pt[q] = pv[p]; pre = true; }
-            if (!pre) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)ks[q] * CG_BLOCK + tid, L);
-        }
+        for (int q = 0; q < 4; q++)
+            if (e[q]) pt[q] = load_xyzi<LAYOUT>(fb, (e[q] >> 8) * CG_BLOCK + w * 64 + ((e[q] >> 2) & 63u), L);
         bool sv[4];
         uint32_t ns = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             sv[q] = false;
-            if (ks[q] < 0) continue;
+            if (!e[q]) continue;
             bool kept = true;
-            if (GROUND && amb.get(ks[q])) {
+            if (GROUND && (e[q] & 2u)) {
                 kept = pass2_exact(P, fs->tkey, pt[q].x, pt[q].y, pt[q].z);
                 kamb += kept ? 1u : 0u;
             }
-            sv[q] = kept && (!FILTER || posm.get(ks[q]));
+            sv[q] = kept && (e[q] & 1u);
             ns += sv[q] ? 1u : 0u;
         }
         const uint32_t incl = wave_incl_scan(ns);
@@ -379,23 +381,10 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
         uint32_t pos = wbase + incl - ns;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (!sv[q]) continue;
-            const uint32_t idx = (uint32_t)ks[q] * CG_BLOCK + tid;   // point index
-            if (pos < lcap) {
-                Wl.P[pos] = pt[q];
-                Wl.IDX[pos] = idx;
-            } else if (FRONT) {   // device-coherent: a backend workgroup on any XCD reads them
-                st_f4(&Wg.P[pos], pt[q]);
-                st_rlx(&Wg.IDX[pos], idx);
-            } else {
-                Wg.P[pos] = pt[q];
-                Wg.IDX[pos] = idx;
-            }
-            bound(pt[q]);
-            pos++;
-        }
-    }
+        for (int q = 0; q < 4; q++)
+            if (sv[q]) { put(pos, pt[q], (e[q] >> 8) * CG_BLOCK + w * 64 + ((e[q] >> 2) & 63u)); pos++; }
+        r0 += 256u;
+    } while (r0 < T);
     if (GROUND) {
         const uint32_t kc = wave_sum(keepgm.count() + kamb);
         if (l == 0) atomicAdd(&fs->scal[S_K], kc);
