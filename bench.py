@@ -772,7 +772,8 @@ def single_frame_latency(cp, params, raw, device, reps=200, order=None):
     dt = (time.perf_counter() - t0) / reps
     return {"latency_ms": dt * 1e3, "frames_per_s": 1.0 / dt,
             "includes": "C2: one 64k-point PointCloud2 in pageable host memory through the synchronous "
-                        "ConePipeline.cloud_handler (staging copy into pinned memory, the split kernel reading "
+                        "ConePipeline.cloud_handler (the split kernel launched first; the host copies the message into "
+                        "pinned memory chunk by chunk, publishing each chunk to the workgroup reading "
                         "it over PCIe, its last workgroup writing the packed results into pinned host memory, "
                         "one synchronisation, Python result objects)"}
 
@@ -787,7 +788,8 @@ def single_frame_cpp(reps=500):
         return {"error": (r.stderr or r.stdout)[-500:]}
     out = json.loads(r.stdout.strip().splitlines()[-1])
     out["includes"] = ("C2 in C++: ConePipeline::cloud_handler (cones_nodes.hpp) on one 64k-point PointCloud2 in "
-                       "pageable memory: cg_pipeline (staging into pinned memory, split kernel reading it over "
+                       "pageable memory: cg_pipeline (split kernel launched, message staged into pinned memory chunk "
+                       "by chunk behind it, each chunk workgroup reading its chunk over "
                        "PCIe, results written to pinned host memory, one synchronisation), result vectors")
     return out
 

@@ -58,7 +58,10 @@ struct cg_handle {
     // single-frame staging
     uint8_t* d_in = nullptr;
     size_t d_in_bytes = 0;
-    uint8_t* h_stage = nullptr;   // pinned
+    uint8_t* h_stage = nullptr;   // pinned, coherent (split kernels read it while the host fills it)
+    uint32_t* h_flags = nullptr;  // pinned, coherent: per-chunk publish words of the staging buffer
+    uint32_t* h_flags_dev = nullptr;
+    uint32_t stage_seq = 0;
     size_t h_stage_bytes = 0;
     // last batch
     uint32_t last_frames = 0, last_points = 0;
@@ -195,7 +198,9 @@ int check_view(const cg_cloud_view* v) { return cg_check_view(v); }
 // Stage a PointCloud2 data block as one contiguous device frame. Aligned, unpadded rows are
 // uploaded verbatim; padded rows or unaligned fields are re-packed (pure byte moves, the
 // memcpy half of pcl::fromROSMsg) to x,y,z,intensity at 0,4,8,12.
-int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L, bool zero_copy = false) {
+// defer (with zero_copy, verbatim layouts): the bytes are not copied here; the caller copies
+// them after the launch with publish_chunks.
+int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L, bool zero_copy = false, bool* deferred = nullptr) {
     const uint32_t n = v->width * v->height;
     const bool aligned = v->point_step % 4 == 0 && (v->off_x < 0 || v->off_x % 4 == 0) &&
                          (v->off_y < 0 || v->off_y % 4 == 0) && (v->off_z < 0 || v->off_z % 4 == 0) &&
@@ -205,9 +210,12 @@ int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L, bool zero_cop
     const uint32_t step = verbatim ? v->point_step : 16;
     const size_t bytes = std::max<size_t>((size_t)n * step, 16);
     if (bytes > h->h_stage_bytes) {
+        // (the publish words h_flags do not depend on the frame size: they live as long as the
+        // handle; freeing them here with the staging buffer left the host and the already
+        // launched chunk workgroups on an unmapped page, the round-3 fault)
         if (h->h_stage) (void)hipHostFree(h->h_stage);
         h->h_stage = nullptr;
-        HIPCHK(hipHostMalloc(&h->h_stage, bytes, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&h->h_stage, bytes, hipHostMallocCoherent));
         h->h_stage_bytes = bytes;
     }
     if (bytes > h->d_in_bytes) {
@@ -217,8 +225,9 @@ int stage_frame(cg_handle* h, const cg_cloud_view* v, CgLaunch& L, bool zero_cop
         h->d_in_bytes = bytes;
     }
     const uint8_t* src = (const uint8_t*)v->data;
+    if (deferred) *deferred = zero_copy && verbatim && n;
     if (verbatim) {
-        if (n) std::memcpy(h->h_stage, src, (size_t)n * step);
+        if (n && !(deferred && *deferred)) std::memcpy(h->h_stage, src, (size_t)n * step);
         L.point_step = v->point_step;
         L.off_x = v->off_x; L.off_y = v->off_y; L.off_z = v->off_z; L.off_i = v->off_intensity;
     } else {
@@ -459,6 +468,24 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
     return CG_OK;
 }
 
+// The staging buffer's chunks (CG_SPLIT_CHUNK points each): copied from the message (unless
+// `only_flags`: already staged) and published to the split kernel's chunk workgroups one by
+// one (release: the chunk's bytes before its word).
+void publish_chunks(cg_handle* h, const cg_cloud_view* v, uint32_t n, uint32_t step, bool only_flags) {
+    // every workgroup of the launch waits for its word: one even for an empty frame
+    const uint32_t nch = std::max<uint32_t>(1, (n + CG_SPLIT_CHUNK - 1) / CG_SPLIT_CHUNK);
+    const uint8_t* src = (const uint8_t*)v->data;
+    for (uint32_t c = 0; c < nch; c++) {
+        if (!only_flags && (uint64_t)c * CG_SPLIT_CHUNK < n) {
+            const size_t b0 = (size_t)c * CG_SPLIT_CHUNK * step;
+            const size_t nb = (size_t)std::min<uint32_t>(CG_SPLIT_CHUNK, n - c * CG_SPLIT_CHUNK) * step;
+            std::memcpy(h->h_stage + b0, src + b0, nb);
+        }
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);   // also orders a memcpy's non-temporal stores
+        __atomic_store_n(&h->h_flags[c], h->stage_seq, __ATOMIC_RELEASE);
+    }
+}
+
 int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_result* dres,
                cg_ground_result* gres) {
     if (!h) return fail(CG_E_INVALID, "null handle");
@@ -474,12 +501,24 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
     // the one-workgroup frame kernel, for comparisons)
     const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4);
-    rc = stage_frame(h, in, L, split && h->route == 0);   // route 4: split, input by DMA
+    bool staged_later = false;
+    rc = stage_frame(h, in, L, split && h->route == 0, &staged_later);   // route 4: split, input by DMA
     if (rc) return rc;
     fill_launch_outputs(h, L);
     h->last_single = false;
     if (kmode == CG_KMODE_PIPELINE) {
         L.seckeys = h->d_seckeys;
+    }
+    if (split && h->route == 0) {   // the input's chunks published after the launch
+        if (!h->h_flags) {
+            HIPCHK(hipHostMalloc((void**)&h->h_flags, 64 * 4, hipHostMallocCoherent));
+            std::memset(h->h_flags, 0, 64 * 4);
+            HIPCHK(hipHostGetDevicePointer((void**)&h->h_flags_dev, h->h_flags, 0));
+        }
+        h->stage_seq = h->stage_seq + 1 ? h->stage_seq + 1 : 1;
+        L.in_flags = h->h_flags_dev;
+        L.in_seq = h->stage_seq;
+        if (!staged_later) publish_chunks(h, in, n, 0, true);   // already staged: publish every chunk
     }
     if (split) {
         if (!h->d_split) {
@@ -495,6 +534,7 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     h->packed = L.pack != nullptr;
     rc = launch_frames(h, L, kmode, h->stream);
     if (rc) return rc;
+    if (staged_later) publish_chunks(h, in, n, L.point_step, false);   // overlaps the chunk workgroups
     h->last_frames = 1; h->last_points = n; h->last_mode = kmode; h->last_stream = h->stream;
     h->last_in = L;
     if (kmode == CG_KMODE_GROUND) {
@@ -517,6 +557,8 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     }
     rc = fetch_frame(h, h->stream, 0, dres);
     if (rc) return rc;
+    if (L.in_flags && __atomic_load_n(&h->h_flags[CG_STAGE_ERR], __ATOMIC_ACQUIRE) == L.in_seq)
+        return fail(CG_E_DEVICE, "the split kernel timed out waiting for the staged input");
     h->last_k = h->h_hdr[CG_HDR_K];
     h->last_single = true;
     return CG_OK;
@@ -606,6 +648,7 @@ int cg_destroy(cg_handle* h) {
     if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);
     if (h->d_rc_out) (void)hipFree(h->d_rc_out);
     if (h->h_stage) (void)hipHostFree(h->h_stage);
+    if (h->h_flags) (void)hipHostFree(h->h_flags);
     if (h->h_ground) (void)hipHostFree(h->h_ground);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;

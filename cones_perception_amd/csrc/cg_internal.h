@@ -102,11 +102,19 @@ struct CgLaunch {
     // served batches: [2] a backend workgroup's wait timed out, [4 + f] frame f's survivors
     // are in its slot (= epoch); or null
     uint32_t* serve;
+    // split launch with in_host: the host fills the staging buffer chunk by chunk after the
+    // launch and publishes chunk c by storing in_seq to in_flags[c] (pinned, coherent); each
+    // chunk workgroup waits for its word (CG_STAGE_TIMEOUT bound: then in_flags[CG_STAGE_ERR]
+    // is set and the call fails). Null: the buffer is complete before the launch.
+    uint32_t* in_flags;
+    uint32_t in_seq;
 };
 #define CG_SERVE_WORDS(F) ((F) + 4)
 // The pair launch's exchange area: the last CG_PAIR_X_BYTES of each frame's scratch slot
 // (header words, a half's z codes, its filter bits), zeroed when the slots are allocated.
 #define CG_PAIR_X_BYTES (128 + CG_MAX_POINTS / 2 + 2 * 256 * 8 + 128)
+#define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
+#define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms
 // A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
 // for pass 1; the last chunk to finish runs the rest of the frame kernel. State words: [0]
 // finished chunks, [1] used sector bins, [2, 20) sector-minimum keys (all reset by the last

@@ -130,6 +130,20 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         const uint32_t c = blockIdx.x, c0 = c * CG_SPLIT_CHUNK;
         const uint32_t Nc = N > c0 ? min((uint32_t)CG_SPLIT_CHUNK, N - c0) : 0u;
         if (L.in_host) {   // the chunk over PCIe from pinned host memory into the device copy
+            if (L.in_flags) {   // the host publishes the chunk after the launch (run_single)
+                if (tid == 0) {
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__hip_atomic_load(&L.in_flags[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != L.in_seq) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > CG_STAGE_TIMEOUT) {
+                            __hip_atomic_store(&L.in_flags[CG_STAGE_ERR], L.in_seq, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                            break;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
             const uint64_t b0 = (uint64_t)c0 * L.point_step, nb = (uint64_t)Nc * L.point_step;
             uint8_t* dst = (uint8_t*)L.in + b0;
             const uint8_t* src = L.in_host + b0;

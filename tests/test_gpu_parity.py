@@ -94,6 +94,21 @@ def test_pipeline_matches_oracle(params, pipe, rings, cols, frame):
     assert_same_detection(got, ref, f"pipeline {rings}x{cols} f{frame}")
 
 
+def test_single_frame_staging_grows_and_shrinks(params):
+    """One fresh handle, frames whose sizes grow and shrink the pinned staging buffer between
+    calls: each chunk workgroup waits for its chunk's publish word, which the host stores after
+    copying the chunk (after the launch). The round-3 fault was the publish words freed with a
+    growing staging buffer (a 16k frame, then a 64k one)."""
+    pipe = cp.ConePipeline(params)
+    for rings, cols, frame in [(1, 100, 0), (16, 1024, 1), (64, 1024, 2), (3, 1000, 3), (64, 1024, 4),
+                               (8, 1000, 5)]:
+        raw = cp.synth_frames(1, first_frame=frame, rings=rings, cols=cols)
+        msg = cp.frame_cloud(raw[0])
+        got = pipe.cloud_handler(msg)
+        ref, _ = O.run(params, msg, O.MODE_PIPELINE)
+        assert_same_detection(got, ref, f"staged {rings}x{cols} f{frame}")
+
+
 @pytest.mark.parametrize("frame", [0, 3])
 def test_detector_matches_oracle(params, det, frame):
     raw = cp.synth_frames(1, first_frame=frame, rings=64, cols=1024)
