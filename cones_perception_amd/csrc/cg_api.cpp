@@ -264,11 +264,14 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
     L.biglist = h->d_biglist;
     L.stamps = nullptr;
     if (h->stamps_on) {
-        if (h->stamps_frames < h->cap_frames) {
+        // stamps are indexed by workgroup: a split single-frame launch has one workgroup per
+        // chunk (up to CG_MAX_POINTS / CG_SPLIT_CHUNK), more than the handle's frame capacity
+        const uint32_t need = std::max<uint32_t>(h->cap_frames, CG_MAX_POINTS / CG_SPLIT_CHUNK);
+        if (h->stamps_frames < need) {
             (void)hipFree(h->d_stamps);
             h->d_stamps = nullptr;
-            if (hipMalloc(&h->d_stamps, (size_t)h->cap_frames * 32 * 8) == hipSuccess)
-                h->stamps_frames = h->cap_frames;
+            if (hipMalloc(&h->d_stamps, (size_t)need * 32 * 8) == hipSuccess)
+                h->stamps_frames = need;
             else
                 h->stamps_frames = 0;
         }

@@ -144,51 +144,68 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
                 }
                 __syncthreads();
             }
+            STAMP(27);   // the chunk is published
             const uint64_t b0 = (uint64_t)c0 * L.point_step, nb = (uint64_t)Nc * L.point_step;
             uint8_t* dst = (uint8_t*)L.in + b0;
             const uint8_t* src = L.in_host + b0;
             const uint64_t n16 = nb / 16;
             // four 16-byte reads in flight per lane; named registers (an array with
             // conditional elements was kept in scratch)
+            // The device copy is written device-coherently (the last workgroup, on any XCD,
+            // re-reads survivors from it): the hand-off below then needs no L2 writeback
             const uint4* s4 = (const uint4*)src;
-            uint4* d4 = (uint4*)dst;
+            uint64_t* d8 = (uint64_t*)dst;
+            auto put16 = [&](uint64_t i, const uint4& v) {
+                st64(d8 + 2 * i, ((uint64_t)v.y << 32) | v.x);
+                st64(d8 + 2 * i + 1, ((uint64_t)v.w << 32) | v.z);
+            };
             for (uint64_t i = tid; i < n16; i += CG_BLOCK * 4) {
                 const uint64_t i1 = i + CG_BLOCK, i2 = i + 2 * CG_BLOCK, i3 = i + 3 * CG_BLOCK;
                 const uint4 v0 = s4[i];
                 const uint4 v1 = s4[i1 < n16 ? i1 : i];
                 const uint4 v2 = s4[i2 < n16 ? i2 : i];
                 const uint4 v3 = s4[i3 < n16 ? i3 : i];
-                d4[i] = v0;
-                if (i1 < n16) d4[i1] = v1;
-                if (i2 < n16) d4[i2] = v2;
-                if (i3 < n16) d4[i3] = v3;
+                put16(i, v0);
+                if (i1 < n16) put16(i1, v1);
+                if (i2 < n16) put16(i2, v2);
+                if (i3 < n16) put16(i3, v3);
             }
             for (uint64_t i = n16 * 16 + 4 * (uint64_t)tid; i < nb; i += 4 * CG_BLOCK)
-                *(uint32_t*)(dst + i) = *(const uint32_t*)(src + i);
-            __threadfence();
+                st_rlx((uint32_t*)(dst + i), *(const uint32_t*)(src + i));
+            __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this lane's stores are done
             __syncthreads();
+            STAMP(28);   // the chunk is on the device
         }
         LaneBits<1> pm;
         uint2 code = make_uint2(0u, 0u);
         stream_pass1<CG_SPLIT_CHUNK / CG_BLOCK, LAYOUT, GROUND, FILTER>(
             fb + (uint64_t)c0 * L.point_step, Nc, L, P, fs->sec_key, fs->rays, pm, touched,
             [&](int, uint2 cw) { code = cw; });
-        sp_codes[c * CG_BLOCK + tid] = code;
-        ((uint8_t*)(L.split + CG_SPLIT_POSM))[c * CG_BLOCK + tid] = (uint8_t)pm.w[0];
+        // codes and filter bits device-coherently too (four lanes' bytes as one word); the
+        // chunk's part is complete once every lane's stores and atomics are (vmcnt(0) and the
+        // barrier), then a relaxed count: no release / acquire fences, whose L2 writeback and
+        // invalidate on every chunk workgroup cost ~5 us of the frame's critical path
+        st64((uint64_t*)&sp_codes[c * CG_BLOCK + tid], ((uint64_t)code.y << 32) | code.x);
+        {
+            const uint32_t b = (uint32_t)(uint8_t)pm.w[0];
+            const uint32_t wv = b | ((uint32_t)__shfl_down((int)b, 1, 64) << 8) |
+                                ((uint32_t)__shfl_down((int)b, 2, 64) << 16) | ((uint32_t)__shfl_down((int)b, 3, 64) << 24);
+            if ((tid & 3u) == 0) st_rlx(L.split + CG_SPLIT_POSM + (c * CG_BLOCK + tid) / 4, wv);
+        }
         if (GROUND) {
             touched = wave_or(touched);
             if (l == 0 && touched) atomicOr(L.split + 1, touched);
         }
         __syncthreads();   // the chunk's sector minima are final in LDS
+        STAMP(29);
         if (GROUND && tid <= CG_NUM_BINS) atomicMin(L.split + 2 + tid, fs->sec_key[tid]);
-        __threadfence();
+        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
         __syncthreads();
         if (tid == 0)
-            fs->scal[S_LAST] = __hip_atomic_fetch_add(L.split, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+            fs->scal[S_LAST] = __hip_atomic_fetch_add(L.split, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                                gridDim.x - 1;
         __syncthreads();
         if (!fs->scal[S_LAST]) return;
-        __threadfence();
         // the last workgroup: the frame's sector keys and used bins (state reset for the next
         // frame), every lane's filter bits over the chunks
         if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = atomicExch(L.split + 2 + tid, 0xffffffffu);
