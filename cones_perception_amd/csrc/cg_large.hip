@@ -766,6 +766,26 @@ __device__ __forceinline__ void lg_dgrid_count_one(const LgScratch& S, uint32_t 
     S.uk[v] = k;
     S.ca[v] = atomicAdd(&S.cstart[k], 1u);
 }
+// Sequential float sums over lanes 0..n-1 of a wave (n wave-uniform), in lane order: blocks
+// of eight lanes with immediate lane indices (no lane-select SGPR, no per-member branch);
+// the lanes of the last block past n must hold +0.0f.
+__device__ __forceinline__ void lg_sum_lanes(uint32_t n, float a, float b, float c, float d, float& sa, float& sb,
+                                             float& sc, float& sd) {
+#define LG_ACC(k)                                                                \
+    sa += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a), k));       \
+    sb += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b), k));       \
+    sc += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c), k));       \
+    sd += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), k));
+#define LG_BLK(k0)                                                                                          \
+    if (n > k0) {                                                                                           \
+        LG_ACC(k0) LG_ACC(k0 + 1) LG_ACC(k0 + 2) LG_ACC(k0 + 3) LG_ACC(k0 + 4) LG_ACC(k0 + 5) LG_ACC(k0 + 6) \
+        LG_ACC(k0 + 7)                                                                                      \
+    }
+    LG_BLK(0) LG_BLK(8) LG_BLK(16) LG_BLK(24) LG_BLK(32) LG_BLK(40) LG_BLK(48) LG_BLK(56)
+#undef LG_BLK
+#undef LG_ACC
+}
+
 // CentroidPoint: float sums in ascending frame index / float(n); passthrough copies the point.
 // One wave per voxel: the lanes fetch 64 members at a time, the sums run through them in
 // member order.
@@ -790,18 +810,17 @@ __device__ __forceinline__ void lg_voxel_centroids_one(const CgLaunch& L, const 
         }
         return;
     }
-    const uint32_t s = S.run[v], e = v + 1 < V ? S.run[v + 1] : m[LG_NFIN_ALL];
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.run[v]);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(v + 1 < V ? S.run[v + 1] : m[LG_NFIN_ALL]));
     float sx = 0.f, sy = 0.f, sz = 0.f, si = 0.f;
     for (uint32_t g0 = s; g0 < e; g0 += 64) {
         const uint32_t n = min(64u, e - g0);
         float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
         if (l < n) p = lg_point(S, val[g0 + l], Ms);
-        for (uint32_t b = 0; b < n; b++) {
-            sx += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.x), (int)b));
-            sy += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.y), (int)b));
-            sz += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.z), (int)b));
-            si += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p.w), (int)b));
-        }
+        // lanes in blocks of eight with immediate lane indices; a block's lanes past n hold
+        // +0.0f, and adding +0.0f to a sum that starts at +0.0f is exact (the sum is never -0.0
+        // under round-to-nearest), so the sums are bit-identical to the member-by-member loop
+        lg_sum_lanes(n, p.x, p.y, p.z, p.w, sx, sy, sz, si);
     }
     if (l != 0) return;
     const float nn = (float)(e - s);
@@ -1480,7 +1499,8 @@ __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevP
     // one wave per cluster: the lanes fetch 64 members at a time, the sums run through them in
     // ascending member order (lane order), as the reference's loop does
     const uint32_t l = lane_id();
-    const uint32_t s = S.off[k], e = S.off[k + 1];
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.off[k]);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.off[k + 1]);
     float x = 0.0f, y = 0.0f;
     for (uint32_t g0 = s; g0 < e; g0 += 8 * 64) {   // eight chunks of 64 members in flight
         float px[8], py[8];
@@ -1499,10 +1519,8 @@ __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevP
         for (int c = 0; c < 8; c++) {
             const uint32_t i0 = g0 + 64 * c;
             const uint32_t n = i0 < e ? min(64u, e - i0) : 0u;
-            for (uint32_t b = 0; b < n; b++) {
-                x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[c]), (int)b));
-                y += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[c]), (int)b));
-            }
+            float z0 = 0.f, z1 = 0.f;   // two sums only (lg_sum_lanes' zero terms stay zero)
+            lg_sum_lanes(n, px[c], py[c], 0.f, 0.f, x, y, z0, z1);
         }
     }
     if (l != 0) return;
