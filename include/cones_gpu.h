@@ -130,6 +130,10 @@ typedef struct cg_detect_result {
     const int32_t* cluster_indices;  /* cluster_offsets[C] voxel indices, ascending per cluster */
     const float*   centroids;        /* C x 2: x, y after the radial push (z = 0) */
 } cg_detect_result;
+/* Synchronous. A frame of <= 65,536 points is launched before its bytes are staged: the call
+ * copies in->data into pinned memory chunk by chunk behind the launch, and each chunk's
+ * workgroup reads its chunk over PCIe once published. in->data is read until the call
+ * returns; CG_E_DEVICE if a chunk is not published within 200 ms. */
 int cg_detect(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out);
 
 /* ground_removal -> cone_detection composition of launch/cones_perception.launch:17-37
