@@ -8,14 +8,17 @@ batch. Frames are independent units: each rank processes its own batch (weak sca
 data-path collective); the timed region is bracketed by barrier + synchronize and the max
 over ranks is reported.
 
+The timed region is one host call: the K steps are enqueued by one cg_run_batches crossing
+(step s on engine s mod S and its stream), so the host's per-call latency cannot pace the GPU.
+
 The roofline object prices the dominant kernel by the algorithmic bytes B = 16 N + 20 V + 8 C
-+ 64 per frame over its average execution span, which the kernel stamps itself
-(s_memrealtime: first workgroup start to last workgroup end, cg_debug_launch_span). A batch is
-one launch of the fused frame kernel, cg_frame_kernel: one workgroup per frame. The
-diagnostic structures --split (front launch + backend launches; the front is then the priced
-kernel, cg_debug_front_span) and --pair (two half-frame workgroups per frame) are measured
-slower. cpu_baseline times the CPU restatement (oracle/, one core and the job's CPU share,
-same frames) on a bounded sample on rank 0.
++ 64 per frame over its average execution span, which each timed launch stamps
+itself (s_memrealtime: first workgroup start to last workgroup end, cg_debug_launch_spans,
+armed before the timed region: no host call between the launches). A batch is one launch of
+the fused frame kernel, cg_frame_kernel: one workgroup per frame. HIP events on the launch
+streams are recorded in a separate, identical pass after it (avg_launch_ms_events).
+cpu_baseline times the CPU restatement (oracle/, one core and the job's CPU share, same
+frames) on a bounded sample on rank 0.
 
 `--gpus N` without a launcher environment starts N ranks itself (torch.distributed.run on
 127.0.0.1, before any GPU call); under a launcher WORLD_SIZE must equal N. At N > 1 the C4
@@ -66,24 +69,11 @@ def main():
     ap.add_argument("--scatter", action="store_true",
                     help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
                          "scatter to ranks, process, gather per-frame headers (reported separately)")
-    ap.add_argument("--no-events", action="store_true", help="experiment: no per-launch HIP events")
+    ap.add_argument("--no-events", action="store_true", help="skip the HIP-event pass after the timed region")
     ap.add_argument("--streams", type=int, default=3,
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
     ap.add_argument("--no-scatter", action="store_true", help="at N>1, skip the C4 scatter/gather leg")
-    ap.add_argument("--split-streams", default="",
-                    help="F,B: each batch's front launch on one of F front streams and its backend launches on "
-                         "one of B back streams (cg_run_batch_split); --streams engines rotate over them")
-    ap.add_argument("--split", action="store_true",
-                    help="experiment: each batch as a front launch + backend launches (cg_debug_route 6) instead "
-                         "of one fused workgroup per frame")
-    ap.add_argument("--serve", action="store_true",
-                    help="experiment: each batch's backend launch beside its front launch, taking each frame as "
-                         "its front publishes it (cg_debug_route 8; backends on --split-streams' back streams, "
-                         "default 3,1)")
-    ap.add_argument("--pair", action="store_true",
-                    help="experiment: each frame as two half-frame workgroups (cg_debug_route 7, cg_pair.hip) "
-                         "instead of one fused workgroup per frame")
     ap.add_argument("--voxel-order", choices=["pcl", "point"], default="pcl",
                     help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
                          "every voxel bit as the reference) or ascending point order")
@@ -146,73 +136,76 @@ def main():
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
     vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
     engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
-    if args.split or args.pair or args.serve:
-        for e in engines:
-            e.debug_route(6 if args.split else (7 if args.pair else 8))
-    if args.serve and not args.split_streams:
-        args.split_streams = "3,1"
-    split_fb = [int(x) for x in args.split_streams.split(",")] if args.split_streams else None
-    if split_fb:   # F front streams, B back streams
-        streams = [torch.cuda.Stream(dev) for _ in range(split_fb[0])]
-        backs = [torch.cuda.Stream(dev) for _ in range(split_fb[1])]
-    else:
-        streams = [torch.cuda.Stream(dev) for _ in range(S)]
-        backs = []
-    assert all(st.cuda_stream != 0 for st in streams + backs)
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    assert all(st.cuda_stream != 0 for st in streams)
     eng, stream = engines[0], streams[0]
     counter = [0]
 
     def step(idx=None):
         i = counter[0] if idx is None else idx
         counter[0] += 1
-        e, st = engines[i % S], streams[i % len(streams)]
-        bs = backs[i % len(backs)].cuda_stream if backs else 0
-        e.run(d_ins[i % S].data_ptr(), F, N, 16, stream=st.cuda_stream, back_stream=bs)
+        e, st = engines[i % S], streams[i % S]
+        e.run(d_ins[i % S].data_ptr(), F, N, 16, stream=st.cuda_stream)
         return st
 
+    # the K timed steps as one cg_run_batches crossing: step s on engine s % S, its input copy
+    # and its stream (the rotation step() follows)
+    def queue(k):
+        return cp.BatchQueue([engines[i % S] for i in range(k)],
+                             [cp.batch_desc(d_ins[i % S].data_ptr(), F, N, 16) for i in range(k)],
+                             [streams[i % S].cuda_stream for i in range(k)])
+
     torch.cuda.synchronize(dev)
-    for _ in range(args.warmup):
-        step()
+    if args.warmup:
+        queue(args.warmup).run()
     torch.cuda.synchronize(dev)
+    timed = queue(args.steps)
+    # each timed launch stamps its own execution span (first workgroup start, last workgroup
+    # end: what rocprofv3's kernel trace reports); armed per engine before the region
+    spans = torch.zeros((args.steps, 2), dtype=torch.int64, device=dev)
+    spans[:, 0] = 2 ** 63 - 1
+    per_eng = [list(range(k, args.steps, S)) for k in range(S)]
+    span_bufs = [torch.zeros((max(1, len(ix)), 2), dtype=torch.int64, device=dev) for ix in per_eng]
+    for k in range(S):
+        span_bufs[k][:, 0] = 2 ** 63 - 1
+    torch.cuda.synchronize(dev)
+    for k in range(S):
+        engines[k].spans(span_bufs[k].data_ptr(), len(per_eng[k]))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    # each timed launch also stamps its own execution span (first workgroup start, last
-    # workgroup end: what rocprofv3's kernel trace reports); events on a stream with queued
-    # work also count the wait for CU slots behind the other streams' launches
-    # [step start, step end, front start, front end]: a detector batch is a front launch (all the
-    # frame streaming) and a backend launch on the same stream
-    spans = torch.zeros((args.steps, 4), dtype=torch.int64, device=dev)
-    spans[:, 0] = 2 ** 63 - 1
-    spans[:, 2] = 2 ** 63 - 1
-    torch.cuda.synchronize(dev)
-    lib = cp.lib()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        st = streams[(counter[0]) % len(streams)]
-        lib.cg_debug_launch_span(engines[counter[0] % S].handle, spans[s].data_ptr())
-        lib.cg_debug_front_span(engines[counter[0] % S].handle, spans[s, 2:].data_ptr())
-        if not args.no_events:
-            evs[s][0].record(st)
-        step()
-        if not args.no_events:
-            evs[s][1].record(st)
+    timed.run()
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs] if not args.no_events else [0.0]
-    avg_event_ms = sum(kern_ms) / len(kern_ms)
+    counter[0] = args.warmup + args.steps
+    for k in range(S):
+        if per_eng[k]:
+            spans[per_eng[k]] = span_bufs[k][: len(per_eng[k])]
     sp = spans.cpu().numpy()
     spans_ok = bool((sp[:, 0] < 2 ** 63 - 1).all() and (sp[:, 1] > sp[:, 0]).all())
+    # HIP events on the launch streams, in an identical untimed pass: with queued launches on
+    # three streams a start event fires when its predecessor ends, and the kernel may still
+    # wait for CU slots, so this reads above the in-kernel span
+    avg_event_ms = None
+    if not args.no_events:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        torch.cuda.synchronize(dev)
+        for s_ in range(args.steps):
+            st = streams[counter[0] % S]
+            evs[s_][0].record(st)
+            step()
+            evs[s_][1].record(st)
+        torch.cuda.synchronize(dev)
+        kern_ms = [a.elapsed_time(b) for a, b in evs]
+        avg_event_ms = sum(kern_ms) / len(kern_ms)
     step_span_ms = float((sp[:, 1] - sp[:, 0]).mean()) * 1e-5 if spans_ok else avg_event_ms   # 100 MHz ticks
-    front_ok = bool((sp[:, 2] < 2 ** 63 - 1).all() and (sp[:, 3] > sp[:, 2]).all())
-    split = front_ok   # front launch + backend launches (--split / --split-streams; default: one fused kernel)
-    avg_kernel_ms = float((sp[:, 3] - sp[:, 2]).mean()) * 1e-5 if split else step_span_ms
+    avg_kernel_ms = step_span_ms
 
     # algorithmic bytes of one launch, from the frames' own V and C
     res = engines[(counter[0] - 1) % S].results()
@@ -305,17 +298,16 @@ def main():
                                    "simulation params), ground_removal + cone_detection fused",
                        "frames_per_gpu": F, "points_per_frame": N, "global_batch": F * world,
                        "parallelism": f"frame-shard x{world}", "streams_per_gpu": S,
-                       "launches": "front + served backend" if args.serve else
-                       ("front + backend" if (args.split or args.split_streams) else
-                        ("half-frame pair kernel" if args.pair else "fused frame kernel")),
-                       "split_streams": args.split_streams or None,
+                       "launches": "fused frame kernel, one workgroup per frame",
+                       "enqueue": "one cg_run_batches call for the timed steps",
                        "voxel_order": args.voxel_order},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic_per_launch(F),
-                         "kernel": "cg_front_kernel" if split else ("cg_pair_kernel" if args.pair else "cg_frame_kernel"),
+                         "traffic_source": traffic_source(),
+                         "kernel": "cg_frame_kernel",
                          "avg_kernel_ms": avg_kernel_ms,
-                         "avg_kernel_ms_source": "in-kernel span (s_memrealtime)" if spans_ok else "HIP events",
-                         # the step's device work: front launch start to backend launch end
+                         "avg_kernel_ms_source": ("in-kernel span (s_memrealtime) of the timed launches" if spans_ok
+                                                  else "HIP events (untimed pass)"),
                          "step_span_ms": step_span_ms,
                          "step_span_ms_max": float((sp[:, 1] - sp[:, 0]).max()) * 1e-5 if spans_ok else None,
                          "step_span_frac": bytes_per_launch / (step_span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -330,8 +322,6 @@ def main():
                          / HBM_COPY_GBS},
             "cpu_baseline": cpu,
             "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
-            # the pair launch's never-expected wait timeouts, in the last batch's frame flags
-            "pair_timeouts": int(((hdr_np[:, 5] & 0x10) != 0).sum()) if args.pair else None,
         }
         if single is not None:
             line["single_frame"] = single
@@ -437,18 +427,29 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
-def traffic_per_launch(F):
-    """HBM bytes per launch from the newest committed PMC summary (profiles/rNN_traffic.json:
-    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction), scaled to this launch's frames."""
+def _newest_traffic():
     import glob
     got = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*_traffic.json")),
                  key=lambda q: int(os.path.basename(q)[1:].split("_")[0]))
-    if not got:
+    return got[-1] if got else None
+
+
+def traffic_per_launch(F):
+    """HBM bytes per launch from the newest committed PMC summary (profiles/rNN_traffic.json:
+    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction), scaled to this launch's frames.
+    Not measured in this run: rocprofv3 --pmc passes are separate runs (traffic_source)."""
+    p = _newest_traffic()
+    if not p:
         return None
-    p = got[-1]
     with open(p) as fh:
         t = json.load(fh)
     return t["hbm_bytes_per_frame"] * F
+
+
+def traffic_source():
+    p = _newest_traffic()
+    return (f"not measured in this run: {os.path.relpath(p, ROOT)} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+            "per frame) x frames per launch") if p else None
 
 
 def fetch_headers(res, F):

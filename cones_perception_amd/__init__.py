@@ -19,7 +19,7 @@ import numpy as np
 from . import _abi
 from ._abi import (CG_VOXEL_ORDER_PCL, CG_VOXEL_ORDER_POINT, CG_F_VOXEL_POINT_ORDER,  # noqa: F401
                    CG_MODE_DETECT, CG_MODE_PIPELINE, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL,
-                   CG_F_VOXEL_PASSTHROUGH, CG_F_PAIR_TIMEOUT, CgError, check, lib)
+                   CG_F_VOXEL_PASSTHROUGH, CgError, check, lib)
 
 lib()   # fail loudly at import if the gfx950 library is missing
 
@@ -440,21 +440,15 @@ class BatchEngine(_Handle):
 
     def run(self, d_ptr: int, n_frames: int, n_points: int, point_step: int = 16,
             frame_stride: Optional[int] = None, mode: int = CG_MODE_PIPELINE, stream: int = 0,
-            offsets=(0, 4, 8, 12), is_dense: bool = True, back_stream: int = 0):
-        """back_stream (with stream): the backend launches of a split batch on their own stream
-        (cg_run_batch_split); the results are complete once back_stream has run them."""
-        b = _abi.cg_batch()
-        b.d_data = d_ptr
-        b.frame_stride = frame_stride if frame_stride is not None else n_points * point_step
-        b.n_frames, b.n_points, b.point_step = n_frames, n_points, point_step
-        b.off_x, b.off_y, b.off_z, b.off_intensity = offsets
-        b.is_dense = 1 if is_dense else 0
-        if back_stream:
-            if not stream:
-                raise ValueError("back_stream needs an explicit front stream")
-            check(lib().cg_run_batch_split(self._h, C.byref(b), mode, C.c_void_p(stream), C.c_void_p(back_stream)))
-        else:
-            check(lib().cg_run_batch(self._h, C.byref(b), mode, C.c_void_p(stream) if stream else None))
+            offsets=(0, 4, 8, 12), is_dense: bool = True):
+        """cg_run_batch on `stream` (0: the handle's own)."""
+        b = batch_desc(d_ptr, n_frames, n_points, point_step, frame_stride, offsets, is_dense)
+        check(lib().cg_run_batch(self._h, C.byref(b), mode, C.c_void_p(stream) if stream else None))
+
+    def spans(self, d_spans: int, n_launches: int):
+        """cg_debug_launch_spans: the next n_launches launches record their execution spans."""
+        check(lib().cg_debug_launch_spans(self._h, C.c_void_p(d_spans), n_launches))
+        return self
 
     def results(self) -> _abi.cg_batch_results:
         r = _abi.cg_batch_results()
@@ -470,6 +464,39 @@ class BatchEngine(_Handle):
         """get_reconstructed_cone for frame `frame` of the last batch (cg_batch_recrop): the
         batch's input must still be resident."""
         return _recrop(self._h, centers, frame)
+
+
+def batch_desc(d_ptr: int, n_frames: int, n_points: int, point_step: int = 16,
+               frame_stride: Optional[int] = None, offsets=(0, 4, 8, 12), is_dense: bool = True) -> _abi.cg_batch:
+    """A cg_batch for frames in device memory."""
+    b = _abi.cg_batch()
+    b.d_data = d_ptr
+    b.frame_stride = frame_stride if frame_stride is not None else n_points * point_step
+    b.n_frames, b.n_points, b.point_step = n_frames, n_points, point_step
+    b.off_x, b.off_y, b.off_z, b.off_intensity = offsets
+    b.is_dense = 1 if is_dense else 0
+    return b
+
+
+class BatchQueue:
+    """A sequence of batch calls enqueued in one cg_run_batches crossing: call i runs batches[i]
+    on engines[i] on streams[i] (stream handles; 0 = the engine's own). Built once, run many
+    times (the descriptors stay in ctypes arrays)."""
+
+    def __init__(self, engines, batches, streams, mode: int = CG_MODE_PIPELINE):
+        n = len(engines)
+        if not (len(batches) == len(streams) == n):
+            raise ValueError("engines, batches and streams differ in length")
+        self.n, self.mode = n, mode
+        self._keep = list(engines)
+        self._h = (C.c_void_p * n)(*[e.handle.value for e in engines])
+        self._b = (_abi.cg_batch * n)(*batches)
+        self._s = (C.c_void_p * n)(*[s or None for s in streams])
+        self._done = C.c_uint32(0)
+
+    def run(self) -> int:
+        check(lib().cg_run_batches(self._h, self._b, self.n, self.mode, self._s, C.byref(self._done)))
+        return self._done.value
 
 
 # ---------------------------------------------------------------------------------------

@@ -13,7 +13,6 @@ LIB_PATH = os.environ.get("CONES_GPU_LIB") or os.path.join(_HERE, "lib", "libcon
 
 CG_OK, CG_E_INVALID, CG_E_DEVICE, CG_E_OOM, CG_E_CAPACITY = 0, 1, 2, 3, 4
 CG_F_VOXEL_PASSTHROUGH, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL, CG_F_VOXEL_POINT_ORDER = 0x1, 0x2, 0x4, 0x8
-CG_F_PAIR_TIMEOUT = 0x10
 CG_VOXEL_ORDER_POINT, CG_VOXEL_ORDER_PCL = 0, 1
 CG_MODE_PIPELINE, CG_MODE_DETECT = 0, 1
 CG_HDR_N, CG_HDR_K, CG_HDR_M, CG_HDR_V, CG_HDR_C, CG_HDR_FLAGS, CG_HDR_WORDS = 0, 1, 2, 3, 4, 5, 8
@@ -136,7 +135,8 @@ _SIGS = {
     "cg_detect": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_detect_result)]),
     "cg_pipeline": (C.c_int, [C.c_void_p, C.POINTER(cg_cloud_view), C.POINTER(cg_detect_result)]),
     "cg_run_batch": (C.c_int, [C.c_void_p, C.POINTER(cg_batch), C.c_int, C.c_void_p]),
-    "cg_run_batch_split": (C.c_int, [C.c_void_p, C.POINTER(cg_batch), C.c_int, C.c_void_p, C.c_void_p]),
+    "cg_run_batches": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(cg_batch), C.c_uint32, C.c_int,
+                                 C.POINTER(C.c_void_p), C.POINTER(C.c_uint32)]),
     "cg_tile_front": (C.c_int, [C.c_void_p, C.POINTER(cg_tile), C.c_void_p]),
     "cg_tile_decide": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "cg_tile_survivors": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
@@ -163,7 +163,7 @@ _SIGS = {
     "cg_debug_stamps": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_debug_route": (C.c_int, [C.c_void_p, C.c_int]),
     "cg_debug_launch_span": (C.c_int, [C.c_void_p, C.c_void_p]),
-    "cg_debug_front_span": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "cg_debug_launch_spans": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_debug_large_meta": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "cg_debug_large_buffer": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64]),
     "cg_debug_stamps_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),

@@ -57,14 +57,6 @@ def build(verbose=False, force=False):
         if force or _stale(o, [src] + HEADERS):
             jobs.append([HIPCC, "-x", "hip", *HIP_FLAGS, "-c", src, "-o", o])
         objs.append(o)
-    # the backend launch and the half-frame pair kernel of batch frames: the same device code
-    # at 256 threads per workgroup
-    for name in ("cg_back.hip", "cg_pair.hip"):
-        src = os.path.join(CSRC, name)
-        o = os.path.join(OBJ, name.rsplit(".", 1)[0] + ".o")
-        if force or _stale(o, [src] + HEADERS):
-            jobs.append([HIPCC, "-x", "hip", *HIP_FLAGS, "-DCG_BLOCK=256", "-c", src, "-o", o])
-        objs.append(o)
     if jobs:   # the translation units compile independently (hipcc is single-threaded)
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(min(len(jobs), max(1, (os.cpu_count() or 1)))) as ex:

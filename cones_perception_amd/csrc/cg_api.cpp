@@ -67,10 +67,9 @@ struct cg_handle {
     uint32_t last_frames = 0, last_points = 0;
     int last_mode = -1;
     hipStream_t last_stream = nullptr;
-    // split batches on two streams (cg_run_batch_split): the front launch's completion, and the
-    // last backend launch's (the next front on this handle reuses the survivor slots)
-    hipEvent_t ev_front = nullptr, ev_back = nullptr;
-    hipStream_t back_stream_pending = nullptr;   // stream of the backend launches not yet waited on
+    // orders a batch call on another stream after the handle's previous work (its result and
+    // scratch slots are reused): recorded on the previous stream at the switch
+    hipEvent_t ev_switch = nullptr;
     // host results
     uint32_t h_hdr[CG_HDR_WORDS] = {};
     uint32_t* d_split = nullptr;     // split single-frame launch state (CG_SPLIT_WORDS)
@@ -93,9 +92,9 @@ struct cg_handle {
     uint32_t large2_points = 0;
     LgScratch lg{};
     int route = 0;                // cg_debug_route
-    uint32_t pair_epoch = 0;      // pair launches so far (cg_pair.hip ready words)
-    unsigned long long* next_span = nullptr;   // cg_debug_launch_span
-    unsigned long long* next_front_span = nullptr;   // cg_debug_front_span
+    uint32_t retries = 0;         // single-frame calls re-run by DMA after a staging timeout
+    unsigned long long* next_span = nullptr;   // cg_debug_launch_spans: the next launch's span slot
+    uint32_t spans_left = 0;                   //   and how many launches still record
     cg_tile tile{};               // the rank's tile (cg_tile_front .. cg_tile_decide)
     bool tile_ready = false;
     // the last single-frame call, for cg_recrop
@@ -107,9 +106,6 @@ struct cg_handle {
     bool batch_valid = false;
     uint32_t last_k = 0;
     uint32_t* d_seckeys = nullptr;   // 18 words per frame inside d_hdr (not owned)
-    uint32_t* d_biglist = nullptr;   // split batches' large-capacity frame list inside d_hdr (not owned)
-    uint32_t* d_serve = nullptr;     // served batches' publish words inside d_hdr (not owned)
-    uint32_t serve_epoch = 0;        // served batches so far
     RcBox* d_boxes = nullptr;
     uint32_t* d_rc_cnt = nullptr;    // boxes x blocks, twice (counts, offsets)
     size_t rc_cnt_cap = 0;
@@ -140,17 +136,11 @@ int own_stream(cg_handle* h) {
 }
 
 void free_batch(cg_handle* h) {
-    if (h->back_stream_pending && h->ev_back) {   // a split batch's backends still read the slots
-        (void)hipEventSynchronize(h->ev_back);
-        h->back_stream_pending = nullptr;
-    }
     (void)hipFree(h->d_hdr); (void)hipFree(h->d_vox); (void)hipFree(h->d_lab); (void)hipFree(h->d_offs);
     (void)hipFree(h->d_idx); (void)hipFree(h->d_cen); (void)hipFree(h->d_ground); (void)hipFree(h->d_scratch);
     h->d_hdr = nullptr; h->d_vox = nullptr; h->d_lab = nullptr; h->d_offs = nullptr;
     h->d_idx = nullptr; h->d_cen = nullptr; h->d_ground = nullptr; h->d_scratch = nullptr;
     h->d_seckeys = nullptr;
-    h->d_biglist = nullptr;
-    h->d_serve = nullptr;
     h->cap_frames = h->cap_points = 0;
 }
 
@@ -166,15 +156,8 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     free_batch(h);
     const uint64_t F = nf, C = np;
     // headers, then each frame's 18 final sector-minimum keys (cg_recrop of a pipeline frame)
-    // headers, sector keys, then the split batch's list of large-capacity frames (F + 2 words,
-    // zeroed here; each batch's cg_back_big clears it again), then the served batch's words
-    // (zeroed here; the publish words hold the batch's epoch)
-    HIPCHK(hipMalloc(&h->d_hdr, (F * (CG_HDR_WORDS + CG_NUM_BINS + 1) + F + 2 + CG_SERVE_WORDS(F)) * 4));
+    HIPCHK(hipMalloc(&h->d_hdr, F * (CG_HDR_WORDS + CG_NUM_BINS + 1) * 4));
     h->d_seckeys = h->d_hdr + F * CG_HDR_WORDS;
-    h->d_biglist = h->d_seckeys + F * (CG_NUM_BINS + 1);
-    h->d_serve = h->d_biglist + F + 2;
-    HIPCHK(hipMemset(h->d_biglist, 0, (F + 2 + CG_SERVE_WORDS(F)) * 4));
-    h->serve_epoch = 0;
     HIPCHK(hipMalloc(&h->d_vox, F * C * 16));
     HIPCHK(hipMalloc(&h->d_lab, F * C * 4));
     HIPCHK(hipMalloc(&h->d_offs, F * (C + 1) * 4));
@@ -183,10 +166,6 @@ int ensure_batch(cg_handle* h, uint32_t frames, uint32_t points, bool ground) {
     // the frame kernel's HBM fallback (M > CG_MMAX) serves frames of <= CG_MAX_POINTS points
     h->scratch_stride = (cg_scratch_bytes(std::min<uint32_t>(np, CG_MAX_POINTS)) + 255) & ~255ull;
     HIPCHK(hipMalloc(&h->d_scratch, F * h->scratch_stride));
-    HIPCHK(hipMemset(h->d_scratch, 0, F * h->scratch_stride));   // the pair launch's exchange words
-    // the zeroed words before any launch on the caller's (non-blocking) streams
-    HIPCHK(hipStreamSynchronize(nullptr));
-    h->pair_epoch = 0;
     if (had_ground) HIPCHK(hipMalloc(&h->d_ground, F * C * 32));
     h->cap_frames = nf;
     h->cap_points = np;
@@ -261,7 +240,6 @@ void fill_launch_outputs(cg_handle* h, CgLaunch& L) {
     L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
     L.idx = h->d_idx; L.cen = h->d_cen; L.ground = h->d_ground;
     L.scratch = h->d_scratch; L.scratch_stride = h->scratch_stride;
-    L.biglist = h->d_biglist;
     L.stamps = nullptr;
     if (h->stamps_on) {
         // stamps are indexed by workgroup: a split single-frame launch has one workgroup per
@@ -320,57 +298,42 @@ int ensure_large2(cg_handle* h, uint32_t n) {
     return CG_OK;
 }
 
-int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s, hipStream_t s_back = nullptr) {
+// Work enqueued on stream s reuses the handle's result and scratch slots: when the handle's last
+// work went to another stream, s waits for it (the handle's calls stay ordered whatever stream
+// each names). Calls on one stream pay nothing.
+int order_after_last(cg_handle* h, hipStream_t s) {
+    if (!h->last_stream || h->last_stream == s) return CG_OK;
+    if (!h->ev_switch) HIPCHK(hipEventCreateWithFlags(&h->ev_switch, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(h->ev_switch, h->last_stream));
+    HIPCHK(hipStreamWaitEvent(s, h->ev_switch, 0));
+    return CG_OK;
+}
+
+// order_after_last, then s is the handle's last stream (entry points that enqueue on the
+// handle's buffers)
+int use_stream(cg_handle* h, hipStream_t s) {
+    int rc = order_after_last(h, s);
+    if (!rc) h->last_stream = s;
+    return rc;
+}
+
+// The next launch's span slot (cg_debug_launch_spans), or null.
+unsigned long long* take_span(cg_handle* h) {
+    if (!h->spans_left) return nullptr;
+    unsigned long long* p = h->next_span;
+    h->next_span += 2;
+    h->spans_left--;
+    return p;
+}
+
+int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
     const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2 || h->route == 5) && L.n_points > 0);
     if (!large && L.split) {
         HIPCHK((hipError_t)cg_launch_split(L, h->dp, kmode, s));
         return CG_OK;
     }
-    if (!large) {
-        if (h->route == 8 && kmode != CG_KMODE_GROUND) {
-            // served batch: the front on s publishes each frame; the backend launch on s_back
-            // (s when none) takes each as it comes, with no dependency on the front's end. The
-            // next front of this handle waits for it (the slots are read until then).
-            hipStream_t sb = s_back ? s_back : s;
-            if (!h->ev_back) HIPCHK(hipEventCreateWithFlags(&h->ev_back, hipEventDisableTiming));
-            if (h->back_stream_pending) HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
-            L.serve = h->d_serve;
-            L.epoch = ++h->serve_epoch;
-            L.stamps = nullptr;
-            HIPCHK((hipError_t)cg_launch_front(L, h->dp, kmode, s));
-            HIPCHK((hipError_t)cg_launch_serve(L, h->dp, sb));
-            HIPCHK(hipEventRecord(h->ev_back, sb));
-            h->back_stream_pending = sb;
-            return CG_OK;
-        }
-        if (s_back && s_back != s) {
-            // the front on s; the backend launches on s_back once the front is done; the next
-            // front of this handle waits for them (cg_run_batch_split)
-            if (!h->ev_front) HIPCHK(hipEventCreateWithFlags(&h->ev_front, hipEventDisableTiming));
-            if (!h->ev_back) HIPCHK(hipEventCreateWithFlags(&h->ev_back, hipEventDisableTiming));
-            if (h->back_stream_pending) HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
-            HIPCHK((hipError_t)cg_launch_front(L, h->dp, kmode, s));
-            HIPCHK(hipEventRecord(h->ev_front, s));
-            HIPCHK(hipStreamWaitEvent(s_back, h->ev_front, 0));
-            HIPCHK((hipError_t)cg_launch_backends(L, h->dp, s_back));
-            HIPCHK(hipEventRecord(h->ev_back, s_back));
-            h->back_stream_pending = s_back;
-            return CG_OK;
-        }
-        if (h->back_stream_pending) {   // a split batch's backend may still read the survivor slots
-            HIPCHK(hipStreamWaitEvent(s, h->ev_back, 0));
-            h->back_stream_pending = nullptr;
-        }
-        if (h->route == 7 && kmode == CG_KMODE_PIPELINE && L.n_points > CG_MAX_POINTS / 2) {
-            // two half-frame workgroups per frame (cg_pair.hip); no phase stamps (they are
-            // indexed by workgroup, and this grid has twice as many as the buffer has frames)
-            L.epoch = ++h->pair_epoch;
-            L.stamps = nullptr;
-            HIPCHK((hipError_t)cg_launch_pair(L, h->dp, s));
-            return CG_OK;
-        }
-        // one fused workgroup per frame; cg_debug_route 6: the front launch + backend launches
-        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s, h->route != 6));
+    if (!large) {   // one fused workgroup per frame
+        HIPCHK((hipError_t)cg_launch_batch(L, h->dp, kmode, s));
         return CG_OK;
     }
     int rc = ensure_large(h, L.n_points);
@@ -489,30 +452,36 @@ void publish_chunks(cg_handle* h, const cg_cloud_view* v, uint32_t n, uint32_t s
     }
 }
 
+// dma_retry: the frame again with its input staged whole and copied by DMA (route 4's form),
+// after a zero-copy call whose chunk workgroups gave up waiting for the host's publish words
+// (a host thread descheduled for CG_STAGE_TIMEOUT): the call is then only slower, never failed.
 int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_result* dres,
-               cg_ground_result* gres) {
+               cg_ground_result* gres, bool dma_retry = false) {
     if (!h) return fail(CG_E_INVALID, "null handle");
     int rc = check_view(in);
     if (rc) return rc;
     HIPCHK(hipSetDevice(h->device));
     rc = own_stream(h);
     if (rc) return rc;
+    if ((rc = order_after_last(h, h->stream))) return rc;
     const uint32_t n = in->width * in->height;
     rc = ensure_batch(h, 1, n, kmode == CG_KMODE_GROUND);
     if (rc) return rc;
     CgLaunch L{};
     // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
     // the one-workgroup frame kernel, for comparisons)
-    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4);
+    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4 || h->route == 6);
     bool staged_later = false;
-    rc = stage_frame(h, in, L, split && h->route == 0, &staged_later);   // route 4: split, input by DMA
+    // route 4: split, input by DMA; route 6 (tests): zero-copy with no chunk ever published
+    const bool zero_copy = split && (h->route == 0 || h->route == 6) && !dma_retry;
+    rc = stage_frame(h, in, L, zero_copy, &staged_later);
     if (rc) return rc;
     fill_launch_outputs(h, L);
     h->last_single = false;
     if (kmode == CG_KMODE_PIPELINE) {
         L.seckeys = h->d_seckeys;
     }
-    if (split && h->route == 0) {   // the input's chunks published after the launch
+    if (zero_copy) {   // the input's chunks published after the launch
         if (!h->h_flags) {
             HIPCHK(hipHostMalloc((void**)&h->h_flags, 64 * 4, hipHostMallocCoherent));
             std::memset(h->h_flags, 0, 64 * 4);
@@ -521,7 +490,7 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         h->stage_seq = h->stage_seq + 1 ? h->stage_seq + 1 : 1;
         L.in_flags = h->h_flags_dev;
         L.in_seq = h->stage_seq;
-        if (!staged_later) publish_chunks(h, in, n, 0, true);   // already staged: publish every chunk
+        if (!staged_later && h->route != 6) publish_chunks(h, in, n, 0, true);   // already staged: publish every chunk
     }
     if (split) {
         if (!h->d_split) {
@@ -537,7 +506,7 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     h->packed = L.pack != nullptr;
     rc = launch_frames(h, L, kmode, h->stream);
     if (rc) return rc;
-    if (staged_later) publish_chunks(h, in, n, L.point_step, false);   // overlaps the chunk workgroups
+    if (staged_later && h->route != 6) publish_chunks(h, in, n, L.point_step, false);   // overlaps the chunk workgroups
     h->last_frames = 1; h->last_points = n; h->last_mode = kmode; h->last_stream = h->stream;
     h->last_in = L;
     if (kmode == CG_KMODE_GROUND) {
@@ -560,8 +529,12 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     }
     rc = fetch_frame(h, h->stream, 0, dres);
     if (rc) return rc;
-    if (L.in_flags && __atomic_load_n(&h->h_flags[CG_STAGE_ERR], __ATOMIC_ACQUIRE) == L.in_seq)
-        return fail(CG_E_DEVICE, "the split kernel timed out waiting for the staged input");
+    if (L.in_flags && __atomic_load_n(&h->h_flags[CG_STAGE_ERR], __ATOMIC_ACQUIRE) == L.in_seq) {
+        // a chunk was processed before its bytes were published: the results are void; the
+        // staging buffer is complete now, so the frame runs again with its input by DMA
+        h->retries++;
+        return run_single(h, in, kmode, dres, gres, true);
+    }
     h->last_k = h->h_hdr[CG_HDR_K];
     h->last_single = true;
     return CG_OK;
@@ -633,8 +606,7 @@ int cg_destroy(cg_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)cg_stream_wait(h->stream);
     free_batch(h);
-    if (h->ev_front) (void)hipEventDestroy(h->ev_front);
-    if (h->ev_back) (void)hipEventDestroy(h->ev_back);
+    if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
     if (h->d_stamps) (void)hipFree(h->d_stamps);
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->h_meta) (void)hipHostFree(h->h_meta);
@@ -793,21 +765,8 @@ int cg_batch_recrop(cg_handle* h, uint32_t frame, const float* centers_xy, uint3
 }
 
 namespace {
-int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream, void* back_stream);
-}  // namespace
-
-int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
-    return run_batch(h, b, mode, hip_stream, nullptr);
-}
-
-int cg_run_batch_split(cg_handle* h, const cg_batch* b, int mode, void* front_stream, void* back_stream) {
-    if (!front_stream || !back_stream) return fail(CG_E_INVALID, "cg_run_batch_split needs two streams");
-    return run_batch(h, b, mode, front_stream, back_stream);
-}
-
-namespace {
-int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream, void* back_stream) {
-    if (!h || !b) return fail(CG_E_INVALID, "null argument");
+int check_batch(const cg_batch* b, int mode) {
+    if (!b) return fail(CG_E_INVALID, "null batch");
     if (mode != CG_MODE_PIPELINE && mode != CG_MODE_DETECT) return fail(CG_E_INVALID, "bad mode %d", mode);
     if (b->n_points > CG_MAX_FRAME_POINTS)
         return fail(CG_E_CAPACITY, "frames of %u points; the engine supports <= %u", b->n_points,
@@ -820,7 +779,11 @@ int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream, void*
     for (int32_t o : offs)
         if (o >= 0 && (o % 4 || (uint32_t)o + 4 > b->point_step))
             return fail(CG_E_INVALID, "field offset %d invalid for point_step %u", o, b->point_step);
-    HIPCHK(hipSetDevice(h->device));
+    return CG_OK;
+}
+
+// One checked batch call on the handle's device (already current).
+int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
     int rc = ensure_batch(h, b->n_frames, b->n_points, false);
     if (rc) return rc;
     CgLaunch L{};
@@ -837,24 +800,52 @@ int run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream, void*
         if (rc) return rc;
     }
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
-    L.span = h->next_span;
-    h->next_span = nullptr;
-    L.span_front = h->next_front_span;
-    h->next_front_span = nullptr;
+    if ((rc = order_after_last(h, s))) return rc;
+    L.span = take_span(h);
     const int kmode = mode == CG_MODE_PIPELINE ? CG_KMODE_PIPELINE : CG_KMODE_DETECT;
     if (kmode == CG_KMODE_PIPELINE) L.seckeys = h->d_seckeys;   // per frame, for cg_batch_recrop
-    rc = launch_frames(h, L, kmode, s, (hipStream_t)back_stream);
+    rc = launch_frames(h, L, kmode, s);
     if (rc) return rc;
     h->last_batch = L;
     h->batch_kmode = kmode;
     h->batch_valid = true;
     h->last_frames = b->n_frames; h->last_points = b->n_points; h->last_mode = mode;
-    // the results are complete where the last launch of the batch ran
-    h->last_stream = h->back_stream_pending ? h->back_stream_pending : s;
+    h->last_stream = s;
     h->last_single = false;
     return CG_OK;
 }
 }  // namespace
+
+int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream) {
+    if (!h || !b) return fail(CG_E_INVALID, "null argument");
+    int rc = check_batch(b, mode);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(h->device));
+    return run_batch(h, b, mode, hip_stream);
+}
+
+int cg_run_batches(cg_handle* const* handles, const cg_batch* batches, uint32_t n_calls, int mode,
+                   void* const* hip_streams, uint32_t* n_done) {
+    if (n_done) *n_done = 0;
+    if (n_calls && (!handles || !batches || !hip_streams)) return fail(CG_E_INVALID, "null argument");
+    for (uint32_t i = 0; i < n_calls; i++) {   // every call checked before any is enqueued
+        if (!handles[i]) return fail(CG_E_INVALID, "null handle at call %u", i);
+        int rc = check_batch(&batches[i], mode);
+        if (rc) return rc;
+    }
+    int dev = -1;
+    for (uint32_t i = 0; i < n_calls; i++) {
+        cg_handle* h = handles[i];
+        if (h->device != dev) {
+            HIPCHK(hipSetDevice(h->device));
+            dev = h->device;
+        }
+        int rc = run_batch(h, &batches[i], mode, hip_streams[i]);
+        if (rc) return rc;
+        if (n_done) *n_done = i + 1;
+    }
+    return CG_OK;
+}
 
 int cg_batch_results_get(cg_handle* h, cg_batch_results* out) {
     if (!h || !out) return fail(CG_E_INVALID, "null argument");
@@ -904,6 +895,7 @@ int cg_tile_front(cg_handle* h, const cg_tile* t, uint32_t* keys) {
     int rc = own_stream(h);
     if (rc) return rc;
     rc = ensure_large(h, std::max<uint32_t>(t->n, 1));
+    if (!rc) rc = use_stream(h, h->stream);
     if (rc) return rc;
     h->tile = *t;
     CgLaunch L = tile_launch(*t);
@@ -920,6 +912,7 @@ int cg_tile_decide(cg_handle* h, const uint32_t* merged_keys, uint32_t* counts) 
     if (!h || !merged_keys || !counts) return fail(CG_E_INVALID, "null argument");
     if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_decide before cg_tile_front");
     HIPCHK(hipSetDevice(h->device));
+    if (int rc = use_stream(h, h->stream)) return rc;
     LgScratch S = route_scratch(h);
     S.pidx_base = h->tile.first;
     HIPCHK(hipMemcpyAsync(S.meta + LG_SECKEY, merged_keys, CG_TILE_KEYS * 4, hipMemcpyHostToDevice, h->stream));
@@ -939,6 +932,7 @@ int cg_tile_survivors(cg_handle* h, float* d_points, uint32_t* d_index, uint32_t
     if (!h) return fail(CG_E_INVALID, "null handle");
     if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_survivors before cg_tile_front");
     HIPCHK(hipSetDevice(h->device));
+    if (int rc = use_stream(h, h->stream)) return rc;
     uint32_t n = 0;
     HIPCHK(hipMemcpyAsync(&n, h->lg.meta + LG_MS, 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(cg_stream_wait(h->stream));
@@ -966,10 +960,10 @@ int cg_tile_backend(cg_handle* h, const float* d_points, const uint32_t* d_index
     rc = ensure_large(h, n_total);
     if (rc) return rc;
     rc = ensure_batch(h, 1, n_total, false);
+    if (!rc) rc = use_stream(h, h->stream);
     if (rc) return rc;
     LgScratch S = route_scratch(h);
     S.pidx_base = 0;
-    S.force_global = h->route == 2 ? 1u : 0u;
     HIPCHK((hipError_t)cg_large_set_survivors(S, h->dp, d_points, d_index, n_survivors, merged_counts, h->stream));
     CgLaunch L{};
     L.n_frames = 1;
@@ -996,6 +990,7 @@ int cg_tile_front_async(cg_handle* h, const cg_tile* t, uint32_t* d_keys, void* 
     if ((rc = own_stream(h))) return rc;
     if ((rc = ensure_large(h, std::max<uint32_t>(t->n, 1)))) return rc;
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    if ((rc = use_stream(h, s))) return rc;
     h->tile = *t;
     LgScratch S = route_scratch(h);
     S.pidx_base = t->first;
@@ -1010,6 +1005,7 @@ int cg_tile_decide_async(cg_handle* h, const uint32_t* d_merged_keys, uint32_t* 
     if (!h->tile_ready) return fail(CG_E_INVALID, "cg_tile_decide_async before cg_tile_front_async");
     HIPCHK(hipSetDevice(h->device));
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    if (int rc = use_stream(h, s)) return rc;
     LgScratch S = route_scratch(h);
     S.pidx_base = h->tile.first;
     HIPCHK(hipMemcpyAsync(S.meta + LG_SECKEY, d_merged_keys, CG_TILE_KEYS * 4, hipMemcpyDeviceToDevice, s));
@@ -1025,6 +1021,7 @@ int cg_tile_survivors_async(cg_handle* h, float* d_points, uint32_t* d_index, ui
     if (n && (!d_points || !d_index)) return fail(CG_E_INVALID, "null output buffers");
     HIPCHK(hipSetDevice(h->device));
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    if (int rc = use_stream(h, s)) return rc;
     if (n) {
         HIPCHK(hipMemcpyAsync(d_points, h->lg.surv_p, (size_t)n * 16, hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(d_index, h->lg.surv_i, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
@@ -1042,9 +1039,9 @@ int cg_tile_backend_own(cg_handle* h, uint32_t n_total, void* hip_stream) {
     int rc = ensure_batch(h, 1, n_total, false);
     if (rc) return rc;
     const hipStream_t s = hip_stream ? (hipStream_t)hip_stream : h->stream;
+    if ((rc = use_stream(h, s))) return rc;
     LgScratch S = route_scratch(h);
     S.pidx_base = 0;
-    S.force_global = h->route == 2 ? 1u : 0u;
     CgLaunch L{};
     L.n_frames = 1;
     L.n_points = n_total;
@@ -1081,6 +1078,7 @@ int cg_halo_owner(cg_handle* h, const cg_halo_plan* plan, const float* d_points,
     if (n && (!d_points || !d_slab)) return fail(CG_E_INVALID, "null buffers");
     HIPCHK(hipSetDevice(h->device));
     rc = own_stream(h);
+    if (!rc) rc = use_stream(h, h->stream);
     if (rc) return rc;
     HIPCHK((hipError_t)cg_launch_halo_owner(d_points, n, h->dp.inv_leaf[0], plan->min_b[0], plan->slab_w, plan->slabs,
                                             d_slab, h->stream));
@@ -1104,6 +1102,7 @@ int cg_halo_local(cg_handle* h, const cg_halo_plan* plan, const float* d_points,
     rc = own_stream(h);
     if (!rc) rc = ensure_large(h, n_total);
     if (!rc) rc = ensure_batch(h, 1, n_total, false);
+    if (!rc) rc = use_stream(h, h->stream);
     if (rc) return rc;
     LgScratch S = route_scratch(h);
     S.pidx_base = 0;
@@ -1124,6 +1123,7 @@ int cg_halo_edges(cg_handle* h, const uint32_t* d_own, uint32_t n_own, const uin
     HIPCHK(hipSetDevice(h->device));
     int rc = own_stream(h);
     if (!rc) rc = ensure_large(h, 1);
+    if (!rc) rc = use_stream(h, h->stream);
     if (rc) return rc;
     uint32_t* d_count = h->lg.meta + LG_META_WORDS - 1;
     HIPCHK((hipError_t)cg_halo_edges_run(d_own, n_own, d_halo, n_halo, h->dp.r2, d_pairs, capacity, d_count,
@@ -1147,6 +1147,7 @@ int cg_halo_merge(cg_handle* h, const cg_halo_plan* plan, const uint32_t* d_rec,
     rc = own_stream(h);
     if (!rc) rc = ensure_large(h, n_total);
     if (!rc) rc = ensure_batch(h, 1, n_total, false);
+    if (!rc) rc = use_stream(h, h->stream);
     if (rc) return rc;
     LgScratch S = route_scratch(h);
     S.pidx_base = 0;
@@ -1240,21 +1241,19 @@ int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
     return CG_OK;
 }
 
-int cg_debug_launch_span(cg_handle* h, void* d_span) {
-    if (!h) return fail(CG_E_INVALID, "null handle");
-    h->next_span = (unsigned long long*)d_span;
-    return CG_OK;
-}
+int cg_debug_launch_span(cg_handle* h, void* d_span) { return cg_debug_launch_spans(h, d_span, d_span ? 1u : 0u); }
 
-int cg_debug_front_span(cg_handle* h, void* d_span) {
+int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    h->next_front_span = (unsigned long long*)d_span;
+    if (n_launches && !d_spans) return fail(CG_E_INVALID, "null span buffer");
+    h->next_span = (unsigned long long*)d_spans;
+    h->spans_left = n_launches;
     return CG_OK;
 }
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 8) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 6) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

@@ -1,7 +1,6 @@
 // cg_backend.h — the frame backend (VoxelGrid, Euclidean clustering, cluster order, CSR,
-// centroids) for one frame's detector points, shared by the fused frame kernel
-// (cg_kernels.hip, 512 threads) and the separate backend launch of batch frames (cg_back.hip,
-// built with CG_BLOCK = 256 so that it fits beside two streaming workgroups on a CU).
+// centroids) for one frame's detector points, in one 512-lane workgroup: the fused frame kernel
+// and the large path's LDS backend (cg_kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "cg_internal.h"
@@ -28,8 +27,7 @@ struct FrontShared {
 };
 #define FRONT_BYTES ((sizeof(FrontShared) + 255) & ~(size_t)255)
 
-// The backend's arrays in LDS for up to CAP detector points (the frame kernel: CG_MMAX; the
-// separate backend launch, cg_back.hip: CG_BACK_CAP).
+// The backend's arrays in LDS for up to CAP detector points (the frame kernel: CG_MMAX).
 constexpr uint32_t cg_pow2_ceil(uint32_t n) { uint32_t p = 1; while (p < n) p <<= 1; return p; }
 template <uint32_t CAP>
 struct BackLdsT {
@@ -78,13 +76,12 @@ enum {
 
 
 // The backend's arrays in a frame's HBM scratch slot (M > the LDS capacity), sized for n
-// points; cg_work_bytes(n) bytes, then the front record (CG_FREC_*) of a split frame launch.
+// points; cg_work_bytes(n) bytes.
 __host__ __device__ inline uint64_t cg_work_bytes(uint32_t n) {
     uint64_t n2 = 1; while (n2 < n) n2 <<= 1;
     const uint64_t c = (uint64_t)n + 4;
     return 16 * c + 16 * c + 8 * n2 + 4 * c * 8;
 }
-enum { CG_FREC_MS = 0, CG_FREC_M, CG_FREC_NFIN, CG_FREC_BMIN, CG_FREC_BMAX = CG_FREC_BMIN + 3, CG_FREC_WORDS = 16 };
 __device__ __forceinline__ Work global_work(uint8_t* base, uint32_t n) {
     uint64_t n2 = 1; while (n2 < n) n2 <<= 1;
     const uint64_t c = (uint64_t)n + 4;
@@ -110,11 +107,9 @@ __device__ __forceinline__ Work global_work(uint8_t* base, uint32_t n) {
 // for point indices of a 64k frame; fewer when W.IDX holds ranks).
 // lds_cap: the LDS capacity when W is in LDS (the out-of-place sort buffer starts at VOX's
 // second half, E + lds_cap).
-// bail_v: a frame with more voxels than this stops after its voxel centroids and joins the
-// split batch's large-capacity list (L.biglist) instead (0: never); uniform per workgroup.
 __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* fs, const CgLaunch& L,
                                         const CgDevParams& P, uint32_t f, uint32_t flags, uint32_t nbw,
-                                        uint32_t lds_cap, uint32_t bail_v = 0) {
+                                        uint32_t lds_cap) {
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     uint32_t* red = fs->red;
     // ---- voxel grid: getMinMax3D (finite points; bounds gathered by the frontend) ----
@@ -237,13 +232,6 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         __syncthreads();
     }
     STAMP(10);
-    if (bail_v && V > bail_v) {   // all-pairs clustering here stops at bail_v voxels: cg_back_big
-        if (tid == 0) {
-            const uint32_t q = atomicAdd(&L.biglist[0], 1u);
-            L.biglist[2 + q] = f;
-        }
-        return;
-    }
     // ---- Euclidean clustering over the V voxel points ----
     uint32_t C = 0;
     if (V > 0) {
@@ -597,66 +585,3 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
 }
 
 
-// One frame of a split batch from its HBM slot: the survivors the front gathered (wave order)
-// and its front record -> the backend, in LDS (capacity CAP, the frame's M <= CAP) or, with
-// CAP = 0, on the slot itself. In LDS the survivors are put in point order: with room for
-// pcl_index_vector's 2,048-word point bitmap in VOX they keep their point indices; otherwise
-// (the 256-lane launch) they are ranked by point index and take the rank as point index, so
-// index_vector (cloud order) and the point-order ties are the frame kernel's either way.
-// COH (served batches, cg_serve_kernel): the front ran concurrently on any XCD, so the record
-// and the survivors are read with device-coherent loads, and the slot-resident backend starts
-// with an agent-scope acquire (this XCD's caches invalidated).
-template <uint32_t CAP, bool COH = false>
-__device__ __forceinline__ void back_frame(const CgLaunch& L, const CgDevParams& P, uint32_t f, FrontShared* fs,
-                                           BackLdsT<(CAP ? CAP : 1)>* bl) {
-    constexpr uint32_t C = CAP ? CAP : 1;
-    constexpr bool RANK = sizeof(BackLdsT<C>::VOX) < 4096 * sizeof(uint32_t);
-    static_assert(!CAP || !RANK || CAP <= CG_RANK_SORT_MAX, "survivors ranked by one rank sort");
-    const uint32_t tid = threadIdx.x, N = L.n_points;
-    uint8_t* const slot = L.scratch + (uint64_t)f * L.scratch_stride;
-    uint32_t* const rec = (uint32_t*)(slot + cg_work_bytes(N));
-    const Work Wg = global_work(slot, N);
-    auto rd = [&](uint32_t* p) -> uint32_t { return COH ? ld_rlx(p) : *p; };
-    auto rd4 = [&](const float4* p) -> float4 { return COH ? ld_f4(p) : *p; };
-    const uint32_t Ms = rd(&rec[CG_FREC_MS]), M = rd(&rec[CG_FREC_M]);
-    if (tid < 64) {
-        uint32_t v = 0;
-        if (tid == S_MS) v = Ms;
-        else if (tid == S_MF) v = rd(&rec[CG_FREC_NFIN]);
-        else if (tid >= S_BMIN0 && tid <= S_BMIN2) v = rd(&rec[CG_FREC_BMIN + (tid - S_BMIN0)]);
-        else if (tid >= S_BMAX0 && tid <= S_BMAX2) v = rd(&rec[CG_FREC_BMAX + (tid - S_BMAX0)]);
-        fs->scal[tid] = v;
-    }
-    if constexpr (CAP == 0) {
-        if (COH) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __syncthreads();
-        backend(Wg, M, fs, L, P, f, 0x2u, CG_MAX_POINTS / 32, 0);
-    } else {
-        const Work W = lds_work(bl);
-        if constexpr (RANK) {
-            uint64_t* const tmp = (uint64_t*)W.VOX;   // free until pcl_index_vector
-            for (uint32_t j = tid; j < Ms; j += CG_BLOCK) tmp[j] = ((uint64_t)rd(&Wg.IDX[j]) << 16) | j;
-            __syncthreads();
-            rank_sort(tmp, W.KEY, Ms);
-            for (uint32_t r = tid; r < Ms; r += CG_BLOCK) {
-                W.P[r] = rd4(&Wg.P[(uint32_t)(W.KEY[r] & 0xffffu)]);
-                W.IDX[r] = r;
-            }
-        } else {
-            for (uint32_t j = tid; j < Ms; j += CG_BLOCK) {
-                W.P[j] = rd4(&Wg.P[j]);
-                W.IDX[j] = rd(&Wg.IDX[j]);
-            }
-        }
-        for (uint32_t j = Ms + tid; j < M; j += CG_BLOCK) {   // PointXYZI() pads after every kept point
-            W.P[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            W.IDX[j] = 0xffffu;
-        }
-        __syncthreads();
-        // the 256-lane launch's all-pairs clustering covers CG_BRUTE_V voxels (its adjacency rows
-        // overlay KEY); a frame with more goes on to cg_back_big
-        // (a served frame has no later launch: it clusters more voxels on the neighbour grid here)
-        backend(W, M, fs, L, P, f, 0u, RANK ? (Ms + 32) / 32 : CG_MAX_POINTS / 32, CAP,
-                RANK && !COH ? CG_BRUTE_V : 0u);
-    }
-}

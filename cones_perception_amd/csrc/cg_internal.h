@@ -82,12 +82,6 @@ struct CgLaunch {
     // timing: [first workgroup start, last workgroup end] of the launch (s_memrealtime,
     // 100 MHz), or null (cg_debug_launch_span)
     unsigned long long* span;
-    // timing: [first front workgroup start, last front workgroup end] of a split batch's front
-    // launch (cg_debug_front_span), or null
-    unsigned long long* span_front;
-    // split batches: frames whose detector points exceed CG_BACK_CAP, listed by the front for
-    // the large-capacity backend launch: [0] count, [1] finished workgroups, then frame indices
-    uint32_t* biglist;
     // split single-frame launch (cg_launch_split): CG_SPLIT_WORDS of state, or null
     uint32_t* split;
     // split launch: the frame's results also packed here (CG_PACK_WORDS) at the end, or null
@@ -95,13 +89,6 @@ struct CgLaunch {
     // split launch: the frame in pinned host memory; each chunk workgroup copies its chunk to
     // `in` (the device copy) before pass 1, or null (`in` already holds the frame)
     const uint8_t* in_host;
-    // pair launch (cg_pair.hip): this batch's number, the value of a frame's ready word once
-    // its first half has published (the words start zeroed; a handle's batches count from 1);
-    // served batches (cg_debug_route 8): the same for the front's publish words
-    uint32_t epoch;
-    // served batches: [2] a backend workgroup's wait timed out, [4 + f] frame f's survivors
-    // are in its slot (= epoch); or null
-    uint32_t* serve;
     // split launch with in_host: the host fills the staging buffer chunk by chunk after the
     // launch and publishes chunk c by storing in_seq to in_flags[c] (pinned, coherent); each
     // chunk workgroup waits for its word (CG_STAGE_TIMEOUT bound: then in_flags[CG_STAGE_ERR]
@@ -109,10 +96,6 @@ struct CgLaunch {
     uint32_t* in_flags;
     uint32_t in_seq;
 };
-#define CG_SERVE_WORDS(F) ((F) + 4)
-// The pair launch's exchange area: the last CG_PAIR_X_BYTES of each frame's scratch slot
-// (header words, a half's z codes, its filter bits), zeroed when the slots are allocated.
-#define CG_PAIR_X_BYTES (128 + CG_MAX_POINTS / 2 + 2 * 256 * 8 + 128)
 #define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
 #define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms
 // A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
@@ -143,9 +126,6 @@ static inline hipError_t cg_stream_wait(hipStream_t s) {
 
 #ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU
-#endif
-#ifndef CG_BACK_CAP
-#define CG_BACK_CAP 392        // the backend launch's LDS capacity (cg_back.hip); more: cg_back_big
 #endif
 #ifndef CG_MMAX
 #define CG_MMAX 1024           // LDS-path capacity (points surviving the filter)
@@ -243,24 +223,8 @@ int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScr
 
 // Bytes of HBM scratch one frame of n points needs for the global (non-LDS) path.
 uint64_t cg_scratch_bytes(uint32_t n_points);
-// Enqueue the batch kernel. Returns a hipError_t.
-// Batch frames of <= CG_MAX_POINTS points. Detector batches run as a front launch plus the
-// backend launch (cg_launch_back, cg_back.hip); `fused` keeps each frame in one workgroup.
-int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused = false);
-int cg_launch_back(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
-// the halves of a split detector batch (frames of <= CG_MAX_POINTS points)
-int cg_launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
-int cg_launch_backends(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
-// Pipeline batches of frames of CG_MAX_POINTS / 2 < n <= CG_MAX_POINTS points as two half-frame
-// workgroups per frame (cg_pair.hip, cg_debug_route 7); frames of more detector points than
-// the pair kernel's LDS backend holds are listed (L.biglist) for cg_launch_back_list (HBM
-// slot, > CG_MMAX) and cg_launch_back_big (LDS, <= CG_MMAX; clears the list), launched after it.
-int cg_launch_pair(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
-int cg_launch_back_list(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
-// Served batches (cg_debug_route 8): the front launch publishes each frame (L.serve) and the
-// backend launch beside it (cg_back.hip) takes each frame as soon as it is published.
-int cg_launch_serve(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
-int cg_launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s);
+// Enqueue the batch kernel (one fused workgroup per frame). Returns a hipError_t.
+int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
 // Cone re-crop (cg_recrop.hip): exact float form of the reference's double box compares.
 struct RcBox { float lox, hix, loy, hiy; };
 #define CG_RECROP_MAX_BOXES 256   // boxes per launch (more: several launches)

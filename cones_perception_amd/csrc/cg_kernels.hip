@@ -56,8 +56,7 @@ static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overla
 static_assert(CG_MAX_POINTS / 64 * sizeof(uint32_t) <= CG_MAX_POINTS, "ground counts fit the code area");
 
 uint64_t cg_scratch_bytes(uint32_t n) {
-    // the work arrays, the front record, then the pair launch's exchange area at the slot's end
-    const uint64_t b = cg_work_bytes(n) + 256 + CG_PAIR_X_BYTES;
+    const uint64_t b = cg_work_bytes(n);
 #ifdef CG_CODES_HBM
     return b > CG_MAX_POINTS ? b : (uint64_t)CG_MAX_POINTS;   // the codes overlay it until compaction
 #else
@@ -84,25 +83,16 @@ __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32
 // bits to HBM and merging its sector minima into the frame's keys with atomics; the last
 // workgroup to finish (release/acquire on a counter) continues with the frame's thresholds,
 // pass 2 and backend below, codes and bits read back from L2.
-//
-// FRONT (batch frames, cg_launch_batch): the kernel stops after the gather. The survivors go to
-// the frame's HBM scratch slot (global_work) with a front record (count, bounds) after it, and a
-// separate launch runs the backend (cg_back.hip): the streaming workgroup's LDS is the codes and
-// FrontShared only (65 KB), its VGPRs at most 96 (5 waves per SIMD), so two of them and one
-// backend workgroup (256 threads, ~29 KB) share a CU, and one frame's latency-bound backend runs
-// beside two frames' streaming passes instead of holding a streaming slot.
-template <int PPT, int LAYOUT, int KMODE, bool SPLIT = false, bool FRONT = false>
+template <int PPT, int LAYOUT, int KMODE, bool SPLIT = false>
 __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams& P) {
     constexpr int G = 8;                          // points per load group (double-buffered)
     constexpr int NW = (PPT + 63) / 64;
     static_assert(PPT % (2 * G) == 0, "PPT must be a multiple of two load groups");
-    static_assert(!(FRONT && (SPLIT || KMODE == CG_KMODE_GROUND)), "the front launch serves detector batches");
     constexpr bool GROUND = KMODE != CG_KMODE_DETECT;
     constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
     // a split launch's 16 workgroups take a CU each: LDS past half a CU says so to the compiler,
     // which then sizes registers for 2 waves per SIMD (no SGPR spill reaches scratch)
-    constexpr size_t SMEM = FRONT ? FRONT_BYTES + CG_MAX_POINTS
-                                  : (SPLIT && SMEM_BYTES <= 81920 ? 81920 + 256 : SMEM_BYTES);
+    constexpr size_t SMEM = SPLIT && SMEM_BYTES <= 81920 ? 81920 + 256 : SMEM_BYTES;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
     FrontShared* fs = (FrontShared*)smem;
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
@@ -113,7 +103,6 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     const uint32_t N = L.n_points;
     STAMP(0);
     if (L.span && tid == 0) atomicMin(&L.span[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    if (FRONT && L.span_front && tid == 0) atomicMin(&L.span_front[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
     init_rays<FILTER>(P, fs->rays, tid);
@@ -328,7 +317,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     // to the frame's HBM slot (moved whole below when M does not fit) ----
     __syncthreads();   // every wave is past the codes: LDS survivor slots overlay them from here
     STAMP(3);
-    const uint32_t lcap = FRONT ? 0u : (uint32_t)CG_MMAX;
+    const uint32_t lcap = CG_MMAX;
     const Work Wl = lds_work(bl);
     const Work Wg = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -344,9 +333,6 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         if (pos < lcap) {
             Wl.P[pos] = pt;
             Wl.IDX[pos] = idx;
-        } else if (FRONT) {   // device-coherent: a backend workgroup on any XCD reads them
-            st_f4(&Wg.P[pos], pt);
-            st_rlx(&Wg.IDX[pos], idx);
         } else {
             Wg.P[pos] = pt;
             Wg.IDX[pos] = idx;
@@ -435,7 +421,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     // PointXYZI() points survive the filter iff P.zero_pass (src/cone_detection.cpp:195-201)
     const uint32_t npad = (KMODE == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
     const uint32_t M = Ms + npad;
-    const bool use_lds = !FRONT && M <= CG_MMAX;
+    const bool use_lds = M <= CG_MMAX;
     const uint32_t flags = use_lds ? 0u : 0x2u;
     if (tid == 0) {
         uint32_t* h = L.hdr + (uint64_t)f * 8;
@@ -452,13 +438,8 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     }
     for (uint32_t j = tid; j < npad; j += CG_BLOCK) {
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (FRONT) {
-            st_f4(&W.P[Ms + j], z4);
-            st_rlx(&W.IDX[Ms + j], 0xffffu);
-        } else {
-            W.P[Ms + j] = z4;
-            W.IDX[Ms + j] = 0xffffu;   // after every kept point; exact-zero terms are order-free
-        }
+        W.P[Ms + j] = z4;
+        W.IDX[Ms + j] = 0xffffu;   // after every kept point; exact-zero terms are order-free
         bound(z4);
     }
     {
@@ -484,30 +465,6 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     return;
 #endif
-    if constexpr (FRONT) {   // the front record for the backend launch (cg_back.hip)
-        if (tid == 0) {
-            uint32_t* rec = (uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(N));
-            st_rlx(&rec[CG_FREC_MS], Ms);
-            st_rlx(&rec[CG_FREC_M], M);
-            st_rlx(&rec[CG_FREC_NFIN], fs->scal[S_MF]);
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                st_rlx(&rec[CG_FREC_BMIN + a], fs->scal[S_BMIN0 + a]);
-                st_rlx(&rec[CG_FREC_BMAX + a], fs->scal[S_BMAX0 + a]);
-            }
-            if (!L.serve && M > CG_BACK_CAP && M <= CG_MMAX) {   // beyond the backend launch's LDS: cg_back_big
-                const uint32_t q = atomicAdd(&L.biglist[0], 1u);
-                L.biglist[2 + q] = f;
-            }
-            if (L.span_front) atomicMax(&L.span_front[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        }
-        if (L.serve) {   // served batch: the frame published once every lane's stores are complete
-            __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
-            __syncthreads();
-            if (tid == 0) st_rlx(&L.serve[4 + f], L.epoch);
-        }
-        return;
-    }
     if (use_lds) {
         backend(lds_work(bl), M, fs, L, P, f, flags, CG_MAX_POINTS / 32, CG_MMAX);
     } else {
@@ -523,56 +480,17 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
-// The kernels: the batch frame kernel (two workgroups per CU: <= 128 VGPRs); the front of a
-// split batch (<= 96 VGPRs, the register file's share that leaves one wave per SIMD for the
-// backend launch beside two front workgroups; the compiler would otherwise size it for the
-// occupancy its own LDS allows); the single-frame split kernel (its 16 workgroups have a CU
-// each: 2 waves per SIMD, room to keep every spill out of scratch).
+// The kernels: the batch frame kernel (two workgroups per CU: <= 128 VGPRs); the single-frame
+// split kernel (its 16 workgroups have a CU each: 2 waves per SIMD, room to keep every spill out
+// of scratch).
 template <int PPT, int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDevParams P) {
     frame_body<PPT, LAYOUT, KMODE>(L, P);
 }
 template <int PPT, int LAYOUT, int KMODE>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, CG_BLOCK), amdgpu_num_vgpr(96))) void cg_front_kernel(
-    CgLaunch L, CgDevParams P) {
-    frame_body<PPT, LAYOUT, KMODE, false, true>(L, P);
-}
-template <int PPT, int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 2) void cg_split_kernel(CgLaunch L, CgDevParams P) {
     frame_body<PPT, LAYOUT, KMODE, true>(L, P);
 }
-
-// Split batches: the frames the front listed (CG_BACK_CAP < M <= CG_MMAX, a few per C3 batch)
-// in the frame kernel's LDS capacity, after the backend launch on the same stream. The last workgroup to finish clears the list for the next batch.
-#define BACK_BIG_GRID 32
-__global__ __launch_bounds__(CG_BLOCK, 2) void cg_back_big_kernel(CgLaunch L, CgDevParams P) {
-    // one workgroup per CU (LDS past half a CU): registers for 2 waves per SIMD, no spills
-    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES <= 81920 ? 81920 + 256 : SMEM_BYTES];
-    uint32_t* const list = L.biglist;
-    const uint32_t n = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma clang loop unroll(disable)
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const uint32_t f = list[2 + i];
-        // the pair launch also lists frames past CG_MMAX: cg_back_list_kernel ran them on the slot
-        const uint32_t* const rec = (const uint32_t*)(L.scratch + (uint64_t)f * L.scratch_stride + cg_work_bytes(L.n_points));
-        if (rec[CG_FREC_M] > CG_MMAX) continue;
-        back_frame<CG_MMAX>(L, P, f, (FrontShared*)smem, (BackLds*)(smem + FRONT_BYTES));
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        if (L.span) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-        // every workgroup read the count before it counts itself done
-        if (__hip_atomic_fetch_add(&list[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-            __hip_atomic_store(&list[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&list[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-static hipError_t launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
-    hipLaunchKernelGGL(cg_back_big_kernel, dim3(BACK_BIG_GRID), dim3(CG_BLOCK), 0, s, L, P);
-    return hipGetLastError();
-}
-int cg_launch_back_big(const CgLaunch& L, const CgDevParams& P, hipStream_t s) { return launch_back_big(L, P, s); }
 
 // ------------------------------------------------------------------------------------------
 // Large frames whose detector input fits the LDS path (M <= CG_MMAX): the survivors come from
@@ -634,30 +552,16 @@ int cg_launch_lg_back_small(const CgLaunch& L, const CgDevParams& P, const LgScr
 }
 
 // ------------------------------------------------------------------------------------------
-// Launchers.
-// Detector batches (pipeline, detect): one fused workgroup per frame, or (not `fused`,
-// cg_debug_route 6 / cg_run_batch_split) the front launch plus the backend launches.
+// Launchers. Batches: one fused workgroup per frame.
 template <int PPT, int LAYOUT>
-static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused) {
+static hipError_t launch3(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
     const dim3 grid(L.n_frames), block(CG_BLOCK);
     switch (kmode) {
         case CG_KMODE_PIPELINE:
-            if (fused) {
-                hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
-            } else {
-                hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
-                if (hipError_t e = (hipError_t)cg_launch_back(L, P, s)) return e;
-                return launch_back_big(L, P, s);
-            }
+            hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
             break;
         case CG_KMODE_DETECT:
-            if (fused) {
-                hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
-            } else {
-                hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
-                if (hipError_t e = (hipError_t)cg_launch_back(L, P, s)) return e;
-                return launch_back_big(L, P, s);
-            }
+            hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
             break;
         default:
             hipLaunchKernelGGL((cg_frame_kernel<PPT, LAYOUT, CG_KMODE_GROUND>), grid, block, 0, s, L, P);
@@ -681,43 +585,16 @@ int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
     return hipGetLastError();
 }
 
-// The two halves of a split batch, for callers that run them on different streams.
-template <int PPT, int LAYOUT>
-static void launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
-    const dim3 grid(L.n_frames), block(CG_BLOCK);
-    if (kmode == CG_KMODE_PIPELINE)
-        hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
-    else
-        hipLaunchKernelGGL((cg_front_kernel<PPT, LAYOUT, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
-}
-int cg_launch_front(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
-    if (L.n_frames == 0) return hipSuccess;
-    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
-    if (L.n_points <= 32 * CG_BLOCK) {
-        if (xyzi16) launch_front<32, CG_LAYOUT_XYZI16>(L, P, kmode, s);
-        else launch_front<32, CG_LAYOUT_GENERIC>(L, P, kmode, s);
-    } else {
-        if (xyzi16) launch_front<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_XYZI16>(L, P, kmode, s);
-        else launch_front<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_GENERIC>(L, P, kmode, s);
-    }
-    return hipGetLastError();
-}
-int cg_launch_backends(const CgLaunch& L, const CgDevParams& P, hipStream_t s) {
-    if (L.n_frames == 0) return hipSuccess;
-    if (hipError_t e = (hipError_t)cg_launch_back(L, P, s)) return e;
-    return launch_back_big(L, P, s);
-}
-
-int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s, bool fused) {
+int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
     if (L.n_frames == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 &&
                         L.off_i == 12;
     if (L.n_points <= 32 * CG_BLOCK) {
-        return xyzi16 ? launch3<32, CG_LAYOUT_XYZI16>(L, P, kmode, s, fused)
-                      : launch3<32, CG_LAYOUT_GENERIC>(L, P, kmode, s, fused);
+        return xyzi16 ? launch3<32, CG_LAYOUT_XYZI16>(L, P, kmode, s)
+                      : launch3<32, CG_LAYOUT_GENERIC>(L, P, kmode, s);
     }
-    return xyzi16 ? launch3<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_XYZI16>(L, P, kmode, s, fused)
-                  : launch3<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_GENERIC>(L, P, kmode, s, fused);
+    return xyzi16 ? launch3<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_XYZI16>(L, P, kmode, s)
+                  : launch3<CG_MAX_POINTS / CG_BLOCK, CG_LAYOUT_GENERIC>(L, P, kmode, s);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -39,10 +39,6 @@ extern "C" {
                                         std::sort may order equal-size clusters differently */
 #define CG_F_VOXEL_POINT_ORDER 0x8u  /* voxel sums ran in ascending point order, not in PCL's
                                         std::sort order (cg_set_voxel_order, the halo form) */
-#define CG_F_PAIR_TIMEOUT      0x10u /* diagnostic (cg_debug_route 7): the frame's second half
-                                        gave up waiting for the first's data after 100 ms; the
-                                        result is invalid. Never expected: the first half is
-                                        running whenever the second waits */
 
 /* ---- parameters --------------------------------------------------------------------- */
 /* Field names are the YAML keys, misspellings kept (config/ *.yaml). */
@@ -133,7 +129,9 @@ typedef struct cg_detect_result {
 /* Synchronous. A frame of <= 65,536 points is launched before its bytes are staged: the call
  * copies in->data into pinned memory chunk by chunk behind the launch, and each chunk's
  * workgroup reads its chunk over PCIe once published. in->data is read until the call
- * returns; CG_E_DEVICE if a chunk is not published within 200 ms. */
+ * returns. A chunk workgroup waits at most 200 ms for its chunk (a host thread descheduled
+ * that long); the call then runs the frame again with the whole message copied by DMA, so a
+ * slow host makes the call slower, never failed. */
 int cg_detect(cg_handle* h, const cg_cloud_view* in, cg_detect_result* out);
 
 /* ground_removal -> cone_detection composition of launch/cones_perception.launch:17-37
@@ -156,21 +154,21 @@ typedef struct cg_batch {
 #define CG_MODE_DETECT   1   /* detector only (cg_detect semantics) */
 
 /* Enqueue one pass of the hot path over the batch on `hip_stream` (hipStream_t; NULL = the
- * handle's own stream). Results stay on the device until the next batch call. Frames of more
- * than 65,536 points run through the multi-workgroup large-frame path one frame at a time,
- * and the call synchronises the stream (it sizes each frame's backend from its counts). */
+ * handle's own stream). Results stay on the device until the next call on the handle. Frames
+ * of up to 65,536 points run as one launch, one workgroup per frame. Frames of more run
+ * through the multi-workgroup large-frame path one frame at a time, and the call synchronises
+ * the stream (it sizes each frame's backend from its counts).
+ * A handle's calls are ordered whatever stream each names: a call on another stream than the
+ * handle's previous call waits for that stream's work queued so far (which must still exist). */
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream);
 
-/* cg_run_batch over two streams. A detector batch of frames of <= 65,536 points is a front
- * launch (the frame streaming: ground decisions, position filter, survivors) and backend
- * launches (voxel grid, clustering, centroids); here the front runs on front_stream and the
- * backends on back_stream once it is done, so the backends of one batch overlap the next
- * batch's front (another handle's, on another front stream). The results are complete when
- * back_stream reaches this call's work (cg_batch_fetch waits there); this handle's next batch
- * waits for these backends before its front reuses their inputs. Other batches run as in
- * cg_run_batch on front_stream. (Measured slower than cg_run_batch's fused frames on C3:
- * DESIGN.md (d); kept for callers whose frames carry heavier backends.) */
-int cg_run_batch_split(cg_handle* h, const cg_batch* b, int mode, void* front_stream, void* back_stream);
+/* n_calls batch calls in one: call i is cg_run_batch(handles[i], &batches[i], mode,
+ * hip_streams[i]), in order (a handle may appear several times). Every call's arguments are
+ * checked before any is enqueued; a call that fails stops the sequence, and *n_done (optional)
+ * is the number of calls enqueued. For a server that enqueues many batches over several
+ * handles and streams at once: one crossing of the ABI, and the device selected once. */
+int cg_run_batches(cg_handle* const* handles, const cg_batch* batches, uint32_t n_calls, int mode,
+                   void* const* hip_streams, uint32_t* n_done);
 
 /* Per-frame header words in the device result buffer. */
 #define CG_HDR_N      0
@@ -370,10 +368,9 @@ int cg_debug_stamps(cg_handle* h, int enable);
  * start and the last workgroup's end, s_memrealtime ticks (100 MHz). One atomic per workgroup
  * at each end; frames of more than 65,536 points (large-frame path) do not record. */
 int cg_debug_launch_span(cg_handle* h, void* d_span);
-/* Timing: the next cg_run_batch call that runs as a front launch plus a backend launch (detector
- * batches of <= 65,536-point frames) records the front launch's own span in d_span (2 x uint64,
- * as above); cg_debug_launch_span then spans both launches (front start to backend end). */
-int cg_debug_front_span(cg_handle* h, void* d_span);
+/* The same for the handle's next n_launches batch launches, launch k into d_spans[2k, 2k + 1]
+ * (no host call between the launches). */
+int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches);
 int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
 
 /* Diagnostics: route every frame through the large-frame path (1), and also through its
@@ -381,11 +378,9 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * calls in one workgroup instead of the per-chunk split launch (3), or split with the input
  * copied by DMA instead of read by the kernel from pinned memory (4); the global backend with
  * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
- * are finished in HBM side by side (5); detector batches of <= 65,536-point frames as a front
- * launch plus backend launches instead of one fused workgroup per frame (6); pipeline batches
- * of 32,769-65,536-point frames as two half-frame workgroups per frame (7); detector batches
- * whose backend launch runs beside the front launch, on cg_run_batch_split's back stream, taking
- * each frame as its front publishes it (8); 0 = automatic. */
+ * are finished in HBM side by side (5); single-frame calls whose staged chunks are never
+ * published, so every chunk workgroup times out and the call re-runs the frame by DMA (6,
+ * tests of that retry); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

@@ -131,20 +131,15 @@ def test_occupancy_contracts(tmp_path):
     """The residency each launch structure is designed around, from the code-object metadata
     (160 KiB of LDS and 512 VGPRs per SIMD lane on a gfx950 CU; a 512-lane workgroup puts two
     waves on each SIMD, a 256-lane one one wave):
-      - the fused frame kernel: two workgroups per CU (LDS <= 80 KiB, <= 128 VGPRs);
-      - the batch front + backend launches (routes 6 and 8): two fronts and one backend
-        workgroup per CU;
-      - the half-frame pair kernel: four workgroups per CU."""
+      - the fused frame kernel: two workgroups per CU (LDS <= 80 KiB, <= 128 VGPRs).
+    And the batch entry point has one launch structure: none of the slower diagnostic batch
+    structures of round 3 (front + backend launches, served backends, half-frame pairs, with
+    cross-launch waits) is in the library."""
     k = _kernel_metadata(tmp_path)
     lds = lambda m: int(m[".group_segment_fixed_size"])
-    for n, m in _find(k, "_Z15cg_frame_kernelILi128E"):
+    frames = _find(k, "_Z15cg_frame_kernelILi128E")
+    for n, m in frames:
         assert 2 * lds(m) <= 163840 and 4 * _vgprs(m) <= 512, (n, lds(m), m[".vgpr_count"])
-    fronts = _find(k, "_Z15cg_front_kernelILi128E")
-    front_lds = max(lds(m) for _, m in fronts)
-    front_vgpr = max(_vgprs(m) for n, m in fronts if "ELi0EE" in n)   # the pipeline fronts
-    for name in ("_Z14cg_back_kernel", "_Z15cg_serve_kernel"):
-        for n, m in _find(k, name):
-            assert 2 * front_lds + lds(m) <= 163840, (n, front_lds, lds(m))
-            assert 4 * front_vgpr + _vgprs(m) <= 512, (n, front_vgpr, m[".vgpr_count"])
-    for n, m in _find(k, "_Z14cg_pair_kernel"):
-        assert 4 * lds(m) <= 163840 and 4 * _vgprs(m) <= 512, (n, lds(m), m[".vgpr_count"])
+    for gone in ("cg_front_kernel", "cg_back_kernel", "cg_serve_kernel", "cg_pair_kernel", "cg_back_big_kernel",
+                 "cg_back_list_kernel"):
+        assert not [n for n, _ in k if n and gone in n], gone

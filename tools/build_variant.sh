@@ -17,8 +17,6 @@ C=$R/cones_perception_amd/csrc
 /opt/rocm/bin/hipcc $F -c $C/cg_track.cpp -o $O/cg_track.o &
 /opt/rocm/bin/hipcc $F ${API_FLAGS:-} -c $C/cg_api.cpp -o $O/cg_api.o &
 /opt/rocm/bin/hipcc $F -c $C/cg_host.cpp -o $O/cg_host.o &
-/opt/rocm/bin/hipcc $F "$@" -DCG_BLOCK=256 -c $C/cg_back.hip -o $O/cg_back.o &
-/opt/rocm/bin/hipcc $F "$@" -DCG_BLOCK=256 -c $C/cg_pair.hip -o $O/cg_pair.o &
 gcc -O2 -fPIC -ffp-contract=off -std=c11 -Wall -c $C/cg_synth.c -o $O/cg_synth.o
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $O/libcones_gpu.so $O/*.o -lpthread
