@@ -91,6 +91,7 @@ struct cg_handle {
     uint32_t* h_meta2 = nullptr;
     uint32_t large2_points = 0;
     LgScratch lg{};
+    LgGraphs* lg_graphs = nullptr;   // captured large frames (cg_run_large), for its scratch set
     int route = 0;                // cg_debug_route
     uint32_t retries = 0;         // single-frame calls re-run by DMA after a staging timeout
     unsigned long long* next_span = nullptr;   // cg_debug_launch_spans: the next launch's span slot
@@ -270,7 +271,9 @@ LgScratch route_scratch(cg_handle* h, bool second = false) {
 
 int ensure_large(cg_handle* h, uint32_t n) {
     if (n <= h->large_points && h->d_large) return CG_OK;
-    if (h->d_large) (void)hipFree(h->d_large);
+    if (h->d_large) (void)hipFree(h->d_large);   // (waits for the device: no graph still runs)
+    cg_large_graphs_free(h->lg_graphs);           // they name the old scratch
+    h->lg_graphs = nullptr;
     h->d_large = nullptr;
     h->large_points = 0;
     HIPCHK(hipMalloc(&h->d_large, cg_large_bytes(n)));
@@ -339,14 +342,16 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
     int rc = ensure_large(h, L.n_points);
     if (rc) return rc;
     L.stamps = nullptr;
-    if (L.n_frames > 1 && kmode != CG_KMODE_GROUND) {   // two scratch sets: frames pipelined
+    const bool dev_sized = kmode != CG_KMODE_GROUND && h->dp.voxel_order == CG_VOXEL_ORDER_PCL &&
+                           L.n_points <= LG_DEV_MAX_POINTS;
+    if (L.n_frames > 1 && kmode != CG_KMODE_GROUND && !dev_sized) {   // two scratch sets: frames pipelined
         rc = ensure_large2(h, L.n_points);
         if (rc) return rc;
         const LgScratch S2 = route_scratch(h, true);
         HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, &S2));
         return CG_OK;
     }
-    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s));
+    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, nullptr, &h->lg_graphs));
     return CG_OK;
 }
 
@@ -611,6 +616,7 @@ int cg_destroy(cg_handle* h) {
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->h_meta) (void)hipHostFree(h->h_meta);
     if (h->d_large) (void)hipFree(h->d_large);
+    cg_large_graphs_free(h->lg_graphs);
     if (h->h_meta2) (void)hipHostFree(h->h_meta2);
     if (h->d_large2) (void)hipFree(h->d_large2);
     if (h->d_cn_w) (void)hipFree(h->d_cn_w);

@@ -153,6 +153,12 @@ enum {
     LG_DGINV, LG_DGN = LG_DGINV + 3, LG_NCELL = LG_DGN + 3,   // dense neighbour grid
     LG_SORT_LIM,               // cluster-order sort: key bits in use (digits past it are skipped)
     LG_PCL_N,                  // PCL voxel order: finite points in index_vector (compaction total)
+    // the backend sized on the device (cg_run_large): written by the decisions' fold
+    LG_MALL,                   //   detector input points M = survivors + pads
+    LG_MTOT,                   //   M for the global backend's launches (0 when the LDS backend runs)
+    LG_NPAD,                   //   PointXYZI() pads after the kept points
+    LG_KHDR,                   //   K for the header
+    LG_SMALL,                  //   1: the LDS backend (one workgroup) takes the frame
     LG_META_WORDS = 64
 };
 struct LgScratch {
@@ -184,16 +190,27 @@ struct LgScratch {
 uint64_t cg_large_bytes(uint32_t n_points);
 uint32_t cg_large_pq_words();   // words of the PCL sort's range lists (diagnostics)
 void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
-// Run n_frames frames of more than CG_MAX_POINTS points, one at a time (synchronises s).
+// Run n_frames frames of more than CG_MAX_POINTS points, one at a time. Frames of up to
+// LG_DEV_MAX_POINTS points in pipeline or detect mode with PCL's voxel order are sized on the
+// device (every launch from N, counts read where they are used): enqueued without a host round
+// trip, and replayed from a captured hipGraph per (frame, arguments) when `graphs` is given.
+// Other frames synchronise s once per frame (the survivor count sizes the backend).
+// (PCL's order keeps at most PQ_MAXR ranges per partition level: 4M detector points)
+#define LG_DEV_MAX_POINTS (1u << 22)
+struct LgGraphs;   // cg_large.hip: the handle's captured per-frame graphs
+void cg_large_graphs_free(LgGraphs* g);
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
-                 const LgScratch* S2 = nullptr);
+                 const LgScratch* S2 = nullptr, LgGraphs** graphs = nullptr);
 // The phases of cg_run_large for one frame f (also the tiles of cg_tile_*):
 //   front: meta init + pass 1 (ground-only mode: the whole ground output);
 //   decide: thresholds from meta, pass 2, candidates -> survivors (pipeline mode);
 //   backend: detector backend over meta[LG_MS] survivors + npad pads, header N = n_total, K.
+// szfl: 0, or (cg_run_large's device-sized backend) LG_SZ_ON | flags: the decisions' fold also
+// writes the detector input's size and backend (LG_MALL ... LG_SMALL).
 int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
-                   bool init);
-int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f);
+                   bool init, uint32_t szfl = 0);
+int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f,
+                    uint32_t szfl = 0);
 #define CG_K_FROM_META 0xffffffffu   // cg_large_backend: read K from the frame's meta words
 int cg_large_backend(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
                      uint32_t n_total, uint32_t K);

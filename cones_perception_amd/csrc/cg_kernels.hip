@@ -496,12 +496,19 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void cg_split_kernel(CgLaunch L, CgDev
 // Large frames whose detector input fits the LDS path (M <= CG_MMAX): the survivors come from
 // HBM in append order; sorted by frame index they get ranks as point indices, so the voxel
 // keys order ties exactly as the frame kernel does. npad PointXYZI() pads follow.
+// npad = CG_K_FROM_META (the backend sized on the device): npad and K from the meta words, and
+// the launch returns unless the decisions' fold chose this backend (LG_SMALL).
 __global__ __launch_bounds__(CG_BLOCK, 2) void cg_lg_back_small(CgLaunch L, CgDevParams P, LgScratch S,
                                                                 uint32_t f, uint32_t npad, uint32_t K) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
     FrontShared* fs = (FrontShared*)smem;
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
     const uint32_t tid = threadIdx.x;
+    if (npad == CG_K_FROM_META) {
+        if (!S.meta[LG_SMALL]) return;
+        npad = S.meta[LG_NPAD];
+        K = S.meta[LG_KHDR];
+    }
     const uint32_t Ms = S.meta[LG_MS], M = Ms + npad;
     if (tid < 64) fs->scal[tid] = 0;
     __syncthreads();

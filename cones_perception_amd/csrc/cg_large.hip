@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 #include "cg_internal.h"
 #include "../../include/cones_gpu.h"
 #include "cg_math.h"
@@ -127,8 +128,16 @@ __device__ __forceinline__ void lg_store_survivor_bits(LgScratch& S, uint32_t c,
 
 // One workgroup folds the per-chunk statistics into the meta words: the sector keys (MIN) and
 // used bins (OR) after the front; K, survivor count, finite count (SUM) and the VoxelGrid
-// bounds (MIN / MAX keys) after the decisions. what: bit 0 keys, bit 1 K, bit 2 survivors.
-__device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32_t what) {
+// bounds (MIN / MAX keys) after the decisions. what: bit 0 keys, bit 1 K, bit 2 survivors,
+// bit 3 (LG_FOLD_SIZE, with bit 2) the detector input's size and backend for the launches
+// sized on the device (szfl: LG_SZ_*; N the frame's points).
+#define LG_FOLD_SIZE 8u
+#define LG_SZ_PIPE 1u     // K from the ground stage (detector mode: K = N)
+#define LG_SZ_ZPAD 2u     // the N - K PointXYZI() pads survive the filter (P.zero_pass)
+#define LG_SZ_GLOBAL 4u   // the global backend even when M fits the LDS one (diagnostics)
+#define LG_SZ_ON 0x80000000u   // (host side: cg_large_front / cg_large_decide fold the sizes)
+__device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32_t what, uint32_t N = 0,
+                                               uint32_t szfl = 0) {
     __shared__ uint32_t part[16][LG_CS_WORDS];
     const uint32_t tid = threadIdx.x, w = tid & 31, q = tid >> 5;   // word, one of 16 chunk strides
     const bool mn = (w <= CG_NUM_BINS) || (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3);
@@ -152,6 +161,20 @@ __device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32
         a = mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v;
     }
     uint32_t* m = S.meta;
+    if (what & LG_FOLD_SIZE) {   // (all 32 lanes of wave 0 are here)
+        const uint32_t k = (uint32_t)__shfl((int)a, LG_CS_K, 64), ms = (uint32_t)__shfl((int)a, LG_CS_MS, 64);
+        if (tid == 0) {
+            const uint32_t K = (szfl & LG_SZ_PIPE) ? k : N;
+            const uint32_t npad = (szfl & LG_SZ_ZPAD) ? N - K : 0u;
+            const uint32_t Mt = ms + npad;
+            const bool small = Mt <= CG_MMAX && !(szfl & LG_SZ_GLOBAL);
+            m[LG_KHDR] = K;
+            m[LG_NPAD] = npad;
+            m[LG_MALL] = Mt;
+            m[LG_MTOT] = small ? 0u : Mt;
+            m[LG_SMALL] = small ? 1u : 0u;
+        }
+    }
     if ((what & 1u) && w <= CG_NUM_BINS) m[LG_SECKEY + w] = a;
     if ((what & 1u) && w == LG_CS_TOUCHED) m[LG_TOUCHED] = a;
     if ((what & 2u) && w == LG_CS_K) m[LG_K] = a;
@@ -163,8 +186,9 @@ __device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32
     }
 }
 
-__global__ __launch_bounds__(CG_BLOCK) void lg_reduce_chunks(LgScratch S, uint32_t nch, uint32_t what) {
-    lg_fold_chunks(S, nch, what);
+__global__ __launch_bounds__(CG_BLOCK) void lg_reduce_chunks(LgScratch S, uint32_t nch, uint32_t what, uint32_t N,
+                                                             uint32_t szfl) {
+    lg_fold_chunks(S, nch, what, N, szfl);
 }
 // (Folding in the last workgroup of the chunk launch instead, behind a release/acquire counter,
 // measured 7 -> 53 us per launch on a 256-chunk frame: every workgroup's agent-scope release
@@ -492,6 +516,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint
     __shared__ uint32_t h[256];
     if (n_dev) n = *n_dev;   // count known on the device only (grid sized for an upper bound)
     if (lim && shift >= *lim) return;   // key width known on the device only: an identity pass
+    if ((uint64_t)blockIdx.x * LG_RS_TILE >= n) return;   // (read by the tiles below n only)
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * LG_RS_TILE;
@@ -500,17 +525,22 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_hist(const uint64_t* key, uint
         if (i < n) atomicAdd(&h[(key[i] >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < 256) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+    const uint32_t nt = (uint32_t)(((uint64_t)n + LG_RS_TILE - 1) / LG_RS_TILE);   // tiles holding elements
+    if (threadIdx.x < 256) hist[threadIdx.x * nt + blockIdx.x] = h[threadIdx.x];
 }
 // hist (raw counts, digit-major) gives each (digit, tile) its output base. Within a tile the
 // elements go in 8 rounds of 512 in index order; a round ranks equal digits per wave with
 // eight ballots (the wave's lanes whose digit matches bit for bit) and offsets waves by the
 // per-wave digit counts of the round, so equal keys keep their input order (stable).
+// skip (with lim): a pass past the keys' width does nothing (the consumer reads the buffer the
+// last real pass wrote, lg_rs_passes); without skip it is a copy.
 __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                                           uint32_t* vout, uint32_t n, uint32_t shift,
                                                           const uint32_t* hist, const uint32_t* n_dev,
-                                                          const uint32_t* lim) {
+                                                          const uint32_t* lim, uint32_t skip) {
     if (n_dev) n = *n_dev;
+    if (lim && shift >= *lim && skip) return;
+    if ((uint64_t)blockIdx.x * LG_RS_TILE >= n) return;
     if (lim && shift >= *lim) {   // digits past the keys' width: the pass is a copy
         for (int q = 0; q < LG_RS_ROUNDS; q++) {
             const uint64_t i = (uint64_t)blockIdx.x * LG_RS_TILE + (uint64_t)q * CG_BLOCK + threadIdx.x;
@@ -525,7 +555,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_scatter(const uint64_t* kin, c
     // this tile's base per digit from the raw (digit-major) counts: the digit's offset (all
     // tiles' counts of smaller digits) plus its count in the tiles before this one
     {
-        const uint32_t nt = gridDim.x, b = blockIdx.x;
+        // the tiles holding elements (the grid may be sized for an upper bound of n)
+        const uint32_t nt = (uint32_t)(((uint64_t)n + LG_RS_TILE - 1) / LG_RS_TILE), b = blockIdx.x;
         uint32_t tot = 0, pre = 0;
         if (tid < 256) {   // eight count loads in flight (a dependent walk costs an L2 trip per tile)
             const uint32_t* h = hist + (uint64_t)tid * nt;
@@ -599,20 +630,22 @@ uint32_t bits_of(uint64_t v) { return cg_bits_of(v); }
 // Stable sort of n pairs in (k[0], v[0]) by key bits [lo, bits); returns the buffer index (0 or
 // 1) that holds the result. The pairs are already in order of the bits below lo. With n_dev,
 // the count is read on the device and n is only its upper bound.
+// skip (with lim): passes past the device-side key width do nothing instead of copying; the
+// result's buffer is then lg_rs_passes(lo, bits, *lim) & 1, known on the device only (returns -1).
 int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t lo = 0,
-               const uint32_t* n_dev = nullptr, const uint32_t* lim = nullptr) {
+               const uint32_t* n_dev = nullptr, const uint32_t* lim = nullptr, bool skip = false) {
     uint64_t* k[2] = {S.key0, S.key1};
     uint32_t* v[2] = {S.val0, S.val1};
     int cur = 0;
-    if (n <= 1) return cur;
-    const uint32_t nt = (uint32_t)(((uint64_t)n + LG_RS_TILE - 1) / LG_RS_TILE);
+    if (n <= 1 && !n_dev) return cur;
+    const uint32_t nt = std::max<uint32_t>(1, (uint32_t)(((uint64_t)n + LG_RS_TILE - 1) / LG_RS_TILE));
     for (uint32_t shift = lo; shift < bits; shift += 8) {
         hipLaunchKernelGGL(lg_rs_hist, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], n, shift, S.hist, n_dev, lim);
         hipLaunchKernelGGL(lg_rs_scatter, dim3(nt), dim3(CG_BLOCK), 0, s, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1], n,
-                           shift, S.hist, n_dev, lim);
+                           shift, S.hist, n_dev, lim, skip ? 1u : 0u);
         cur ^= 1;
     }
-    return cur;
+    return skip && lim ? -1 : cur;
 }
 
 template <class FLAG, class EMIT>
@@ -680,16 +713,26 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
 // Every workgroup derives the grid words from the bounds (lg_grid_setup); workgroup 0 also
 // stores them in the meta words for the kernels after it (a halo slab: with its own count of
 // finite points, nfin_local, for the voxel runs).
+// Mtot = CG_K_FROM_META (the backend sized on the device): Mtot and npad from the meta words
+// (LG_MTOT, LG_NPAD; the grid sized for the frame's N); Mtot 0 (the LDS backend takes the frame)
+// leaves every later global-backend launch without work.
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevParams P, uint32_t Mtot, uint32_t N,
                                                           uint32_t PB, uint32_t npad,
                                                           uint32_t nfin_local = 0xffffffffu) {
     __shared__ uint32_t m[LG_META_WORDS];
     const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const bool dev = Mtot == CG_K_FROM_META;
+    if (dev) {
+        Mtot = S.meta[LG_MTOT];
+        npad = S.meta[LG_NPAD];
+    }
     if (threadIdx.x == 0) {
         lg_grid_setup(S.meta, m, P, npad, Mtot);
+        if (dev && Mtot == 0) m[LG_NCELL] = 0;
         if (blockIdx.x == 0) {
             lg_grid_setup(S.meta, S.meta, P, npad, Mtot);
             if (nfin_local != 0xffffffffu) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = nfin_local;
+            if (dev && Mtot == 0) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = S.meta[LG_NCELL] = 0;
         }
     }
     __syncthreads();
@@ -982,6 +1025,15 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
         S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0; S.pq[PQ_MIDS] = 0;
         const uint32_t n = S.meta[LG_PCL_N];
         if (n <= LG_PCL_CUT) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
+    }
+    {   // workgroups past the level's tiles return before their ticket (a grid sized from the
+        // frame's N): the tiles number at most ceil(n / PQ_T) + one per range
+        const uint32_t n = S.meta[LG_PCL_N];
+        const uint32_t nr0 = level == 0 ? (n > LG_PCL_CUT ? 1u : 0u) : min(S.pq[level % 3u], (uint32_t)PQ_MAXR);
+        if (blockIdx.x >= (n + PQ_T - 1) / PQ_T + nr0) {
+            if (blockIdx.x == 0 && tid == 0) S.ca[0] = 0;   // no tile: lg_pq_swap reads the count
+            return;
+        }
     }
     uint64_t* st = S.pqst;   // [0] tickets, [2 + t] tile t's status; lg_pq_swap zeroes them
     // the ticket first (its latency overlaps the range lists' loads): tickets are handed out
@@ -1534,9 +1586,18 @@ __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevP
 }
 // CSR, header and cluster centroids in one launch: the first cb workgroups write the CSR
 // arrays, the others sum the clusters (member indices from the sorted keys, as lg_csr reads them)
+// (the backend sized on the device: Mtot = K = CG_K_FROM_META read from the meta words, and buf
+// < 0: the sort's buffer from the passes its key width needed, lg_rs_passes over [VB, sort_hi))
+__device__ __forceinline__ uint32_t lg_rs_passes(uint32_t lo, uint32_t hi, uint32_t lim) {
+    const uint32_t top = min(hi, lim);
+    return top > lo ? (top - lo + 7u) / 8u : 0u;
+}
 __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
                                                              uint32_t VB, int buf, uint32_t Mtot, uint32_t K,
-                                                             uint32_t cb) {
+                                                             uint32_t cb, uint32_t sort_hi) {
+    if (Mtot == CG_K_FROM_META) Mtot = S.meta[LG_MALL];
+    if (K == CG_K_FROM_META) K = S.meta[LG_KHDR];
+    if (buf < 0) buf = (int)(lg_rs_passes(VB, sort_hi, S.meta[LG_SORT_LIM]) & 1u);
     if (blockIdx.x < cb) {
         lg_csr_one(L, P, S, f, VB, buf, Mtot, K, blockIdx.x);
         return;
@@ -1589,7 +1650,7 @@ int cg_large_set_survivors(LgScratch S, const CgDevParams& P, const float* d_poi
 // ------------------------------------------------------------------------------------------
 // Host phases (cg_run_large below, and the tiles of cg_tile_*): front, decide, backend.
 int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, uint32_t f,
-                   bool init) {
+                   bool init, uint32_t szfl) {
     const uint32_t N = L.n_points;
     const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
@@ -1602,16 +1663,16 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
 #define LG_FRONT_MODES(LAY)                                                                       \
     if (kmode == CG_KMODE_PIPELINE) {                                                             \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, fi);           \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u);                      \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
     } else if (kmode == CG_KMODE_DETECT) {                                                        \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f);                              \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u);                      \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u | ((szfl & LG_SZ_ON) ? LG_FOLD_SIZE : 0u), N, szfl); \
     } else {                                                                                      \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, fi);             \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u);                      \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
         hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);            \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u);                      \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u, 0u, 0u);                      \
         hipLaunchKernelGGL(lg_ground_out<LAY>, g, b, 0, s, L, P, S, f);                           \
     }
     if (xyzi16) {
@@ -1623,7 +1684,7 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
     return hipGetLastError();
 }
 
-int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f) {
+int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f, uint32_t szfl) {
     const uint32_t nch = (uint32_t)(((uint64_t)L.n_points + LG_CHUNK - 1) / LG_CHUNK);
     if (nch == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
@@ -1635,7 +1696,8 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
         hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f);
     }
-    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u);
+    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u | ((szfl & LG_SZ_ON) ? LG_FOLD_SIZE : 0u),
+                       L.n_points, szfl);
     return hipGetLastError();
 }
 
@@ -1757,8 +1819,140 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
     const int kb = radix_sort(S, Mtot, VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1, s, VB, S.meta + LG_V,
                                S.meta + LG_SORT_LIM);
     const uint32_t cb = blocks_of((uint64_t)Mtot + 1);
-    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, kb, Mtot, K, cb);
+    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, kb, Mtot, K, cb, 0u);
     return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// The backend sized on the device (cg_run_large, PCL's voxel order, survivors in frame-index
+// order): every launch is sized from the frame's N (M <= N) and reads the counts it needs from
+// the meta words, which the decisions' fold filled (LG_MALL ... LG_SMALL). Nothing returns to
+// the host between the front and the results, so a frame is one uninterrupted run of launches
+// (and one hipGraph replay). Workgroups past a launch's work return after one or two loads. The
+// LDS backend (M <= CG_MMAX) runs last and returns unless the fold chose it; then the global
+// launches before it found M = 0 and did nothing.
+static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f,
+                             uint32_t N) {
+    CgLaunch Lh = L;
+    Lh.n_points = N;
+    const uint32_t nmax = std::max<uint32_t>(N, 1);
+    hipLaunchKernelGGL(lg_voxel_keys, dim3(blocks_of(nmax)), dim3(CG_BLOCK), 0, s, S, P, CG_K_FROM_META, N, 0u, 0u,
+                       0xffffffffu);
+    uint64_t* kb[2] = {S.key0, S.key1};
+    uint32_t* vb2[2] = {S.val0, S.val1};
+    // index_vector (finite points in frame-index order) as (idx, slot) records, then std::sort's
+    // permutation of it: levels for the frame's N (levels with no range return at once)
+    scan_emit(S, nmax, LG_MTOT, PclCompactFlag{kb[0], 0u}, PclCompactEmit{kb[0], vb2[0], kb[1], 0u}, LG_PCL_N, s);
+    uint32_t levels = 0;
+    while (((uint64_t)LG_PCL_CUT << levels) < nmax) levels++;
+    if (levels) levels = std::min<uint32_t>(levels + LG_PQ_SPARE, LG_PQ_LEVELS_MAX);
+    if (S.pcl_levels_cap) levels = std::min(levels, S.pcl_levels_cap);
+    const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
+    hipLaunchKernelGGL(lg_pq_split, dim3(tb), dim3(CG_BLOCK), 0, s, S, kb[1], 0u);
+    for (uint32_t lv = 0; lv < levels; lv++) {
+        uint64_t* const Ein = lv % 2 ? kb[0] : kb[1];
+        uint64_t* const Eout = lv % 2 ? kb[1] : kb[0];
+        const uint32_t grid = tb + (1u << lv);
+        if (lv) hipLaunchKernelGGL(lg_pq_split, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, lv);
+        hipLaunchKernelGGL(lg_pq_swap, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
+    }
+    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S, kb[1],
+                       kb[0], kb[0], vb2[0]);
+    hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
+                       kb[0], vb2[0]);
+    hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, nmax / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s, S,
+                       kb[1], kb[0], kb[0], vb2[0]);
+    // voxel runs over the finite points (LG_SCAN_N; every point if passthrough), centroids
+    scan_emit(S, nmax, LG_SCAN_N, VoxelHead{S.key0, S.meta, 0u}, VoxelEmit{S.run}, LG_V, s);
+    hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(nmax)), dim3(CG_BLOCK), 0, s, Lh, S, f, nmax, 0);
+    const uint32_t VB = bits_of(nmax);
+    const uint32_t vb = blocks_of(nmax), wb = lg_wave_blocks(nmax);
+    const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
+    hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
+    hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
+    hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    scan_emit(S, nmax, LG_V, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
+    hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, S, f, VB);
+    // the CSR: a stable sort of the rank bits; passes past the device-side cluster count skip
+    const uint32_t cmax = P.min_cl > 1 ? nmax / P.min_cl : nmax;
+    const uint32_t hi = VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1;
+    radix_sort(S, nmax, hi, s, VB, S.meta + LG_V, S.meta + LG_SORT_LIM, true);
+    const uint32_t cb = blocks_of((uint64_t)nmax + 1);
+    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, -1, CG_K_FROM_META,
+                       CG_K_FROM_META, cb, hi);
+    return cg_launch_lg_back_small(Lh, P, S, f, CG_K_FROM_META, 0u, s);
+}
+
+// One frame through the device-sized path: front, decisions (their fold sizes the backend),
+// backend. Pipeline and detect modes.
+static int large_frame_dev(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
+                           uint32_t f) {
+    const uint32_t szfl = LG_SZ_ON | (kmode == CG_KMODE_PIPELINE ? LG_SZ_PIPE : 0u) |
+                          (kmode == CG_KMODE_PIPELINE && P.zero_pass ? LG_SZ_ZPAD : 0u) |
+                          (S.force_global ? LG_SZ_GLOBAL : 0u);
+    int e;
+    if ((e = cg_large_front(L, P, kmode, S, s, f, true, szfl)) != hipSuccess) return e;
+    if (kmode == CG_KMODE_PIPELINE && (e = cg_large_decide(L, P, S, s, f, szfl)) != hipSuccess) return e;
+    if ((e = large_backend_dev(L, P, S, s, f, L.n_points)) != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+// Captured frames: one hipGraph per (launch arguments, frame), instantiated once and replayed:
+// the frame's ~40 launches cost the host one graph launch instead of one call each. Captured on
+// a private stream (nothing runs there); at most LG_GRAPHS entries, then frames run eagerly.
+#define LG_GRAPHS 32
+struct LgGraphs {
+    hipStream_t cap = nullptr;
+    struct Entry {
+        std::vector<unsigned char> key;
+        hipGraphExec_t exec;
+    };
+    std::vector<Entry> e;
+};
+void cg_large_graphs_free(LgGraphs* g) {
+    if (!g) return;
+    for (auto& x : g->e) (void)hipGraphExecDestroy(x.exec);
+    if (g->cap) (void)hipStreamDestroy(g->cap);
+    delete g;
+}
+static std::vector<unsigned char> lg_graph_key(const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
+                                               uint32_t f) {
+    std::vector<unsigned char> k(sizeof(L) + sizeof(P) + sizeof(S) + 2 * sizeof(uint32_t));
+    unsigned char* q = k.data();
+    std::memcpy(q, &L, sizeof(L)); q += sizeof(L);
+    std::memcpy(q, &P, sizeof(P)); q += sizeof(P);
+    std::memcpy(q, &S, sizeof(S)); q += sizeof(S);
+    const uint32_t t[2] = {(uint32_t)kmode, f};
+    std::memcpy(q, t, sizeof(t));
+    return k;
+}
+static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
+                             hipStream_t s, uint32_t f) {
+    std::vector<unsigned char> key = lg_graph_key(L, P, kmode, S, f);
+    for (auto& x : g->e)
+        if (x.key == key) return hipGraphLaunch(x.exec, s);
+    if (g->e.size() >= LG_GRAPHS) return large_frame_dev(L, P, kmode, S, s, f);
+    hipError_t e;
+    if (!g->cap && (e = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
+    const int rc = large_frame_dev(L, P, kmode, S, g->cap, f);
+    hipGraph_t graph = nullptr;
+    e = hipStreamEndCapture(g->cap, &graph);
+    if (rc != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+    }
+    if (e != hipSuccess) return e;
+    hipGraphExec_t exec = nullptr;
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) return e;
+    g->e.push_back({std::move(key), exec});
+    return hipGraphLaunch(exec, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1770,10 +1964,19 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
 // the stream holds work while the host reads frame f's counts and sizes its backend. The
 // stream order keeps every set's reads before its next writes (frame f + 2's front follows
 // frame f's backend).
-int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, const LgScratch* S2) {
+int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, const LgScratch* S2,
+                 LgGraphs** graphs) {
     const uint32_t N = L.n_points;
     hipError_t e;
     S.pidx_base = 0;
+    if (kmode != CG_KMODE_GROUND && P.voxel_order == CG_VOXEL_ORDER_PCL && N > 0 && N <= LG_DEV_MAX_POINTS) {
+        if (graphs && !*graphs) *graphs = new LgGraphs();
+        for (uint32_t f = 0; f < L.n_frames; f++) {
+            const int rc = graphs ? large_frame_graph(*graphs, L, P, kmode, S, s, f) : large_frame_dev(L, P, kmode, S, s, f);
+            if (rc != hipSuccess) return rc;
+        }
+        return hipSuccess;
+    }
     if (S2 && L.n_frames > 1 && kmode != CG_KMODE_GROUND && S.hmeta && S2->hmeta) {
         LgScratch set[2] = {S, *S2};
         set[1].pidx_base = 0;
@@ -2068,7 +2271,7 @@ int cg_halo_merge_run(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipS
     const uint32_t cb = blocks_of((uint64_t)n + 1);
     CgDevParams Pm = P;
     Pm.voxel_order = CG_VOXEL_ORDER_POINT;   // each slab summed its voxels in frame-index order
-    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, L, Pm, S, 0u, VB, kb, Mtot, K, cb);
+    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, L, Pm, S, 0u, VB, kb, Mtot, K, cb, 0u);
     return hipGetLastError();
 }
 int cg_launch_halo_owner(const float* pts, uint32_t n, float inv0, int32_t min_b0, uint32_t slab_w, uint32_t slabs,

@@ -156,8 +156,10 @@ typedef struct cg_batch {
 /* Enqueue one pass of the hot path over the batch on `hip_stream` (hipStream_t; NULL = the
  * handle's own stream). Results stay on the device until the next call on the handle. Frames
  * of up to 65,536 points run as one launch, one workgroup per frame. Frames of more run
- * through the multi-workgroup large-frame path one frame at a time, and the call synchronises
- * the stream (it sizes each frame's backend from its counts).
+ * through the multi-workgroup large-frame path one frame at a time: with PCL's voxel order (the
+ * default) and up to 2^22 points, sized on the device and replayed from a captured hipGraph per
+ * frame, nothing synchronised; otherwise the call synchronises the stream once per frame (the
+ * frame's counts size its backend).
  * A handle's calls are ordered whatever stream each names: a call on another stream than the
  * handle's previous call waits for that stream's work queued so far (which must still exist). */
 int cg_run_batch(cg_handle* h, const cg_batch* b, int mode, void* hip_stream);
