@@ -457,11 +457,16 @@ void publish_chunks(cg_handle* h, const cg_cloud_view* v, uint32_t n, uint32_t s
     }
 }
 
-// dma_retry: the frame again with its input staged whole and copied by DMA (route 4's form),
-// after a zero-copy call whose chunk workgroups gave up waiting for the host's publish words
-// (a host thread descheduled for CG_STAGE_TIMEOUT): the call is then only slower, never failed.
+// Retries (the call is then only slower, never failed):
+//   RETRY_DMA: the frame again with its input staged whole and copied by DMA (route 4's form),
+//   after a zero-copy call whose chunk workgroups gave up waiting for the host's publish words
+//   (a host thread descheduled for CG_STAGE_TIMEOUT);
+//   RETRY_ONE_WG: the frame again in one workgroup (route 3's form), after a split launch whose
+//   chunk workgroups gave up waiting for each other (CG_SPLIT_TIMEOUT: other work held the CUs).
+enum { RETRY_DMA = 1, RETRY_ONE_WG = 2 };
 int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_result* dres,
-               cg_ground_result* gres, bool dma_retry = false) {
+               cg_ground_result* gres, int retry = 0) {
+    const bool dma_retry = (retry & RETRY_DMA) != 0;
     if (!h) return fail(CG_E_INVALID, "null handle");
     int rc = check_view(in);
     if (rc) return rc;
@@ -475,7 +480,8 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     CgLaunch L{};
     // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
     // the one-workgroup frame kernel, for comparisons)
-    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4 || h->route == 6);
+    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4 || h->route == 6) &&
+                       !(retry & RETRY_ONE_WG);
     bool staged_later = false;
     // route 4: split, input by DMA; route 6 (tests): zero-copy with no chunk ever published
     const bool zero_copy = split && (h->route == 0 || h->route == 6) && !dma_retry;
@@ -500,8 +506,10 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     if (split) {
         if (!h->d_split) {
             HIPCHK(hipMalloc(&h->d_split, CG_SPLIT_WORDS * 4));
-            HIPCHK(hipMemsetAsync(h->d_split, 0, 8, h->stream));
-            HIPCHK(hipMemsetAsync(h->d_split + 2, 0xff, (CG_NUM_BINS + 1) * 4, h->stream));
+            // the state words as the kernel's last workgroup leaves them: zero, the minima all ones
+            HIPCHK(hipMemsetAsync(h->d_split, 0, SP_STATE * 4, h->stream));
+            HIPCHK(hipMemsetAsync(h->d_split + SP_KEYS, 0xff, (CG_NUM_BINS + 1) * 4, h->stream));
+            HIPCHK(hipMemsetAsync(h->d_split + SP_BMIN, 0xff, 3 * 4, h->stream));
         }
         L.split = h->d_split;
         rc = ensure_pack(h);
@@ -538,7 +546,11 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         // a chunk was processed before its bytes were published: the results are void; the
         // staging buffer is complete now, so the frame runs again with its input by DMA
         h->retries++;
-        return run_single(h, in, kmode, dres, gres, true);
+        return run_single(h, in, kmode, dres, gres, retry | RETRY_DMA);
+    }
+    if (split && h->h_hdr[CG_HDR_WORDS - 1]) {   // (the kernel's own flag: header word 7)
+        h->retries++;
+        return run_single(h, in, kmode, dres, gres, retry | RETRY_ONE_WG);
     }
     h->last_k = h->h_hdr[CG_HDR_K];
     h->last_single = true;

@@ -70,7 +70,8 @@ enum {
     S_K = 0, S_MS, S_M, S_MF, S_V, S_C, S_U, S_FLAGS, S_PASS,
     S_MINB0, S_MINB1, S_MINB2, S_MUL1, S_MUL2,
     S_ORGX, S_ORGY, S_ORGZ, S_TKMIN, S_TKMAX, S_TOUCHED,
-    S_BMIN0, S_BMIN1, S_BMIN2, S_BMAX0, S_BMAX1, S_BMAX2, S_TMP, S_LAST
+    S_BMIN0, S_BMIN1, S_BMIN2, S_BMAX0, S_BMAX1, S_BMAX2, S_TMP, S_LAST,
+    S_ERR = 40   // (the backend's flatten rounds use S_TMP .. S_TMP + 2)
 };
 
 

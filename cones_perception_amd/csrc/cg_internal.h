@@ -98,15 +98,25 @@ struct CgLaunch {
 };
 #define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
 #define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms
-// A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk
-// for pass 1; the last chunk to finish runs the rest of the frame kernel. State words: [0]
-// finished chunks, [1] used sector bins, [2, 20) sector-minimum keys (all reset by the last
-// workgroup), then the z codes (one uint2 per chunk and lane) and filter bits (one byte per
-// chunk and lane).
+// A single frame of <= CG_MAX_POINTS points spread over one workgroup per 4,096-point chunk:
+// pass 1 per chunk; once every chunk's sector minima are merged, pass 2 and the survivors per
+// chunk; the last chunk to finish gathers the survivors and runs the backend. State words (SP_*,
+// reset by the last workgroup; the host zeroes them once, keys and bounds minima to all ones),
+// then the frame's survivors: x, y, z, intensity (float4) and point index per slot.
 #define CG_SPLIT_CHUNK (8 * CG_BLOCK)   // 8 points per lane: one uint2 of codes, one byte of bits
-#define CG_SPLIT_CODES 64
-#define CG_SPLIT_POSM (CG_SPLIT_CODES + 2 * (CG_MAX_POINTS / 8))
-#define CG_SPLIT_WORDS (CG_SPLIT_POSM + CG_MAX_POINTS / 8 / 4)
+enum {
+    SP_ARRIVE = 0,      // chunks whose sector minima are merged
+    SP_TOUCHED = 1,     // used sector bins (OR)
+    SP_KEYS = 2,        // 18 sector-minimum keys (MIN)
+    SP_DONE = 20,       // chunks done with their survivors
+    SP_MS, SP_K,        // survivors, kept points (SUM)
+    SP_BMIN, SP_BMAX = SP_BMIN + 3, SP_NFIN = SP_BMAX + 3,   // VoxelGrid bounds keys, finite survivors
+    SP_ERR,             // a chunk gave up waiting for the others (CG_SPLIT_TIMEOUT)
+    SP_STATE = 64,
+    SP_SURV = SP_STATE
+};
+#define CG_SPLIT_WORDS (SP_SURV + 5 * CG_MAX_POINTS)
+#define CG_SPLIT_TIMEOUT 40000000ull   // s_memrealtime ticks (100 MHz): 400 ms
 int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
 
 // Host wait for a stream's queued work. Default: hipStreamSynchronize. CG_SPIN_SYNC (a variant
@@ -182,6 +192,10 @@ struct LgScratch {
     uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
     uint32_t pq_cap;          //   entries
     uint64_t* pqst;           //   the partition levels' look-back words (tickets, finished, per tile)
+    // the persistent PCL sort (lg_pcl_run, the device-sized backend): header words, range
+    // table (LG_PS_RW words per range), work queue (64-bit items), per-tile look-back words
+    uint32_t* ps_hdr; uint32_t* ps_rd; uint64_t* ps_q; uint64_t* ps_st;
+    uint32_t ps_rcap, ps_qcap, ps_tcap;
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)

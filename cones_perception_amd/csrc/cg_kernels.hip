@@ -112,7 +112,6 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     // ---- pass 1: stream the frame ----
     LaneBits<NW> posm;
     uint32_t touched = 0;
-    uint2* const sp_codes = SPLIT ? (uint2*)(L.split + CG_SPLIT_CODES) : nullptr;
     if constexpr (SPLIT) {
         static_assert(PPT * CG_BLOCK == CG_MAX_POINTS, "split frames use the 64k tail");
         static_assert(CG_SPLIT_CHUNK == 8 * CG_BLOCK, "a chunk's codes are one uint2 and its bits one byte per lane");
@@ -170,44 +169,159 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         stream_pass1<CG_SPLIT_CHUNK / CG_BLOCK, LAYOUT, GROUND, FILTER>(
             fb + (uint64_t)c0 * L.point_step, Nc, L, P, fs->sec_key, fs->rays, pm, touched,
             [&](int, uint2 cw) { code = cw; });
-        // codes and filter bits device-coherently too (four lanes' bytes as one word); the
-        // chunk's part is complete once every lane's stores and atomics are (vmcnt(0) and the
-        // barrier), then a relaxed count: no release / acquire fences, whose L2 writeback and
-        // invalidate on every chunk workgroup cost ~5 us of the frame's critical path
-        st64((uint64_t*)&sp_codes[c * CG_BLOCK + tid], ((uint64_t)code.y << 32) | code.x);
-        {
-            const uint32_t b = (uint32_t)(uint8_t)pm.w[0];
-            const uint32_t wv = b | ((uint32_t)__shfl_down((int)b, 1, 64) << 8) |
-                                ((uint32_t)__shfl_down((int)b, 2, 64) << 16) | ((uint32_t)__shfl_down((int)b, 3, 64) << 24);
-            if ((tid & 3u) == 0) st_rlx(L.split + CG_SPLIT_POSM + (c * CG_BLOCK + tid) / 4, wv);
-        }
+        // Every chunk decides its own points once all the frame's sector minima are merged: the
+        // chunks publish their minima (atomics), count themselves (a relaxed count after their
+        // atomics completed) and wait for the count; then each takes the thresholds from the
+        // merged keys, runs pass 2 on its own codes (still in registers) and appends its
+        // survivors, K and bounds to the frame's state with device-coherent stores and atomics.
+        // The last chunk to count itself done gathers the survivors and runs the backend. No
+        // release / acquire fences (their L2 writeback and invalidate cost ~5 us per workgroup);
+        // every cross-workgroup word is an atomic or an sc1 (device-coherent) access.
         if (GROUND) {
             touched = wave_or(touched);
-            if (l == 0 && touched) atomicOr(L.split + 1, touched);
+            if (l == 0 && touched) atomicOr(L.split + SP_TOUCHED, touched);
         }
         __syncthreads();   // the chunk's sector minima are final in LDS
         STAMP(29);
-        if (GROUND && tid <= CG_NUM_BINS) atomicMin(L.split + 2 + tid, fs->sec_key[tid]);
+        if (GROUND && tid <= CG_NUM_BINS) atomicMin(L.split + SP_KEYS + tid, fs->sec_key[tid]);
         __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
         __syncthreads();
+        if (tid == 0) {
+            __hip_atomic_fetch_add(L.split + SP_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // bounded: all chunk workgroups are running unless other work holds the CUs; past
+            // the bound the frame is flagged and the host runs it again in one workgroup
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t ok = 1;
+            while (ld_rlx(L.split + SP_ARRIVE) < gridDim.x) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > CG_SPLIT_TIMEOUT) {
+                    st_rlx(L.split + SP_ERR, 1u);
+                    ok = 0;
+                    break;
+                }
+            }
+            fs->scal[S_LAST] = ok;
+        }
+        __syncthreads();
+        STAMP(30);
+        if (fs->scal[S_LAST]) {
+            if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = ld_rlx(L.split + SP_KEYS + tid);
+            if (tid == 0) fs->scal[S_TOUCHED] = GROUND ? ld_rlx(L.split + SP_TOUCHED) : 0u;
+            __syncthreads();
+            if (GROUND && tid < 64)
+                sector_thresholds(fs->sec_key, fs->scal[S_TOUCHED], P, fs->thr, fs->tkey, &fs->scal[S_TKMIN],
+                                  &fs->scal[S_TKMAX]);
+            __syncthreads();
+            LaneBits<1> kp, am;
+            if (GROUND) {
+                pass2_codes<8>(Nc, fs->scal[S_TKMIN], fs->scal[S_TKMAX], [&](int) { return code; }, kp, am);
+            } else {
+                kp.clear();
+                am.clear();
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    if ((uint32_t)k * CG_BLOCK + tid < Nc) kp.w[0] |= 1ull << k;
+            }
+            // the lane's points to load (at most 8): kept filter survivors and ambiguous points
+            const uint32_t todo = (uint32_t)((kp.w[0] & pm.w[0]) | am.w[0]);
+            float4 pt[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if ((todo >> k) & 1u) pt[k] = load_xyzi<LAYOUT>(fb, c0 + (uint32_t)k * CG_BLOCK + tid, L);
+            uint32_t sv = 0, kamb = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (!((todo >> k) & 1u)) continue;
+                bool kept = true;
+                if (GROUND && ((am.w[0] >> k) & 1ull)) {
+                    kept = pass2_exact(P, fs->tkey, pt[k].x, pt[k].y, pt[k].z);
+                    kamb += kept ? 1u : 0u;
+                }
+                if (kept && ((pm.w[0] >> k) & 1ull)) sv |= 1u << k;
+            }
+            const uint32_t ns = (uint32_t)__builtin_popcount(sv);
+            const uint32_t incl = wave_incl_scan(ns);
+            uint32_t wbase = 0;
+            if (l == 63 && incl) wbase = __hip_atomic_fetch_add(L.split + SP_MS, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
+            uint32_t pos = wbase + incl - ns;
+            float4* const sp_p = (float4*)(L.split + SP_SURV);
+            uint32_t* const sp_i = L.split + SP_SURV + 4 * CG_MAX_POINTS;
+            float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t nf = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (!((sv >> k) & 1u)) continue;
+                st_f4(&sp_p[pos], pt[k]);
+                st_rlx(&sp_i[pos], c0 + (uint32_t)k * CG_BLOCK + tid);
+                pos++;
+                if (isfinite(pt[k].x) && isfinite(pt[k].y) && isfinite(pt[k].z)) {
+                    bmn[0] = fminf(bmn[0], pt[k].x); bmn[1] = fminf(bmn[1], pt[k].y); bmn[2] = fminf(bmn[2], pt[k].z);
+                    bmx[0] = fmaxf(bmx[0], pt[k].x); bmx[1] = fmaxf(bmx[1], pt[k].y); bmx[2] = fmaxf(bmx[2], pt[k].z);
+                    nf++;
+                }
+            }
+            float r[6];
+#pragma unroll
+            for (int a = 0; a < 3; a++) { r[a] = wave_min(bmn[a]); r[3 + a] = wave_max(bmx[a]); }
+            const uint32_t nfw = wave_sum(nf);
+            const uint32_t kc = GROUND ? wave_sum((uint32_t)__popcll(kp.w[0]) + kamb) : 0u;
+            if (l == 0) {
+                if (nfw) {
+#pragma unroll
+                    for (int a = 0; a < 3; a++) {
+                        atomicMin(L.split + SP_BMIN + a, cg_fkey(r[a]));
+                        atomicMax(L.split + SP_BMAX + a, cg_fkey(r[3 + a]));
+                    }
+                    atomicAdd(L.split + SP_NFIN, nfw);
+                }
+                if (kc) atomicAdd(L.split + SP_K, kc);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0x0070);   // every lane's stores and atomics are complete
+        __syncthreads();
         if (tid == 0)
-            fs->scal[S_LAST] = __hip_atomic_fetch_add(L.split, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            fs->scal[S_LAST] = __hip_atomic_fetch_add(L.split + SP_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                                gridDim.x - 1;
         __syncthreads();
         if (!fs->scal[S_LAST]) return;
-        // the last workgroup: the frame's sector keys and used bins (state reset for the next
-        // frame), every lane's filter bits over the chunks
-        if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = atomicExch(L.split + 2 + tid, 0xffffffffu);
+        STAMP(31);
+        // the last workgroup: the frame's counts and bounds (the state reset for the next frame:
+        // every chunk has read the keys and added its counts), then the survivors
         if (tid == 0) {
-            fs->scal[S_TOUCHED] = GROUND ? atomicExch(L.split + 1, 0u) : 0u;
-            atomicExch(L.split, 0u);
-        }
-        posm.clear();
-        const uint8_t* pb = (const uint8_t*)(L.split + CG_SPLIT_POSM);
-        const uint32_t nch = (N + CG_SPLIT_CHUNK - 1) / CG_SPLIT_CHUNK;
+            fs->scal[S_MS] = ld_rlx(L.split + SP_MS);
+            fs->scal[S_K] = ld_rlx(L.split + SP_K);
+            fs->scal[S_MF] = ld_rlx(L.split + SP_NFIN);
+            fs->scal[S_ERR] = ld_rlx(L.split + SP_ERR);
 #pragma unroll
-        for (int cc = 0; cc < PPT / 8; cc++)
-            if ((uint32_t)cc < nch) posm.set_byte(cc, pb[cc * CG_BLOCK + tid]);
+            for (int a = 0; a < 3; a++) {
+                fs->scal[S_BMIN0 + a] = ld_rlx(L.split + SP_BMIN + a);
+                fs->scal[S_BMAX0 + a] = ld_rlx(L.split + SP_BMAX + a);
+            }
+        }
+        __syncthreads();
+        if (fs->scal[S_ERR]) {   // (the keys of chunks that gave up were never read here)
+            if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = ld_rlx(L.split + SP_KEYS + tid);
+            if (tid == 0) { fs->scal[S_MS] = 0; fs->scal[S_MF] = 0; }
+        }
+        if (L.seckeys && GROUND && tid <= CG_NUM_BINS) L.seckeys[tid] = fs->sec_key[tid];
+        if (tid < SP_STATE) {
+            const bool keyw = (tid >= SP_KEYS && tid < SP_KEYS + CG_NUM_BINS + 1) || (tid >= SP_BMIN && tid < SP_BMIN + 3);
+            st_rlx(L.split + tid, keyw ? 0xffffffffu : 0u);
+        }
+        {
+            const uint32_t Ms = fs->scal[S_MS];
+            const float4* const sp_p = (const float4*)(L.split + SP_SURV);
+            uint32_t* const sp_i = L.split + SP_SURV + 4 * CG_MAX_POINTS;
+            const Work Wl = lds_work(bl);
+            const Work Wg = global_work(L.scratch, N);
+            for (uint32_t j = tid; j < Ms; j += CG_BLOCK) {
+                const float4 p = ld_f4(&sp_p[j]);
+                const uint32_t ix = ld_rlx(&sp_i[j]);
+                if (j < (uint32_t)CG_MMAX) { Wl.P[j] = p; Wl.IDX[j] = ix; }
+                else { Wg.P[j] = p; Wg.IDX[j] = ix; }
+            }
+        }
         __syncthreads();
     } else {
 #ifdef CG_CODES_HBM
@@ -234,6 +348,19 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     return;
 #endif
+    const uint32_t lcap = CG_MMAX;
+    const Work Wl = lds_work(bl);
+    const Work Wg = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t nfin = 0;
+    auto bound = [&](const float4& p) {
+        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+            nfin++;
+        }
+    };
+  if constexpr (!SPLIT) {   // (split frames: the chunks decided their points above)
     if (GROUND && tid < 64) {
         sector_thresholds(fs->sec_key, fs->scal[S_TOUCHED], P, fs->thr, fs->tkey, &fs->scal[S_TKMIN], &fs->scal[S_TKMAX]);
         if (L.seckeys && tid <= CG_NUM_BINS) L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = fs->sec_key[tid];
@@ -244,10 +371,9 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     // ---- pass 2: ground decisions from the codes ----
     auto codes_of = [&](int g) {
 #ifdef CG_CODES_HBM
-        return SPLIT ? sp_codes[g * CG_BLOCK + tid]
-                     : ((const uint2*)(L.scratch + (uint64_t)f * L.scratch_stride))[g * CG_BLOCK + tid];
+        return ((const uint2*)(L.scratch + (uint64_t)f * L.scratch_stride))[g * CG_BLOCK + tid];
 #else
-        return SPLIT ? sp_codes[g * CG_BLOCK + tid] : ((const uint2*)zq)[g * CG_BLOCK + tid];
+        return ((const uint2*)zq)[g * CG_BLOCK + tid];
 #endif
     };
     LaneBits<NW> keepgm, amb;
@@ -317,18 +443,6 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     // to the frame's HBM slot (moved whole below when M does not fit) ----
     __syncthreads();   // every wave is past the codes: LDS survivor slots overlay them from here
     STAMP(3);
-    const uint32_t lcap = CG_MMAX;
-    const Work Wl = lds_work(bl);
-    const Work Wg = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    uint32_t nfin = 0;
-    auto bound = [&](const float4& p) {
-        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
-            mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-            mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-            nfin++;
-        }
-    };
     auto put = [&](uint32_t pos, const float4& pt, uint32_t idx) {
         if (pos < lcap) {
             Wl.P[pos] = pt;
@@ -408,6 +522,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     }
     STAMP(25);
     __syncthreads();   // counts complete
+  }
     STAMP(4);
 
 #if defined(CG_EXP_STOP) && CG_EXP_STOP == 2
@@ -471,6 +586,8 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         backend(W, M, fs, L, P, f, flags, CG_MAX_POINTS / 32, 0);
     }
     if constexpr (SPLIT) {   // the results packed for the host's one copy (fetch_frame)
+        // header word 7: a chunk gave up waiting for the others (the host runs the frame again)
+        if (tid == 0) L.hdr[CG_HDR_WORDS - 1] = fs->scal[S_ERR];
         if (L.pack) {
             __threadfence();
             __syncthreads();
