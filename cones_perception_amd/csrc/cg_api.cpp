@@ -92,6 +92,7 @@ struct cg_handle {
     uint32_t large2_points = 0;
     LgScratch lg{};
     LgGraphs* lg_graphs = nullptr;   // captured large frames (cg_run_large), for its scratch set
+    uint32_t* h_hint = nullptr;      // pinned: the device-sized large path's level hint (LgScratch::hint)
     int route = 0;                // cg_debug_route
     uint32_t retries = 0;         // single-frame calls re-run by DMA after a staging timeout
     unsigned long long* next_span = nullptr;   // cg_debug_launch_spans: the next launch's span slot
@@ -281,6 +282,11 @@ int ensure_large(cg_handle* h, uint32_t n) {
     cg_large_layout(h->d_large, n, h->lg);
     if (!h->h_meta) HIPCHK(hipHostMalloc((void**)&h->h_meta, LG_META_WORDS * 4, hipHostMallocDefault));
     h->lg.hmeta = h->h_meta;
+    if (!h->h_hint) {
+        HIPCHK(hipHostMalloc((void**)&h->h_hint, 64, hipHostMallocCoherent));
+        *h->h_hint = 0;
+    }
+    HIPCHK(hipHostGetDevicePointer((void**)&h->lg.hint, h->h_hint, 0));
     h->large_points = n;
     return CG_OK;
 }
@@ -351,7 +357,9 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
         HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, &S2));
         return CG_OK;
     }
-    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, nullptr, &h->lg_graphs));
+    // (the hint is whatever the last finished frame wrote: no synchronisation)
+    const uint32_t hint = h->h_hint ? __atomic_load_n(h->h_hint, __ATOMIC_RELAXED) : 0u;
+    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, nullptr, &h->lg_graphs, hint));
     return CG_OK;
 }
 
@@ -627,6 +635,7 @@ int cg_destroy(cg_handle* h) {
     if (h->d_stamps) (void)hipFree(h->d_stamps);
     if (h->d_in) (void)hipFree(h->d_in);
     if (h->h_meta) (void)hipHostFree(h->h_meta);
+    if (h->h_hint) (void)hipHostFree(h->h_hint);
     if (h->d_large) (void)hipFree(h->d_large);
     cg_large_graphs_free(h->lg_graphs);
     if (h->h_meta2) (void)hipHostFree(h->h_meta2);

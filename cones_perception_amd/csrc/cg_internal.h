@@ -187,15 +187,13 @@ struct LgScratch {
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
     uint32_t* cstart;         // dense neighbour grid: per-cell start in ord (LG_DCELLS_MAX + 2)
     uint32_t* hmeta;          // pinned host copy of the meta words (the one round trip per frame)
+    uint32_t* hint;           // pinned host word (device address), or null: 1 + the last device-sized
+                              // frame's index_vector length, the partition levels' hint for the next
     uint32_t* cstat;          // per-chunk statistics [chunk][LG_CS_WORDS], reduced into meta by
                               // one workgroup (same-address atomics from every chunk serialise)
     uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
     uint32_t pq_cap;          //   entries
     uint64_t* pqst;           //   the partition levels' look-back words (tickets, finished, per tile)
-    // the persistent PCL sort (lg_pcl_run, the device-sized backend): header words, range
-    // table (LG_PS_RW words per range), work queue (64-bit items), per-tile look-back words
-    uint32_t* ps_hdr; uint32_t* ps_rd; uint64_t* ps_q; uint64_t* ps_st;
-    uint32_t ps_rcap, ps_qcap, ps_tcap;
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
@@ -213,8 +211,10 @@ void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
 #define LG_DEV_MAX_POINTS (1u << 22)
 struct LgGraphs;   // cg_large.hip: the handle's captured per-frame graphs
 void cg_large_graphs_free(LgGraphs* g);
+// pcl_hint: 1 + the previous frame's index_vector length (0: none), which sizes the partition
+// levels of the device-sized path; a frame that needs more finishes its longer ranges in HBM.
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
-                 const LgScratch* S2 = nullptr, LgGraphs** graphs = nullptr);
+                 const LgScratch* S2 = nullptr, LgGraphs** graphs = nullptr, uint32_t pcl_hint = 0);
 // The phases of cg_run_large for one frame f (also the tiles of cg_tile_*):
 //   front: meta init + pass 1 (ground-only mode: the whole ground output);
 //   decide: thresholds from meta, pass 2, candidates -> survivors (pipeline mode);

@@ -27,7 +27,6 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstring>
-#include <type_traits>
 #include <vector>
 #include "cg_internal.h"
 #include "../../include/cones_gpu.h"
@@ -488,10 +487,7 @@ __device__ __forceinline__ uint32_t lg_tile_scan(uint32_t* st, uint32_t t, uint3
 }
 
 // Exclusive scan of flag(i) over i < n (count from meta[n_word] when n_word >= 0), calling
-// emit(i, position) for every flagged i; the total goes to meta[total_word]. One launch. An
-// EMIT with a last(total) member has it called by every thread of the last tile.
-template <class T, class = void> struct lg_has_last : std::false_type {};
-template <class T> struct lg_has_last<T, decltype((void)&T::last)> : std::true_type {};
+// emit(i, position) for every flagged i; the total goes to meta[total_word]. One launch.
 template <class FLAG, class EMIT>
 __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, uint32_t* meta, FLAG flag,
                                                          EMIT emit, uint32_t* st, int total_word) {
@@ -507,10 +503,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word,
 #pragma unroll
     for (int q = 0; q < 8; q++)
         if (fl[q]) emit((uint32_t)(b0 + q), pos++);
-    if constexpr (lg_has_last<EMIT>::value) {
-        // the last tile hands the total on (its lane 0 of wave 0 wrote it, before a barrier)
-        if (t == active - 1) emit.last(ld_rlx(meta + total_word));
-    }
     lg_tile_done(st, active);
 }
 
@@ -656,6 +648,67 @@ int radix_sort(LgScratch& S, uint32_t n, uint32_t bits, hipStream_t s, uint32_t 
     return skip && lim ? -1 : cur;
 }
 
+}  // namespace
+
+// The LSD passes at shifts [lo, hi) that the device-side key width (*lim) still needs, after the
+// first pass of a sort whose data are now in buffer 1, by one workgroup (an identity launch for
+// the usual key widths: the CSR's cluster ranks fit one 8-bit digit below 255 clusters). Stable:
+// the tiles go in order, a tile's equal digits ranked in lane order by ballots as lg_rs_scatter.
+__global__ __launch_bounds__(CG_BLOCK) void lg_rs_rest(LgScratch S, uint32_t lo, uint32_t hi, const uint32_t* n_dev,
+                                                       const uint32_t* lim) {
+    const uint32_t top = min(hi, *lim);
+    if (lo >= top) return;
+    __shared__ uint32_t base[256];
+    __shared__ uint32_t wcnt[WAVES][256];
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t n = *n_dev, tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint64_t lt = (1ull << l) - 1ull;
+    int cur = 1;
+    for (uint32_t shift = lo; shift < top; shift += 8, cur ^= 1) {
+        const uint64_t* kin = cur ? S.key1 : S.key0;
+        const uint32_t* vin = cur ? S.val1 : S.val0;
+        uint64_t* kout = cur ? S.key0 : S.key1;
+        uint32_t* vout = cur ? S.val0 : S.val1;
+        if (tid < 256) base[tid] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += CG_BLOCK) atomicAdd(&base[(kin[i] >> shift) & 255u], 1u);
+        __syncthreads();
+        block_scan(256, [&](uint32_t d) -> uint32_t { return base[d]; }, [&](uint32_t d, uint32_t e) { base[d] = e; }, red);
+        for (uint32_t t0 = 0; t0 < n; t0 += CG_BLOCK) {
+            for (uint32_t x = tid; x < WAVES * 256; x += CG_BLOCK) (&wcnt[0][0])[x] = 0;
+            __syncthreads();
+            const uint32_t i = t0 + tid;
+            const bool valid = i < n;
+            uint64_t k = 0;
+            uint32_t v = 0, d = 0;
+            if (valid) { k = kin[i]; v = vin[i]; d = (uint32_t)(k >> shift) & 255u; }
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const uint64_t bb = __ballot((d >> b) & 1u);
+                m &= ((d >> b) & 1u) ? bb : ~bb;
+            }
+            const uint32_t rank = (uint32_t)__popcll(m & lt);
+            if (valid && rank == 0) wcnt[w][d] = (uint32_t)__popcll(m);
+            __syncthreads();
+            if (valid) {
+                uint32_t pos = base[d] + rank;
+                for (uint32_t u = 0; u < w; u++) pos += wcnt[u][d];
+                kout[pos] = k;
+                vout[pos] = v;
+            }
+            __syncthreads();
+            if (tid < 256) {
+                uint32_t t = 0;
+                for (int u = 0; u < WAVES; u++) t += wcnt[u][tid];
+                base[tid] += t;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+namespace {
 template <class FLAG, class EMIT>
 void scan_emit(LgScratch& S, uint32_t n_max, int n_word, FLAG flag, EMIT emit, int total_word, hipStream_t s) {
     const uint32_t nt = std::max<uint32_t>(1, tiles_of(n_max));
@@ -934,13 +987,6 @@ struct PclCompactEmit {
     __device__ void operator()(uint32_t j, uint32_t r) const {
         E[r] = ((uint64_t)(uint32_t)(key[j] >> PB) << 32) | val[j];
     }
-};
-
-// forward: the persistent sort's first range (below)
-__device__ __forceinline__ void lg_ps_init(const LgScratch& S, uint32_t n);
-struct PclCompactEmitPs : PclCompactEmit {   // ... and the persistent sort's work queue set up
-    LgScratch S;
-    __device__ void last(uint32_t n) const { lg_ps_init(S, n); }
 };
 
 __device__ __forceinline__ uint32_t pq_key(const uint64_t* E, uint32_t x) {
@@ -1296,393 +1342,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_waves(LgScratch S, uint64_t* 
 }
 
 // ------------------------------------------------------------------------------------------
-// The same introsort as one persistent launch (the device-sized backend): every partition level,
-// every leaf and every 65-512-record range, taken from a work queue by one workgroup per CU, so a
-// range is partitioned as soon as its parent's partition is done and a leaf sorted as soon as it
-// exists (no launch boundary, no level launched for nothing). Work items:
-//   SPLIT (range r, tile q): lg_pq_split's tile work (median of three, >= / <= look-back within
-//     the range, the L and R lists, each element's ranks);
-//   SWAP (r, q): once every SPLIT tile of r has counted itself, lg_pq_swap's tile work; the
-//     last SWAP tile of r sets up both children (a child longer than LG_PCL_CUT with budget
-//     left: its SPLIT and SWAP tiles; else a LEAF) and queues them;
-//   LEAF (r): lg_pcl_leaf's work on the range (in LDS up to LG_PCL_LEAF records); its ranges of
-//     65-512 records become MID items, those of 17-64 go to lg_pcl_waves (the next launch);
-//   MID (first, size, depth, buffer): lg_pcl_mid's work.
-// Queue: a workgroup takes a slot (an atomic on the head) and waits for the slot's item (an sc1
-// poll; items are written whole, 64-bit). A slot's item is pushed by a workgroup that is running
-// (the last SWAP tile of the parent range, a LEAF, or the launch before this one), and a SWAP
-// tile only waits on SPLIT tiles queued before it, so the launch cannot deadlock whatever the
-// residency. `pending` counts the ranges not yet finished; the workgroup that takes it to zero
-// sets `done`, which releases the workgroups waiting on empty slots. Every word another
-// workgroup of the launch wrote is read with an sc1 load or an atomic and written with an sc1
-// store or an atomic after the writer's own stores completed (vmcnt(0)); no fences. Every wait is
-// bounded (LG_PS_TIMEOUT): past it the launch stops and the frame is flagged (CG_F_DEVICE_ERROR).
-// The per-tile look-back words and the queue slots are zeroed again by their last user, so the
-// next frame finds them zeroed; the launch before (the compaction, lg_ps_init) sets the header.
-#define LG_PS_RW 16             // range words: first, last, depth, buffer, tiles, tile slot, nL, nR,
-enum { PR_F = 0, PR_E, PR_D, PR_BUF, PR_NT, PR_TS, PR_NL, PR_NR,   // SPLIT tiles done, SWAP tiles done,
-       PR_SPLIT, PR_SWAP, PR_CUT, PR_M, PR_P, PR_LEVEL };           // cut, median, pivot, level
-enum { PH_HEAD = 0, PH_TAIL, PH_PENDING, PH_DONE, PH_NRANGE, PH_NTSLOT, PH_ERR, PH_WORDS = 16 };
-#define PS_SPLIT 1ull
-#define PS_SWAP 2ull
-#define PS_LEAF 3ull
-#define PS_MID 4ull
-#define LG_PS_TIMEOUT 100000000ull   // s_memrealtime ticks (100 MHz): 1 s
-__device__ __forceinline__ uint64_t ps_tile_item(uint64_t type, uint32_t r, uint32_t q) {
-    return (type << 60) | ((uint64_t)q << 24) | r;
-}
-__device__ __forceinline__ uint64_t ps_mid_item(uint32_t first, uint32_t size, uint32_t depth, uint32_t buf) {
-    return (PS_MID << 60) | ((uint64_t)buf << 46) | ((uint64_t)(depth & 0xffu) << 38) | ((uint64_t)size << 28) | first;
-}
-__device__ __forceinline__ uint32_t ps_tiles(uint32_t f, uint32_t e) { return (e - f - 1 + PQ_T - 1) / PQ_T; }
-// Queue slots [slot, slot + n) reserved (one lane): the range is never past the capacity (then
-// the launch is flagged and stopped instead).
-__device__ __forceinline__ uint32_t ps_reserve(const LgScratch& S, uint32_t n) {
-    const uint32_t slot = __hip_atomic_fetch_add(&S.ps_hdr[PH_TAIL], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (slot + n > S.ps_qcap) {
-        st_rlx(&S.ps_hdr[PH_ERR], 1u);
-        st_rlx(&S.ps_hdr[PH_DONE], 1u);
-        return 0xffffffffu;
-    }
-    return slot;
-}
-__device__ __forceinline__ void ps_pending_add(const LgScratch& S, int32_t d) {
-    const uint32_t old = __hip_atomic_fetch_add(&S.ps_hdr[PH_PENDING], (uint32_t)d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + (uint32_t)d == 0u) st_rlx(&S.ps_hdr[PH_DONE], 1u);
-}
-// A range [f, e) with budget d, records in buffer buf, at partition level lv: a table entry and
-// whether it is partitioned (its tile count, look-back slots) or a leaf. One lane. Returns the
-// items it needs (2 * tiles, or 1) in *n_items; the entry index is returned (~0u: no room).
-__device__ __forceinline__ uint32_t ps_new_range(const LgScratch& S, uint32_t f, uint32_t e, uint32_t d, uint32_t buf,
-                                                 uint32_t lv, bool part, uint32_t* n_items) {
-    const uint32_t r = __hip_atomic_fetch_add(&S.ps_hdr[PH_NRANGE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r >= S.ps_rcap) {
-        st_rlx(&S.ps_hdr[PH_ERR], 1u);
-        *n_items = 0;
-        return 0xffffffffu;
-    }
-    uint32_t nt = 0, ts = 0;
-    if (part) {
-        nt = ps_tiles(f, e);
-        ts = __hip_atomic_fetch_add(&S.ps_hdr[PH_NTSLOT], nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (ts + nt > S.ps_tcap) part = false, nt = 0;   // no look-back room: sorted as a leaf (in HBM)
-    }
-    uint32_t* rd = S.ps_rd + (uint64_t)r * LG_PS_RW;
-    st_rlx(rd + PR_F, f); st_rlx(rd + PR_E, e); st_rlx(rd + PR_D, d); st_rlx(rd + PR_BUF, buf);
-    st_rlx(rd + PR_NT, nt); st_rlx(rd + PR_TS, ts); st_rlx(rd + PR_SPLIT, 0u); st_rlx(rd + PR_SWAP, 0u);
-    st_rlx(rd + PR_LEVEL, lv);
-    *n_items = part ? 2 * nt : 1u;
-    return r;
-}
-// item k of range r's items (tiles: the SPLIT tiles, then the SWAP tiles; or the LEAF)
-__device__ __forceinline__ uint64_t ps_range_item(uint32_t r, uint32_t n_items, uint32_t k) {
-    if (n_items == 1) return ps_tile_item(PS_LEAF, r, 0);
-    const uint32_t nt = n_items / 2;
-    return k < nt ? ps_tile_item(PS_SPLIT, r, k) : ps_tile_item(PS_SWAP, r, k - nt);
-}
-// The frame's first range (index_vector, n records in key1), by the compaction launch's last
-// workgroup: the header reset and the range's items queued (every thread calls). After a frame
-// that stopped at a bound, the look-back words and queue slots it left are zeroed first.
-__device__ __forceinline__ void lg_ps_init(const LgScratch& S, uint32_t n) {
-    __shared__ uint32_t ni, dirty;
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) dirty = S.ps_hdr[PH_ERR];
-    __syncthreads();
-    if (dirty) {
-        for (uint32_t i = tid; i < S.ps_tcap; i += CG_BLOCK) S.ps_st[i] = 0ull;
-        for (uint32_t i = tid; i < S.ps_qcap; i += CG_BLOCK) S.ps_q[i] = 0ull;
-    }
-    __syncthreads();
-    const uint32_t d = (uint32_t)(2 * cg_lg((long)n));
-    const bool part = n > LG_PCL_CUT;
-    if (tid == 0) {
-        uint32_t* h = S.ps_hdr;
-        h[PH_HEAD] = 0; h[PH_PENDING] = 1; h[PH_DONE] = 0; h[PH_ERR] = 0;
-        h[PH_NRANGE] = 1;
-        S.pq[PQ_WAVES] = 0;
-        const uint32_t nt = part ? ps_tiles(0, n) : 0u;
-        h[PH_NTSLOT] = nt;
-        uint32_t* rd = S.ps_rd;
-        rd[PR_F] = 0; rd[PR_E] = n; rd[PR_D] = d; rd[PR_BUF] = 1; rd[PR_NT] = nt; rd[PR_TS] = 0;
-        rd[PR_SPLIT] = 0; rd[PR_SWAP] = 0; rd[PR_LEVEL] = 0;
-        ni = part ? 2 * nt : 1u;
-        h[PH_TAIL] = ni;
-    }
-    __syncthreads();
-    for (uint32_t k = tid; k < ni; k += CG_BLOCK) S.ps_q[k] = ps_range_item(0, ni, k);
-}
-
-// PqDefer's form for the persistent launch: ranges of 65-512 records become MID items (their
-// records written back device-coherently first, `pending` raised before the item shows), those
-// of 17-64 go to lg_pcl_waves' list as before. One wave calls it per range.
-struct PsDefer {
-    LgScratch S; uint64_t* Eh; uint32_t base, buf;
-    template <class P64, class OUT>
-    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT) const {
-        const uint32_t l = lane_id();
-        if (m <= PW_MAX) {
-            for (uint32_t i = l; i < m; i += 64) Eh[base + f + i] = E[f + i];
-            if (l == 0) {
-                const uint32_t q = atomicAdd(S.pq + PQ_WAVES, 1u);
-                S.droot[2 * q] = base + f;
-                S.droot[2 * q + 1] = m | (d << 16) | (buf << 24);
-            }
-            return;
-        }
-        for (uint32_t i = l; i < m; i += 64) st64(Eh + base + f + i, E[f + i]);
-        __builtin_amdgcn_s_waitcnt(0x0070);   // the records before the item
-        if (l == 0) {
-            ps_pending_add(S, 1);
-            __builtin_amdgcn_s_waitcnt(0x0070);
-            const uint32_t slot = ps_reserve(S, 1u);
-            if (slot != 0xffffffffu) st64(S.ps_q + slot, ps_mid_item(base + f, m, d, buf));
-        }
-    }
-};
-
-// SPLIT tile q of range r (lg_pq_split's body on one range)
-__device__ __forceinline__ void ps_split(const LgScratch& S, uint32_t r, uint32_t q, uint32_t* sm) {
-    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
-    uint32_t* const rd = S.ps_rd + (uint64_t)r * LG_PS_RW;
-    if (tid < 8) sm[tid] = ld_rlx(rd + tid);   // f, e, d, buf, tiles, tile slot
-    __syncthreads();
-    const uint32_t f = sm[PR_F], e = sm[PR_E], buf = sm[PR_BUF], nt = sm[PR_NT], ts = sm[PR_TS];
-    uint64_t* const E = buf ? S.key1 : S.key0;
-    const uint32_t x = f + 1 + q * PQ_T + tid;
-    const bool valid = x < e;
-    const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
-    const uint32_t ka = (uint32_t)(ld64(E + a) >> 32), kb = (uint32_t)(ld64(E + b) >> 32);
-    const uint32_t kc = (uint32_t)(ld64(E + c) >> 32), kf = (uint32_t)(ld64(E + f) >> 32);
-    const uint32_t kx = valid ? (uint32_t)(ld64(E + x) >> 32) : 0u;
-    const uint32_t m = pb_median(a, b, c, ka, kb, kc);
-    const uint32_t p = m == a ? ka : (m == b ? kb : kc);
-    if (q == 0 && tid == 0) { st_rlx(rd + PR_M, m); st_rlx(rd + PR_P, p); }
-    const uint32_t k = valid ? (x == m ? kf : kx) : 0u;
-    const bool ge = valid && k >= p, le = valid && k <= p;
-    const uint64_t gm = __ballot(ge), lm = __ballot(le);
-    uint32_t* const cg = sm + 16;
-    uint32_t* const cl = sm + 16 + WAVES;
-    uint64_t* const tb = (uint64_t*)(sm + 16 + 2 * WAVES);
-    if (l == 0) { cg[w] = (uint32_t)__popcll(gm); cl[w] = (uint32_t)__popcll(lm); }
-    __syncthreads();
-    if (w == 0) {
-        uint32_t tg = 0, tl = 0;
-        for (uint32_t v = 0; v < WAVES; v++) { tg += cg[v]; tl += cl[v]; }
-        const uint64_t base = pq_lookback(S.ps_st + ts, 0u, q, ((uint64_t)tg << 32) | tl);
-        if (l == 0) {
-            *tb = base;
-            if (q == nt - 1) {   // the range's last tile: both totals
-                st_rlx(rd + PR_NL, (uint32_t)(base >> 32) + tg);
-                st_rlx(rd + PR_NR, (uint32_t)base + tl);
-            }
-        }
-    }
-    __syncthreads();
-    const uint64_t tbase = *tb;
-    uint32_t gi = (uint32_t)(tbase >> 32) + mbcnt(gm), li = (uint32_t)tbase + mbcnt(lm);
-    for (uint32_t v = 0; v < w; v++) { gi += cg[v]; li += cl[v]; }
-    if (ge) st_rlx(S.par + f + 1 + gi, x);
-    if (le) st_rlx(S.cnt + f + 1 + li, x);
-    if (valid) st64((uint64_t*)S.vox + x, ((uint64_t)gi << 32) | li);
-    __builtin_amdgcn_s_waitcnt(0x0070);
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(rd + PR_SPLIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// SWAP tile q of range r (lg_pq_swap's body); the range's last tile queues the children
-__device__ __forceinline__ void ps_swap(const LgScratch& S, uint32_t r, uint32_t q, uint32_t* sm, uint32_t levels_cap) {
-    const uint32_t tid = threadIdx.x;
-    uint32_t* const rd = S.ps_rd + (uint64_t)r * LG_PS_RW;
-    if (tid == 0) {   // every SPLIT tile of the range has counted itself
-        const uint32_t nt = ld_rlx(rd + PR_NT);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t ok = 1;
-        while (ld_rlx(rd + PR_SPLIT) < nt) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > LG_PS_TIMEOUT) { ok = 0; break; }
-        }
-        if (!ok) { st_rlx(&S.ps_hdr[PH_ERR], 1u); st_rlx(&S.ps_hdr[PH_DONE], 1u); }
-        sm[15] = ok;
-    }
-    __syncthreads();
-    if (!sm[15]) return;
-    if (tid < 14) sm[tid] = ld_rlx(rd + tid);
-    __syncthreads();
-    const uint32_t f = sm[PR_F], e = sm[PR_E], d = sm[PR_D], buf = sm[PR_BUF], nt = sm[PR_NT], ts = sm[PR_TS];
-    const uint32_t nL = sm[PR_NL], nR = sm[PR_NR], m = sm[PR_M], p = sm[PR_P], lv = sm[PR_LEVEL];
-    uint64_t* const E = buf ? S.key1 : S.key0;
-    uint64_t* const Eo = buf ? S.key0 : S.key1;
-    const uint32_t x = f + 1 + q * PQ_T + tid;
-    const uint64_t rf = ld64(E + f);
-    if (q == 0 && tid == 0) st64(Eo + f, ld64(E + m));
-    if (x < e) {
-        const uint64_t rx = ld64(E + x);
-        const uint64_t rk = ld64((uint64_t*)S.vox + x);
-        const uint64_t vx = x == m ? rf : rx;
-        const uint32_t k = pcl_key(vx);
-        const bool ge = k >= p, le = k <= p;
-        const uint32_t gi = (uint32_t)(rk >> 32), li = (uint32_t)rk;
-        uint32_t partner = x;
-        bool cutter = false;
-        uint32_t cut = 0;
-        if (ge && gi < nR) {
-            const uint32_t j = ld_rlx(S.cnt + f + 1 + (nR - 1 - gi));   // R_gi
-            if (x < j) {
-                partner = j;
-                const bool nx = gi + 1 < min(nL, nR);
-                const uint32_t l2 = nx ? ld_rlx(S.par + f + 2 + gi) : 0xffffffffu;
-                const uint32_t r2 = nx ? ld_rlx(S.cnt + f + 1 + (nR - 2 - gi)) : 0u;
-                if (!nx || !(l2 < r2)) {   // swap gi is the last: s = gi + 1
-                    cutter = true;
-                    cut = min(gi + 1 < nL ? ld_rlx(S.par + f + 2 + gi) : 0xffffffffu, j);
-                }
-            } else if (gi == 0) {   // no swap at all: the left scan stops at L_0
-                cutter = true;
-                cut = x;
-            }
-        }
-        if (le) {
-            const uint32_t ri = nR - 1 - li;
-            if (ri < nL) {
-                const uint32_t i = ld_rlx(S.par + f + 1 + ri);   // L_ri
-                if (i < x) partner = i;
-            }
-        }
-        st64(Eo + x, partner == x ? vx : (partner == m ? rf : ld64(E + partner)));
-        if (cutter) st_rlx(rd + PR_CUT, cut);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0070);
-    __syncthreads();
-    if (tid == 0)
-        sm[15] = __hip_atomic_fetch_add(rd + PR_SWAP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nt - 1;
-    __syncthreads();
-    if (!sm[15]) return;
-    // the range's last tile: its look-back words zeroed for the next frame (every SPLIT tile is
-    // done with them), the children set up and queued
-    for (uint32_t i = tid; i < nt; i += CG_BLOCK) S.ps_st[ts + i] = 0ull;
-    if (tid == 0) {
-        const uint32_t cut = ld_rlx(rd + PR_CUT);
-        const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
-        uint32_t total = 0;
-        for (int c = 0; c < 2; c++) {
-            const bool part = hi[c] - lo[c] > LG_PCL_CUT && d > 1 && (levels_cap == 0 || lv + 1 < levels_cap);
-            uint32_t n_items = 0;
-            const uint32_t rc = ps_new_range(S, lo[c], hi[c], d - 1u, buf ^ 1u, lv + 1, part, &n_items);
-            sm[16 + 2 * c] = rc;
-            sm[17 + 2 * c] = n_items;
-            total += n_items;
-        }
-        // the children count before they show (this range's own count goes with it)
-        ps_pending_add(S, (sm[16] != 0xffffffffu ? 1 : 0) + (sm[18] != 0xffffffffu ? 1 : 0) - 1);
-        __builtin_amdgcn_s_waitcnt(0x0070);
-        sm[20] = total ? ps_reserve(S, total) : 0xffffffffu;
-    }
-    __syncthreads();
-    const uint32_t slot = sm[20];
-    if (slot == 0xffffffffu) return;
-    const uint32_t n0 = sm[16] != 0xffffffffu ? sm[17] : 0u, n1 = sm[18] != 0xffffffffu ? sm[19] : 0u;
-    for (uint32_t k = tid; k < n0 + n1; k += CG_BLOCK)
-        st64(S.ps_q + slot + k, k < n0 ? ps_range_item(sm[16], n0, k) : ps_range_item(sm[18], n1, k - n0));
-}
-
-#define LG_PS_LDS (LG_PCL_LDS > LG_MID_LDS ? LG_PCL_LDS : LG_MID_LDS)
-__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_run(LgScratch S, uint64_t* kout, uint32_t* vout,
-                                                       uint32_t levels_cap) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PS_LDS];
-    __shared__ uint32_t red[8 * WAVES];
-    __shared__ __attribute__((aligned(16))) uint32_t sm[64];
-    __shared__ uint64_t item;
-    const uint32_t tid = threadIdx.x;
-    for (;;) {
-        if (tid == 0) {   // the next slot's item, or the end
-            const uint32_t k = __hip_atomic_fetch_add(&S.ps_hdr[PH_HEAD], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t it = 0;
-            if (k < S.ps_qcap) {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                while ((it = ld64(S.ps_q + k)) == 0ull) {
-                    if (ld_rlx(&S.ps_hdr[PH_DONE])) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > LG_PS_TIMEOUT) {
-                        st_rlx(&S.ps_hdr[PH_ERR], 1u);
-                        st_rlx(&S.ps_hdr[PH_DONE], 1u);
-                        break;
-                    }
-                }
-                if (it) st64(S.ps_q + k, 0ull);   // the slot zeroed for the next frame
-            }
-            item = it;
-        }
-        __syncthreads();
-        const uint64_t it = item;
-        __syncthreads();
-        if (!it) break;
-        const uint32_t type = (uint32_t)(it >> 60);
-        if (type == PS_SPLIT || type == PS_SWAP) {
-            const uint32_t r = (uint32_t)(it & 0xffffffu), q = (uint32_t)((it >> 24) & 0xffffffu);
-            if (type == PS_SPLIT) ps_split(S, r, q, sm);
-            else ps_swap(S, r, q, sm, levels_cap);
-            __syncthreads();
-            continue;
-        }
-        // LEAF / MID: a range sorted to the end by this workgroup
-        uint32_t first, size, depth, buf;
-        if (type == PS_LEAF) {
-            const uint32_t* rd = S.ps_rd + (uint64_t)(it & 0xffffffu) * LG_PS_RW;
-            if (tid < 4) sm[tid] = ld_rlx((uint32_t*)rd + tid);
-            __syncthreads();
-            first = sm[PR_F]; size = sm[PR_E] - first; depth = sm[PR_D]; buf = sm[PR_BUF];
-        } else {
-            first = (uint32_t)(it & 0xfffffffu); size = (uint32_t)((it >> 28) & 0x3ffu);
-            depth = (uint32_t)((it >> 38) & 0xffu); buf = (uint32_t)((it >> 46) & 1u);
-        }
-        uint64_t* const E = buf ? S.key1 : S.key0;
-        const PqLeafOut out{kout, vout, first};
-        const PsDefer wt{S, E, first, buf};
-        lds_u32* const Rl = (lds_u32*)red;
-        if (type == PS_MID) {
-            lds_u64* const El = (lds_u64*)(uint64_t*)smem;
-            lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * PQ_MID);
-            const PbScratch<PbLds> PS{w0, w0 + (PQ_MID + 4), w0 + 2 * (PQ_MID + 4), w0 + 3 * (PQ_MID + 4),
-                                      w0 + 4 * (PQ_MID + 4), w0 + 5 * (PQ_MID + 4)};
-            for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = ld64(E + first + i);
-            __syncthreads();
-            // (ranges of <= 64 records only: every range it hands on goes to lg_pcl_waves)
-            pcl_block_sort<1, PbLds, PqLeafOut, false, PsDefer>(El, out, size, depth, PS, Rl, nullptr, wt);
-        } else if (size <= LG_PCL_LEAF) {
-            lds_u64* const El = (lds_u64*)(uint64_t*)smem;
-            lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * LG_PCL_LEAF);
-            const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4),
-                                      w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
-            for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = ld64(E + first + i);
-            __syncthreads();
-            if (size <= CG_BLOCK)
-                pcl_block_sort<1, PbLds, PqLeafOut, false, PsDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else if (size <= 2 * CG_BLOCK)
-                pcl_block_sort<2, PbLds, PqLeafOut, false, PsDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else if (size <= 4 * CG_BLOCK)
-                pcl_block_sort<4, PbLds, PqLeafOut, false, PsDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else pcl_block_sort<8, PbLds, PqLeafOut, false, PsDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-        } else {   // a degenerate cut left it longer than a leaf: in HBM, on the range's own span
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (plain loads of other workgroups' records)
-            __syncthreads();
-            Work W{};
-            W.KEY = (uint64_t*)S.vox + 2ull * first;
-            W.A = S.lab + first; W.PAR = S.par + first; W.CNT = S.cnt + first; W.UK = S.uk + first;
-            W.ORD = S.ord + first; W.LAB = (int32_t*)S.rank + first; W.OFF = S.off + first;
-            pcl_sort<2, false>(W, E + first, size, red, (int)depth);
-            for (uint32_t i = tid; i < size; i += CG_BLOCK) {
-                const uint64_t rr = W.KEY[i];
-                kout[first + i] = rr >> 32;
-                vout[first + i] = (uint32_t)rr;
-            }
-        }
-        __syncthreads();
-        if (tid == 0) ps_pending_add(S, -1);
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // Euclidean clustering over the V voxels (FLANN L2_Simple predicate, PCL's seed = the lowest
 // index of each component):
 //   dense neighbour grid: voxel -> cell (atomic slot), exclusive scan of the cell counts,
@@ -1930,7 +1589,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_labels(CgLaunch L, LgScratch S, u
 // CSR indices (ascending voxel index inside each cluster), per-cluster centroid + radial push
 // (src/cone_detection.cpp:261-279), offsets and the frame header
 __device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
-                                           uint32_t VB, int buf, uint32_t Mtot, uint32_t K, uint32_t b, uint32_t err) {
+                                           uint32_t VB, int buf, uint32_t Mtot, uint32_t K, uint32_t b) {
     const uint32_t i = b * CG_BLOCK + threadIdx.x;
     const uint32_t* m = S.meta;
     const uint32_t C = m[LG_C], tot = C ? S.off[C] : 0u;
@@ -1945,7 +1604,7 @@ __device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const CgDevParams&
         h[CG_HDR_V] = m[LG_V];
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
-                          (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER) | err;
+                          (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
     }
 }
 __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S,
@@ -1999,11 +1658,12 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
                                                              uint32_t cb, uint32_t sort_hi) {
     if (Mtot == CG_K_FROM_META) Mtot = S.meta[LG_MALL];
     if (K == CG_K_FROM_META) K = S.meta[LG_KHDR];
-    // (device-sized: a persistent launch that gave up a bounded wait flags the frame)
-    const uint32_t err = buf < 0 && S.ps_hdr[PH_ERR] ? CG_F_DEVICE_ERROR : 0u;
-    if (buf < 0) buf = (int)(lg_rs_passes(VB, sort_hi, S.meta[LG_SORT_LIM]) & 1u);
+    if (buf < 0) {   // (device-sized: the next frame's partition levels are sized from this one's)
+        buf = (int)(lg_rs_passes(VB, sort_hi, S.meta[LG_SORT_LIM]) & 1u);
+        if (blockIdx.x == 0 && threadIdx.x == 0 && S.hint) *S.hint = S.meta[LG_PCL_N] + 1u;
+    }
     if (blockIdx.x < cb) {
-        lg_csr_one(L, P, S, f, VB, buf, Mtot, K, blockIdx.x, err);
+        lg_csr_one(L, P, S, f, VB, buf, Mtot, K, blockIdx.x);
         return;
     }
     const uint64_t* key = buf ? S.key1 : S.key0;
@@ -2235,16 +1895,19 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
 // (and one hipGraph replay). Workgroups past a launch's work return after one or two loads. The
 // LDS backend (M <= CG_MMAX) runs last and returns unless the fold chose it; then the global
 // launches before it found M = 0 and did nothing.
-// workgroups of the persistent launches: one per CU (their LDS takes most of one)
-static uint32_t lg_cu_count() {
-    static int n[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!n[dev] && hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n[dev] = 0;
-    return n[dev] > 0 ? (uint32_t)n[dev] : 256u;
+// The partition levels the device-sized path launches for index_vector length n (upper bound
+// or a previous frame's length): an even split's until every range fits a leaf, three more for
+// uneven median-of-three cuts (LG_PQ_SPARE). Levels past a frame's need return at once; ranges
+// still longer than a leaf after the last are finished in HBM (lg_pcl_leaf).
+static uint32_t lg_levels_for(uint32_t n, uint32_t cap) {
+    uint32_t levels = 0;
+    while (((uint64_t)LG_PCL_CUT << levels) < n) levels++;
+    if (levels) levels = std::min<uint32_t>(levels + LG_PQ_SPARE, LG_PQ_LEVELS_MAX);
+    if (cap) levels = std::min(levels, cap);
+    return levels;
 }
 static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f,
-                             uint32_t N) {
+                             uint32_t N, uint32_t levels) {
     CgLaunch Lh = L;
     Lh.n_points = N;
     const uint32_t nmax = std::max<uint32_t>(N, 1);
@@ -2254,14 +1917,22 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     uint32_t* vb2[2] = {S.val0, S.val1};
     // index_vector (finite points in frame-index order) as (idx, slot) records, then std::sort's
     // permutation of it: levels for the frame's N (levels with no range return at once)
-    // (the compaction's last tile queues the first range for the persistent sort)
-    PclCompactEmitPs ce;
-    static_cast<PclCompactEmit&>(ce) = PclCompactEmit{kb[0], vb2[0], kb[1], 0u};
-    ce.S = S;
-    scan_emit(S, nmax, LG_MTOT, PclCompactFlag{kb[0], 0u}, ce, LG_PCL_N, s);
-    hipLaunchKernelGGL(lg_pcl_run, dim3(lg_cu_count()), dim3(CG_BLOCK), 0, s, S, kb[0], vb2[0], S.pcl_levels_cap);
+    scan_emit(S, nmax, LG_MTOT, PclCompactFlag{kb[0], 0u}, PclCompactEmit{kb[0], vb2[0], kb[1], 0u}, LG_PCL_N, s);
+    const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
+    hipLaunchKernelGGL(lg_pq_split, dim3(tb), dim3(CG_BLOCK), 0, s, S, kb[1], 0u);
+    for (uint32_t lv = 0; lv < levels; lv++) {
+        uint64_t* const Ein = lv % 2 ? kb[0] : kb[1];
+        uint64_t* const Eout = lv % 2 ? kb[1] : kb[0];
+        const uint32_t grid = tb + (1u << lv);
+        if (lv) hipLaunchKernelGGL(lg_pq_split, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, lv);
+        hipLaunchKernelGGL(lg_pq_swap, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
+    }
+    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S, kb[1],
+                       kb[0], kb[0], vb2[0]);
+    hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
+                       kb[0], vb2[0]);
     hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, nmax / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s, S,
-                       kb[0], kb[1], kb[0], vb2[0]);
+                       kb[1], kb[0], kb[0], vb2[0]);
     // voxel runs over the finite points (LG_SCAN_N; every point if passthrough), centroids
     scan_emit(S, nmax, LG_SCAN_N, VoxelHead{S.key0, S.meta, 0u}, VoxelEmit{S.run}, LG_V, s);
     hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(nmax)), dim3(CG_BLOCK), 0, s, Lh, S, f, nmax, 0);
@@ -2280,7 +1951,9 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     // the CSR: a stable sort of the rank bits; passes past the device-side cluster count skip
     const uint32_t cmax = P.min_cl > 1 ? nmax / P.min_cl : nmax;
     const uint32_t hi = VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1;
-    radix_sort(S, nmax, hi, s, VB, S.meta + LG_V, S.meta + LG_SORT_LIM, true);
+    radix_sort(S, nmax, std::min(hi, VB + 8), s, VB, S.meta + LG_V, S.meta + LG_SORT_LIM, true);
+    if (hi > VB + 8) hipLaunchKernelGGL(lg_rs_rest, dim3(1), dim3(CG_BLOCK), 0, s, S, VB + 8, hi, S.meta + LG_V,
+                                        S.meta + LG_SORT_LIM);
     const uint32_t cb = blocks_of((uint64_t)nmax + 1);
     hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, -1, CG_K_FROM_META,
                        CG_K_FROM_META, cb, hi);
@@ -2290,14 +1963,14 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
 // One frame through the device-sized path: front, decisions (their fold sizes the backend),
 // backend. Pipeline and detect modes.
 static int large_frame_dev(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
-                           uint32_t f) {
+                           uint32_t f, uint32_t levels) {
     const uint32_t szfl = LG_SZ_ON | (kmode == CG_KMODE_PIPELINE ? LG_SZ_PIPE : 0u) |
                           (kmode == CG_KMODE_PIPELINE && P.zero_pass ? LG_SZ_ZPAD : 0u) |
                           (S.force_global ? LG_SZ_GLOBAL : 0u);
     int e;
     if ((e = cg_large_front(L, P, kmode, S, s, f, true, szfl)) != hipSuccess) return e;
     if (kmode == CG_KMODE_PIPELINE && (e = cg_large_decide(L, P, S, s, f, szfl)) != hipSuccess) return e;
-    if ((e = large_backend_dev(L, P, S, s, f, L.n_points)) != hipSuccess) return e;
+    if ((e = large_backend_dev(L, P, S, s, f, L.n_points, levels)) != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -2320,26 +1993,26 @@ void cg_large_graphs_free(LgGraphs* g) {
     delete g;
 }
 static std::vector<unsigned char> lg_graph_key(const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
-                                               uint32_t f) {
-    std::vector<unsigned char> k(sizeof(L) + sizeof(P) + sizeof(S) + 2 * sizeof(uint32_t));
+                                               uint32_t f, uint32_t levels) {
+    std::vector<unsigned char> k(sizeof(L) + sizeof(P) + sizeof(S) + 3 * sizeof(uint32_t));
     unsigned char* q = k.data();
     std::memcpy(q, &L, sizeof(L)); q += sizeof(L);
     std::memcpy(q, &P, sizeof(P)); q += sizeof(P);
     std::memcpy(q, &S, sizeof(S)); q += sizeof(S);
-    const uint32_t t[2] = {(uint32_t)kmode, f};
+    const uint32_t t[3] = {(uint32_t)kmode, f, levels};
     std::memcpy(q, t, sizeof(t));
     return k;
 }
 static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
-                             hipStream_t s, uint32_t f) {
-    std::vector<unsigned char> key = lg_graph_key(L, P, kmode, S, f);
+                             hipStream_t s, uint32_t f, uint32_t levels) {
+    std::vector<unsigned char> key = lg_graph_key(L, P, kmode, S, f, levels);
     for (auto& x : g->e)
         if (x.key == key) return hipGraphLaunch(x.exec, s);
-    if (g->e.size() >= LG_GRAPHS) return large_frame_dev(L, P, kmode, S, s, f);
+    if (g->e.size() >= LG_GRAPHS) return large_frame_dev(L, P, kmode, S, s, f, levels);
     hipError_t e;
     if (!g->cap && (e = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return e;
     if ((e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
-    const int rc = large_frame_dev(L, P, kmode, S, g->cap, f);
+    const int rc = large_frame_dev(L, P, kmode, S, g->cap, f, levels);
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(g->cap, &graph);
     if (rc != hipSuccess) {
@@ -2365,14 +2038,22 @@ static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& 
 // stream order keeps every set's reads before its next writes (frame f + 2's front follows
 // frame f's backend).
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, const LgScratch* S2,
-                 LgGraphs** graphs) {
+                 LgGraphs** graphs, uint32_t pcl_hint) {
     const uint32_t N = L.n_points;
     hipError_t e;
     S.pidx_base = 0;
     if (kmode != CG_KMODE_GROUND && P.voxel_order == CG_VOXEL_ORDER_PCL && N > 0 && N <= LG_DEV_MAX_POINTS) {
         if (graphs && !*graphs) *graphs = new LgGraphs();
+        // levels for the previous frame's index_vector (the hint) with one level to spare, or
+        // for N before any frame has run
+#ifdef LG_NO_HINT   // (variant builds: levels for N)
+        pcl_hint = 0;
+#endif
+        const uint32_t n_lv = pcl_hint ? std::min<uint32_t>(N, 2 * (pcl_hint - 1)) : N;
+        const uint32_t levels = lg_levels_for(n_lv, S.pcl_levels_cap);
         for (uint32_t f = 0; f < L.n_frames; f++) {
-            const int rc = graphs ? large_frame_graph(*graphs, L, P, kmode, S, s, f) : large_frame_dev(L, P, kmode, S, s, f);
+            const int rc = graphs ? large_frame_graph(*graphs, L, P, kmode, S, s, f, levels)
+                                  : large_frame_dev(L, P, kmode, S, s, f, levels);
             if (rc != hipSuccess) return rc;
         }
         return hipSuccess;
@@ -2416,12 +2097,7 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
 // ------------------------------------------------------------------------------------------
 // Scratch layout (one frame at a time).
 namespace {
-// the persistent sort's capacities: partitioned ranges are longer than LG_PCL_CUT and disjoint
-// within a level, so a level holds at most N / 4096 of them and N / 512 + that many tiles; the
-// bounds allow ~30 levels (the depth budget of a degenerate frame ends earlier)
-uint64_t lg_ps_rcap(uint64_t N) { return N / 64 + 4096; }
-uint64_t lg_ps_qcap(uint64_t N) { return N / 4 + 65536; }
-uint64_t lg_ps_tcap(uint64_t N) { return N / 8 + 32768; }
+
 template <class F>
 uint64_t lg_walk(uint32_t n, F place) {
     const uint64_t N = std::max<uint32_t>(n, 1), nch = (N + LG_CHUNK - 1) / LG_CHUNK, nt = tiles_of(N);
@@ -2444,10 +2120,6 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(29, take(nch * LG_CS_WORDS * 4));
     place(30, take((LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP) * 4));   // PCL sort range lists
     place(31, take((2 + (N + PQ_T - 1) / PQ_T + PQ_MAXR + 2) * 8));   // their look-back words
-    place(32, take(PH_WORDS * 4));                                     // the persistent sort: header,
-    place(33, take(lg_ps_rcap(N) * LG_PS_RW * 4));                     //   ranges,
-    place(34, take(lg_ps_qcap(N) * 8));                                //   work queue,
-    place(35, take(lg_ps_tcap(N) * 8));                                //   look-back words
     return off;
 }
 }  // namespace
@@ -2476,10 +2148,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 29: S.cstat = (uint32_t*)p; break;
             case 30: S.pq = (uint32_t*)p; S.pq_cap = LG_PQ_CAP; break;
             case 31: S.pqst = (uint64_t*)p; break;
-            case 32: S.ps_hdr = (uint32_t*)p; break;
-            case 33: S.ps_rd = (uint32_t*)p; S.ps_rcap = (uint32_t)lg_ps_rcap(std::max<uint32_t>(n, 1)); break;
-            case 34: S.ps_q = (uint64_t*)p; S.ps_qcap = (uint32_t)lg_ps_qcap(std::max<uint32_t>(n, 1)); break;
-            case 35: S.ps_st = (uint64_t*)p; S.ps_tcap = (uint32_t)lg_ps_tcap(std::max<uint32_t>(n, 1)); break;
+
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
     });

@@ -39,9 +39,6 @@ extern "C" {
                                         std::sort may order equal-size clusters differently */
 #define CG_F_VOXEL_POINT_ORDER 0x8u  /* voxel sums ran in ascending point order, not in PCL's
                                         std::sort order (cg_set_voxel_order, the halo form) */
-#define CG_F_DEVICE_ERROR      0x80u /* a bounded wait inside a persistent launch of the large-frame
-                                        path gave up (other work held the GPU for 200 ms): the
-                                        frame's results are invalid; run it again */
 
 /* ---- parameters --------------------------------------------------------------------- */
 /* Field names are the YAML keys, misspellings kept (config/ *.yaml). */
