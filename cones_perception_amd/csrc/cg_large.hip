@@ -980,7 +980,12 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 #define LG_PQ_CAP ((2u << LG_PQ_LEVELS_MAX) + 64)   // entries per list: a level pushes <= 2 per range
 struct PclCompactFlag {   // finite points (non-finite keys carry idx 0xffffffff)
     const uint64_t* key; uint32_t PB;
-    __device__ uint32_t operator()(uint32_t j) const { return (uint32_t)(key[j] >> PB) != 0xffffffffu ? 1u : 0u; }
+    const uint32_t* meta;   // (the device-sized path: a passthrough frame lists nothing, so its
+                            // points keep lg_voxel_keys' frame-index order: PCL does not sort them)
+    __device__ uint32_t operator()(uint32_t j) const {
+        if (meta && meta[LG_PASS]) return 0u;
+        return (uint32_t)(key[j] >> PB) != 0xffffffffu ? 1u : 0u;
+    }
 };
 struct PclCompactEmit {
     const uint64_t* key; const uint32_t* val; uint64_t* E; uint32_t PB;
@@ -1832,7 +1837,7 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
         buf = PB ? radix_sort(S, Mtot, PB, s) : 0;   // unsorted tiles: frame-index order first
         uint64_t* kb[2] = {S.key0, S.key1};
         uint32_t* vb2[2] = {S.val0, S.val1};
-        scan_emit(S, Mtot, -1, PclCompactFlag{kb[buf], PB}, PclCompactEmit{kb[buf], vb2[buf], kb[buf ^ 1], PB},
+        scan_emit(S, Mtot, -1, PclCompactFlag{kb[buf], PB, nullptr}, PclCompactEmit{kb[buf], vb2[buf], kb[buf ^ 1], PB},
                   LG_PCL_N, s);
         // the levels an even split needs until every range fits a leaf, three more for uneven
         // median-of-three cuts; levels with no range to cut return at once; then the leaves
@@ -1917,7 +1922,7 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     uint32_t* vb2[2] = {S.val0, S.val1};
     // index_vector (finite points in frame-index order) as (idx, slot) records, then std::sort's
     // permutation of it: levels for the frame's N (levels with no range return at once)
-    scan_emit(S, nmax, LG_MTOT, PclCompactFlag{kb[0], 0u}, PclCompactEmit{kb[0], vb2[0], kb[1], 0u}, LG_PCL_N, s);
+    scan_emit(S, nmax, LG_MTOT, PclCompactFlag{kb[0], 0u, S.meta}, PclCompactEmit{kb[0], vb2[0], kb[1], 0u}, LG_PCL_N, s);
     const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
     hipLaunchKernelGGL(lg_pq_split, dim3(tb), dim3(CG_BLOCK), 0, s, S, kb[1], 0u);
     for (uint32_t lv = 0; lv < levels; lv++) {

@@ -82,6 +82,22 @@ def test_forced_route_matches_oracle(params, route, frame):
     assert_same_detection(got, ref, f"route {route}")
 
 
+@pytest.mark.parametrize("route", [0, 2])
+def test_large_passthrough_frame(route):
+    """PCL's overflow guard on a large frame (points 1 km up; the distance filter opened so they
+    and the far wall reach the voxel grid): the voxel cloud is the detector input in point order,
+    unsorted, through the device-sized backend (route 0) and the host-sized one (route 2)."""
+    params = cp.load_params("simulation", {"distance_treshold_max": 1e5})
+    raw = cp.synth_frames(1, first_frame=4, rings=128, cols=1024, clutter=40, cones_per_row=10)
+    pts = raw[0].view(np.float32).reshape(-1, 4)
+    pts[5::20011, 2] = 1000.0
+    msg = cp.frame_cloud(raw[0])
+    got = cp.ConePipeline(params).debug_route(route).cloud_handler(msg)
+    ref, hdr = O.run(params, msg, O.MODE_PIPELINE)
+    assert got.flags & cp.CG_F_VOXEL_PASSTHROUGH and int(hdr[2]) > 4096
+    assert_same_detection(got, ref, f"passthrough route {route}")
+
+
 @pytest.mark.parametrize("route", [1, 2])
 def test_forced_route_dense_frame(params, route):
     msg = _frame(64, 1024, frame=2, clutter=40, cpr=10)
