@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -106,6 +107,7 @@ struct cg_handle {
     CgLaunch last_batch{};
     int batch_kmode = 0;
     bool batch_valid = false;
+    uint32_t pack_seq = 0;   // the last split launch's done word (CG_PACK_DONE)
     uint32_t last_k = 0;
     uint32_t* d_seckeys = nullptr;   // 18 words per frame inside d_hdr (not owned)
     RcBox* d_boxes = nullptr;
@@ -366,10 +368,31 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
 int ensure_pack(cg_handle* h) {
     if (!h->d_pack) {
         HIPCHK(hipMalloc(&h->d_pack, CG_PACK_WORDS * 4));
-        HIPCHK(hipHostMalloc((void**)&h->h_pack, CG_PACK_WORDS * 4, hipHostMallocDefault));
+        // coherent: the split kernel's done word follows its packed words there (CG_PACK_DONE)
+        HIPCHK(hipHostMalloc((void**)&h->h_pack, CG_PACK_WORDS * 4, hipHostMallocCoherent));
+        std::memset(h->h_pack, 0, CG_PACK_WORDS * 4);
         HIPCHK(hipHostGetDevicePointer((void**)&h->h_pack_dev, h->h_pack, 0));
     }
     return CG_OK;
+}
+
+#ifndef CG_PACK_SPIN_US
+#define CG_PACK_SPIN_US 2000
+#endif
+// true once *w == seq (acquire: the packed words before it are visible), false after
+// CG_PACK_SPIN_US microseconds
+bool wait_done_word(const uint32_t* w, uint32_t seq) {
+#ifdef CG_NO_DONE_WORD   // (variant builds: the stream wait only)
+    return false;
+#endif
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 1;; k++) {
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return true;
+        __builtin_ia32_pause();
+        if ((k & 255) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(CG_PACK_SPIN_US))
+            return false;
+    }
 }
 
 int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* out) {
@@ -385,12 +408,15 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
         L.hdr = h->d_hdr; L.vox = h->d_vox; L.lab = h->d_lab; L.offs = h->d_offs;
         L.idx = h->d_idx; L.cen = h->d_cen;
         const bool prepacked = h->packed && frame == 0;   // by the single-frame launch just run
+        const uint32_t done = prepacked ? h->pack_seq : 0u;
         h->packed = false;
         if (!prepacked) {
             HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
             HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
         }
-        HIPCHK(cg_stream_wait(s));
+        // the split launch's done word, polled in host memory (no runtime call); a frame still
+        // running after CG_PACK_SPIN_US (a slow backend, a staging timeout) waits on the stream
+        if (!(done && wait_done_word(h->h_pack + CG_PACK_DONE, done))) HIPCHK(cg_stream_wait(s));
         const uint32_t* p = h->h_pack;
         const uint32_t V = p[CG_HDR_V], C = p[CG_HDR_C];
         if (V <= CG_PACK_MAX && C <= CG_PACK_MAX && (C == 0 || p[CG_PACK_OFFS + C] <= CG_PACK_MAX)) {
@@ -523,6 +549,8 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         rc = ensure_pack(h);
         if (rc) return rc;
         L.pack = h->h_pack_dev;   // the kernel packs the results itself, into pinned host memory
+        h->pack_seq = h->pack_seq + 1 ? h->pack_seq + 1 : 1;
+        L.pack_seq = h->pack_seq;
     }
     h->packed = L.pack != nullptr;
     rc = launch_frames(h, L, kmode, h->stream);
@@ -1121,6 +1149,35 @@ int cg_halo_local(cg_handle* h, const cg_halo_plan* plan, const float* d_points,
     if (!rc) rc = halo_counts_ok(merged_counts, n_total);
     if (rc) return rc;
     if (n && (!d_points || !d_index)) return fail(CG_E_INVALID, "null survivors");
+    if (plan->slabs == 1) {
+        // one slab has no boundary: its backend is the frame's, run on every survivor (non-finite
+        // ones included, as cg_tile_backend) in frame-index voxel order, results in the handle
+        if (n != merged_counts[1] || n_pads != plan->n_pads)
+            return fail(CG_E_INVALID, "one slab takes all %u survivors and %u pads (got %u + %u)", merged_counts[1],
+                        plan->n_pads, n, n_pads);
+        HIPCHK(hipSetDevice(h->device));
+        rc = own_stream(h);
+        if (!rc) rc = ensure_large(h, n_total);
+        if (!rc) rc = ensure_batch(h, 1, n_total, false);
+        if (!rc) rc = use_stream(h, h->stream);
+        if (rc) return rc;
+        LgScratch S = route_scratch(h);
+        S.pidx_base = 0;
+        HIPCHK((hipError_t)cg_large_set_survivors(S, h->dp, d_points, d_index, n, merged_counts, h->stream));
+        CgLaunch L{};
+        L.n_frames = 1;
+        L.n_points = n_total;
+        fill_launch_outputs(h, L);
+        L.stamps = nullptr;
+        CgDevParams Pm = h->dp;
+        Pm.voxel_order = CG_VOXEL_ORDER_POINT;
+        HIPCHK((hipError_t)cg_large_backend(L, Pm, CG_KMODE_PIPELINE, S, h->stream, 0, n_total, merged_counts[0]));
+        h->last_frames = 1; h->last_points = n_total; h->last_mode = CG_MODE_PIPELINE; h->last_stream = h->stream;
+        h->last_single = false;
+        h->batch_valid = false;
+        *n_vox = 0;
+        return CG_OK;
+    }
     if ((uint64_t)n + n_pads > n_total || n > merged_counts[2] || (n_pads && n_pads != plan->n_pads))
         return fail(CG_E_INVALID, "%u survivors + %u pads do not fit the frame's counts", n, n_pads);
     if ((uint64_t)n + n_pads > capacity || (capacity && !d_rec))

@@ -95,6 +95,9 @@ struct CgLaunch {
     // is set and the call fails). Null: the buffer is complete before the launch.
     uint32_t* in_flags;
     uint32_t in_seq;
+    // split launch with pack: the last workgroup stores pack_seq to pack[CG_PACK_DONE] once
+    // every packed word is in host memory (the host returns on it; 0: no done word)
+    uint32_t pack_seq;
 };
 #define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
 #define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms
@@ -275,7 +278,8 @@ int cg_launch_recrop(const CgLaunch& L, const CgDevParams& P, bool pipeline, con
 #define CG_PACK_OFFS (CG_PACK_LAB + CG_PACK_MAX)
 #define CG_PACK_IDX (CG_PACK_OFFS + CG_PACK_MAX + 1)
 #define CG_PACK_CEN (CG_PACK_IDX + CG_PACK_MAX)
-#define CG_PACK_WORDS (CG_PACK_CEN + 2 * CG_PACK_MAX)
+#define CG_PACK_DONE (CG_PACK_CEN + 2 * CG_PACK_MAX)
+#define CG_PACK_WORDS (CG_PACK_DONE + 1)
 int cg_launch_pack(const CgLaunch& L, uint32_t f, uint32_t* out, hipStream_t s);
 // Colour classifier (cg_colornet.hip): one workgroup per cone cloud.
 int cg_launch_colornet(const float4* pts, const uint32_t* offs, uint32_t n_cones, const float* w, int32_t* colors,

@@ -126,6 +126,8 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
                         if (__builtin_amdgcn_s_memrealtime() - t0 > CG_STAGE_TIMEOUT) {
                             __hip_atomic_store(&L.in_flags[CG_STAGE_ERR], L.in_seq, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_SYSTEM);
+                            // in host memory before this chunk arrives (so before the done word)
+                            __builtin_amdgcn_s_waitcnt(0x0070);
                             break;
                         }
                     }
@@ -592,6 +594,14 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
             __threadfence();
             __syncthreads();
             pack_frame(L, f, L.pack);
+            if (L.pack_seq) {
+                // the done word after every packed word: the pack is coherent (uncached) host
+                // memory, so a lane's stores are in host memory once they complete (vmcnt(0))
+                __builtin_amdgcn_s_waitcnt(0x0070);
+                __syncthreads();
+                if (tid == 0)
+                    __hip_atomic_store(&L.pack[CG_PACK_DONE], L.pack_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
     if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());

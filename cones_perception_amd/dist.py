@@ -249,7 +249,7 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
     if halo:
         total, sizes, sp, si = _tile_front_decide_dev(engine, d_tile_ptr, first, n, n_total, device, point_step,
                                                       offsets)
-        det = run_halo_backend(engine, total, sp, si, n_total, device, dst, fetch=fetch)
+        det = run_halo_backend(engine, total, sp, si, n_total, device, dst, fetch=fetch, sizes=sizes)
         if det is not False:
             return det
         gp, gi = gather_survivors(sp, si, device, dst, sizes=sizes)
@@ -326,8 +326,9 @@ def _split_exchange(rows, dest, world_size, device):
     cnt = torch.bincount(dest[keep].to(torch.int64), minlength=world_size).to(cd)
     rcnt = torch.empty_like(cnt)
     dist.all_to_all_single(rcnt, cnt)
-    out = torch.empty((int(rcnt.sum().item()), rows.shape[1]), dtype=rows.dtype, device=cd)
-    dist.all_to_all_single(out, send, [int(x) for x in rcnt.tolist()], [int(x) for x in cnt.tolist()])
+    rc, sc = torch.stack([rcnt, cnt]).cpu().tolist()   # the one host read: both split lists
+    out = torch.empty((sum(rc), rows.shape[1]), dtype=rows.dtype, device=cd)
+    dist.all_to_all_single(out, send, rc, sc)
     return out.to(device)
 
 
@@ -342,11 +343,12 @@ def _all_gather_ints(vals, device):
 last_halo_stats = {}   # the rank's figures of its last run_halo_backend call (tests, bench)
 
 
-def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, fetch: bool = True):
+def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, fetch: bool = True, sizes=None):
     """The backend of a tiled frame from every rank's survivors (sp (ns, 4) float32, si (ns,)
     frame indices) and the merged counts: slab voxelisation and clustering, halo edges, merge on
     dst. Returns the Detection on dst, None elsewhere, or False when the frame has no voxel
-    lattice (PCL's overflow guard) and the caller must gather instead."""
+    lattice (PCL's overflow guard) and the caller must gather instead. `sizes`: every rank's
+    survivor count (the one-slab case gathers the survivors to dst)."""
     import ctypes as C
     from . import _abi
     lib, h = _abi.lib(), engine.handle
@@ -357,6 +359,21 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     if plan.passthrough:
         return False
     ns = int(sp.shape[0])
+    if plan.slabs == 1:
+        # one slab has no boundary: its backend is the frame's, so cg_halo_local takes every
+        # survivor (on dst) and writes the results itself, asynchronously; no records, no merge
+        last_halo_stats.clear()   # voxels: None on dst (on the device), 0 elsewhere
+        last_halo_stats.update(slabs=1, slab_w=int(plan.slab_w), band=int(plan.band), survivors=ns,
+                               voxels=None if rank == dst else 0, halo_sent=0, halo_received=0, pairs=0)
+        if _distributed():
+            sp, si = gather_survivors(sp, si, device, dst, sizes=sizes)
+            if rank != dst:
+                return None
+            ns = int(sp.shape[0])
+        nv = C.c_uint32(0)
+        _abi.check(lib.cg_halo_local(h, C.byref(plan), sp.data_ptr(), si.data_ptr(), ns, plan.n_pads,
+                                     total.ctypes.data, n_total, None, 0, C.byref(nv)))
+        return engine.fetch(0) if fetch else True
     slab = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
     _abi.check(lib.cg_halo_owner(h, C.byref(plan), sp.data_ptr(), ns, slab.data_ptr()))
     slab = slab[:ns]

@@ -254,7 +254,13 @@ int cg_tile_backend_own(cg_handle* h, uint32_t n_total, void* hip_stream);
  *      n_pairs when it exceeds capacity;
  *   e. every slab's records and pairs go to one rank: cg_halo_merge orders the voxels, unites
  *      the components and writes the clusters, results as cg_tile_backend's.
- * Results are bit-identical to the single-GPU call on the whole frame. */
+ * One slab (plan->slabs == 1: one rank, or a lattice narrower than two bands) has no boundary:
+ * cg_halo_local then takes every survivor of the frame (n = merged_counts[1], non-finite ones
+ * included, n_pads = plan->n_pads; d_rec and capacity unused) and writes the frame's results in
+ * the handle itself, asynchronously on the handle's stream, with *n_vox = 0; steps b, d and e
+ * are skipped.
+ * Results are bit-identical to the single-GPU call on the whole frame in frame-index voxel
+ * order (cg_set_voxel_order CG_VOXEL_ORDER_POINT). */
 #define CG_HALO_REC_WORDS 8
 typedef struct cg_halo_plan {
     uint32_t passthrough;   /* the voxel grid's overflow guard hit (no lattice) */
