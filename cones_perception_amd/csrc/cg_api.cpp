@@ -286,7 +286,7 @@ int ensure_large(cg_handle* h, uint32_t n) {
     h->lg.hmeta = h->h_meta;
     if (!h->h_hint) {
         HIPCHK(hipHostMalloc((void**)&h->h_hint, 64, hipHostMallocCoherent));
-        *h->h_hint = 0;
+        std::memset(h->h_hint, 0, 64);
     }
     HIPCHK(hipHostGetDevicePointer((void**)&h->lg.hint, h->h_hint, 0));
     h->large_points = n;
@@ -360,8 +360,10 @@ int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
         return CG_OK;
     }
     // (the hint is whatever the last finished frame wrote: no synchronisation)
-    const uint32_t hint = h->h_hint ? __atomic_load_n(h->h_hint, __ATOMIC_RELAXED) : 0u;
-    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, nullptr, &h->lg_graphs, hint));
+    uint32_t hint[LG_HINT_WORDS] = {};
+    for (int k = 0; h->h_hint && k < LG_HINT_WORDS; k++) hint[k] = __atomic_load_n(h->h_hint + k, __ATOMIC_RELAXED);
+    HIPCHK((hipError_t)cg_run_large(L, h->dp, kmode, route_scratch(h), s, nullptr, &h->lg_graphs,
+                                    h->h_hint ? hint : nullptr));
     return CG_OK;
 }
 

@@ -190,8 +190,8 @@ struct LgScratch {
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
     uint32_t* cstart;         // dense neighbour grid: per-cell start in ord (LG_DCELLS_MAX + 2)
     uint32_t* hmeta;          // pinned host copy of the meta words (the one round trip per frame)
-    uint32_t* hint;           // pinned host word (device address), or null: 1 + the last device-sized
-                              // frame's index_vector length, the partition levels' hint for the next
+    uint32_t* hint;           // pinned host words (device address), or null: the last frames' sizes,
+                              // which size the next device-sized frame's launches (LG_HINT_*)
     uint32_t* cstat;          // per-chunk statistics [chunk][LG_CS_WORDS], reduced into meta by
                               // one workgroup (same-address atomics from every chunk serialise)
     uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
@@ -214,10 +214,19 @@ void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
 #define LG_DEV_MAX_POINTS (1u << 22)
 struct LgGraphs;   // cg_large.hip: the handle's captured per-frame graphs
 void cg_large_graphs_free(LgGraphs* g);
-// pcl_hint: 1 + the previous frame's index_vector length (0: none), which sizes the partition
-// levels of the device-sized path; a frame that needs more finishes its longer ranges in HBM.
+// The hint words (LgScratch::hint, pinned; the host reads them without synchronising, so they
+// may come from different frames: every combination gives exact results, only launch counts vary):
+enum {
+    LG_HINT_N = 0,        // 1 + index_vector length of the last frame that ran the partition levels
+    LG_HINT_LEVELS = 1,   // partition levels that had a range to cut in that frame
+    LG_HINT_SMALL = 2,    // 1 + (the last frame's detector input fit the LDS backend)
+    LG_HINT_WORDS = 3
+};
+// hint: the LG_HINT_WORDS words as read (null: none). They size the device-sized path's partition
+// levels (a frame that needs more finishes its longer ranges in HBM) and leave the LDS backend's
+// launch out after a large frame (a small frame then takes the global backend).
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
-                 const LgScratch* S2 = nullptr, LgGraphs** graphs = nullptr, uint32_t pcl_hint = 0);
+                 const LgScratch* S2 = nullptr, LgGraphs** graphs = nullptr, const uint32_t* hint = nullptr);
 // The phases of cg_run_large for one frame f (also the tiles of cg_tile_*):
 //   front: meta init + pass 1 (ground-only mode: the whole ground output);
 //   decide: thresholds from meta, pass 2, candidates -> survivors (pipeline mode);

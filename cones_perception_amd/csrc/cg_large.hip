@@ -173,6 +173,7 @@ __device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32
             m[LG_MALL] = Mt;
             m[LG_MTOT] = small ? 0u : Mt;
             m[LG_SMALL] = small ? 1u : 0u;
+            if (S.hint) S.hint[LG_HINT_SMALL] = Mt <= CG_MMAX ? 2u : 1u;   // (forced global or not)
         }
     }
     if ((what & 1u) && w <= CG_NUM_BINS) m[LG_SECKEY + w] = a;
@@ -1096,6 +1097,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
         // frame's N): the tiles number at most ceil(n / PQ_T) + one per range
         const uint32_t n = S.meta[LG_PCL_N];
         const uint32_t nr0 = level == 0 ? (n > LG_PCL_CUT ? 1u : 0u) : min(S.pq[level % 3u], (uint32_t)PQ_MAXR);
+        // the levels this frame cuts, for the next frame's launches (LG_HINT_LEVELS)
+        if (blockIdx.x == 0 && tid == 0 && S.hint && n && (level == 0 || nr0)) S.hint[LG_HINT_LEVELS] = nr0 ? level + 1u : 0u;
         if (blockIdx.x >= (n + PQ_T - 1) / PQ_T + nr0) {
             if (blockIdx.x == 0 && tid == 0) S.ca[0] = 0;   // no tile: lg_pq_swap reads the count
             return;
@@ -1665,7 +1668,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
     if (K == CG_K_FROM_META) K = S.meta[LG_KHDR];
     if (buf < 0) {   // (device-sized: the next frame's partition levels are sized from this one's)
         buf = (int)(lg_rs_passes(VB, sort_hi, S.meta[LG_SORT_LIM]) & 1u);
-        if (blockIdx.x == 0 && threadIdx.x == 0 && S.hint) *S.hint = S.meta[LG_PCL_N] + 1u;
+        // (a frame with no index_vector here, one the LDS backend took or a passthrough, keeps
+        // the hint of the last frame that had one)
+        const uint32_t npcl = S.meta[LG_PCL_N];
+        if (blockIdx.x == 0 && threadIdx.x == 0 && S.hint && npcl) S.hint[LG_HINT_N] = npcl + 1u;
     }
     if (blockIdx.x < cb) {
         lg_csr_one(L, P, S, f, VB, buf, Mtot, K, blockIdx.x);
@@ -1912,7 +1918,7 @@ static uint32_t lg_levels_for(uint32_t n, uint32_t cap) {
     return levels;
 }
 static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f,
-                             uint32_t N, uint32_t levels) {
+                             uint32_t N, uint32_t levels, bool small) {
     CgLaunch Lh = L;
     Lh.n_points = N;
     const uint32_t nmax = std::max<uint32_t>(N, 1);
@@ -1962,20 +1968,21 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     const uint32_t cb = blocks_of((uint64_t)nmax + 1);
     hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, -1, CG_K_FROM_META,
                        CG_K_FROM_META, cb, hi);
-    return cg_launch_lg_back_small(Lh, P, S, f, CG_K_FROM_META, 0u, s);
+    // (left out after a large frame: the fold then hands every frame to the launches above)
+    return small ? cg_launch_lg_back_small(Lh, P, S, f, CG_K_FROM_META, 0u, s) : hipGetLastError();
 }
 
 // One frame through the device-sized path: front, decisions (their fold sizes the backend),
 // backend. Pipeline and detect modes.
 static int large_frame_dev(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
-                           uint32_t f, uint32_t levels) {
+                           uint32_t f, uint32_t levels, bool small) {
     const uint32_t szfl = LG_SZ_ON | (kmode == CG_KMODE_PIPELINE ? LG_SZ_PIPE : 0u) |
                           (kmode == CG_KMODE_PIPELINE && P.zero_pass ? LG_SZ_ZPAD : 0u) |
-                          (S.force_global ? LG_SZ_GLOBAL : 0u);
+                          (S.force_global || !small ? LG_SZ_GLOBAL : 0u);
     int e;
     if ((e = cg_large_front(L, P, kmode, S, s, f, true, szfl)) != hipSuccess) return e;
     if (kmode == CG_KMODE_PIPELINE && (e = cg_large_decide(L, P, S, s, f, szfl)) != hipSuccess) return e;
-    if ((e = large_backend_dev(L, P, S, s, f, L.n_points, levels)) != hipSuccess) return e;
+    if ((e = large_backend_dev(L, P, S, s, f, L.n_points, levels, small)) != hipSuccess) return e;
     return hipGetLastError();
 }
 
@@ -1998,26 +2005,26 @@ void cg_large_graphs_free(LgGraphs* g) {
     delete g;
 }
 static std::vector<unsigned char> lg_graph_key(const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
-                                               uint32_t f, uint32_t levels) {
-    std::vector<unsigned char> k(sizeof(L) + sizeof(P) + sizeof(S) + 3 * sizeof(uint32_t));
+                                               uint32_t f, uint32_t levels, bool small) {
+    std::vector<unsigned char> k(sizeof(L) + sizeof(P) + sizeof(S) + 4 * sizeof(uint32_t));
     unsigned char* q = k.data();
     std::memcpy(q, &L, sizeof(L)); q += sizeof(L);
     std::memcpy(q, &P, sizeof(P)); q += sizeof(P);
     std::memcpy(q, &S, sizeof(S)); q += sizeof(S);
-    const uint32_t t[3] = {(uint32_t)kmode, f, levels};
+    const uint32_t t[4] = {(uint32_t)kmode, f, levels, small ? 1u : 0u};
     std::memcpy(q, t, sizeof(t));
     return k;
 }
 static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
-                             hipStream_t s, uint32_t f, uint32_t levels) {
-    std::vector<unsigned char> key = lg_graph_key(L, P, kmode, S, f, levels);
+                             hipStream_t s, uint32_t f, uint32_t levels, bool small) {
+    std::vector<unsigned char> key = lg_graph_key(L, P, kmode, S, f, levels, small);
     for (auto& x : g->e)
         if (x.key == key) return hipGraphLaunch(x.exec, s);
-    if (g->e.size() >= LG_GRAPHS) return large_frame_dev(L, P, kmode, S, s, f, levels);
+    if (g->e.size() >= LG_GRAPHS) return large_frame_dev(L, P, kmode, S, s, f, levels, small);
     hipError_t e;
     if (!g->cap && (e = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return e;
     if ((e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
-    const int rc = large_frame_dev(L, P, kmode, S, g->cap, f, levels);
+    const int rc = large_frame_dev(L, P, kmode, S, g->cap, f, levels, small);
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(g->cap, &graph);
     if (rc != hipSuccess) {
@@ -2043,22 +2050,30 @@ static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& 
 // stream order keeps every set's reads before its next writes (frame f + 2's front follows
 // frame f's backend).
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s, const LgScratch* S2,
-                 LgGraphs** graphs, uint32_t pcl_hint) {
+                 LgGraphs** graphs, const uint32_t* hint) {
     const uint32_t N = L.n_points;
     hipError_t e;
     S.pidx_base = 0;
     if (kmode != CG_KMODE_GROUND && P.voxel_order == CG_VOXEL_ORDER_PCL && N > 0 && N <= LG_DEV_MAX_POINTS) {
         if (graphs && !*graphs) *graphs = new LgGraphs();
-        // levels for the previous frame's index_vector (the hint) with one level to spare, or
-        // for N before any frame has run
-#ifdef LG_NO_HINT   // (variant builds: levels for N)
-        pcl_hint = 0;
+#ifdef LG_NO_HINT   // (variant builds: launches for N)
+        hint = nullptr;
 #endif
-        const uint32_t n_lv = pcl_hint ? std::min<uint32_t>(N, 2 * (pcl_hint - 1)) : N;
-        const uint32_t levels = lg_levels_for(n_lv, S.pcl_levels_cap);
+        uint32_t levels = lg_levels_for(N, S.pcl_levels_cap);   // before any frame has run
+        bool small = true;
+        if (hint && hint[LG_HINT_N]) {
+            // one level more than the last frame cut, and than an even split of its index_vector
+            // needs (a frame much larger than the last); at least one, so that a range longer than
+            // a leaf is always cut once and its halves queued as leaves
+            uint32_t even = 0;
+            while (((uint64_t)LG_PCL_CUT << even) < hint[LG_HINT_N] - 1) even++;
+            levels = std::min<uint32_t>(std::max(even, hint[LG_HINT_LEVELS]) + 1u, LG_PQ_LEVELS_MAX);
+            if (S.pcl_levels_cap) levels = std::min(levels, S.pcl_levels_cap);
+        }
+        if (hint && hint[LG_HINT_SMALL] == 1u) small = false;   // the last frame was a large one
         for (uint32_t f = 0; f < L.n_frames; f++) {
-            const int rc = graphs ? large_frame_graph(*graphs, L, P, kmode, S, s, f, levels)
-                                  : large_frame_dev(L, P, kmode, S, s, f, levels);
+            const int rc = graphs ? large_frame_graph(*graphs, L, P, kmode, S, s, f, levels, small)
+                                  : large_frame_dev(L, P, kmode, S, s, f, levels, small);
             if (rc != hipSuccess) return rc;
         }
         return hipSuccess;

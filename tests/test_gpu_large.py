@@ -193,3 +193,25 @@ def test_large_batch_pipelined_over_two_scratch_sets(params, mode):
         for f in range(raw.shape[0]):
             ref, _ = O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE if mode == "pipeline" else O.MODE_DETECT)
             assert_same_detection(eng.fetch(f), ref, f"pipelined batch {rep} frame {f}")
+
+
+def test_hint_sequence_small_large_medium(params):
+    """The device-sized path sizes each frame's launches from the previous frames' (the pinned
+    hint words): partition levels from the last index_vector and the levels it cut, and the LDS
+    backend's launch left out after a large frame. One handle runs frames whose sizes jump both
+    ways — a small frame after a large one takes the global backend, a large frame after a small
+    or medium one finishes its longer ranges in HBM — and every frame must stay bit-exact."""
+    seq = [_frame(128, 1024, frame=3),                          # small: the LDS backend
+           _frame(128, 8192, frame=0, clutter=60, cpr=12),      # C5: every partition level
+           _frame(128, 1024, frame=3),                          # small after large: global backend
+           _frame(128, 8192, frame=0, clutter=60, cpr=12),      # large after small
+           _frame(128, 2048, frame=6, clutter=20, cpr=8),       # medium
+           _frame(128, 8192, frame=1, clutter=60, cpr=12)]      # large after medium
+    pipe = cp.ConePipeline(params)
+    ms = []
+    for i, msg in enumerate(seq):
+        got = pipe.cloud_handler(msg)
+        ref, hdr = O.run(params, msg, O.MODE_PIPELINE)
+        ms.append(int(hdr[2]))
+        assert_same_detection(got, ref, f"sequence frame {i} (M {ms[-1]})")
+    assert ms[0] <= 1024 and ms[1] > 8 * 4096, ms
