@@ -136,45 +136,62 @@ __device__ __forceinline__ void lg_store_survivor_bits(LgScratch& S, uint32_t c,
 #define LG_SZ_ZPAD 2u     // the N - K PointXYZI() pads survive the filter (P.zero_pass)
 #define LG_SZ_GLOBAL 4u   // the global backend even when M fits the LDS one (diagnostics)
 #define LG_SZ_ON 0x80000000u   // (host side: cg_large_front / cg_large_decide fold the sizes)
-__device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32_t what, uint32_t N = 0,
-                                               uint32_t szfl = 0) {
-    __shared__ uint32_t part[16][LG_CS_WORDS];
+#define LG_WM_KEYS ((1u << (CG_NUM_BINS + 1)) - 1u)   // fold words: the sector keys,
+#define LG_WM_TOUCHED (1u << LG_CS_TOUCHED)            // the used bins,
+#define LG_WM_COUNTS ((1u << LG_CS_K) | (1u << LG_CS_MS) | (7u << LG_CS_BMIN) | (7u << LG_CS_BMAX) | (1u << LG_CS_NFIN))
+// The fold itself, called by every thread of the block: thread w < LG_CS_WORDS returns word w
+// folded over the nch chunks (words outside wmask: not loaded).
+__device__ __forceinline__ uint32_t lg_fold_core(const LgScratch& S, uint32_t nch, uint32_t wmask,
+                                                 uint32_t (*part)[LG_CS_WORDS]) {
     const uint32_t tid = threadIdx.x, w = tid & 31, q = tid >> 5;   // word, one of 16 chunk strides
     const bool mn = (w <= CG_NUM_BINS) || (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3);
     const bool mx = w >= LG_CS_BMAX && w < LG_CS_BMAX + 3;
     const bool orw = w == LG_CS_TOUCHED;
     uint32_t acc = mn ? 0xffffffffu : 0u;
     auto fold = [&](uint32_t a, uint32_t v) { return mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v; };
-    uint32_t c = q;
-    for (; c + 48 < nch; c += 64) {   // four independent loads per trip
-        const uint32_t v0 = S.cstat[(uint64_t)c * LG_CS_WORDS + w], v1 = S.cstat[(uint64_t)(c + 16) * LG_CS_WORDS + w],
-                       v2 = S.cstat[(uint64_t)(c + 32) * LG_CS_WORDS + w], v3 = S.cstat[(uint64_t)(c + 48) * LG_CS_WORDS + w];
-        acc = fold(fold(acc, v0), fold(v1, fold(v2, v3)));
+    if ((wmask >> w) & 1u) {
+        uint32_t c = q;
+        for (; c + 48 < nch; c += 64) {   // four independent loads per trip
+            const uint32_t v0 = S.cstat[(uint64_t)c * LG_CS_WORDS + w], v1 = S.cstat[(uint64_t)(c + 16) * LG_CS_WORDS + w],
+                           v2 = S.cstat[(uint64_t)(c + 32) * LG_CS_WORDS + w], v3 = S.cstat[(uint64_t)(c + 48) * LG_CS_WORDS + w];
+            acc = fold(fold(acc, v0), fold(v1, fold(v2, v3)));
+        }
+        for (; c < nch; c += 16) acc = fold(acc, S.cstat[(uint64_t)c * LG_CS_WORDS + w]);
     }
-    for (; c < nch; c += 16) acc = fold(acc, S.cstat[(uint64_t)c * LG_CS_WORDS + w]);
     part[q][w] = acc;
     __syncthreads();
-    if (tid >= LG_CS_WORDS) return;
-    uint32_t a = part[0][w];
-    for (int k = 1; k < 16; k++) {
-        const uint32_t v = part[k][w];
-        a = mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v;
+    uint32_t a = 0;
+    if (tid < LG_CS_WORDS) {
+        a = part[0][w];
+        for (int k = 1; k < 16; k++) a = fold(a, part[k][w]);
     }
+    return a;
+}
+// The detector input's size and backend from K (ground kept count) and Ms (survivors), into the
+// meta words m (one thread)
+__device__ __forceinline__ void lg_size_fold(const LgScratch& S, uint32_t* m, uint32_t k, uint32_t ms, uint32_t N,
+                                             uint32_t szfl, bool hint = true) {
+    const uint32_t K = (szfl & LG_SZ_PIPE) ? k : N;
+    const uint32_t npad = (szfl & LG_SZ_ZPAD) ? N - K : 0u;
+    const uint32_t Mt = ms + npad;
+    const bool small = Mt <= CG_MMAX && !(szfl & LG_SZ_GLOBAL);
+    m[LG_KHDR] = K;
+    m[LG_NPAD] = npad;
+    m[LG_MALL] = Mt;
+    m[LG_MTOT] = small ? 0u : Mt;
+    m[LG_SMALL] = small ? 1u : 0u;
+    if (hint && S.hint) S.hint[LG_HINT_SMALL] = Mt <= CG_MMAX ? 2u : 1u;   // (forced global or not)
+}
+__device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32_t what, uint32_t N = 0,
+                                               uint32_t szfl = 0) {
+    __shared__ uint32_t part[16][LG_CS_WORDS];
+    const uint32_t tid = threadIdx.x, w = tid & 31;
+    const uint32_t a = lg_fold_core(S, nch, 0xffffffffu, part);
+    if (tid >= LG_CS_WORDS) return;
     uint32_t* m = S.meta;
     if (what & LG_FOLD_SIZE) {   // (all 32 lanes of wave 0 are here)
         const uint32_t k = (uint32_t)__shfl((int)a, LG_CS_K, 64), ms = (uint32_t)__shfl((int)a, LG_CS_MS, 64);
-        if (tid == 0) {
-            const uint32_t K = (szfl & LG_SZ_PIPE) ? k : N;
-            const uint32_t npad = (szfl & LG_SZ_ZPAD) ? N - K : 0u;
-            const uint32_t Mt = ms + npad;
-            const bool small = Mt <= CG_MMAX && !(szfl & LG_SZ_GLOBAL);
-            m[LG_KHDR] = K;
-            m[LG_NPAD] = npad;
-            m[LG_MALL] = Mt;
-            m[LG_MTOT] = small ? 0u : Mt;
-            m[LG_SMALL] = small ? 1u : 0u;
-            if (S.hint) S.hint[LG_HINT_SMALL] = Mt <= CG_MMAX ? 2u : 1u;   // (forced global or not)
-        }
+        if (tid == 0) lg_size_fold(S, m, k, ms, N, szfl);
     }
     if ((what & 1u) && w <= CG_NUM_BINS) m[LG_SECKEY + w] = a;
     if ((what & 1u) && w == LG_CS_TOUCHED) m[LG_TOUCHED] = a;
@@ -247,20 +264,38 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
 }
 
 // Decide: thresholds, pass 2 per chunk, survivors = ground-kept & filter bits (from lg_front).
+// fold_nch > 0 (the device-sized path): every workgroup folds the front's nch chunk keys itself
+// (no lg_reduce_chunks launch between); workgroup 0 stores them in the meta words
 template <int LAYOUT, int KMODE>
-__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
+                                                        uint32_t fold_nch) {
     constexpr int PPT = LG_CHUNK / CG_BLOCK;
     constexpr int NW = (PPT + 63) / 64;
     __shared__ float thr[CG_NUM_BINS + 1];
     __shared__ uint32_t tkey[CG_NUM_BINS + 1], band[2], kcount;
+    __shared__ uint32_t fk[CG_NUM_BINS + 2];
     const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id();
     const uint64_t base = (uint64_t)c * LG_CHUNK;
     const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
-    if (tid < 64) sector_thresholds(S.meta + LG_SECKEY, S.meta[LG_TOUCHED], P, thr, tkey, &band[0], &band[1]);
+    const uint32_t* keys = S.meta + LG_SECKEY;
+    uint32_t touched;
+    if (fold_nch) {
+        __shared__ uint32_t part[16][LG_CS_WORDS];
+        const uint32_t a = lg_fold_core(S, fold_nch, LG_WM_KEYS | LG_WM_TOUCHED, part);
+        if (tid <= CG_NUM_BINS + 1) fk[tid] = a;   // (LG_CS_KEYS = 0, LG_CS_TOUCHED = CG_NUM_BINS + 1)
+        if (c == 0 && tid <= CG_NUM_BINS) S.meta[LG_SECKEY + tid] = a;
+        if (c == 0 && tid == LG_CS_TOUCHED) S.meta[LG_TOUCHED] = a;
+        __syncthreads();
+        keys = fk;
+        touched = fk[LG_CS_TOUCHED];
+    } else {
+        touched = S.meta[LG_TOUCHED];
+    }
+    if (tid < 64) sector_thresholds(keys, touched, P, thr, tkey, &band[0], &band[1]);
     // the frame's sector keys to the caller's per-frame output (the pipeline's re-crop reads them)
     if (KMODE == CG_KMODE_PIPELINE && c == 0 && tid <= CG_NUM_BINS && L.seckeys)
-        L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = S.meta[LG_SECKEY + tid];
+        L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = keys[tid];
     if (tid == 0) kcount = 0;
     __syncthreads();
     const uint32_t qlo = band[0], qhi = band[1];
@@ -778,21 +813,51 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
 // Mtot = CG_K_FROM_META (the backend sized on the device): Mtot and npad from the meta words
 // (LG_MTOT, LG_NPAD; the grid sized for the frame's N); Mtot 0 (the LDS backend takes the frame)
 // leaves every later global-backend launch without work.
+// szfl (the device-sized path, LG_SZ_ON | flags): every workgroup first folds the decisions'
+// per-chunk counts and bounds itself (lg_fold_core; no lg_reduce_chunks launch before this one)
+// and sizes the detector input (lg_size_fold); workgroup 0 stores those meta words too.
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevParams P, uint32_t Mtot, uint32_t N,
                                                           uint32_t PB, uint32_t npad,
-                                                          uint32_t nfin_local = 0xffffffffu) {
+                                                          uint32_t nfin_local = 0xffffffffu, uint32_t szfl = 0u) {
     __shared__ uint32_t m[LG_META_WORDS];
-    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
+    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x, tid = threadIdx.x;
     const bool dev = Mtot == CG_K_FROM_META;
+    const uint32_t* in = S.meta;   // the counts and bounds words
+    if (szfl & LG_SZ_ON) {
+        __shared__ uint32_t part[16][LG_CS_WORDS];
+        const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
+        const uint32_t a = lg_fold_core(S, nch, LG_WM_COUNTS, part);
+        uint32_t word = 0xffffffffu;   // the meta word of fold word tid
+        if (tid == LG_CS_K && (szfl & LG_SZ_PIPE)) word = LG_K;
+        if (tid == LG_CS_MS) word = LG_MS;
+        if (tid == LG_CS_NFIN) word = LG_NFIN;
+        if (tid >= LG_CS_BMIN && tid < LG_CS_BMIN + 3) word = LG_BMIN + (tid - LG_CS_BMIN);
+        if (tid >= LG_CS_BMAX && tid < LG_CS_BMAX + 3) word = LG_BMAX + (tid - LG_CS_BMAX);
+        if (tid == LG_CS_K) m[LG_K] = a;   // (lg_size_fold reads it in pipeline mode only)
+        if (word != 0xffffffffu) {
+            m[word] = a;
+            if (blockIdx.x == 0) S.meta[word] = a;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            lg_size_fold(S, m, m[LG_K], m[LG_MS], N, szfl, blockIdx.x == 0);
+            if (blockIdx.x == 0)
+                for (uint32_t w : {(uint32_t)LG_KHDR, (uint32_t)LG_NPAD, (uint32_t)LG_MALL, (uint32_t)LG_MTOT,
+                                   (uint32_t)LG_SMALL})
+                    S.meta[w] = m[w];
+        }
+        __syncthreads();
+        in = m;
+    }
     if (dev) {
-        Mtot = S.meta[LG_MTOT];
-        npad = S.meta[LG_NPAD];
+        Mtot = in[LG_MTOT];
+        npad = in[LG_NPAD];
     }
     if (threadIdx.x == 0) {
-        lg_grid_setup(S.meta, m, P, npad, Mtot);
+        lg_grid_setup(in, m, P, npad, Mtot);
         if (dev && Mtot == 0) m[LG_NCELL] = 0;
         if (blockIdx.x == 0) {
-            lg_grid_setup(S.meta, S.meta, P, npad, Mtot);
+            lg_grid_setup(in, S.meta, P, npad, Mtot);
             if (nfin_local != 0xffffffffu) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = nfin_local;
             if (dev && Mtot == 0) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = S.meta[LG_NCELL] = 0;
         }
@@ -803,7 +868,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevPara
         for (uint32_t i = j; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
     }
     if (j >= Mtot) return;
-    const uint32_t Ms = S.meta[LG_MS];   // (m holds the grid words only)
+    const uint32_t Ms = in[LG_MS];
     const float4 p = lg_point(S, j, Ms);
     const uint64_t pidx = j < Ms ? S.surv_i[j] : (uint64_t)N + (j - Ms);
     // PB = 0 (survivors in frame-index order): a stable sort by idx alone keeps each voxel's
@@ -1734,19 +1799,22 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
         return hipGetLastError();
     }
     const uint32_t fi = init ? 1u : 0u;   // lg_front's workgroup 0 resets the meta words
+    // the device-sized path: lg_decide folds the chunks' keys, lg_voxel_keys their counts and
+    // bounds (no lg_reduce_chunks launches)
+    const bool dev = (szfl & LG_SZ_ON) != 0;
     const dim3 g(nch), b(CG_BLOCK);
 #define LG_FRONT_MODES(LAY)                                                                       \
     if (kmode == CG_KMODE_PIPELINE) {                                                             \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, fi);           \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
+        if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);            \
     } else if (kmode == CG_KMODE_DETECT) {                                                        \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f);                              \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u | ((szfl & LG_SZ_ON) ? LG_FOLD_SIZE : 0u), N, szfl); \
+        if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u, N, 0u);             \
     } else {                                                                                      \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
-        hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);            \
+        hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, 0u);        \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u, 0u, 0u);                      \
         hipLaunchKernelGGL(lg_ground_out<LAY>, g, b, 0, s, L, P, S, f);                           \
     }
@@ -1764,15 +1832,15 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
     if (nch == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
     const dim3 g(nch), b(CG_BLOCK);
+    const bool dev = (szfl & LG_SZ_ON) != 0;   // (the folds in lg_decide and lg_voxel_keys)
     if (xyzi16) {
-        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
         hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f);
     } else {
-        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
         hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f);
     }
-    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u | ((szfl & LG_SZ_ON) ? LG_FOLD_SIZE : 0u),
-                       L.n_points, szfl);
+    if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u, L.n_points, 0u);
     return hipGetLastError();
 }
 
@@ -1918,12 +1986,12 @@ static uint32_t lg_levels_for(uint32_t n, uint32_t cap) {
     return levels;
 }
 static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStream_t s, uint32_t f,
-                             uint32_t N, uint32_t levels, bool small) {
+                             uint32_t N, uint32_t levels, bool small, uint32_t szfl) {
     CgLaunch Lh = L;
     Lh.n_points = N;
     const uint32_t nmax = std::max<uint32_t>(N, 1);
     hipLaunchKernelGGL(lg_voxel_keys, dim3(blocks_of(nmax)), dim3(CG_BLOCK), 0, s, S, P, CG_K_FROM_META, N, 0u, 0u,
-                       0xffffffffu);
+                       0xffffffffu, szfl);
     uint64_t* kb[2] = {S.key0, S.key1};
     uint32_t* vb2[2] = {S.val0, S.val1};
     // index_vector (finite points in frame-index order) as (idx, slot) records, then std::sort's
@@ -1982,7 +2050,7 @@ static int large_frame_dev(const CgLaunch& L, const CgDevParams& P, int kmode, L
     int e;
     if ((e = cg_large_front(L, P, kmode, S, s, f, true, szfl)) != hipSuccess) return e;
     if (kmode == CG_KMODE_PIPELINE && (e = cg_large_decide(L, P, S, s, f, szfl)) != hipSuccess) return e;
-    if ((e = large_backend_dev(L, P, S, s, f, L.n_points, levels, small)) != hipSuccess) return e;
+    if ((e = large_backend_dev(L, P, S, s, f, L.n_points, levels, small, szfl)) != hipSuccess) return e;
     return hipGetLastError();
 }
 
