@@ -76,6 +76,7 @@ uint64_t cg_scratch_bytes(uint32_t n) {
 // a code below q(min T) is ground in every sector, one above q(max T) is kept in every sector.
 // Only points whose code equals a band code re-read x, y, z from HBM and recompute their
 // sector (tens of points per frame on flat ground: the code step is 1/64 m).
+template <bool SYS = false>
 __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32_t* out);
 //
 // SPLIT (single frames, cg_launch_split): pass 1 runs in one workgroup per 4,096-point chunk
@@ -593,10 +594,11 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         if (L.pack) {
             __threadfence();
             __syncthreads();
-            pack_frame(L, f, L.pack);
+            if (L.pack_seq) pack_frame<true>(L, f, L.pack);
+            else pack_frame(L, f, L.pack);
             if (L.pack_seq) {
-                // the done word after every packed word: the pack is coherent (uncached) host
-                // memory, so a lane's stores are in host memory once they complete (vmcnt(0))
+                // the done word after every packed word: system-scope stores are visible to the
+                // host once they complete (vmcnt(0) in every wave, then the barrier)
                 __builtin_amdgcn_s_waitcnt(0x0070);
                 __syncthreads();
                 if (tid == 0)
@@ -735,7 +737,15 @@ int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 // Self-test kernels: the device restatements, evaluated element-wise for host comparison.
 // Results of one frame packed for a single device-to-host copy (fetch_frame): the header, then
 // up to CG_PACK_MAX entries of each result array at fixed offsets (cg_internal.h CG_PACK_*).
+// SYS (the split launch's pack in host memory, followed by a done word): every word is a
+// system-scope store, complete (vmcnt) only once the host can see it; plain stores to host
+// memory were seen overtaken by the done word (the host read the previous frame's pack)
+template <bool SYS>
 __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32_t* out) {
+    auto put = [](uint32_t* q, uint32_t v) {
+        if constexpr (SYS) __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else *q = v;
+    };
     const uint32_t nt = blockDim.x;
     const uint32_t* hdr = L.hdr + (uint64_t)f * CG_HDR_WORDS;
     const uint32_t V = min(hdr[CG_HDR_V], (uint32_t)CG_PACK_MAX), C = min(hdr[CG_HDR_C], (uint32_t)CG_PACK_MAX);
@@ -745,18 +755,19 @@ __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32
     const int32_t* lab = L.lab + (uint64_t)f * L.cap;
     const int32_t* idx = L.idx + (uint64_t)f * L.cap;
     const float2* cen = L.cen + (uint64_t)f * L.cap;
-    for (uint32_t i = threadIdx.x; i < CG_HDR_WORDS; i += nt) out[i] = hdr[i];
+    for (uint32_t i = threadIdx.x; i < CG_HDR_WORDS; i += nt) put(out + i, hdr[i]);
     for (uint32_t i = threadIdx.x; i < V; i += nt) {
         const float4 p = vox[i];
         uint32_t* q = out + CG_PACK_VOX + 4 * i;
-        q[0] = __float_as_uint(p.x); q[1] = __float_as_uint(p.y); q[2] = __float_as_uint(p.z); q[3] = __float_as_uint(p.w);
-        out[CG_PACK_LAB + i] = (uint32_t)lab[i];
+        put(q, __float_as_uint(p.x)); put(q + 1, __float_as_uint(p.y));
+        put(q + 2, __float_as_uint(p.z)); put(q + 3, __float_as_uint(p.w));
+        put(out + CG_PACK_LAB + i, (uint32_t)lab[i]);
     }
-    for (uint32_t i = threadIdx.x; i <= C; i += nt) out[CG_PACK_OFFS + i] = (uint32_t)offs[i];
-    for (uint32_t i = threadIdx.x; i < nidx; i += nt) out[CG_PACK_IDX + i] = (uint32_t)idx[i];
+    for (uint32_t i = threadIdx.x; i <= C; i += nt) put(out + CG_PACK_OFFS + i, (uint32_t)offs[i]);
+    for (uint32_t i = threadIdx.x; i < nidx; i += nt) put(out + CG_PACK_IDX + i, (uint32_t)idx[i]);
     for (uint32_t i = threadIdx.x; i < C; i += nt) {
-        out[CG_PACK_CEN + 2 * i] = __float_as_uint(cen[i].x);
-        out[CG_PACK_CEN + 2 * i + 1] = __float_as_uint(cen[i].y);
+        put(out + CG_PACK_CEN + 2 * i, __float_as_uint(cen[i].x));
+        put(out + CG_PACK_CEN + 2 * i + 1, __float_as_uint(cen[i].y));
     }
 }
 __global__ __launch_bounds__(256) void cg_pack_results(CgLaunch L, uint32_t f, uint32_t* out) {
