@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--voxel-order", choices=["pcl", "point"], default="pcl",
                     help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
                          "every voxel bit as the reference) or ascending point order")
+    ap.add_argument("--route", type=int, default=0,
+                    help="diagnostic: cg_debug_route for the C3 engines (7: chunked batches)")
     ap.add_argument("--dry-run", action="store_true",
                     help="plumbing rehearsal without a GPU: launcher, gloo ranks, barrier + max-over-ranks "
                          "timing and the JSON line (value null); used by the CPU tests")
@@ -136,6 +138,9 @@ def main():
     # handle is 0, which the C-ABI reads as "use the handle's own stream"
     vorder = cp.CG_VOXEL_ORDER_PCL if args.voxel_order == "pcl" else cp.CG_VOXEL_ORDER_POINT
     engines = [cp.BatchEngine(params, device=local).set_voxel_order(vorder) for _ in range(S)]
+    if args.route:
+        for e_ in engines:
+            e_.debug_route(args.route)
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
     assert all(st.cuda_stream != 0 for st in streams)
     eng, stream = engines[0], streams[0]

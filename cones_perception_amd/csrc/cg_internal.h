@@ -98,6 +98,10 @@ struct CgLaunch {
     // split launch with pack: the last workgroup stores pack_seq to pack[CG_PACK_DONE] once
     // every packed word is in host memory (the host returns on it; 0: no done word)
     uint32_t pack_seq;
+    // split batch (cg_launch_split_batch): chunk workgroups per frame (0: a single split frame,
+    // one workgroup per chunk) and the words between frames' split state
+    uint32_t split_nch;
+    uint64_t split_stride;
 };
 #define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
 #define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms
@@ -121,6 +125,10 @@ enum {
 #define CG_SPLIT_WORDS (SP_SURV + 5 * CG_MAX_POINTS)
 #define CG_SPLIT_TIMEOUT 40000000ull   // s_memrealtime ticks (100 MHz): 400 ms
 int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
+// The split kernel over a batch: L.split_nch chunk workgroups per frame, frame f's state at
+// L.split + f * L.split_stride (initialised once by cg_launch_split_state_init).
+int cg_launch_split_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
+int cg_launch_split_state_init(uint32_t* sp, uint64_t stride, uint32_t n_frames, hipStream_t s);
 
 // Host wait for a stream's queued work. Default: hipStreamSynchronize. CG_SPIN_SYNC (a variant
 // build, tools/build_variant.sh): busy-poll hipStreamQuery on the calling thread, trading a

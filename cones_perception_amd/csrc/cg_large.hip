@@ -2127,6 +2127,10 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
 #ifdef LG_NO_HINT   // (variant builds: launches for N)
         hint = nullptr;
 #endif
+#ifdef LG_NO_HINT_WRITE   // (variant builds: the kernels write no hint words to host memory)
+        hint = nullptr;
+        S.hint = nullptr;
+#endif
         uint32_t levels = lg_levels_for(N, S.pcl_levels_cap);   // before any frame has run
         bool small = true;
         if (hint && hint[LG_HINT_N]) {
