@@ -78,7 +78,7 @@ def main():
                     help="voxel summation order (cg_set_voxel_order): PCL's std::sort permutation (default, "
                          "every voxel bit as the reference) or ascending point order")
     ap.add_argument("--route", type=int, default=0,
-                    help="diagnostic: cg_debug_route for the C3 engines (7: chunked batches)")
+                    help="diagnostic: cg_debug_route for the C3 engines")
     ap.add_argument("--dry-run", action="store_true",
                     help="plumbing rehearsal without a GPU: launcher, gloo ranks, barrier + max-over-ranks "
                          "timing and the JSON line (value null); used by the CPU tests")

@@ -74,8 +74,6 @@ struct cg_handle {
     // host results
     uint32_t h_hdr[CG_HDR_WORDS] = {};
     uint32_t* d_split = nullptr;     // split single-frame launch state (CG_SPLIT_WORDS)
-    uint32_t* d_bsplit = nullptr;    // split batch state (CG_SPLIT_WORDS per frame)
-    uint32_t bsplit_frames = 0;
     bool packed = false;             // the last single-frame launch left its results in d_pack
     uint32_t* d_pack = nullptr;      // fetch_frame: one frame's results packed (CG_PACK_WORDS)
     uint32_t* h_pack = nullptr;      // pinned copy of it; the results handed out point into it
@@ -339,35 +337,8 @@ unsigned long long* take_span(cg_handle* h) {
     return p;
 }
 
-// Split batch state for n frames (route 7): allocated and initialised once, then every frame's
-// last workgroup resets its own words.
-int ensure_bsplit(cg_handle* h, uint32_t n, hipStream_t s) {
-    if (n <= h->bsplit_frames && h->d_bsplit) return CG_OK;
-    if (h->d_bsplit) {
-        HIPCHK(hipDeviceSynchronize());   // (no launch may still use the old state)
-        (void)hipFree(h->d_bsplit);
-    }
-    h->d_bsplit = nullptr;
-    h->bsplit_frames = 0;
-    HIPCHK(hipMalloc(&h->d_bsplit, (size_t)n * CG_SPLIT_WORDS * 4));
-    HIPCHK((hipError_t)cg_launch_split_state_init(h->d_bsplit, CG_SPLIT_WORDS, n, s));
-    h->bsplit_frames = n;
-    return CG_OK;
-}
-
 int launch_frames(cg_handle* h, CgLaunch& L, int kmode, hipStream_t s) {
     const bool large = L.n_points > CG_MAX_POINTS || ((h->route == 1 || h->route == 2 || h->route == 5) && L.n_points > 0);
-    if (!large && !L.split && h->route == 7 && kmode != CG_KMODE_GROUND && L.n_points > 0) {
-        int rc = ensure_bsplit(h, L.n_frames, s);
-        if (rc) return rc;
-        L.split = h->d_bsplit;
-        L.split_stride = CG_SPLIT_WORDS;
-        L.split_nch = (L.n_points + CG_SPLIT_CHUNK - 1) / CG_SPLIT_CHUNK;
-        L.stamps = nullptr;   // (stamps are per workgroup)
-        HIPCHK((hipError_t)cg_launch_split_batch(L, h->dp, kmode, s));
-        L.split = nullptr;
-        return CG_OK;
-    }
     if (!large && L.split) {
         HIPCHK((hipError_t)cg_launch_split(L, h->dp, kmode, s));
         return CG_OK;
@@ -705,7 +676,6 @@ int cg_destroy(cg_handle* h) {
     if (h->d_pack) (void)hipFree(h->d_pack);
     if (h->h_pack) (void)hipHostFree(h->h_pack);
     if (h->d_split) (void)hipFree(h->d_split);
-    if (h->d_bsplit) (void)hipFree(h->d_bsplit);
     if (h->d_boxes) (void)hipFree(h->d_boxes);
     if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);
     if (h->d_rc_out) (void)hipFree(h->d_rc_out);
@@ -1369,7 +1339,7 @@ int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 7) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || route > 6) return fail(CG_E_INVALID, "bad route %d", route);
     h->route = route;
     return CG_OK;
 }

@@ -98,10 +98,6 @@ struct CgLaunch {
     // split launch with pack: the last workgroup stores pack_seq to pack[CG_PACK_DONE] once
     // every packed word is in host memory (the host returns on it; 0: no done word)
     uint32_t pack_seq;
-    // split batch (cg_launch_split_batch): chunk workgroups per frame (0: a single split frame,
-    // one workgroup per chunk) and the words between frames' split state
-    uint32_t split_nch;
-    uint64_t split_stride;
 };
 #define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
 #define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms
@@ -125,10 +121,6 @@ enum {
 #define CG_SPLIT_WORDS (SP_SURV + 5 * CG_MAX_POINTS)
 #define CG_SPLIT_TIMEOUT 40000000ull   // s_memrealtime ticks (100 MHz): 400 ms
 int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
-// The split kernel over a batch: L.split_nch chunk workgroups per frame, frame f's state at
-// L.split + f * L.split_stride (initialised once by cg_launch_split_state_init).
-int cg_launch_split_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
-int cg_launch_split_state_init(uint32_t* sp, uint64_t stride, uint32_t n_frames, hipStream_t s);
 
 // Host wait for a stream's queued work. Default: hipStreamSynchronize. CG_SPIN_SYNC (a variant
 // build, tools/build_variant.sh): busy-poll hipStreamQuery on the calling thread, trading a
@@ -198,8 +190,8 @@ struct LgScratch {
     uint32_t *par, *cnt, *lab, *uk, *ca, *ord, *droot, *dsz, *rank, *fin, *off, *rk;
     uint32_t* cstart;         // dense neighbour grid: per-cell start in ord (LG_DCELLS_MAX + 2)
     uint32_t* hmeta;          // pinned host copy of the meta words (the one round trip per frame)
-    uint32_t* hint;           // pinned host words (device address), or null: the last frames' sizes,
-                              // which size the next device-sized frame's launches (LG_HINT_*)
+    uint32_t* hint;           // pinned host word (device address), or null: whether the last frame
+                              // fit the LDS backend (LG_HINT_SMALL)
     uint32_t* cstat;          // per-chunk statistics [chunk][LG_CS_WORDS], reduced into meta by
                               // one workgroup (same-address atomics from every chunk serialise)
     uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
@@ -222,17 +214,14 @@ void cg_large_layout(uint8_t* base, uint32_t n_points, LgScratch& S);
 #define LG_DEV_MAX_POINTS (1u << 22)
 struct LgGraphs;   // cg_large.hip: the handle's captured per-frame graphs
 void cg_large_graphs_free(LgGraphs* g);
-// The hint words (LgScratch::hint, pinned; the host reads them without synchronising, so they
-// may come from different frames: every combination gives exact results, only launch counts vary):
+// The hint word (LgScratch::hint, pinned; the host reads it without synchronising, so it may
+// come from an earlier frame: either value gives exact results, only the launch count varies):
 enum {
-    LG_HINT_N = 0,        // 1 + index_vector length of the last frame that ran the partition levels
-    LG_HINT_LEVELS = 1,   // partition levels that had a range to cut in that frame
-    LG_HINT_SMALL = 2,    // 1 + (the last frame's detector input fit the LDS backend)
-    LG_HINT_WORDS = 3
+    LG_HINT_SMALL = 0,    // 1 + (the last frame's detector input fit the LDS backend)
+    LG_HINT_WORDS = 1
 };
-// hint: the LG_HINT_WORDS words as read (null: none). They size the device-sized path's partition
-// levels (a frame that needs more finishes its longer ranges in HBM) and leave the LDS backend's
-// launch out after a large frame (a small frame then takes the global backend).
+// hint: the LG_HINT_WORDS words as read (null: none). After a large frame the LDS backend's
+// launch is left out (a small frame then takes the global backend).
 int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S, hipStream_t s,
                  const LgScratch* S2 = nullptr, LgGraphs** graphs = nullptr, const uint32_t* hint = nullptr);
 // The phases of cg_run_large for one frame f (also the tiles of cg_tile_*):

@@ -76,7 +76,6 @@ uint64_t cg_scratch_bytes(uint32_t n) {
 // a code below q(min T) is ground in every sector, one above q(max T) is kept in every sector.
 // Only points whose code equals a band code re-read x, y, z from HBM and recompute their
 // sector (tens of points per frame on flat ground: the code step is 1/64 m).
-template <bool SYS = false>
 __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32_t* out);
 //
 // SPLIT (single frames, cg_launch_split): pass 1 runs in one workgroup per 4,096-point chunk
@@ -84,7 +83,7 @@ __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32
 // bits to HBM and merging its sector minima into the frame's keys with atomics; the last
 // workgroup to finish (release/acquire on a counter) continues with the frame's thresholds,
 // pass 2 and backend below, codes and bits read back from L2.
-template <int PPT, int LAYOUT, int KMODE, bool SPLIT = false, bool BATCH = false>
+template <int PPT, int LAYOUT, int KMODE, bool SPLIT = false>
 __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams& P) {
     constexpr int G = 8;                          // points per load group (double-buffered)
     constexpr int NW = (PPT + 63) / 64;
@@ -93,35 +92,13 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     constexpr bool FILTER = KMODE != CG_KMODE_GROUND;
     // a split launch's 16 workgroups take a CU each: LDS past half a CU says so to the compiler,
     // which then sizes registers for 2 waves per SIMD (no SGPR spill reaches scratch)
-    // (a split batch shares each CU between two workgroups, like the frame kernel)
-    constexpr size_t SMEM = SPLIT && !BATCH && SMEM_BYTES <= 81920 ? 81920 + 256 : SMEM_BYTES;
+    constexpr size_t SMEM = SPLIT && SMEM_BYTES <= 81920 ? 81920 + 256 : SMEM_BYTES;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
     FrontShared* fs = (FrontShared*)smem;
     BackLds* bl = (BackLds*)(smem + FRONT_BYTES);
     uint8_t* zq = (uint8_t*)bl;                   // z codes, [k/8][lane][k%8]
 
-    // split launches: the frame and chunk of this workgroup. A single frame (L.split_nch = 0)
-    // has one workgroup per chunk. A batch (L.split_nch chunks per frame) deals frames to XCDs:
-    // blocks b and b + 8 share an XCD under round-robin placement (speed only), so frame
-    // 8 q + (b mod 8) takes blocks 8 (q nch + c) + (b mod 8), c < nch: its chunks hand off
-    // through one XCD's L2, and frames complete in dispatch order
-    uint32_t f = SPLIT ? 0u : blockIdx.x, sc = 0, snch = 1;
-    if constexpr (SPLIT) {
-        if (L.split_nch) {
-            // (the division runs on the VALU: readfirstlane keeps f and everything addressed
-            // from it in SGPRs)
-            const uint32_t j = blockIdx.x >> 3, q = (uint32_t)__builtin_amdgcn_readfirstlane((int)(j / L.split_nch));
-            f = q * 8u + (blockIdx.x & 7u);
-            sc = j - q * L.split_nch;
-            snch = L.split_nch;
-            if (f >= L.n_frames) return;   // (the grid is padded to whole groups of 8 frames)
-        } else {
-            sc = blockIdx.x;
-            snch = gridDim.x;
-        }
-    }
-    uint32_t* const spw = SPLIT ? L.split + (uint64_t)f * L.split_stride : nullptr;
-    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint32_t f = SPLIT ? 0u : blockIdx.x, tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
     const uint32_t N = L.n_points;
     STAMP(0);
@@ -138,9 +115,9 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     if constexpr (SPLIT) {
         static_assert(PPT * CG_BLOCK == CG_MAX_POINTS, "split frames use the 64k tail");
         static_assert(CG_SPLIT_CHUNK == 8 * CG_BLOCK, "a chunk's codes are one uint2 and its bits one byte per lane");
-        const uint32_t c = sc, c0 = c * CG_SPLIT_CHUNK;
+        const uint32_t c = blockIdx.x, c0 = c * CG_SPLIT_CHUNK;
         const uint32_t Nc = N > c0 ? min((uint32_t)CG_SPLIT_CHUNK, N - c0) : 0u;
-        if (!BATCH && L.in_host) {   // the chunk over PCIe from pinned host memory into the device copy
+        if (L.in_host) {   // the chunk over PCIe from pinned host memory into the device copy
             if (L.in_flags) {   // the host publishes the chunk after the launch (run_single)
                 if (tid == 0) {
                     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -204,23 +181,23 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         // every cross-workgroup word is an atomic or an sc1 (device-coherent) access.
         if (GROUND) {
             touched = wave_or(touched);
-            if (l == 0 && touched) atomicOr(spw + SP_TOUCHED, touched);
+            if (l == 0 && touched) atomicOr(L.split + SP_TOUCHED, touched);
         }
         __syncthreads();   // the chunk's sector minima are final in LDS
         STAMP(29);
-        if (GROUND && tid <= CG_NUM_BINS) atomicMin(spw + SP_KEYS + tid, fs->sec_key[tid]);
+        if (GROUND && tid <= CG_NUM_BINS) atomicMin(L.split + SP_KEYS + tid, fs->sec_key[tid]);
         __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
         __syncthreads();
         if (tid == 0) {
-            __hip_atomic_fetch_add(spw + SP_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(L.split + SP_ARRIVE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // bounded: all chunk workgroups are running unless other work holds the CUs; past
             // the bound the frame is flagged and the host runs it again in one workgroup
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             uint32_t ok = 1;
-            while (ld_rlx(spw + SP_ARRIVE) < snch) {
+            while (ld_rlx(L.split + SP_ARRIVE) < gridDim.x) {
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > CG_SPLIT_TIMEOUT) {
-                    st_rlx(spw + SP_ERR, 1u);
+                    st_rlx(L.split + SP_ERR, 1u);
                     ok = 0;
                     break;
                 }
@@ -230,8 +207,8 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         __syncthreads();
         STAMP(30);
         if (fs->scal[S_LAST]) {
-            if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = ld_rlx(spw + SP_KEYS + tid);
-            if (tid == 0) fs->scal[S_TOUCHED] = GROUND ? ld_rlx(spw + SP_TOUCHED) : 0u;
+            if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = ld_rlx(L.split + SP_KEYS + tid);
+            if (tid == 0) fs->scal[S_TOUCHED] = GROUND ? ld_rlx(L.split + SP_TOUCHED) : 0u;
             __syncthreads();
             if (GROUND && tid < 64)
                 sector_thresholds(fs->sec_key, fs->scal[S_TOUCHED], P, fs->thr, fs->tkey, &fs->scal[S_TKMIN],
@@ -247,49 +224,43 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
                 for (int k = 0; k < 8; k++)
                     if ((uint32_t)k * CG_BLOCK + tid < Nc) kp.w[0] |= 1ull << k;
             }
-            // the lane's points to load (at most 8): kept filter survivors and ambiguous points;
-            // two rounds of four loads (registers for a split batch's two workgroups per CU)
+            // the lane's points to load (at most 8): kept filter survivors and ambiguous points
             const uint32_t todo = (uint32_t)((kp.w[0] & pm.w[0]) | am.w[0]);
-            float4* const sp_p = (float4*)(spw + SP_SURV);
-            uint32_t* const sp_i = spw + SP_SURV + 4 * CG_MAX_POINTS;
-            float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
-            uint32_t nf = 0, kamb = 0;
+            float4 pt[8];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if (h && !__builtin_amdgcn_ballot_w64((todo >> 4) != 0u)) break;   // (wave-uniform)
-                float4 pt[4];
+            for (int k = 0; k < 8; k++)
+                if ((todo >> k) & 1u) pt[k] = load_xyzi<LAYOUT>(fb, c0 + (uint32_t)k * CG_BLOCK + tid, L);
+            uint32_t sv = 0, kamb = 0;
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if ((todo >> (4 * h + q)) & 1u) pt[q] = load_xyzi<LAYOUT>(fb, c0 + (uint32_t)(4 * h + q) * CG_BLOCK + tid, L);
-                uint32_t sv = 0;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int k = 4 * h + q;
-                    if (!((todo >> k) & 1u)) continue;
-                    bool kept = true;
-                    if (GROUND && ((am.w[0] >> k) & 1ull)) {
-                        kept = pass2_exact(P, fs->tkey, pt[q].x, pt[q].y, pt[q].z);
-                        kamb += kept ? 1u : 0u;
-                    }
-                    if (kept && ((pm.w[0] >> k) & 1ull)) sv |= 1u << q;
+            for (int k = 0; k < 8; k++) {
+                if (!((todo >> k) & 1u)) continue;
+                bool kept = true;
+                if (GROUND && ((am.w[0] >> k) & 1ull)) {
+                    kept = pass2_exact(P, fs->tkey, pt[k].x, pt[k].y, pt[k].z);
+                    kamb += kept ? 1u : 0u;
                 }
-                const uint32_t ns = (uint32_t)__builtin_popcount(sv);
-                const uint32_t incl = wave_incl_scan(ns);
-                uint32_t wbase = 0;
-                if (l == 63 && incl) wbase = __hip_atomic_fetch_add(spw + SP_MS, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
-                uint32_t pos = wbase + incl - ns;
+                if (kept && ((pm.w[0] >> k) & 1ull)) sv |= 1u << k;
+            }
+            const uint32_t ns = (uint32_t)__builtin_popcount(sv);
+            const uint32_t incl = wave_incl_scan(ns);
+            uint32_t wbase = 0;
+            if (l == 63 && incl) wbase = __hip_atomic_fetch_add(L.split + SP_MS, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, 63);
+            uint32_t pos = wbase + incl - ns;
+            float4* const sp_p = (float4*)(L.split + SP_SURV);
+            uint32_t* const sp_i = L.split + SP_SURV + 4 * CG_MAX_POINTS;
+            float bmn[3] = {INFINITY, INFINITY, INFINITY}, bmx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t nf = 0;
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (!((sv >> q) & 1u)) continue;
-                    st_f4(&sp_p[pos], pt[q]);
-                    st_rlx(&sp_i[pos], c0 + (uint32_t)(4 * h + q) * CG_BLOCK + tid);
-                    pos++;
-                    if (isfinite(pt[q].x) && isfinite(pt[q].y) && isfinite(pt[q].z)) {
-                        bmn[0] = fminf(bmn[0], pt[q].x); bmn[1] = fminf(bmn[1], pt[q].y); bmn[2] = fminf(bmn[2], pt[q].z);
-                        bmx[0] = fmaxf(bmx[0], pt[q].x); bmx[1] = fmaxf(bmx[1], pt[q].y); bmx[2] = fmaxf(bmx[2], pt[q].z);
-                        nf++;
-                    }
+            for (int k = 0; k < 8; k++) {
+                if (!((sv >> k) & 1u)) continue;
+                st_f4(&sp_p[pos], pt[k]);
+                st_rlx(&sp_i[pos], c0 + (uint32_t)k * CG_BLOCK + tid);
+                pos++;
+                if (isfinite(pt[k].x) && isfinite(pt[k].y) && isfinite(pt[k].z)) {
+                    bmn[0] = fminf(bmn[0], pt[k].x); bmn[1] = fminf(bmn[1], pt[k].y); bmn[2] = fminf(bmn[2], pt[k].z);
+                    bmx[0] = fmaxf(bmx[0], pt[k].x); bmx[1] = fmaxf(bmx[1], pt[k].y); bmx[2] = fmaxf(bmx[2], pt[k].z);
+                    nf++;
                 }
             }
             float r[6];
@@ -301,51 +272,51 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
                 if (nfw) {
 #pragma unroll
                     for (int a = 0; a < 3; a++) {
-                        atomicMin(spw + SP_BMIN + a, cg_fkey(r[a]));
-                        atomicMax(spw + SP_BMAX + a, cg_fkey(r[3 + a]));
+                        atomicMin(L.split + SP_BMIN + a, cg_fkey(r[a]));
+                        atomicMax(L.split + SP_BMAX + a, cg_fkey(r[3 + a]));
                     }
-                    atomicAdd(spw + SP_NFIN, nfw);
+                    atomicAdd(L.split + SP_NFIN, nfw);
                 }
-                if (kc) atomicAdd(spw + SP_K, kc);
+                if (kc) atomicAdd(L.split + SP_K, kc);
             }
         }
         __builtin_amdgcn_s_waitcnt(0x0070);   // every lane's stores and atomics are complete
         __syncthreads();
         if (tid == 0)
-            fs->scal[S_LAST] = __hip_atomic_fetch_add(spw + SP_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                               snch - 1;
+            fs->scal[S_LAST] = __hip_atomic_fetch_add(L.split + SP_DONE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                               gridDim.x - 1;
         __syncthreads();
         if (!fs->scal[S_LAST]) return;
         STAMP(31);
         // the last workgroup: the frame's counts and bounds (the state reset for the next frame:
         // every chunk has read the keys and added its counts), then the survivors
         if (tid == 0) {
-            fs->scal[S_MS] = ld_rlx(spw + SP_MS);
-            fs->scal[S_K] = ld_rlx(spw + SP_K);
-            fs->scal[S_MF] = ld_rlx(spw + SP_NFIN);
-            fs->scal[S_ERR] = ld_rlx(spw + SP_ERR);
+            fs->scal[S_MS] = ld_rlx(L.split + SP_MS);
+            fs->scal[S_K] = ld_rlx(L.split + SP_K);
+            fs->scal[S_MF] = ld_rlx(L.split + SP_NFIN);
+            fs->scal[S_ERR] = ld_rlx(L.split + SP_ERR);
 #pragma unroll
             for (int a = 0; a < 3; a++) {
-                fs->scal[S_BMIN0 + a] = ld_rlx(spw + SP_BMIN + a);
-                fs->scal[S_BMAX0 + a] = ld_rlx(spw + SP_BMAX + a);
+                fs->scal[S_BMIN0 + a] = ld_rlx(L.split + SP_BMIN + a);
+                fs->scal[S_BMAX0 + a] = ld_rlx(L.split + SP_BMAX + a);
             }
         }
         __syncthreads();
         if (fs->scal[S_ERR]) {   // (the keys of chunks that gave up were never read here)
-            if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = ld_rlx(spw + SP_KEYS + tid);
+            if (GROUND && tid <= CG_NUM_BINS) fs->sec_key[tid] = ld_rlx(L.split + SP_KEYS + tid);
             if (tid == 0) { fs->scal[S_MS] = 0; fs->scal[S_MF] = 0; }
         }
-        if (L.seckeys && GROUND && tid <= CG_NUM_BINS) L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = fs->sec_key[tid];
+        if (L.seckeys && GROUND && tid <= CG_NUM_BINS) L.seckeys[tid] = fs->sec_key[tid];
         if (tid < SP_STATE) {
             const bool keyw = (tid >= SP_KEYS && tid < SP_KEYS + CG_NUM_BINS + 1) || (tid >= SP_BMIN && tid < SP_BMIN + 3);
-            st_rlx(spw + tid, keyw ? 0xffffffffu : 0u);
+            st_rlx(L.split + tid, keyw ? 0xffffffffu : 0u);
         }
         {
             const uint32_t Ms = fs->scal[S_MS];
-            const float4* const sp_p = (const float4*)(spw + SP_SURV);
-            uint32_t* const sp_i = spw + SP_SURV + 4 * CG_MAX_POINTS;
+            const float4* const sp_p = (const float4*)(L.split + SP_SURV);
+            uint32_t* const sp_i = L.split + SP_SURV + 4 * CG_MAX_POINTS;
             const Work Wl = lds_work(bl);
-            const Work Wg = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
+            const Work Wg = global_work(L.scratch, N);
             for (uint32_t j = tid; j < Ms; j += CG_BLOCK) {
                 const float4 p = ld_f4(&sp_p[j]);
                 const uint32_t ix = ld_rlx(&sp_i[j]);
@@ -616,34 +587,26 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     } else {
         backend(W, M, fs, L, P, f, flags, CG_MAX_POINTS / 32, 0);
     }
-    // header word 7 of a split frame: a chunk gave up waiting for the others (the frame is
-    // run again)
-    if constexpr (SPLIT)
-        if (tid == 0) L.hdr[(uint64_t)f * CG_HDR_WORDS + CG_HDR_WORDS - 1] = fs->scal[S_ERR];
-    if constexpr (SPLIT && !BATCH) {   // the results packed for the host's one copy (fetch_frame)
+    if constexpr (SPLIT) {   // the results packed for the host's one copy (fetch_frame)
+        // header word 7: a chunk gave up waiting for the others (the host runs the frame again)
+        if (tid == 0) L.hdr[CG_HDR_WORDS - 1] = fs->scal[S_ERR];
         if (L.pack) {
             __threadfence();
             __syncthreads();
-#ifdef CG_PACK_FENCE   // (variant: plain stores, one system-scope release before the done word)
             pack_frame(L, f, L.pack);
             if (L.pack_seq) {
+                // the done word after every packed word: every wave's stores complete
+                // (vmcnt(0)), the barrier, then one system-scope release (the L2 write-back that
+                // puts the packed words in host memory: plain stores alone were seen overtaken by
+                // the done word, and a system-scope store per word cost ~80 us per call,
+                // profiles/r4_chunk_batch_reverted.txt), then the word
                 __builtin_amdgcn_s_waitcnt(0x0070);
                 __syncthreads();
                 if (tid == 0) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-#else
-            if (L.pack_seq) pack_frame<true>(L, f, L.pack);
-            else pack_frame(L, f, L.pack);
-            if (L.pack_seq) {
-#endif
-                // the done word after every packed word: system-scope stores are visible to the
-                // host once they complete (vmcnt(0) in every wave, then the barrier)
-                __builtin_amdgcn_s_waitcnt(0x0070);
-                __syncthreads();
-                if (tid == 0)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the fence's wait, kept)
                     __hip_atomic_store(&L.pack[CG_PACK_DONE], L.pack_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
     }
@@ -660,12 +623,6 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void cg_frame_kernel(CgLaunch L, CgDev
 template <int PPT, int LAYOUT, int KMODE>
 __global__ __launch_bounds__(CG_BLOCK, 2) void cg_split_kernel(CgLaunch L, CgDevParams P) {
     frame_body<PPT, LAYOUT, KMODE, true>(L, P);
-}
-// Split batches (cg_launch_split_batch): the split kernel's chunk workgroups for every frame of
-// a batch in one grid, two workgroups per CU (<= 128 VGPRs, as the frame kernel).
-template <int PPT, int LAYOUT, int KMODE>
-__global__ __launch_bounds__(CG_BLOCK, 4) void cg_bsplit_kernel(CgLaunch L, CgDevParams P) {
-    frame_body<PPT, LAYOUT, KMODE, true, true>(L, P);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -768,35 +725,6 @@ int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
     return hipGetLastError();
 }
 
-int cg_launch_split_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
-    constexpr int PPT = CG_MAX_POINTS / CG_BLOCK;
-    if (L.n_frames == 0) return hipSuccess;
-    const uint32_t groups = (L.n_frames + 7) / 8;
-    const dim3 grid(groups * 8 * L.split_nch), block(CG_BLOCK);
-    const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
-    if (kmode == CG_KMODE_PIPELINE) {
-        if (xyzi16) hipLaunchKernelGGL((cg_bsplit_kernel<PPT, CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
-        else hipLaunchKernelGGL((cg_bsplit_kernel<PPT, CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), grid, block, 0, s, L, P);
-    } else {
-        if (xyzi16) hipLaunchKernelGGL((cg_bsplit_kernel<PPT, CG_LAYOUT_XYZI16, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
-        else hipLaunchKernelGGL((cg_bsplit_kernel<PPT, CG_LAYOUT_GENERIC, CG_KMODE_DETECT>), grid, block, 0, s, L, P);
-    }
-    return hipGetLastError();
-}
-
-// The state words of n_frames split-batch frames (stride words apart): zero, keys and bounds
-// minima all ones (the last workgroup of each frame resets its own after that)
-__global__ void cg_split_state_init(uint32_t* sp, uint64_t stride, uint32_t n_frames) {
-    const uint32_t f = blockIdx.x, t = threadIdx.x;
-    if (f >= n_frames || t >= SP_STATE) return;
-    const bool keyw = (t >= SP_KEYS && t < SP_KEYS + CG_NUM_BINS + 1) || (t >= SP_BMIN && t < SP_BMIN + 3);
-    sp[(uint64_t)f * stride + t] = keyw ? 0xffffffffu : 0u;
-}
-int cg_launch_split_state_init(uint32_t* sp, uint64_t stride, uint32_t n_frames, hipStream_t s) {
-    if (n_frames) hipLaunchKernelGGL(cg_split_state_init, dim3(n_frames), dim3(64), 0, s, sp, stride, n_frames);
-    return hipGetLastError();
-}
-
 int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s) {
     if (L.n_frames == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 &&
@@ -813,15 +741,8 @@ int cg_launch_batch(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 // Self-test kernels: the device restatements, evaluated element-wise for host comparison.
 // Results of one frame packed for a single device-to-host copy (fetch_frame): the header, then
 // up to CG_PACK_MAX entries of each result array at fixed offsets (cg_internal.h CG_PACK_*).
-// SYS (the split launch's pack in host memory, followed by a done word): every word is a
-// system-scope store, complete (vmcnt) only once the host can see it; plain stores to host
-// memory were seen overtaken by the done word (the host read the previous frame's pack)
-template <bool SYS>
 __device__ __forceinline__ void pack_frame(const CgLaunch& L, uint32_t f, uint32_t* out) {
-    auto put = [](uint32_t* q, uint32_t v) {
-        if constexpr (SYS) __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else *q = v;
-    };
+    auto put = [](uint32_t* q, uint32_t v) { *q = v; };
     const uint32_t nt = blockDim.x;
     const uint32_t* hdr = L.hdr + (uint64_t)f * CG_HDR_WORDS;
     const uint32_t V = min(hdr[CG_HDR_V], (uint32_t)CG_PACK_MAX), C = min(hdr[CG_HDR_C], (uint32_t)CG_PACK_MAX);

@@ -1162,8 +1162,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
         // frame's N): the tiles number at most ceil(n / PQ_T) + one per range
         const uint32_t n = S.meta[LG_PCL_N];
         const uint32_t nr0 = level == 0 ? (n > LG_PCL_CUT ? 1u : 0u) : min(S.pq[level % 3u], (uint32_t)PQ_MAXR);
-        // the levels this frame cuts, for the next frame's launches (LG_HINT_LEVELS)
-        if (blockIdx.x == 0 && tid == 0 && S.hint && n && (level == 0 || nr0)) S.hint[LG_HINT_LEVELS] = nr0 ? level + 1u : 0u;
         if (blockIdx.x >= (n + PQ_T - 1) / PQ_T + nr0) {
             if (blockIdx.x == 0 && tid == 0) S.ca[0] = 0;   // no tile: lg_pq_swap reads the count
             return;
@@ -1731,13 +1729,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
                                                              uint32_t cb, uint32_t sort_hi) {
     if (Mtot == CG_K_FROM_META) Mtot = S.meta[LG_MALL];
     if (K == CG_K_FROM_META) K = S.meta[LG_KHDR];
-    if (buf < 0) {   // (device-sized: the next frame's partition levels are sized from this one's)
-        buf = (int)(lg_rs_passes(VB, sort_hi, S.meta[LG_SORT_LIM]) & 1u);
-        // (a frame with no index_vector here, one the LDS backend took or a passthrough, keeps
-        // the hint of the last frame that had one)
-        const uint32_t npcl = S.meta[LG_PCL_N];
-        if (blockIdx.x == 0 && threadIdx.x == 0 && S.hint && npcl) S.hint[LG_HINT_N] = npcl + 1u;
-    }
+    if (buf < 0) buf = (int)(lg_rs_passes(VB, sort_hi, S.meta[LG_SORT_LIM]) & 1u);   // (device-sized)
     if (blockIdx.x < cb) {
         lg_csr_one(L, P, S, f, VB, buf, Mtot, K, blockIdx.x);
         return;
@@ -2124,24 +2116,11 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
     S.pidx_base = 0;
     if (kmode != CG_KMODE_GROUND && P.voxel_order == CG_VOXEL_ORDER_PCL && N > 0 && N <= LG_DEV_MAX_POINTS) {
         if (graphs && !*graphs) *graphs = new LgGraphs();
-#ifdef LG_NO_HINT   // (variant builds: launches for N)
-        hint = nullptr;
-#endif
-#ifdef LG_NO_HINT_WRITE   // (variant builds: the kernels write no hint words to host memory)
-        hint = nullptr;
-        S.hint = nullptr;
-#endif
-        uint32_t levels = lg_levels_for(N, S.pcl_levels_cap);   // before any frame has run
+        // partition levels from N (levels with no range to cut return at once). Round 4 sized
+        // them from the previous frame's index_vector instead (fewer launches): 575-580 against
+        // 309-311 us per C5 frame, reverted (profiles/r4_c5_hint_reverted.txt)
+        const uint32_t levels = lg_levels_for(N, S.pcl_levels_cap);
         bool small = true;
-        if (hint && hint[LG_HINT_N]) {
-            // one level more than the last frame cut, and than an even split of its index_vector
-            // needs (a frame much larger than the last); at least one, so that a range longer than
-            // a leaf is always cut once and its halves queued as leaves
-            uint32_t even = 0;
-            while (((uint64_t)LG_PCL_CUT << even) < hint[LG_HINT_N] - 1) even++;
-            levels = std::min<uint32_t>(std::max(even, hint[LG_HINT_LEVELS]) + 1u, LG_PQ_LEVELS_MAX);
-            if (S.pcl_levels_cap) levels = std::min(levels, S.pcl_levels_cap);
-        }
         if (hint && hint[LG_HINT_SMALL] == 1u) small = false;   // the last frame was a large one
         for (uint32_t f = 0; f < L.n_frames; f++) {
             const int rc = graphs ? large_frame_graph(*graphs, L, P, kmode, S, s, f, levels, small)

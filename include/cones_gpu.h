@@ -388,8 +388,7 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
  * are finished in HBM side by side (5); single-frame calls whose staged chunks are never
  * published, so every chunk workgroup times out and the call re-runs the frame by DMA (6,
- * tests of that retry); batches of <= 65,536-point frames through the split kernel, one
- * workgroup per 4,096-point chunk of every frame in one launch (7); 0 = automatic. */
+ * tests of that retry); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

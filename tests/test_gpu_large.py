@@ -196,11 +196,9 @@ def test_large_batch_pipelined_over_two_scratch_sets(params, mode):
 
 
 def test_hint_sequence_small_large_medium(params):
-    """The device-sized path sizes each frame's launches from the previous frames' (the pinned
-    hint words): partition levels from the last index_vector and the levels it cut, and the LDS
-    backend's launch left out after a large frame. One handle runs frames whose sizes jump both
-    ways — a small frame after a large one takes the global backend, a large frame after a small
-    or medium one finishes its longer ranges in HBM — and every frame must stay bit-exact."""
+    """The device-sized path leaves the LDS backend's launch out after a large frame (the
+    pinned hint word). One handle runs frames whose sizes jump both ways (a small frame after a
+    large one takes the global backend) and every frame must stay bit-exact."""
     seq = [_frame(128, 1024, frame=3),                          # small: the LDS backend
            _frame(128, 8192, frame=0, clutter=60, cpr=12),      # C5: every partition level
            _frame(128, 1024, frame=3),                          # small after large: global backend

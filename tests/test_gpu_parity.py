@@ -109,6 +109,23 @@ def test_single_frame_staging_grows_and_shrinks(params):
         assert_same_detection(got, ref, f"staged {rings}x{cols} f{frame}")
 
 
+def test_single_frame_done_word_never_stale(params):
+    """The split launch packs its results into pinned host memory and then stores a done word
+    the host polls: every packed word must be visible before the word. Frames with different
+    results alternate for 300 calls on one handle; a result read before its pack landed would
+    carry the previous frame's counts or centroids."""
+    pipe = cp.ConePipeline(params)
+    frames = []
+    for f, clutter, cpr in ((0, 0, 5), (1, 60, 9), (2, 20, 3)):
+        msg = cp.frame_cloud(cp.synth_frames(1, first_frame=f, rings=64, cols=1024, clutter=clutter,
+                                             cones_per_row=cpr)[0])
+        frames.append((msg, O.run(params, msg, O.MODE_PIPELINE)[0]))
+    assert len({r.voxels.shape[0] for _, r in frames}) == 3   # distinguishable results
+    for i in range(300):
+        msg, ref = frames[i % 3]
+        assert_same_detection(pipe.cloud_handler(msg), ref, f"call {i}")
+
+
 @pytest.mark.parametrize("frame", [0, 3])
 def test_detector_matches_oracle(params, det, frame):
     raw = cp.synth_frames(1, first_frame=frame, rings=64, cols=1024)
