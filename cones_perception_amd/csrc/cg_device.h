@@ -382,6 +382,10 @@ struct LaneBits {
 // coded by this same function, so the rounding and the window (zq_bias) only decide how many
 // points are ambiguous, never a result.
 #define CG_ZQ_SCALE (-64.0f)
+// cache policy (aux) bits of pass 1's streaming buffer loads (variant builds: 2 = nt)
+#ifndef CG_PASS1_AUX
+#define CG_PASS1_AUX 0
+#endif
 __device__ __forceinline__ uint32_t zcode_into(float z, float zq_bias, uint32_t byte, uint32_t word) {
     return __builtin_amdgcn_cvt_pk_u8_f32(fmaf(z, CG_ZQ_SCALE, zq_bias), byte, word);
 }
@@ -469,7 +473,8 @@ __device__ __forceinline__ void stream_pass1(const uint8_t* fb, uint32_t N, cons
             typedef uint32_t v3u __attribute__((ext_vector_type(3)));
 #pragma unroll
             for (int j = 0; j < G; j++) {
-                const v3u v = __builtin_amdgcn_raw_buffer_load_b96(rs, tid * 16u, (gc * G + (uint32_t)j) * (CG_BLOCK * 16u), 0);
+                const v3u v = __builtin_amdgcn_raw_buffer_load_b96(rs, tid * 16u, (gc * G + (uint32_t)j) * (CG_BLOCK * 16u),
+                                                                   CG_PASS1_AUX);
                 buf[j] = make_float3(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z));
             }
         } else {
