@@ -80,13 +80,15 @@ print("hbm bytes per frame:", hbm / F)
 print(json.dumps(json.load(open(os.path.join(DST, f"{RND}_sq_counters.json")))["wave_time_fraction"]))
 
 # timing check: the bench's in-kernel launch span vs rocprofv3's kernel trace over the same
-# timed launches (the last `steps` dispatches of the stats run; the first `warmup` are untimed)
+# timed launches: dispatches [warmup, warmup + steps) of the stats run (the warmup steps come
+# first; the untimed event pass and the later legs follow the timed region)
 trace = [r for r in csv.DictReader(open(os.path.join(DST, f"{RND}_kernel_trace.csv"))) if KERNEL in r["Kernel_Name"]]
 dur_us = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in trace]
 bench = [json.loads(x) for x in open(os.path.join(SRC, "stats.log")) if x.startswith("{")][0]
 steps = bench["steps"]
 roof = bench["roofline"]
-timed = statistics.mean(dur_us[-steps:])
+warm = bench["warmup"]
+timed = statistics.mean(dur_us[warm:warm + steps])
 json.dump({"kernel": KERNEL, "launches_traced": len(dur_us), "timed_launches": steps,
            "rocprof_avg_us_timed": timed, "rocprof_avg_us_all": statistics.mean(dur_us),
            "bench_avg_kernel_us": roof["avg_kernel_ms"] * 1e3, "bench_source": roof.get("avg_kernel_ms_source"),
