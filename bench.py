@@ -54,6 +54,7 @@ def main():
                     help="threads of the frame-parallel CPU leg (0: the process's CPU share, see cpu_share())")
     ap.add_argument("--single-frame", action="store_true",
                     help="also time C2 single-frame latency at N>1 (always at N=1)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 single-frame leg (diagnostic builds)")
     ap.add_argument("--colornet", action="store_true",
                     help="also time the colour classifier service (cg_classify_colors) on re-crops of "
                          "the synthetic frames: one call per frame's cones, and batched calls")
@@ -254,7 +255,7 @@ def main():
                "halo": c5_tiled(cp, cd, params, local, rank, world, halo=True)}
 
     single = None
-    if rank == 0 and (args.single_frame or world == 1):   # C2: the ROS node's synchronous call
+    if rank == 0 and (args.single_frame or world == 1) and not args.no_c2:   # C2: the ROS node's synchronous call
         try:
             single = single_frame_latency(cp, params, raw, local, order=vorder)
         except Exception as e:  # noqa: BLE001

@@ -137,8 +137,7 @@ __device__ __forceinline__ void lg_store_survivor_bits(LgScratch& S, uint32_t c,
 #define LG_SZ_GLOBAL 4u   // the global backend even when M fits the LDS one (diagnostics)
 #define LG_SZ_ON 0x80000000u   // (host side: cg_large_front / cg_large_decide fold the sizes)
 #define LG_WM_KEYS ((1u << (CG_NUM_BINS + 1)) - 1u)   // fold words: the sector keys,
-#define LG_WM_TOUCHED (1u << LG_CS_TOUCHED)            // the used bins,
-#define LG_WM_COUNTS ((1u << LG_CS_K) | (1u << LG_CS_MS) | (7u << LG_CS_BMIN) | (7u << LG_CS_BMAX) | (1u << LG_CS_NFIN))
+#define LG_WM_TOUCHED (1u << LG_CS_TOUCHED)            // the used bins
 // The fold itself, called by every thread of the block: thread w < LG_CS_WORDS returns word w
 // folded over the nch chunks (words outside wmask: not loaded).
 __device__ __forceinline__ uint32_t lg_fold_core(const LgScratch& S, uint32_t nch, uint32_t wmask,
@@ -813,42 +812,13 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
 // Mtot = CG_K_FROM_META (the backend sized on the device): Mtot and npad from the meta words
 // (LG_MTOT, LG_NPAD; the grid sized for the frame's N); Mtot 0 (the LDS backend takes the frame)
 // leaves every later global-backend launch without work.
-// szfl (the device-sized path, LG_SZ_ON | flags): every workgroup first folds the decisions'
-// per-chunk counts and bounds itself (lg_fold_core; no lg_reduce_chunks launch before this one)
-// and sizes the detector input (lg_size_fold); workgroup 0 stores those meta words too.
 __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_keys(LgScratch S, CgDevParams P, uint32_t Mtot, uint32_t N,
                                                           uint32_t PB, uint32_t npad,
-                                                          uint32_t nfin_local = 0xffffffffu, uint32_t szfl = 0u) {
+                                                          uint32_t nfin_local = 0xffffffffu) {
     __shared__ uint32_t m[LG_META_WORDS];
-    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x, tid = threadIdx.x;
+    const uint32_t j = blockIdx.x * CG_BLOCK + threadIdx.x;
     const bool dev = Mtot == CG_K_FROM_META;
     const uint32_t* in = S.meta;   // the counts and bounds words
-    if (szfl & LG_SZ_ON) {
-        __shared__ uint32_t part[16][LG_CS_WORDS];
-        const uint32_t nch = (uint32_t)(((uint64_t)N + LG_CHUNK - 1) / LG_CHUNK);
-        const uint32_t a = lg_fold_core(S, nch, LG_WM_COUNTS, part);
-        uint32_t word = 0xffffffffu;   // the meta word of fold word tid
-        if (tid == LG_CS_K && (szfl & LG_SZ_PIPE)) word = LG_K;
-        if (tid == LG_CS_MS) word = LG_MS;
-        if (tid == LG_CS_NFIN) word = LG_NFIN;
-        if (tid >= LG_CS_BMIN && tid < LG_CS_BMIN + 3) word = LG_BMIN + (tid - LG_CS_BMIN);
-        if (tid >= LG_CS_BMAX && tid < LG_CS_BMAX + 3) word = LG_BMAX + (tid - LG_CS_BMAX);
-        if (tid == LG_CS_K) m[LG_K] = a;   // (lg_size_fold reads it in pipeline mode only)
-        if (word != 0xffffffffu) {
-            m[word] = a;
-            if (blockIdx.x == 0) S.meta[word] = a;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            lg_size_fold(S, m, m[LG_K], m[LG_MS], N, szfl, blockIdx.x == 0);
-            if (blockIdx.x == 0)
-                for (uint32_t w : {(uint32_t)LG_KHDR, (uint32_t)LG_NPAD, (uint32_t)LG_MALL, (uint32_t)LG_MTOT,
-                                   (uint32_t)LG_SMALL})
-                    S.meta[w] = m[w];
-        }
-        __syncthreads();
-        in = m;
-    }
     if (dev) {
         Mtot = in[LG_MTOT];
         npad = in[LG_NPAD];
@@ -1791,8 +1761,8 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
         return hipGetLastError();
     }
     const uint32_t fi = init ? 1u : 0u;   // lg_front's workgroup 0 resets the meta words
-    // the device-sized path: lg_decide folds the chunks' keys, lg_voxel_keys their counts and
-    // bounds (no lg_reduce_chunks launches)
+    // the device-sized path: lg_decide folds the chunks' keys (no lg_reduce_chunks launch after
+    // the pipeline front); the counts' fold also sizes the detector input (LG_FOLD_SIZE)
     const bool dev = (szfl & LG_SZ_ON) != 0;
     const dim3 g(nch), b(CG_BLOCK);
 #define LG_FRONT_MODES(LAY)                                                                       \
@@ -1802,7 +1772,7 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
     } else if (kmode == CG_KMODE_DETECT) {                                                        \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f);                              \
-        if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u, N, 0u);             \
+        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u | (dev ? LG_FOLD_SIZE : 0u), N, szfl); \
     } else {                                                                                      \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
@@ -1824,7 +1794,7 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
     if (nch == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
     const dim3 g(nch), b(CG_BLOCK);
-    const bool dev = (szfl & LG_SZ_ON) != 0;   // (the folds in lg_decide and lg_voxel_keys)
+    const bool dev = (szfl & LG_SZ_ON) != 0;   // (lg_decide folds the front's chunk keys)
     if (xyzi16) {
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
         hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f);
@@ -1832,7 +1802,10 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
         hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f);
     }
-    if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u, L.n_points, 0u);
+    // the decisions' counts and bounds folded by one workgroup (folded in every lg_voxel_keys
+    // workgroup instead, 2,048 of them on C5 each reading the 256 chunk records: 15.6 against
+    // 5.0 + 5.0 us, profiles/r4_c5_fold_ab.txt)
+    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u | (dev ? LG_FOLD_SIZE : 0u), L.n_points, szfl);
     return hipGetLastError();
 }
 
@@ -1982,8 +1955,7 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     CgLaunch Lh = L;
     Lh.n_points = N;
     const uint32_t nmax = std::max<uint32_t>(N, 1);
-    hipLaunchKernelGGL(lg_voxel_keys, dim3(blocks_of(nmax)), dim3(CG_BLOCK), 0, s, S, P, CG_K_FROM_META, N, 0u, 0u,
-                       0xffffffffu, szfl);
+    hipLaunchKernelGGL(lg_voxel_keys, dim3(blocks_of(nmax)), dim3(CG_BLOCK), 0, s, S, P, CG_K_FROM_META, N, 0u, 0u);
     uint64_t* kb[2] = {S.key0, S.key1};
     uint32_t* vb2[2] = {S.val0, S.val1};
     // index_vector (finite points in frame-index order) as (idx, slot) records, then std::sort's
