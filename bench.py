@@ -691,7 +691,8 @@ def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):
            "points": n_total, "tile_points": hi - lo,
            "includes": ("device-resident tiles; 2 collectives to decide the points, then voxel slabs per rank: "
                         "all-to-all of the survivors, point-to-point halo to the slab below, gather of voxel "
-                        "records and component pairs to rank 0, merge there") if halo else
+                        "records and component pairs to rank 0, merge there; at one rank one slab: its backend "
+                        "(voxel sums in point order) on the survivors where decide left them") if halo else
                        "device-resident tiles; keys and counts merged on the device (cg_tile_*_async), one host read of the gathered counts at N>1; backend on rank 0 (at one rank on its own survivors)"}
     if halo:
         out["halo"] = dict(cd.last_halo_stats)

@@ -181,14 +181,21 @@ class Detection:
         return [self.cluster_indices[o[i]:o[i + 1]] for i in range(len(o) - 1)]
 
 
+def _copied(ptr, n: int, dtype) -> np.ndarray:
+    """n elements at a result pointer, copied into a new writable array (ctypes.string_at and
+    np.frombuffer: ~1.3 us less per array than np.ctypeslib.as_array on the synchronous call)."""
+    dt = np.dtype(dtype)
+    return np.frombuffer(C.string_at(ptr, n * dt.itemsize), dt).copy() if n else np.zeros(0, dt)
+
+
 def _detection(r: _abi.cg_detect_result) -> Detection:
     V, Cn = r.n_voxels, r.n_clusters
-    vox = np.ctypeslib.as_array(r.voxels, (V * 4,)).reshape(V, 4).copy() if V else np.zeros((0, 4), np.float32)
-    lab = np.ctypeslib.as_array(r.labels, (V,)).copy() if V else np.zeros(0, np.int32)
-    offs = np.ctypeslib.as_array(r.cluster_offsets, (Cn + 1,)).copy()
+    vox = _copied(r.voxels, V * 4, np.float32).reshape(V, 4)
+    lab = _copied(r.labels, V, np.int32)
+    offs = _copied(r.cluster_offsets, Cn + 1, np.int32)
     nidx = int(offs[-1]) if Cn else 0
-    idx = np.ctypeslib.as_array(r.cluster_indices, (nidx,)).copy() if nidx else np.zeros(0, np.int32)
-    cen = np.ctypeslib.as_array(r.centroids, (Cn * 2,)).reshape(Cn, 2).copy() if Cn else np.zeros((0, 2), np.float32)
+    idx = _copied(r.cluster_indices, nidx, np.int32)
+    cen = _copied(r.centroids, Cn * 2, np.float32).reshape(Cn, 2)
     return Detection(r.n_points, r.n_kept, r.n_filtered, vox, lab, offs, idx, cen, r.flags)
 
 
@@ -198,6 +205,7 @@ class _Handle:
         h = C.c_void_p()
         check(lib().cg_create(C.byref(self.params), device, C.byref(h)))
         self._h = h
+        self.voxel_order = _abi.CG_VOXEL_ORDER_PCL   # (cg_create's default)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -218,6 +226,7 @@ class _Handle:
         """CG_VOXEL_ORDER_PCL (default): each voxel's float sums in PCL's std::sort order, every
         voxel bit as the reference; CG_VOXEL_ORDER_POINT: in ascending point order."""
         check(lib().cg_set_voxel_order(self._h, order))
+        self.voxel_order = order
         return self
 
     def debug_route(self, route: int):

@@ -246,6 +246,15 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
     fetch=False leaves the result in the handle's device buffers (engine.fetch(0) reads it)
     and returns True on dst."""
     from . import _abi
+    if halo and not _distributed():
+        # one rank: one slab and no halo, so the slab's backend is the frame's, with its voxel
+        # sums in point order as every slab's; it runs on the survivors where decide left them
+        # (the gather form's one-rank path), with no survivor copy, plan or records
+        last_halo_stats.clear()
+        last_halo_stats.update(slabs=1, slab_w=None, band=None, survivors=None, voxels=None, halo_sent=0,
+                               halo_received=0, pairs=0)
+        return _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets, dst, fetch,
+                                 order=_abi.CG_VOXEL_ORDER_POINT)
     if halo:
         total, sizes, sp, si = _tile_front_decide_dev(engine, d_tile_ptr, first, n, n_total, device, point_step,
                                                       offsets)
@@ -271,7 +280,7 @@ def _tile_stream(engine, device):
     return st
 
 
-def _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets, dst, fetch):
+def _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets, dst, fetch, order=None):
     """The gather form with the keys and counts on the device (cg_tile_*_async): the keys
     merge with a MIN all-reduce on the GPU; one rank (its tile the whole frame) runs the
     backend on its own survivors where they are; several ranks merge the counts with one
@@ -291,7 +300,15 @@ def _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step,
         counts = torch.empty(_abi.CG_TILE_COUNTS, dtype=torch.int32, device=device)
         _abi.check(lib.cg_tile_decide_async(h, merged.data_ptr(), counts.data_ptr(), s))
         if not _distributed():
-            _abi.check(lib.cg_tile_backend_own(h, n_total, s))
+            if order is None:
+                _abi.check(lib.cg_tile_backend_own(h, n_total, s))
+            else:   # (the voxel order is read when the backend's launches are enqueued)
+                prev = engine.voxel_order
+                engine.set_voxel_order(order)
+                try:
+                    _abi.check(lib.cg_tile_backend_own(h, n_total, s))
+                finally:
+                    engine.set_voxel_order(prev)
             # the caller's stream waits for the frame: its tile buffer and the handle's
             # outputs are safe to reuse or read there once this returns (fetch=False)
             caller.wait_stream(st)
