@@ -1,6 +1,8 @@
 #!/bin/bash
 # GPU, one call: C3 at 2, 3 and 4 streams (20-step bench runs, twice, interleaved), and pass 1
-# with cache policy sc0 | nt (lib_variants/nt3) against the default nt.
+# with cache policy sc0 | nt (lib_variants/nt3) against the default nt. The variant libraries are
+# built beforehand: tools/build_variant.sh nt3 -DCG_PASS1_AUX=3, stop1 -DCG_EXP_STOP=1,
+# stop3 -DCG_EXP_STOP=3 (results: profiles/r4_streams_stop_ab.txt, r4_c5_fold_ab.txt).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
