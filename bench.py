@@ -71,6 +71,9 @@ def main():
                     help="also time the C4 composition: rank 0 holds the whole batch, RCCL "
                          "scatter to ranks, process, gather per-frame headers (reported separately)")
     ap.add_argument("--no-events", action="store_true", help="skip the HIP-event pass after the timed region")
+    ap.add_argument("--sustained-steps", type=int, default=200,
+                    help="after the timed region, the same rotation for this many steps in one more "
+                         "cg_run_batches call, reported as `sustained` (0: skip)")
     ap.add_argument("--streams", type=int, default=3,
                     help="independent batch engines on their own HIP streams, used round-robin "
                          "by consecutive steps (a step's kernel overlaps the previous step's tail)")
@@ -108,7 +111,7 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     # --scatter at one rank: a world-size-1 RCCL group with collectives forced on, so the C4
     # scatter/gather runs under RCCL on a one-GPU box too
-    solo_pg = world == 1 and args.scatter
+    solo_pg = world == 1 and (args.scatter or args.c5_tiled)
     if solo_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(free_port()))
@@ -212,6 +215,9 @@ def main():
         avg_event_ms = sum(kern_ms) / len(kern_ms)
     step_span_ms = float((sp[:, 1] - sp[:, 0]).mean()) * 1e-5 if spans_ok else avg_event_ms   # 100 MHz ticks
     avg_kernel_ms = step_span_ms
+    sustained = None
+    if args.sustained_steps > 0:
+        sustained = sustained_pass(args, world, dev, engines, queue, S, F, N)
 
     # algorithmic bytes of one launch, from the frames' own V and C
     res = engines[(counter[0] - 1) % S].results()
@@ -223,6 +229,7 @@ def main():
 
     from cones_perception_amd import dist as cd
     elapsed = cd.max_over_ranks(elapsed, dev)
+    census = rank_census(world, local)
     total_frames = F * args.steps * world
     fps = total_frames / elapsed
 
@@ -251,8 +258,12 @@ def main():
 
     c5t = None
     if args.c5_tiled:
-        c5t = {"gather": c5_tiled(cp, cd, params, local, rank, world),
-               "halo": c5_tiled(cp, cd, params, local, rank, world, halo=True)}
+        c5t = {"gather": c5_tiled(cp, cd, params, local, rank, world)}
+        h = c5_tiled(cp, cd, params, local, rank, world, halo=True)
+        # the halo form's name only when its code path ran (run_halo_backend); a rank without
+        # collectives runs the gather form's backend in point order instead
+        ran_halo = str(h.get("halo", {}).get("path", "")).startswith("run_halo_backend")
+        c5t["halo" if ran_halo else "gather_backend_point_order"] = h
 
     single = None
     if rank == 0 and (args.single_frame or world == 1) and not args.no_c2:   # C2: the ROS node's synchronous call
@@ -328,7 +339,10 @@ def main():
                          / HBM_COPY_GBS},
             "cpu_baseline": cpu,
             "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+            "ranks": census,
         }
+        if sustained is not None:
+            line["sustained"] = sustained
         if single is not None:
             line["single_frame"] = single
         if colornet is not None:
@@ -344,6 +358,101 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1 or solo_pg:
         dist.destroy_process_group()
+
+
+def rank_census(world, local):
+    """Which devices the ranks run on, as every rank sees it: each rank's device UUID (or PCI
+    location), all-gathered over the job's process group. At N > 1 this is the line's proof that
+    N ranks ran on N distinct GPUs (two ranks sharing a GPU show distinct_devices 1)."""
+    import torch.distributed as dist
+    ident = "none (no device)"
+    if local is not None:
+        import torch
+        p = torch.cuda.get_device_properties(local)
+        uuid = str(getattr(p, "uuid", "") or "")
+        pci = ":".join(str(getattr(p, a)) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id") if hasattr(p, a))
+        ident = f"uuid {uuid}" if uuid else (f"pci {pci}" if pci else f"{p.name} #{local}")
+    ids = [ident]
+    backend = None
+    if dist.is_initialized():
+        backend = str(dist.get_backend())
+        ids = [None] * dist.get_world_size()
+        dist.all_gather_object(ids, ident)
+    devs = {i for i in ids if not i.startswith("none")}
+    return {"ranks_seen": len(ids), "world_size_env": world, "distinct_devices": len(devs),
+            "backend": backend, "devices": ids[:16]}
+
+
+def sustained_pass(args, world, dev, engines, queue, S, F, N):
+    """The timed rotation again for --sustained-steps steps in one more cg_run_batches call,
+    after the timed region (untimed for `value`). Reports the rate, the aggregate HBM fraction and
+    every launch's in-kernel span, split into quarters: per-launch duration drifting upward over
+    the run (clock or power) shows as a longer span at equal overlap; queueing shows as more
+    launches in flight (overlap depth = sum of spans / wall extent of the quarter)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from cones_perception_amd import dist as cd
+    K = args.sustained_steps
+    q = queue(K)
+    per_eng = [list(range(k, K, S)) for k in range(S)]
+    bufs = [torch.zeros((max(1, len(ix)), 2), dtype=torch.int64, device=dev) for ix in per_eng]
+    for b in bufs:
+        b[:, 0] = 2 ** 63 - 1
+    torch.cuda.synchronize(dev)
+    for k in range(S):
+        engines[k].spans(bufs[k].data_ptr(), len(per_eng[k]))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    q.run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = cd.max_over_ranks(time.perf_counter() - t0, dev)
+    sp = np.zeros((K, 2), np.int64)
+    for k in range(S):
+        if per_eng[k]:
+            sp[per_eng[k]] = bufs[k][: len(per_eng[k])].cpu().numpy()
+    if not ((sp[:, 0] < 2 ** 63 - 1).all() and (sp[:, 1] > sp[:, 0]).all()):
+        return {"steps": K, "error": "spans not recorded"}
+    res = engines[(K - 1) % S].results()
+    hdr = fetch_headers(res, F)
+    B = float((16.0 * N + 20.0 * hdr[:, 3].astype(np.float64) + 8.0 * hdr[:, 4].astype(np.float64) + 64.0).sum())
+    dur = (sp[:, 1] - sp[:, 0]) * 1e-5          # ms (100 MHz ticks)
+    quarters = []
+    for a in range(4):
+        ix = np.arange(a * K // 4, (a + 1) * K // 4)
+        if ix.size < 2:
+            continue
+        ext = (sp[ix, 1].max() - sp[ix, 0].min()) * 1e-5
+        quarters.append({"launches": [int(ix[0]), int(ix[-1])],
+                         "span_ms_mean": float(dur[ix].mean()),
+                         "overlap_depth": float(dur[ix].sum() / ext),
+                         "ms_per_step": float(ext / ix.size),
+                         "aggregate_frac": B * ix.size / (ext * 1e-3) / 1e9 / HBM_PEAK_GBS})
+    d0, d3 = quarters[0], quarters[-1]
+    drift = d3["span_ms_mean"] / d0["span_ms_mean"] - 1.0
+    deeper = d3["overlap_depth"] / d0["overlap_depth"] - 1.0
+    pace = d3["ms_per_step"] / d0["ms_per_step"] - 1.0
+    if abs(pace) < 0.03:
+        finding = "steady: last quarter's step time within 3% of the first's"
+    elif drift > 0.03 and abs(deeper) < 0.03:
+        finding = "per-launch duration drifts upward at equal overlap (clock / power)"
+    elif deeper > 0.03:
+        finding = "overlap depth grows (launches queue behind each other)"
+    else:
+        finding = "step time changes with neither span nor overlap alone"
+    return {"steps": K, "value": F * K * world / el, "unit": "frames/s", "ms_per_step": el / K * 1e3,
+            "aggregate_frac": B * K / el / 1e9 / HBM_PEAK_GBS,
+            "span_ms_mean": float(dur.mean()), "span_ms_p50": float(np.median(dur)),
+            "span_ms_max": float(dur.max()),
+            "span_frac": B / (float(dur.mean()) * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "quarters": quarters, "span_drift_last_vs_first": drift, "overlap_growth_last_vs_first": deeper,
+            "step_time_change_last_vs_first": pace, "finding": finding,
+            "includes": f"one more cg_run_batches call of {K} steps after the timed region (same engines, "
+                        "inputs and stream rotation), in-kernel spans of every launch"}
 
 
 def free_port():
@@ -421,12 +530,13 @@ def dry_run(args, world, rank):
         m = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
         el = float(m.item())
+    census = rank_census(world, None)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": el / max(args.steps, 1) * 1e3, "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "none (dry run)",
-                          "dry_run": True, "ranks_seen": world, "host": host_info(),
+                          "dry_run": True, "ranks_seen": world, "ranks": census, "host": host_info(),
                           "config": {"workload": "dry run: no device work", "parallelism": f"frame-shard x{world}"}}),
               flush=True)
     if world > 1:
@@ -495,7 +605,13 @@ def phase_stamps(eng, step, F, around=None, tag="alone"):
     _abi.check(lib.cg_debug_stamps_fetch(eng.handle, st.ctypes.data, F))
     _abi.check(lib.cg_debug_stamps(eng.handle, 0))
     t = st.astype(np.int64)
-    out = {"tag": tag, "batch_span_us": float((t[:, 20].max() - t[:, 0].min()) / 100.0),
+    # frames whose workgroup left no start stamp (not run by this launch) are left out of every
+    # figure: their zero stamps would read as times 0 in the spans and percentiles
+    t = t[t[:, 0] > 0]
+    if t.shape[0] == 0:
+        print("STAMPS " + json.dumps({"tag": tag, "error": "no frame stamped"}), flush=True)
+        return
+    out = {"tag": tag, "frames_stamped": int(t.shape[0]), "batch_span_us": float((t[:, 20].max() - t[:, 0].min()) / 100.0),
            "wg_end_spread_us": float((t[:, 20].max() - t[:, 20].min()) / 100.0)}
     prev = t[:, 0].copy()
     for i in range(1, 21):
@@ -524,7 +640,7 @@ def phase_stamps(eng, step, F, around=None, tag="alone"):
     life = (t[:, 20] - t[:, 0]) / 100.0
     out["wg_lifetime_us_p10_p50_p90"] = [round(float(np.percentile(life, q)), 1) for q in (10, 50, 90)]
     pct = lambda x: [round(float(np.percentile(x, q)), 1) for q in (0, 10, 50, 90, 100)]
-    both = (t[:, 6] > 0) & (t[:, 5] > 0) & (t[:, 20] > 0)
+    both = (t[:, 0] > 0) & (t[:, 6] > 0) & (t[:, 5] > 0) & (t[:, 20] > 0)
     if both.sum() > 1:   # split batches: front (0-5) and backend (6-20) workgroups
         t = t[both]
         out["split_frames_stamped"] = int(both.sum())
@@ -614,8 +730,10 @@ def c5_single_gpu(cp, params, device, reps=50, order=None, batch=8, breps=6):
     out = {"_det": (raw, r), "ms_per_frame": dt * 1e3, "frames_per_s": 1.0 / dt, "points": n, "K": r.n_kept,
            "M": r.n_filtered, "V": V, "C": C,
            "algorithmic_GBs": algo / dt / 1e9, "hbm_frac": algo / dt / 1e9 / HBM_PEAK_GBS,
-           "includes": "device-resident input; one frame per call: one host round trip per frame (survivor "
-                       "count and bounds size the backend); backend latency-bound (sorts, union-find)"}
+           "includes": "device-resident input; one frame per call, replayed from a captured hipGraph: every "
+                       "backend launch sized from the frame's N, counts read on the device (no host round "
+                       "trip inside the frame); one stream synchronisation per call; backend latency-bound "
+                       "(partition levels, leaves, union-find)"}
     if batch > 1:   # a stream of C5 frames: batches of distinct frames, pipelined over two scratch sets
         # the same frame in `batch` distinct buffers: per-frame cost comparable with the leg above
         db = torch.from_numpy(np.repeat(raw, batch, axis=0)).to(torch.device("cuda", device))

@@ -384,9 +384,7 @@ int ensure_pack(cg_handle* h) {
 // true once *w == seq (acquire: the packed words before it are visible), false after
 // CG_PACK_SPIN_US microseconds
 bool wait_done_word(const uint32_t* w, uint32_t seq) {
-#ifdef CG_NO_DONE_WORD   // (variant builds: the stream wait only)
-    return false;
-#endif
+    if (!CG_HOOK_POLL_DONE_WORD) return false;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t k = 1;; k++) {
         if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return true;
@@ -414,7 +412,9 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
         h->packed = false;
         if (!prepacked) {
             HIPCHK((hipError_t)cg_launch_pack(L, frame, h->d_pack, s));
-            HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_WORDS * 4, hipMemcpyDeviceToHost, s));
+            // every word but the done word: d_pack's copy of it is never written, and a stale
+            // value there must not land where the next split call's wait polls
+            HIPCHK(hipMemcpyAsync(h->h_pack, h->d_pack, CG_PACK_DONE * 4, hipMemcpyDeviceToHost, s));
         }
         // the split launch's done word, polled in host memory (no runtime call); a frame still
         // running after CG_PACK_SPIN_US (a slow backend, a staging timeout) waits on the stream
@@ -611,7 +611,9 @@ RcBox crop_box(float cx, float cy) {
 
 extern "C" {
 
-const char* cg_version(void) { return "cones_gpu 0.1.0 (gfx950)"; }
+// 0.2.0: cg_run_batch_split, cg_debug_front_span and CG_F_PAIR_TIMEOUT removed (round 4;
+// INTEGRATION.md, ABI history)
+const char* cg_version(void) { return "cones_gpu 0.2.0 (gfx950)"; }
 
 void cg_params_init(cg_params* p) {
     if (!p) return;

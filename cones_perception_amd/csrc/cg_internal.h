@@ -122,20 +122,25 @@ enum {
 #define CG_SPLIT_TIMEOUT 40000000ull   // s_memrealtime ticks (100 MHz): 400 ms
 int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStream_t s);
 
-// Host wait for a stream's queued work. Default: hipStreamSynchronize. CG_SPIN_SYNC (a variant
-// build, tools/build_variant.sh): busy-poll hipStreamQuery on the calling thread, trading a
-// host core for the wake-up latency of the blocking wait.
-static inline hipError_t cg_stream_wait(hipStream_t s) {
-#ifdef CG_SPIN_SYNC
-    hipError_t e;
-    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
-    }
-    (void)hipGetLastError();   // the polls' not-ready status is not an error
-    return e;
-#else
-    return hipStreamSynchronize(s);
+// Hooks for experiment builds. tools/build_variant.sh force-includes a header from
+// tools/variants/ that may define them (a kernel stopping after a phase, a spinning stream wait,
+// the done-word poll off); the product build leaves them as below.
+//   CG_HOOK_FRAME_PHASE(k): the frame kernel after phase k (1 pass 1, 2 pass 2 and the
+//     survivor gather, 3 the pads and bounds), every thread, with L, f, N and tid in scope
+//   CG_HOOK_STREAM_WAIT(s): the host's wait for a stream's queued work
+//   CG_HOOK_POLL_DONE_WORD: 0 makes fetch_frame wait on the stream instead of the done word
+#ifndef CG_HOOK_FRAME_PHASE
+#define CG_HOOK_FRAME_PHASE(k) ((void)0)
 #endif
-}
+#ifndef CG_HOOK_STREAM_WAIT
+#define CG_HOOK_STREAM_WAIT(s) hipStreamSynchronize(s)
+#endif
+#ifndef CG_HOOK_POLL_DONE_WORD
+#define CG_HOOK_POLL_DONE_WORD 1
+#endif
+
+// Host wait for a stream's queued work.
+static inline hipError_t cg_stream_wait(hipStream_t s) { return CG_HOOK_STREAM_WAIT(s); }
 
 #ifndef CG_BLOCK
 #define CG_BLOCK 512           // one workgroup (8 waves) per frame, two per CU

@@ -47,22 +47,11 @@ static_assert(SMEM_BYTES <= 163840, "LDS budget");
 static_assert(backend_lds_fits<CG_MMAX, CG_MAX_POINTS / 32>(), "backend overlays fit the LDS arrays");
 // the LDS PCL sort (pcl_sort<2, true>) covers at most two records per thread
 static_assert(CG_MMAX <= 2 * CG_BLOCK, "LDS backend capacity within pcl_block_sort<2>");
-#ifndef CG_CODES_HBM
 static_assert(sizeof(BackLds) >= CG_MAX_POINTS * sizeof(uint8_t), "z-code overlay must fit");
-#endif
-// (experiment, -DCG_CODES_HBM: the z codes in the frame's HBM scratch instead of LDS, so that a
-// smaller CG_MMAX lets more workgroups share a CU)
 // the ground-only mode's per-(k, wave) counts overlay the z codes once pass 2 is done
 static_assert(CG_MAX_POINTS / 64 * sizeof(uint32_t) <= CG_MAX_POINTS, "ground counts fit the code area");
 
-uint64_t cg_scratch_bytes(uint32_t n) {
-    const uint64_t b = cg_work_bytes(n);
-#ifdef CG_CODES_HBM
-    return b > CG_MAX_POINTS ? b : (uint64_t)CG_MAX_POINTS;   // the codes overlay it until compaction
-#else
-    return b;
-#endif
-}
+uint64_t cg_scratch_bytes(uint32_t n) { return cg_work_bytes(n); }
 
 // ------------------------------------------------------------------------------------------
 // Fused per-frame kernel: one 512-lane workgroup per frame, two workgroups per CU (launch
@@ -326,12 +315,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
         }
         __syncthreads();
     } else {
-#ifdef CG_CODES_HBM
-        uint2* const zc = (uint2*)(L.scratch + (uint64_t)f * L.scratch_stride);
-        auto store = [&](int g, uint2 c) { zc[g * CG_BLOCK + tid] = c; };
-#else
         auto store = [&](int g, uint2 c) { ((uint2*)zq)[g * CG_BLOCK + tid] = c; };
-#endif
         if (LAYOUT == CG_LAYOUT_XYZI16 && N == (uint32_t)(PPT * CG_BLOCK))   // whole groups only
             stream_pass1<PPT, LAYOUT, GROUND, FILTER, decltype(store), true>(fb, N, L, P, fs->sec_key, fs->rays,
                                                                           posm, touched, store);
@@ -345,11 +329,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     __syncthreads();
     STAMP(1);
 
-#if defined(CG_EXP_STOP) && CG_EXP_STOP == 1
-    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
-    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    return;
-#endif
+    CG_HOOK_FRAME_PHASE(1);
     const uint32_t lcap = CG_MMAX;
     const Work Wl = lds_work(bl);
     const Work Wg = global_work(L.scratch + (uint64_t)f * L.scratch_stride, N);
@@ -371,13 +351,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     STAMP(2);
 
     // ---- pass 2: ground decisions from the codes ----
-    auto codes_of = [&](int g) {
-#ifdef CG_CODES_HBM
-        return ((const uint2*)(L.scratch + (uint64_t)f * L.scratch_stride))[g * CG_BLOCK + tid];
-#else
-        return ((const uint2*)zq)[g * CG_BLOCK + tid];
-#endif
-    };
+    auto codes_of = [&](int g) { return ((const uint2*)zq)[g * CG_BLOCK + tid]; };
     LaneBits<NW> keepgm, amb;
     keepgm.clear();
     amb.clear();
@@ -527,11 +501,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
   }
     STAMP(4);
 
-#if defined(CG_EXP_STOP) && CG_EXP_STOP == 2
-    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
-    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    return;
-#endif
+    CG_HOOK_FRAME_PHASE(2);
     const uint32_t Ms = fs->scal[S_MS];
     const uint32_t K = GROUND ? fs->scal[S_K] : N;
     // pipeline: the detector input is the groundless cloud, whose N-K trailing
@@ -577,11 +547,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     __syncthreads();
     STAMP(5);
 
-#if defined(CG_EXP_STOP) && CG_EXP_STOP == 3
-    if (tid == 0) { uint32_t* h = L.hdr + (uint64_t)f * 8; h[0] = N; h[1] = h[2] = h[3] = h[4] = h[5] = 0; }
-    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    return;
-#endif
+    CG_HOOK_FRAME_PHASE(3);
     if (use_lds) {
         backend(lds_work(bl), M, fs, L, P, f, flags, CG_MAX_POINTS / 32, CG_MMAX);
     } else {

@@ -252,7 +252,9 @@ def run_tiled_frame(engine, d_tile_ptr: int, first: int, n: int, n_total: int, d
         # (the gather form's one-rank path), with no survivor copy, plan or records
         last_halo_stats.clear()
         last_halo_stats.update(slabs=1, slab_w=None, band=None, survivors=None, voxels=None, halo_sent=0,
-                               halo_received=0, pairs=0)
+                               halo_received=0, pairs=0,
+                               path="one rank, no collectives: the gather form's backend in point order "
+                                    "(no cg_halo_* call)")
         return _run_tiled_gather(engine, d_tile_ptr, first, n, n_total, device, point_step, offsets, dst, fetch,
                                  order=_abi.CG_VOXEL_ORDER_POINT)
     if halo:
@@ -360,6 +362,15 @@ def _all_gather_ints(vals, device):
 last_halo_stats = {}   # the rank's figures of its last run_halo_backend call (tests, bench)
 
 
+def _torch_done(device):
+    """The cg_halo_* calls run on the handle's own stream, which nothing orders after torch's
+    current stream: the tensors they read (gathered, exchanged, sliced there) must be complete
+    first. Every cg_halo_* call returns with its reads done (each ends in a stream wait, and the
+    one-slab cg_halo_local copies its survivors and then waits), so the caller may free or reuse
+    those tensors afterwards."""
+    torch.cuda.current_stream(device).synchronize()
+
+
 def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, fetch: bool = True, sizes=None):
     """The backend of a tiled frame from every rank's survivors (sp (ns, 4) float32, si (ns,)
     frame indices) and the merged counts: slab voxelisation and clustering, halo edges, merge on
@@ -381,17 +392,21 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
         # survivor (on dst) and writes the results itself, asynchronously; no records, no merge
         last_halo_stats.clear()   # voxels: None on dst (on the device), 0 elsewhere
         last_halo_stats.update(slabs=1, slab_w=int(plan.slab_w), band=int(plan.band), survivors=ns,
-                               voxels=None if rank == dst else 0, halo_sent=0, halo_received=0, pairs=0)
+                               voxels=None if rank == dst else 0, halo_sent=0, halo_received=0, pairs=0,
+                               path="run_halo_backend: one slab (cg_halo_plan_frame, survivor gather, "
+                                    "cg_halo_local)")
         if _distributed():
             sp, si = gather_survivors(sp, si, device, dst, sizes=sizes)
             if rank != dst:
                 return None
             ns = int(sp.shape[0])
         nv = C.c_uint32(0)
+        _torch_done(device)
         _abi.check(lib.cg_halo_local(h, C.byref(plan), sp.data_ptr(), si.data_ptr(), ns, plan.n_pads,
                                      total.ctypes.data, n_total, None, 0, C.byref(nv)))
         return engine.fetch(0) if fetch else True
     slab = torch.empty((max(ns, 1),), dtype=torch.int32, device=device)
+    _torch_done(device)
     _abi.check(lib.cg_halo_owner(h, C.byref(plan), sp.data_ptr(), ns, slab.data_ptr()))
     slab = slab[:ns]
     # survivors to their slab's rank; sources hold ascending frame-index ranges, so every rank
@@ -408,6 +423,7 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     cap = n + npad
     rec = torch.empty((max(cap, 1), _abi.CG_HALO_REC_WORDS), dtype=torch.int32, device=device)
     nv = C.c_uint32(0)
+    _torch_done(device)
     _abi.check(lib.cg_halo_local(h, C.byref(plan), mp_.data_ptr(), mi.data_ptr(), n, npad, total.ctypes.data,
                                  n_total, rec.data_ptr(), rec.shape[0], C.byref(nv)))
     rec = rec[: nv.value]
@@ -434,6 +450,7 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     pairs = torch.empty((max(4 * halo.shape[0], 64), 2), dtype=torch.int32, device=device)
     npairs = C.c_uint32(0)
     for _ in range(2 if halo.shape[0] and top.shape[0] else 0):   # no halo rows (the top slab, one rank): no edges
+        _torch_done(device)
         _abi.check(lib.cg_halo_edges(h, top.data_ptr(), top.shape[0], halo.data_ptr(), halo.shape[0],
                                      pairs.data_ptr(), pairs.shape[0], C.byref(npairs)))
         if npairs.value <= pairs.shape[0]:   # once more with room for every pair when the first guess was short
@@ -443,7 +460,9 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
     last_halo_stats.clear()
     last_halo_stats.update(slabs=int(plan.slabs), slab_w=int(plan.slab_w), band=int(plan.band), survivors=n,
                            voxels=int(rec.shape[0]), halo_sent=int(low.shape[0]) if 0 < rank < plan.slabs else 0,
-                           halo_received=int(halo.shape[0]), pairs=int(pairs.shape[0]))
+                           halo_received=int(halo.shape[0]), pairs=int(pairs.shape[0]),
+                           path="run_halo_backend: voxel slabs (all-to-all, cg_halo_local, P2P halo, "
+                                "cg_halo_edges, gather, cg_halo_merge)")
     if _distributed():
         sizes = _all_gather_ints([int(rec.shape[0]), int(pairs.shape[0])], device)
         vmax = max(1, max(s[0] for s in sizes))
@@ -461,6 +480,7 @@ def run_halo_backend(engine, total, sp, si, n_total: int, device, dst: int = 0, 
         pairs = torch.cat([bufs[r][vmax * W: vmax * W + sizes[r][1] * 2].view(-1, 2) for r in range(ws)],
                           0).to(device)
     rec, pairs = rec.contiguous(), pairs.contiguous()
+    _torch_done(device)
     _abi.check(lib.cg_halo_merge(h, C.byref(plan), rec.data_ptr(), rec.shape[0], pairs.data_ptr(), pairs.shape[0],
                                  total.ctypes.data, n_total))
     return engine.fetch(0) if fetch else True

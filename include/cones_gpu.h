@@ -399,6 +399,7 @@ int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words);
 int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes);
 
 /* Exported library version string. */
+/* "cones_gpu MAJOR.MINOR.PATCH (gfx950)"; INTEGRATION.md, ABI history */
 const char* cg_version(void);
 
 /* ---- synthetic frames (harness; src-free of any GPU call) ---------------------------- */

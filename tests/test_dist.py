@@ -94,6 +94,11 @@ def test_bench_gpus_flag_launches_ranks():
     assert rc == 0, err[-2000:]
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["dry_run"] is True
     assert line["config"]["parallelism"] == "frame-shard x2"
+    # the rank census every real run carries: ranks all-gathered over the process group, the
+    # backend, and the distinct devices behind them (none in a dry run)
+    c = line["ranks"]
+    assert c["ranks_seen"] == 2 and c["world_size_env"] == 2 and c["backend"] == "gloo"
+    assert len(c["devices"]) == 2 and c["distinct_devices"] == 0
 
 
 def test_bench_refuses_mismatched_world_size():

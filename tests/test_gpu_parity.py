@@ -126,6 +126,32 @@ def test_single_frame_done_word_never_stale(params):
         assert_same_detection(pipe.cloud_handler(msg), ref, f"call {i}")
 
 
+def test_batch_fetch_between_single_frames(params):
+    """A batch run and a batch fetch on the handle between single-frame calls: the fetch copies
+    the device pack buffer to the pinned one, but never its done word (the split launch's
+    sequence word, which the next single-frame call polls). Every single frame and every fetched
+    batch frame against the oracle."""
+    import torch
+    pipe = cp.ConePipeline(params)
+    frames = []
+    for f, clutter, cpr in ((4, 0, 5), (5, 40, 8), (6, 10, 3)):
+        msg = cp.frame_cloud(cp.synth_frames(1, first_frame=f, rings=64, cols=1024, clutter=clutter,
+                                             cones_per_row=cpr)[0])
+        frames.append((msg, O.run(params, msg, O.MODE_PIPELINE)[0]))
+    raw = cp.synth_frames(2, first_frame=40, rings=64, cols=1024, clutter=20, cones_per_row=6)
+    brefs = [O.run(params, cp.frame_cloud(raw[f]), O.MODE_PIPELINE)[0] for f in range(2)]
+    d = torch.from_numpy(raw).cuda()
+    desc = cp.batch_desc(d.data_ptr(), 2, 65536, 16)
+    lib = _abi.lib()
+    for i in range(60):
+        msg, ref = frames[i % 3]
+        assert_same_detection(pipe.cloud_handler(msg), ref, f"single {i}")
+        _abi.check(lib.cg_run_batch(pipe.handle, C.byref(desc), cp.CG_MODE_PIPELINE, None))
+        r = _abi.cg_detect_result()
+        _abi.check(lib.cg_batch_fetch(pipe.handle, i % 2, C.byref(r)))
+        assert_same_detection(cp._detection(r), brefs[i % 2], f"batch {i}")
+
+
 @pytest.mark.parametrize("frame", [0, 3])
 def test_detector_matches_oracle(params, det, frame):
     raw = cp.synth_frames(1, first_frame=frame, rings=64, cols=1024)
