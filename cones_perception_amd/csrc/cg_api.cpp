@@ -1315,14 +1315,18 @@ int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words) {
 int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
     if (!h || !out) return fail(CG_E_INVALID, "null argument");
     if (!h->d_large) return fail(CG_E_INVALID, "no large frame has run on this handle");
+    // 4: the first 512 bytes of the radix histogram area (phase stamps of variant builds,
+    // tools/variants/lg_stamps.h)
     const void* src = which == 0   ? (const void*)h->lg.meta
                       : which == 1 ? (const void*)h->lg.codes
                       : which == 2 ? (const void*)h->lg.keep
+                      : which == 4 ? (const void*)h->lg.hist
                                    : (const void*)h->lg.pq;
     const uint64_t nch = ((uint64_t)h->large_points + LG_CHUNK - 1) / LG_CHUNK;
     const uint64_t cap = which == 0   ? LG_META_WORDS * 4
                          : which == 1 ? nch * LG_CHUNK
                          : which == 2 ? nch * CG_BLOCK * 16
+                         : which == 4 ? 512
                                       : (uint64_t)cg_large_pq_words() * 4;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, src, std::min(bytes, cap), hipMemcpyDeviceToHost));

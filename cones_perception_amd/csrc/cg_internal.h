@@ -138,6 +138,11 @@ int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 #ifndef CG_HOOK_POLL_DONE_WORD
 #define CG_HOOK_POLL_DONE_WORD 1
 #endif
+//   CG_HOOK_LG_STAMP(S, i): a large-frame kernel's phase i (lg_cluster_tail), thread 0 of the
+//     workgroup, with the LgScratch S in scope
+#ifndef CG_HOOK_LG_STAMP
+#define CG_HOOK_LG_STAMP(S, i) ((void)0)
+#endif
 
 // Host wait for a stream's queued work.
 static inline hipError_t cg_stream_wait(hipStream_t s) { return CG_HOOK_STREAM_WAIT(s); }
@@ -177,6 +182,8 @@ enum {
     LG_NPAD,                   //   PointXYZI() pads after the kept points
     LG_KHDR,                   //   K for the header
     LG_SMALL,                  //   1: the LDS backend (one workgroup) takes the frame
+    LG_PQ_TIMEOUT,             // a partition level's wait for its range gave up (never expected)
+    LG_SW_DONE,                // lg_surv_write's finished workgroups (its last one folds the chunks)
     LG_META_WORDS = 64
 };
 struct LgScratch {
@@ -201,7 +208,9 @@ struct LgScratch {
                               // one workgroup (same-address atomics from every chunk serialise)
     uint32_t* pq;             // PCL voxel order: work queue of introsort ranges (lg_pcl_sort)
     uint32_t pq_cap;          //   entries
-    uint64_t* pqst;           //   the partition levels' look-back words (tickets, finished, per tile)
+    uint64_t* pqst;           //   the partition levels' look-back words (tickets, finished, per tile),
+                              //   two sets of pq_tmax + 2, then two sets of PQ_MAXR range counts
+    uint32_t pq_tmax;         //   tiles a level can have (lg_pq_level)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)

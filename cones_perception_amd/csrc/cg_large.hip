@@ -62,7 +62,8 @@ struct Bounds {
     }
     // whole workgroup: wave partials through LDS (part: 7 * WAVES words), then one lane writes
     // the workgroup's bounds keys and finite count into its chunk statistics words cs
-    __device__ __forceinline__ void merge_block(uint32_t* meta, uint32_t* part) {
+    // rlx: sc1 stores (a workgroup of the same launch folds them, lg_surv_write)
+    __device__ __forceinline__ void merge_block(uint32_t* meta, uint32_t* part, bool rlx = false) {
         float r[6];
 #pragma unroll
         for (int a = 0; a < 3; a++) { r[a] = wave_min(mn[a]); r[3 + a] = wave_max(mx[a]); }
@@ -84,10 +85,12 @@ struct Bounds {
                 t += part[7 * v + 6];
             }
             for (int a = 0; a < 3; a++) {   // (no finite point: keys that change no MIN / MAX)
-                meta[LG_CS_BMIN + a] = t ? cg_fkey(q[a]) : 0xffffffffu;
-                meta[LG_CS_BMAX + a] = t ? cg_fkey(q[3 + a]) : 0u;
+                const uint32_t lo = t ? cg_fkey(q[a]) : 0xffffffffu, hi = t ? cg_fkey(q[3 + a]) : 0u;
+                if (rlx) { st_rlx(meta + LG_CS_BMIN + a, lo); st_rlx(meta + LG_CS_BMAX + a, hi); }
+                else { meta[LG_CS_BMIN + a] = lo; meta[LG_CS_BMAX + a] = hi; }
             }
-            meta[LG_CS_NFIN] = t;
+            if (rlx) st_rlx(meta + LG_CS_NFIN, t);
+            else meta[LG_CS_NFIN] = t;
         }
     }
     __device__ __forceinline__ void merge(uint32_t* meta) {   // every lane of the wave calls
@@ -141,21 +144,23 @@ __device__ __forceinline__ void lg_store_survivor_bits(LgScratch& S, uint32_t c,
 // The fold itself, called by every thread of the block: thread w < LG_CS_WORDS returns word w
 // folded over the nch chunks (words outside wmask: not loaded).
 __device__ __forceinline__ uint32_t lg_fold_core(const LgScratch& S, uint32_t nch, uint32_t wmask,
-                                                 uint32_t (*part)[LG_CS_WORDS]) {
+                                                 uint32_t (*part)[LG_CS_WORDS], bool rlx = false) {
     const uint32_t tid = threadIdx.x, w = tid & 31, q = tid >> 5;   // word, one of 16 chunk strides
     const bool mn = (w <= CG_NUM_BINS) || (w >= LG_CS_BMIN && w < LG_CS_BMIN + 3);
     const bool mx = w >= LG_CS_BMAX && w < LG_CS_BMAX + 3;
     const bool orw = w == LG_CS_TOUCHED;
     uint32_t acc = mn ? 0xffffffffu : 0u;
     auto fold = [&](uint32_t a, uint32_t v) { return mn ? min(a, v) : mx ? max(a, v) : orw ? (a | v) : a + v; };
+    // rlx: sc1 loads (words a workgroup of the same launch stored with sc1)
+    auto ld = [&](uint32_t c) { uint32_t* a = S.cstat + (uint64_t)c * LG_CS_WORDS + w; return rlx ? ld_rlx(a) : *a; };
     if ((wmask >> w) & 1u) {
-        uint32_t c = q;
-        for (; c + 48 < nch; c += 64) {   // four independent loads per trip
-            const uint32_t v0 = S.cstat[(uint64_t)c * LG_CS_WORDS + w], v1 = S.cstat[(uint64_t)(c + 16) * LG_CS_WORDS + w],
-                           v2 = S.cstat[(uint64_t)(c + 32) * LG_CS_WORDS + w], v3 = S.cstat[(uint64_t)(c + 48) * LG_CS_WORDS + w];
-            acc = fold(fold(acc, v0), fold(v1, fold(v2, v3)));
+        for (uint32_t c0 = q; c0 < nch; c0 += 256) {   // sixteen independent loads per trip
+            uint32_t v[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) v[u] = c0 + 16u * u < nch ? ld(c0 + 16u * u) : (mn ? 0xffffffffu : 0u);
+#pragma unroll
+            for (int u = 0; u < 16; u++) acc = fold(acc, v[u]);
         }
-        for (; c < nch; c += 16) acc = fold(acc, S.cstat[(uint64_t)c * LG_CS_WORDS + w]);
     }
     part[q][w] = acc;
     __syncthreads();
@@ -182,10 +187,10 @@ __device__ __forceinline__ void lg_size_fold(const LgScratch& S, uint32_t* m, ui
     if (hint && S.hint) S.hint[LG_HINT_SMALL] = Mt <= CG_MMAX ? 2u : 1u;   // (forced global or not)
 }
 __device__ __forceinline__ void lg_fold_chunks(LgScratch S, uint32_t nch, uint32_t what, uint32_t N = 0,
-                                               uint32_t szfl = 0) {
+                                               uint32_t szfl = 0, bool rlx = false) {
     __shared__ uint32_t part[16][LG_CS_WORDS];
     const uint32_t tid = threadIdx.x, w = tid & 31;
-    const uint32_t a = lg_fold_core(S, nch, 0xffffffffu, part);
+    const uint32_t a = lg_fold_core(S, nch, 0xffffffffu, part, rlx);
     if (tid >= LG_CS_WORDS) return;
     uint32_t* m = S.meta;
     if (what & LG_FOLD_SIZE) {   // (all 32 lanes of wave 0 are here)
@@ -323,8 +328,14 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
 // Survivors of every chunk in frame-index order: the chunk's base is the count of the chunks
 // before it, and within the chunk the order is (k, lane), i.e. the point index. VoxelGrid bounds
 // of the finite survivors merged into the meta words.
+// fold_what != 0 (the device-sized path): the launch's last workgroup to finish folds the chunk
+// statistics (lg_reduce_chunks' work, what = fold_what) instead of a launch after it. The words
+// this launch writes go out with sc1 stores, every thread waits for its stores, then one count
+// per workgroup (meta[LG_SW_DONE], zeroed with the meta words by lg_front); the last reads the
+// words with sc1 loads (MI355X_MICROARCH.md's hand-off table, row 1).
 template <int LAYOUT>
-__global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch S, uint32_t f) {
+__global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch S, uint32_t f, uint32_t fold_what = 0,
+                                                          uint32_t N = 0, uint32_t szfl = 0) {
     constexpr int PPT = LG_CHUNK / CG_BLOCK;
     constexpr int NW = (PPT + 63) / 64;
     __shared__ uint32_t cnt[PPT * WAVES];
@@ -354,7 +365,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
     }
     const uint32_t tot = block_scan(PPT * WAVES, [&](uint32_t i) -> uint32_t { return cnt[i]; },
                                     [&](uint32_t i, uint32_t e) { cnt[i] = e; }, red);
-    if (tid == 0) S.cstat[(uint64_t)c * LG_CS_WORDS + LG_CS_MS] = tot;
+    if (tid == 0) {
+        if (fold_what) st_rlx(S.cstat + (uint64_t)c * LG_CS_WORDS + LG_CS_MS, tot);
+        else S.cstat[(uint64_t)c * LG_CS_WORDS + LG_CS_MS] = tot;
+    }
     const uint32_t b0 = cbase;
     const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t pidx0 = S.pidx_base + (uint32_t)base;
@@ -381,7 +395,15 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
         }
     }
     __shared__ uint32_t part[7 * WAVES];
-    bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, part);
+    bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, part, fold_what != 0);
+    if (!fold_what) return;
+    __shared__ uint32_t last;
+    __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this thread's words are stored
+    __syncthreads();
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(&S.meta[LG_SW_DONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (last) lg_fold_chunks(S, gridDim.x, fold_what, N, szfl, true);
 }
 
 // Ground-only output: each chunk's kept points at its stable offset, then the zero pads.
@@ -805,6 +827,25 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
     m[LG_NCELL] = ncell;
 }
 
+// PCL order's partition levels (lg_pq_*, below): sizes and the range lists' header words
+#define LG_PCL_LEAF 4096       // the longest leaf sorted in LDS
+#ifndef LG_PCL_CUT
+#define LG_PCL_CUT LG_PCL_LEAF   // the levels cut ranges longer than this
+#endif
+#define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
+                               // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
+#define PQ_WAVES 6
+#define PQ_MIDS 7
+#define PQ_TILES 8             // S.ca: [0] a level's tile count; from word 8, eight words per tile
+                               // (range, median, pivot, budget, range index, tile in range):
+                               // lg_pq_split -> lg_pq_swap (<= 8 (N / 512 + 2048) + 8 words)
+#define PQ_LEAFLIST 3
+#define PQ_EW 5                // entry words: first, last, depth, then nL, nR (levels) / buffer (leaves)
+#define PQ_T CG_BLOCK          // elements per tile
+#define PQ_MAXR 2048           // ranges per level (levels <= 11)
+#define LG_PQ_LEVELS_MAX 11
+#define LG_PQ_CAP ((2u << LG_PQ_LEVELS_MAX) + 64)   // entries per list: a level pushes <= 2 per range
+
 // keys: passthrough -> pidx; else (PCL idx << PB | pidx), non-finite idx = 0xffffffff (last)
 // Every workgroup derives the grid words from the bounds (lg_grid_setup); workgroup 0 also
 // stores them in the meta words for the kernels after it (a halo slab: with its own count of
@@ -997,23 +1038,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_voxel_centroids(CgLaunch L, LgScr
 // level with no range returns at once. lg_pcl_leaf finishes each leaf with pcl_block_sort in
 // LDS (up to 4096 records, 8 per thread, results straight to the outputs), with the depth
 // budget left on its path; a range still longer (a degenerate split) in HBM.
-#define LG_PCL_LEAF 4096       // the longest leaf sorted in LDS
-#ifndef LG_PCL_CUT
-#define LG_PCL_CUT LG_PCL_LEAF   // the levels cut ranges longer than this
-#endif
-#define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
-                               // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
-#define PQ_WAVES 6
-#define PQ_MIDS 7
-#define PQ_TILES 8             // S.ca: [0] a level's tile count; from word 8, eight words per tile
-                               // (range, median, pivot, budget, range index, tile in range):
-                               // lg_pq_split -> lg_pq_swap (<= 8 (N / 512 + 2048) + 8 words)
-#define PQ_LEAFLIST 3
-#define PQ_EW 5                // entry words: first, last, depth, then nL, nR (levels) / buffer (leaves)
-#define PQ_T CG_BLOCK          // elements per tile
-#define PQ_MAXR 2048           // ranges per level (levels <= 11)
-#define LG_PQ_LEVELS_MAX 11
-#define LG_PQ_CAP ((2u << LG_PQ_LEVELS_MAX) + 64)   // entries per list: a level pushes <= 2 per range
 struct PclCompactFlag {   // finite points (non-finite keys carry idx 0xffffffff)
     const uint64_t* key; uint32_t PB;
     const uint32_t* meta;   // (the device-sized path: a passthrough frame lists nothing, so its
@@ -1029,6 +1053,72 @@ struct PclCompactEmit {
         E[r] = ((uint64_t)(uint32_t)(key[j] >> PB) << 32) | val[j];
     }
 };
+
+// The device-sized path's index_vector in one launch (lg_voxel_keys + lg_scan_emit with
+// PclCompact*): each tile of LG_TILE survivors computes its points' voxel keys, lists the finite
+// ones in frame-index order through the decoupled look-back and writes their (idx << 32 | slot)
+// records to Eout; the count goes to meta[LG_PCL_N]. The keys and slots also go to key0 / val0
+// (a passthrough frame keeps them as its order). Workgroup 0 writes the grid words to the meta
+// words and empties the partition lists; every workgroup zeroes its share of the neighbour
+// grid's cell counts (lg_voxel_centroids counts into them). Survivors arrive in frame-index
+// order (lg_surv_write), so the keys carry no frame-index bits (PB = 0).
+__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParams P, uint64_t* Eout) {
+    __shared__ uint32_t m[LG_META_WORDS];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t* in = S.meta;
+    const uint32_t Mtot = in[LG_MTOT], npad = in[LG_NPAD];
+    if (tid == 0) {
+        lg_grid_setup(in, m, P, npad, Mtot);
+        if (Mtot == 0) m[LG_NCELL] = 0;
+        if (blockIdx.x == 0) {
+            S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0; S.pq[PQ_MIDS] = 0;
+            lg_grid_setup(in, S.meta, P, npad, Mtot);
+            if (Mtot == 0) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = S.meta[LG_NCELL] = 0;
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t nc = m[LG_NCELL] + 1;
+        for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
+    }
+    const uint32_t active = Mtot ? (Mtot + LG_TILE - 1) / LG_TILE : 1u;
+    if (blockIdx.x >= active) return;
+    const uint32_t t = lg_tile_ticket(S.sstat);
+    const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)tid * 8;
+    const uint32_t Ms = in[LG_MS];
+    const bool pass = m[LG_PASS] != 0;
+    const float mnb0 = (float)(int)m[LG_MINB], mnb1 = (float)(int)m[LG_MINB + 1], mnb2 = (float)(int)m[LG_MINB + 2];
+    const uint32_t mul1 = m[LG_MUL1], mul2 = m[LG_MUL2];
+    uint32_t idx[8], c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const uint64_t j = b0 + q;
+        idx[q] = 0xffffffffu;
+        if (j < Mtot) {
+            const float4 p = lg_point(S, (uint32_t)j, Ms);
+            uint64_t key = 0ull;   // passthrough: frame-index order (nothing listed)
+            if (!pass) {
+                if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
+                    key = 0xffffffffull;
+                } else {   // lg_voxel_keys's arithmetic
+                    const int i0 = (int)(floorf(p.x * P.inv_leaf[0]) - mnb0);
+                    const int i1 = (int)(floorf(p.y * P.inv_leaf[1]) - mnb1);
+                    const int i2 = (int)(floorf(p.z * P.inv_leaf[2]) - mnb2);
+                    key = (uint64_t)((uint32_t)i0 + (uint32_t)i1 * mul1 + (uint32_t)i2 * mul2);
+                    idx[q] = (uint32_t)key;
+                }
+            }
+            S.key0[j] = key;
+            S.val0[j] = (uint32_t)j;
+            c += idx[q] != 0xffffffffu ? 1u : 0u;
+        }
+    }
+    uint32_t pos = lg_tile_scan(S.sstat, t, active, c, S.meta + LG_PCL_N);
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if (idx[q] != 0xffffffffu) Eout[pos++] = ((uint64_t)idx[q] << 32) | (uint32_t)(b0 + q);
+    lg_tile_done(S.sstat, active);
+}
 
 __device__ __forceinline__ uint32_t pq_key(const uint64_t* E, uint32_t x) {
     return ((const uint32_t*)E)[2 * x + 1];
@@ -1256,6 +1346,231 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// One launch per partition level (the device-sized path): lg_pq_split's split and lg_pq_swap's
+// swaps in one launch.
+//   Split phase: workgroups take tiles by ticket and run each tile's split (median of three,
+//   >= / <= counts, the look-back segmented by range, the L / R lists). A workgroup takes its
+//   tickets (at most ceil(tiles / grid)) before it waits on anything, and a tile's look-back
+//   only waits on tiles with smaller tickets, which are held by workgroups still in this phase:
+//   every split finishes, whatever the grid and whatever else holds the CUs.
+//   Swap phase: for each tile it holds, a workgroup waits until every tile of the tile's range
+//   has written its lists, then runs the tile's swaps and, at the range's last swap, queues the
+//   children. The wait is on one 64-bit word per range: every tile adds 1 << 46 | its >= count
+//   << 23 | its <= count once its lists are stored, so the word that shows all the range's tiles
+//   also holds the range's totals nL and nR (< 2^23: ranges of at most LG_DEV_MAX_POINTS).
+// The lists cross workgroups (and XCDs) inside the launch: sc1 stores (st_rlx), every storing
+// wave's vmcnt(0), a barrier, one agent-scope add per tile; the reader polls and loads with sc1
+// (ld_rlx): MI355X_MICROARCH.md's hand-off table, row 1. No release fence (an agent-scope
+// release writes back the XCD's whole L2).
+// The ticket counter, look-back words and range words alternate between two sets by level
+// parity; each level clears the set the next level uses (its last user, the level before, has
+// ended), and lg_pcl_leaf clears the last level's set.
+// A workgroup's first tile keeps its state in registers; further tiles (only when the level has
+// more tiles than the grid) leave theirs in the tile table (S.ca) and their ranks in S.vox.
+#define PQ_OWN 16   // tiles per workgroup and level beyond the first (the host sizes the grid)
+#define PQ_RW_TILE (1ull << 46)
+#define PQ_RW_N ((1ull << 23) - 1ull)
+static_assert(LG_DEV_MAX_POINTS < (1u << 23), "range totals fit 23 bits");
+__device__ __forceinline__ uint64_t* pq_set(const LgScratch& S, uint32_t par) {
+    return S.pqst + (uint64_t)par * (S.pq_tmax + 2u);
+}
+__device__ __forceinline__ uint64_t* pq_done(const LgScratch& S, uint32_t par) {
+    return S.pqst + 2ull * (S.pq_tmax + 2u) + (uint64_t)par * PQ_MAXR;
+}
+// the set of parity par as no level has used it: ticket counter, look-back words of the tiles
+// that took tickets, range words (every thread of the block)
+__device__ __forceinline__ void pq_clear_set(const LgScratch& S, uint32_t par) {
+    uint64_t* const st = pq_set(S, par);
+    const uint32_t used = (uint32_t)min(st[0], (uint64_t)S.pq_tmax);   // tickets handed out
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < used + 2u; i += CG_BLOCK) st[i] = 0ull;
+    uint64_t* const dn = pq_done(S, par);
+    for (uint32_t i = threadIdx.x; i < PQ_MAXR; i += CG_BLOCK) dn[i] = 0ull;
+}
+#define PQ_WAIT_TICKS 20000000ull   // s_memrealtime (100 MHz): 200 ms, then LG_PQ_TIMEOUT
+__global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint64_t* E, uint64_t* Eo, uint32_t level,
+                                                        uint32_t last_level, uint32_t out_buf) {
+    __shared__ uint32_t tp[PQ_MAXR + 1];
+    __shared__ uint32_t red[8 * WAVES];
+    __shared__ uint32_t tk, cg[WAVES], cl[WAVES], nown;
+    __shared__ uint32_t own[PQ_OWN];
+    __shared__ uint64_t tbase, rword;
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint32_t par = level & 1u;
+    uint64_t* const st = pq_set(S, par);
+    uint64_t* const done = pq_done(S, par);
+    const uint32_t n = S.meta[LG_PCL_N];
+    if (blockIdx.x == 0) {
+        pq_clear_set(S, par ^ 1u);   // for level + 1
+        if (tid == 0) {
+            if (level == 0) {   // (the lists' counts were zeroed by lg_pcl_index: this level pushes)
+                if (n <= LG_PCL_CUT) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
+            } else {
+                S.pq[(level + 2u) % 3u] = 0;   // the list level + 1 fills
+            }
+        }
+    }
+    {
+        const uint32_t nr0 = level == 0 ? (n > LG_PCL_CUT ? 1u : 0u) : min(S.pq[level % 3u], (uint32_t)PQ_MAXR);
+        if (nr0 == 0) return;   // nothing to cut at this level
+        // workgroups past the level's tiles (at most one per PQ_T records plus one per range)
+        // return before their ticket: 512 tickets on one word take ~6 us to hand out
+        if (blockIdx.x >= (n + PQ_T - 1) / PQ_T + nr0) return;
+    }
+    // the first ticket before the range lists' loads (its latency overlaps them)
+    if (tid == 0) {
+        tk = (uint32_t)__hip_atomic_fetch_add(&st[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nown = 0;
+    }
+    uint32_t nr;
+    const uint32_t active = pq_tiles(S, level, tp, red, nr);   // ends with a barrier
+    if (tk == 0 && level < 7) CG_HOOK_LG_STAMP(S, 16 + 6 * level);
+    // tickets per workgroup: ceil(active / grid) of them take every tile
+    const uint32_t kmax = min((active + gridDim.x - 1) / gridDim.x, (uint32_t)PQ_OWN + 1u);
+    // the first tile's state (registers)
+    uint32_t t0 = 0xffffffffu, f0 = 0, e0 = 0, m0 = 0, p0 = 0, d0 = 0, r0 = 0, q0 = 0, gi0 = 0, li0 = 0;
+    uint64_t rx0 = 0, rf0 = 0;
+    for (uint32_t it = 0; it < kmax; it++) {
+        if (it > 0) {
+            if (tid == 0) tk = (uint32_t)__hip_atomic_fetch_add(&st[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+        }
+        const uint32_t t = tk;
+        if (t >= active) break;
+        const uint32_t r = pq_find(tp, nr, t), q = t - tp[r];
+        uint32_t f, e, d;
+        pq_range(S, level, r, f, e, d);
+        // the median of three and this element's record in one batch of loads: x > f, and x's
+        // virtual record is E[f] when x is the median (__move_median_to_first's swap)
+        const uint32_t x = f + 1 + q * PQ_T + tid;
+        const bool valid = x < e;
+        const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
+        const uint32_t ka = pq_key(E, a), kb = pq_key(E, b), kc = pq_key(E, c);
+        const uint64_t rf = E[f];
+        const uint64_t rx = valid ? E[x] : 0ull;
+        const uint32_t m = pb_median(a, b, c, ka, kb, kc);
+        const uint32_t p = m == a ? ka : (m == b ? kb : kc);
+        const uint32_t k = valid ? (x == m ? pcl_key(rf) : pcl_key(rx)) : 0u;
+        const bool ge = valid && k >= p, le = valid && k <= p;
+        const uint64_t gm = __ballot(ge), lm = __ballot(le);
+        if (l == 0) { cg[w] = (uint32_t)__popcll(gm); cl[w] = (uint32_t)__popcll(lm); }
+        __syncthreads();
+        uint32_t tg = 0, tl = 0;
+        for (uint32_t v = 0; v < WAVES; v++) { tg += cg[v]; tl += cl[v]; }
+        if (w == 0) {
+            const uint64_t bs = pq_lookback(st + 2, tp[r], t, ((uint64_t)tg << 32) | tl);
+            if (l == 0) tbase = bs;
+        }
+        __syncthreads();
+        if (t == 0 && level < 7) CG_HOOK_LG_STAMP(S, 17 + 6 * level);
+        uint32_t gi = (uint32_t)(tbase >> 32) + mbcnt(gm), li = (uint32_t)tbase + mbcnt(lm);
+        for (uint32_t v = 0; v < w; v++) { gi += cg[v]; li += cl[v]; }
+        if (ge) st_rlx(S.par + f + 1 + gi, x);
+        if (le) st_rlx(S.cnt + f + 1 + li, x);
+        if (it == 0) {
+            t0 = t; f0 = f; e0 = e; m0 = m; p0 = p; d0 = d; r0 = r; q0 = q; gi0 = gi; li0 = li; rx0 = rx; rf0 = rf;
+        } else {   // (a level with more tiles than workgroups) the tile's state for its swaps
+            if (valid) ((uint64_t*)S.vox)[x] = ((uint64_t)gi << 32) | li;
+            if (tid == 0) {
+                uint32_t* tt = S.ca + PQ_TILES + 8u * t;
+                tt[0] = f; tt[1] = e; tt[2] = m; tt[3] = p; tt[4] = d; tt[5] = r; tt[6] = q; tt[7] = 0u;
+                own[it - 1] = t;
+                nown = it;
+            }
+        }
+        // the tile's list stores done in every wave, then its counts into the range's word
+        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
+        __syncthreads();
+        if (t == 0 && level < 7) CG_HOOK_LG_STAMP(S, 18 + 6 * level);
+        if (tid == 0)
+            __hip_atomic_fetch_add(&done[r], PQ_RW_TILE | ((uint64_t)tg << 23) | tl, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 && level < 7) CG_HOOK_LG_STAMP(S, 19 + 6 * level);
+    }
+    if (t0 == 0xffffffffu) return;   // (uniform) no tile for this workgroup
+    const uint32_t extra = nown;
+    for (uint32_t j = 0; j <= extra; j++) {
+        uint32_t f, e, m, p, d, r, q, gi, li;
+        uint64_t rx, rf;
+        if (j == 0) {
+            f = f0; e = e0; m = m0; p = p0; d = d0; r = r0; q = q0; gi = gi0; li = li0; rx = rx0; rf = rf0;
+        } else {
+            const uint32_t t = own[j - 1];
+            const uint4 ta = ((const uint4*)(S.ca + PQ_TILES))[2 * t], tb = ((const uint4*)(S.ca + PQ_TILES))[2 * t + 1];
+            f = ta.x; e = ta.y; m = ta.z; p = ta.w; d = tb.x; r = tb.y; q = tb.z;
+            const uint32_t x = f + 1 + q * PQ_T + tid;
+            rf = E[f];
+            rx = x < e ? E[x] : 0ull;
+            const uint64_t rk = x < e ? ((const uint64_t*)S.vox)[x] : 0ull;
+            gi = (uint32_t)(rk >> 32); li = (uint32_t)rk;
+        }
+        // every tile of the range has stored its lists: the range's word counts them all, and
+        // then holds the totals
+        if (tid == 0) {
+            const uint64_t need = (uint64_t)(tp[r + 1] - tp[r]);
+            const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+            uint64_t wv;
+            while (((wv = ld64(&done[r])) >> 46) < need) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t_0 > PQ_WAIT_TICKS) {   // (never expected)
+                    S.meta[LG_PQ_TIMEOUT] = 1u;
+                    break;
+                }
+            }
+            rword = wv;
+        }
+        if (t0 == 0 && j == 0 && level < 7) CG_HOOK_LG_STAMP(S, 20 + 6 * level);   // (the tile-0 holder)
+        __syncthreads();
+        const uint64_t rw = rword;
+        const uint32_t nL = (uint32_t)(rw >> 23) & (uint32_t)PQ_RW_N, nR = (uint32_t)rw & (uint32_t)PQ_RW_N;
+        const uint32_t x = f + 1 + q * PQ_T + tid;
+        if (q == 0 && tid == 0) Eo[f] = E[m];
+        if (x < e) {
+            const uint64_t vx = x == m ? rf : rx;
+            const uint32_t k = pcl_key(vx);
+            const bool ge = k >= p, le = k <= p;
+            // the partners and the next pair in one batch of loads (indices clamped when unused)
+            const bool hasL = ge && gi < nR;
+            const bool nx = hasL && gi + 1 < min(nL, nR);
+            const uint32_t ri = nR - 1 - li;
+            const bool hasR = le && ri < nL;
+            const uint32_t jj = ld_rlx(S.cnt + f + 1 + (hasL ? nR - 1 - gi : 0u));        // R_gi
+            const uint32_t l2 = ld_rlx(S.par + f + 1 + (gi + 1 < nL ? gi + 1 : 0u));       // L_gi+1
+            const uint32_t r2 = ld_rlx(S.cnt + f + 1 + (nx ? nR - 2 - gi : 0u));           // R_gi+1
+            const uint32_t il = ld_rlx(S.par + f + 1 + (hasR ? ri : 0u));                  // L_ri
+            uint32_t partner = x;
+            bool cutter = false;
+            uint32_t cut = 0;
+            if (hasL) {
+                if (x < jj) {
+                    partner = jj;
+                    if (!nx || !(l2 < r2)) {   // swap gi is the last: s = gi + 1
+                        cutter = true;
+                        cut = min(gi + 1 < nL ? l2 : 0xffffffffu, jj);
+                    }
+                } else if (gi == 0) {   // no swap at all: the left scan stops at L_0
+                    cutter = true;
+                    cut = x;
+                }
+            }
+            if (hasR && il < x) partner = il;
+            Eo[x] = partner == x ? vx : (partner == m ? rf : E[partner]);
+            if (cutter) {
+                const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
+                for (int c = 0; c < 2; c++) {
+                    if (hi[c] - lo[c] > LG_PCL_CUT && d > 1 && level < last_level)
+                        pq_push(S, (level + 1u) % 3u, lo[c], hi[c], d - 1u, 0u);
+                    else
+                        pq_push(S, PQ_LEAFLIST, lo[c], hi[c], d - 1u, out_buf);
+                }
+            }
+        }
+        __syncthreads();   // (rword is rewritten for the next tile)
+    }
+    if (t0 == 0 && level < 7) CG_HOOK_LG_STAMP(S, 21 + 6 * level);
+}
+
 // A leaf's results straight to the outputs: idx in the key array, slot in the value array.
 struct PqLeafOut {
     uint64_t* k; uint32_t* v; uint32_t base;
@@ -1295,13 +1610,18 @@ struct PqDefer {
 // the buffer its last level wrote: in LDS (8 B of record and 24 B of scratch per element),
 // else in HBM (ranges are disjoint, so each uses its own span of the scratch arrays).
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
-                                                        uint32_t* vout) {
+                                                        uint32_t* vout, uint32_t clear_set) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PCL_LDS];
     __shared__ uint32_t red[8 * WAVES];
     const uint32_t n = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
     const uint32_t tid = threadIdx.x;
-    // the split's ticket counter, also when no level followed the level-0 split (no swap)
-    if (blockIdx.x == 0 && tid == 0) S.pqst[0] = 0;
+    // the split's ticket counter, also when no level followed the level-0 split (no swap);
+    // lg_pq_level's levels: the last level's set (clear_set = its parity + 1)
+    if (blockIdx.x == 0 && tid == 0 && !clear_set) S.pqst[0] = 0;
+    if (blockIdx.x == 0 && clear_set) {
+        pq_clear_set(S, clear_set - 1u);
+        __syncthreads();
+    }
     for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
         const uint32_t* ent = pq_list(S, PQ_LEAFLIST) + PQ_EW * b;
         const uint32_t first = ent[0], last = ent[1], depth = ent[2], size = last - first;
@@ -1407,6 +1727,49 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_scan(LgScratch S) {
     for (int q = 0; q < 8; q++)
         if (b0 + q < n) { S.cstart[b0 + q] = pos; pos += x[q]; }
     lg_tile_done(S.sstat, active);
+}
+// lg_dgrid_scan and lg_dgrid_fill in one launch (the device-sized path): the tiles publish
+// their cell starts with sc1 stores, every thread waits for its stores before its tile counts as
+// done, and the last tile to finish fills ord reading the starts with sc1 loads (the hand-off
+// of MI355X_MICROARCH.md's table, row 1; no release fence).
+__global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_scan_fill(LgScratch S) {
+    __shared__ uint32_t last;
+    const uint32_t n = S.meta[LG_NCELL] + 1;
+    const uint32_t active = (n + LG_TILE - 1) / LG_TILE;
+    if (blockIdx.x >= active) return;
+    const uint32_t t = lg_tile_ticket(S.sstat);
+    const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)threadIdx.x * 8;
+    uint32_t x[8], c = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) { x[q] = (b0 + q < n) ? S.cstart[b0 + q] : 0u; c += x[q]; }
+    uint32_t pos = lg_tile_scan(S.sstat, t, active, c, nullptr);
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        if (b0 + q < n) { st_rlx(&S.cstart[b0 + q], pos); pos += x[q]; }
+    __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this thread's starts are stored
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(&S.sstat[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == active - 1;
+    __syncthreads();
+    if (!last) return;
+    for (uint32_t i = threadIdx.x; i < active + 2; i += CG_BLOCK) S.sstat[i] = 0;   // (lg_tile_done's reset)
+    const uint32_t V = S.meta[LG_V];
+    for (uint32_t vb = 0; vb < V; vb += 8 * CG_BLOCK) {   // eight voxels in flight per thread
+        uint32_t uk[8], ca[8], st[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t v = vb + (uint32_t)q * CG_BLOCK + threadIdx.x;
+            uk[q] = v < V ? S.uk[v] : 0u;
+            ca[q] = v < V ? S.ca[v] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) st[q] = vb + (uint32_t)q * CG_BLOCK + threadIdx.x < V ? ld_rlx(&S.cstart[uk[q]]) : 0u;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t v = vb + (uint32_t)q * CG_BLOCK + threadIdx.x;
+            if (v < V) S.ord[st[q] + ca[q]] = v;
+        }
+    }
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_fill(LgScratch S) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
@@ -1710,6 +2073,343 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
         lg_centroids_one(L, P, S, f, k, key, vmask);
 }
 
+// ------------------------------------------------------------------------------------------
+// The clustering's tail in one workgroup (the device-sized path): roots, component sizes, the
+// size filter, PCL's cluster order, labels, the CSR and the per-cluster centroids -- what
+// lg_find, the KeepRoot scan, lg_order, lg_labels, the CSR's rank sort and lg_csr_centroids do
+// in seven launches, here in one (the stages are short: a few thousand voxels, tens of clusters;
+// each launch boundary cost more than its stage). The voxel arrays live in LDS below
+// LG_TAIL_LDS voxels, else in the HBM scratch (same code, slower).
+//   A: parents, then the kept roots (droot, ascending = PCL's discovery order), then the
+//      cluster offsets; B: each voxel's root, then its cluster rank (or ~0);
+//   Cc: component sizes by root, then each root's cluster rank; D: kept sizes (dsz);
+//   Ef: the cluster order (fin), then the CSR member list; B and Cc hold the voxels' x, y for
+//   the centroid sums at the end (LDS form).
+// The CSR lists cluster k's members in ascending voxel index (PCL's extract sorts them): one
+// wave per cluster collects them by ballots over the rank array, so the cost is C * V / 64
+// ballots (C5: 36 clusters, 5,363 voxels).
+#define LG_TAIL_LDS 7168
+// The lanes of the wave whose value v (< 2^nb) equals this lane's, among the lanes of `act`:
+// one ballot per bit (a constant cost, where a loop over the distinct values of a wave costs a
+// round per value).
+__device__ __forceinline__ uint64_t lg_match(uint32_t v, uint32_t nb, uint64_t act) {
+    uint64_t m = act;
+    for (uint32_t b = 0; b < nb; b++) {
+        const bool bit = (v >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+// LDS word add (ds_add_u32) or global atomic add, by pointer kind
+__device__ __forceinline__ void lg_add(lds_u32* p, uint32_t v) { __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+__device__ __forceinline__ void lg_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+template <class K>
+__device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParams& P, const LgScratch& S, uint32_t f,
+                                             uint32_t V, typename K::P32 A, typename K::P32 B, typename K::P32 Cc,
+                                             typename K::P32 D, typename K::P32 Ef, bool lds, uint32_t* red,
+                                             int32_t* stk) {
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint64_t lt = (1ull << l) - 1ull;
+    CG_HOOK_LG_STAMP(S, 1);
+    // 1. parents (flattened by lg_flatten, then united across trees by lg_cross), sixteen
+    //    loads in flight per thread (one round trip for C5's 5,363 voxels)
+    if (lds) {
+        for (uint32_t vb = 0; vb < V; vb += 16 * CG_BLOCK) {
+            uint32_t pv[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+                pv[q] = v < V ? S.par[v] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+                if (v < V) A[v] = pv[q];
+            }
+        }
+        __syncthreads();
+    }
+    CG_HOOK_LG_STAMP(S, 2);
+    // 2. roots (the forest's roots are the components' lowest indices = PCL's seeds)
+    for (uint32_t vb = 0; vb < V; vb += 4 * CG_BLOCK) {   // four chases interleaved
+        uint32_t r[4], p[4];
+        bool go = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) r[q] = min(vb + (uint32_t)q * CG_BLOCK + tid, V - 1);
+        while (go) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) p[q] = A[r[q]];
+            go = false;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                go |= p[q] != r[q];
+                r[q] = p[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+            if (v < V) { B[v] = r[q]; Cc[v] = 0u; }
+        }
+    }
+    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 3);
+    // 3. component sizes (LDS atomics: the LDS unit takes a wave's same-address adds in turn,
+    //    cheaper than matching the lanes' roots first)
+    for (uint32_t v = tid; v < V; v += CG_BLOCK) lg_add(&Cc[B[v]], 1u);
+    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 4);
+    // 4. the size filter over the seeds in ascending order (PCL's discovery order): droot in A,
+    //    sizes in D; each thread scans `per` consecutive voxels
+    const uint32_t per = (V + CG_BLOCK - 1) / CG_BLOCK;
+    const uint32_t v0 = min(V, tid * per), v1 = min(V, v0 + per);
+    uint32_t mine = 0;
+    for (uint32_t v = v0; v < v1; v++) {
+        const uint32_t c = Cc[v];
+        mine += (B[v] == v && c >= P.min_cl && c <= P.max_cl) ? 1u : 0u;
+    }
+    const uint32_t inc = wave_incl_scan(mine);
+    if (l == 63) red[w] = inc;
+    __syncthreads();
+    uint32_t base = inc - mine, C = 0;
+    for (uint32_t q = 0; q < WAVES; q++) {
+        base += q < w ? red[q] : 0u;
+        C += red[q];
+    }
+    for (uint32_t v = v0; v < v1; v++) {
+        const uint32_t c = Cc[v];
+        if (B[v] == v && c >= P.min_cl && c <= P.max_cl) { A[base] = v; D[base] = c; base++; }
+    }
+    __syncthreads();
+    for (uint32_t v = tid; v < V; v += CG_BLOCK) Cc[v] = 0xffffffffu;   // ranks by root (~0: dropped)
+    CG_HOOK_LG_STAMP(S, 5);
+    // 5. PCL's cluster order: the reversed discovery list sorted by size with std::sort
+    //    (cg_sort.h); fin (Ef): cluster k -> its index d in the discovery list
+    if (C > CG_SORT_THRESHOLD && C <= 64) {
+        // one wave, one record (size << 32 | d) per lane: pw_range64 is libstdc++'s introsort on
+        // at most 64 records in registers (the PCL voxel order's wave form), here with the
+        // whole sort's depth budget; the records go out through Ef's upper half (free)
+        if (w == 0) {
+            typename K::P64 rec = (typename K::P64)(Ef + ((LG_TAIL_LDS / 2) & ~1u));
+            if (!lds) rec = (typename K::P64)S.key0;
+            if (l < C) rec[l] = ((uint64_t)D[C - 1 - l] << 32) | (C - 1 - l);
+            pw_range64(rec, 0u, C, (uint32_t)(2 * cg_lg((long)C)), [&](uint32_t i, uint64_t r) {
+                Ef[C - 1 - i] = (uint32_t)r;
+            });
+        }
+    } else if (C > CG_SORT_THRESHOLD) {   // one lane, the records in the HBM scratch (rare)
+        uint64_t* rec = S.key0;
+        for (uint32_t i = tid; i < C; i += CG_BLOCK) {
+            const uint32_t d = C - 1 - i;
+            rec[i] = ((uint64_t)D[d] << 32) | d;
+        }
+        __syncthreads();
+        if (tid == 0) cg_std_sort(rec, (long)C, [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); }, stk);
+        __syncthreads();
+        for (uint32_t k = tid; k < C; k += CG_BLOCK) Ef[k] = (uint32_t)rec[C - 1 - k];
+    } else {   // <= 16 clusters: an insertion sort, (size desc, seed asc)
+        for (uint32_t d = tid; d < C; d += CG_BLOCK) {
+            const uint32_t sd = D[d];
+            uint32_t r = 0;
+            for (uint32_t e = 0; e < C; e++) {
+                const uint32_t se = D[e];
+                r += (se > sd) || (se == sd && e < d);
+            }
+            Ef[r] = d;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < C; k += CG_BLOCK) Cc[A[Ef[k]]] = k;   // each kept root's rank
+    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 6);
+    // 6. cluster offsets in A (the discovery list is used up), each thread over consecutive k
+    {
+        const uint32_t pk = (C + CG_BLOCK - 1) / CG_BLOCK;
+        const uint32_t k0 = min(C, tid * pk), k1 = min(C, k0 + pk);
+        uint32_t s = 0;
+        for (uint32_t k = k0; k < k1; k++) s += D[Ef[k]];
+        const uint32_t in2 = wave_incl_scan(s);
+        if (l == 63) red[w] = in2;
+        __syncthreads();
+        uint32_t b2 = in2 - s, tot = 0;
+        for (uint32_t q = 0; q < WAVES; q++) {
+            b2 += q < w ? red[q] : 0u;
+            tot += red[q];
+        }
+        for (uint32_t k = k0; k < k1; k++) {
+            const uint32_t c = D[Ef[k]];
+            A[k] = b2;
+            b2 += c;
+        }
+        if (tid == 0) A[C] = tot;
+    }
+    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 7);
+    // 7. labels (cluster rank or -1) to the output; B becomes each voxel's rank
+    int32_t* const lab_out = L.lab + (uint64_t)f * L.cap;
+    for (uint32_t v = tid; v < V; v += CG_BLOCK) {
+        const uint32_t rk = Cc[B[v]];
+        lab_out[v] = rk == 0xffffffffu ? -1 : (int32_t)rk;
+        B[v] = rk;
+    }
+    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 8);
+    // 8. the CSR: every cluster's members in ascending voxel index. Each wave takes a block of
+    //    consecutive voxels: it counts its members per cluster (D as WAVES x C counters, free
+    //    now), the counts become each wave's start per cluster, and the wave writes its members
+    //    there in voxel order, one round per distinct cluster in a 64-voxel chunk. (More than
+    //    (V + 2) / WAVES clusters: one wave per cluster collects them by ballots instead.)
+    int32_t* const idx_out = L.idx + (uint64_t)f * L.cap;
+    if ((uint64_t)WAVES * C <= V + 2) {
+        const uint32_t blk = ((V + WAVES * 64 - 1) / (WAVES * 64)) * 64;   // voxels per wave
+        const uint32_t wb0 = min(V, w * blk), wb1 = min(V, wb0 + blk);
+        typename K::P32 cw = D + w * C;
+        for (uint32_t k = l; k < C; k += 64) cw[k] = 0u;
+        const uint32_t cbits = cg_bits_of(C);
+        for (uint32_t v = wb0 + l; v < wb1; v += 64) {
+            const uint32_t rr = B[v];
+            if (rr != 0xffffffffu) lg_add(&cw[rr], 1u);
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < C; k += CG_BLOCK) {   // counts -> each wave's start per cluster
+            uint32_t run = A[k];
+            for (uint32_t q = 0; q < WAVES; q++) {
+                const uint32_t c = D[q * C + k];
+                D[q * C + k] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        for (uint32_t vb = wb0; vb < wb1; vb += 64) {
+            const uint32_t v = vb + l;
+            const uint32_t rr = v < wb1 ? B[v] : 0xffffffffu;
+            const bool in = rr != 0xffffffffu;
+            const uint64_t same = lg_match(rr, cbits, __ballot(in));
+            if (in) {
+                const uint32_t o = cw[rr];   // (every lane of the group reads before its first writes)
+                const uint32_t pos = o + (uint32_t)__popcll(same & lt);
+                Ef[pos] = v;
+                idx_out[pos] = (int32_t)v;
+                if ((same & lt) == 0ull) cw[rr] = o + (uint32_t)__popcll(same);
+            }
+        }
+    } else {
+        for (uint32_t k = w; k < C; k += WAVES) {
+            const uint32_t o = A[k], sz = A[k + 1] - o;
+            uint32_t got = 0;
+            for (uint32_t b0 = 0; b0 < V && got < sz; b0 += 64) {
+                const uint32_t v = b0 + l;
+                const bool hit = v < V && B[v] == k;
+                const uint64_t m = __ballot(hit);
+                if (hit) {
+                    const uint32_t pos = o + got + (uint32_t)__popcll(m & lt);
+                    Ef[pos] = v;
+                    idx_out[pos] = (int32_t)v;
+                }
+                got += (uint32_t)__popcll(m);
+            }
+        }
+    }
+    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 9);
+    // 9. the voxels' x, y next to each other (LDS form: over B and Cc, which are used up)
+    typename K::P32 XY = B;   // (two words per voxel: B and Cc are adjacent)
+    if (lds) {
+        for (uint32_t vb = 0; vb < V; vb += 16 * CG_BLOCK) {   // sixteen loads in flight per thread
+            float cx[16], cy[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {   // (clamped: no branch between the loads)
+                const float4 c = S.vox[min(vb + (uint32_t)q * CG_BLOCK + tid, V - 1)];
+                cx[q] = c.x;
+                cy[q] = c.y;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+                if (v < V) {
+                    XY[2 * v] = __float_as_uint(cx[q]);
+                    XY[2 * v + 1] = __float_as_uint(cy[q]);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    CG_HOOK_LG_STAMP(S, 10);
+    // 10. per-cluster centroid + radial push (src/cone_detection.cpp:261-279): float sums in
+    //     ascending member order (lg_centroids_one's arithmetic), one lane per cluster: each sum
+    //     is a sequential chain, kept in the lane's registers while its loads run ahead
+    float2* const cen_out = L.cen + (uint64_t)f * L.cap;
+    for (uint32_t k = tid; k < C; k += CG_BLOCK) {
+        const uint32_t s0 = A[k], e0 = A[k + 1];
+        float x = 0.0f, y = 0.0f;
+        auto xy = [&](uint32_t i, float& px, float& py) {
+            const uint32_t m = Ef[i];
+            if (lds) {
+                px = __uint_as_float(XY[2 * m]);
+                py = __uint_as_float(XY[2 * m + 1]);
+            } else {
+                const float4 c = S.vox[m];
+                px = c.x;
+                py = c.y;
+            }
+        };
+        uint32_t i = s0;
+        for (; i + 8 <= e0; i += 8) {
+            float px[8], py[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) xy(i + u, px[u], py[u]);
+#pragma unroll
+            for (int u = 0; u < 8; u++) { x += px[u]; y += py[u]; }
+        }
+        for (; i < e0; i++) {
+            float px, py;
+            xy(i, px, py);
+            x += px;
+            y += py;
+        }
+        {
+            const int j = (int)(e0 - s0);
+            const float qx0 = x / (float)j, qy0 = y / (float)j;
+            const double Sq = ((double)qx0 * (double)qx0 + (double)qy0 * (double)qy0) + 0.0;
+            const float len = (float)__builtin_sqrt(Sq);
+            const float qx = (float)((double)qx0 + (double)(qx0 / len) * P.ext);
+            const float qy = (float)((double)qy0 + (double)(qy0 / len) * P.ext);
+            cen_out[k] = make_float2(qx, qy);
+        }
+    }
+    CG_HOOK_LG_STAMP(S, 11);
+    // 11. offsets and the frame header
+    int32_t* const offs_out = L.offs + (uint64_t)f * (L.cap + 1);
+    for (uint32_t i = tid; i <= C; i += CG_BLOCK) offs_out[i] = C ? (int32_t)A[i] : 0;
+    if (tid == 0) {
+        uint32_t* m = S.meta;
+        m[LG_C] = C;
+        uint32_t* h = L.hdr + (uint64_t)f * 8;
+        h[CG_HDR_N] = L.n_points;
+        h[CG_HDR_K] = m[LG_KHDR];
+        h[CG_HDR_M] = m[LG_MALL];
+        h[CG_HDR_V] = V;
+        h[CG_HDR_C] = C;
+        h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
+                          (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
+    }
+    CG_HOOK_LG_STAMP(S, 12);
+}
+__global__ __launch_bounds__(CG_BLOCK) void lg_cluster_tail(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
+    __shared__ uint32_t lds[5 * LG_TAIL_LDS];
+    __shared__ uint32_t red[8 * WAVES];
+    __shared__ int32_t stk[3 * CG_SORT_STACK];
+    const uint32_t V = S.meta[LG_V];
+    if (V < LG_TAIL_LDS) {
+        lds_u32* const b = (lds_u32*)(uint32_t*)lds;
+        lg_tail_body<PbLds>(L, P, S, f, V, b, b + LG_TAIL_LDS, b + 2 * LG_TAIL_LDS, b + 3 * LG_TAIL_LDS,
+                            b + 4 * LG_TAIL_LDS, true, red, stk);
+    } else {
+        lg_tail_body<PbGen>(L, P, S, f, V, S.par, S.lab, S.cnt, S.dsz, S.fin, false, red, stk);
+    }
+}
+
 // Gathered survivors of a tiled frame (cg_tile_backend): meta reset, survivors copied into
 // scratch, the merged counts written where the backend reads them.
 __global__ void lg_set_counts(LgScratch S, uint32_t K, uint32_t Ms, uint32_t nfin, uint32_t b0, uint32_t b1,
@@ -1771,8 +2471,8 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
         if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);            \
     } else if (kmode == CG_KMODE_DETECT) {                                                        \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_DETECT>), g, b, 0, s, L, P, S, f, fi);             \
-        hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f);                              \
-        hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u | (dev ? LG_FOLD_SIZE : 0u), N, szfl); \
+        hipLaunchKernelGGL(lg_surv_write<LAY>, g, b, 0, s, L, S, f, dev ? 4u | LG_FOLD_SIZE : 0u, N, szfl); \
+        if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 4u, N, szfl);     \
     } else {                                                                                      \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
@@ -1795,17 +2495,19 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
     const dim3 g(nch), b(CG_BLOCK);
     const bool dev = (szfl & LG_SZ_ON) != 0;   // (lg_decide folds the front's chunk keys)
+    // the decisions' counts and bounds folded by one workgroup: the device-sized path folds them
+    // in lg_surv_write's last workgroup, otherwise a launch after it (folded in every
+    // lg_voxel_keys workgroup instead, 2,048 of them on C5 each reading the 256 chunk records:
+    // 15.6 against 5.0 + 5.0 us, profiles/r4_c5_fold_ab.txt)
+    const uint32_t fw = dev ? 2u | 4u | LG_FOLD_SIZE : 0u;
     if (xyzi16) {
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
-        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f, fw, L.n_points, szfl);
     } else {
         hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
-        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f, fw, L.n_points, szfl);
     }
-    // the decisions' counts and bounds folded by one workgroup (folded in every lg_voxel_keys
-    // workgroup instead, 2,048 of them on C5 each reading the 256 chunk records: 15.6 against
-    // 5.0 + 5.0 us, profiles/r4_c5_fold_ab.txt)
-    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u | (dev ? LG_FOLD_SIZE : 0u), L.n_points, szfl);
+    if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u, L.n_points, szfl);
     return hipGetLastError();
 }
 
@@ -1894,7 +2596,7 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
             hipLaunchKernelGGL(lg_pq_swap, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
         }
         hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
-                           kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
+                           kb[buf ^ 1], kb[buf], kb[buf], vb2[buf], 0u);
         // ranges of 65-512 records, then of 17-64 records: at most Mtot / 65 and Mtot / 17
         hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, Mtot / 65 + 1)), dim3(CG_BLOCK), 0, s, S,
                            kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
@@ -1955,23 +2657,26 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     CgLaunch Lh = L;
     Lh.n_points = N;
     const uint32_t nmax = std::max<uint32_t>(N, 1);
-    hipLaunchKernelGGL(lg_voxel_keys, dim3(blocks_of(nmax)), dim3(CG_BLOCK), 0, s, S, P, CG_K_FROM_META, N, 0u, 0u);
     uint64_t* kb[2] = {S.key0, S.key1};
     uint32_t* vb2[2] = {S.val0, S.val1};
-    // index_vector (finite points in frame-index order) as (idx, slot) records, then std::sort's
-    // permutation of it: levels for the frame's N (levels with no range return at once)
-    scan_emit(S, nmax, LG_MTOT, PclCompactFlag{kb[0], 0u, S.meta}, PclCompactEmit{kb[0], vb2[0], kb[1], 0u}, LG_PCL_N, s);
+    // index_vector (finite points in frame-index order) as (idx, slot) records, with the voxel
+    // keys computed on the way (lg_pcl_index), then std::sort's permutation of it: levels for the
+    // frame's N (levels with no range return at once)
+    hipLaunchKernelGGL(lg_pcl_index, dim3(std::max<uint32_t>(1, tiles_of(nmax))), dim3(CG_BLOCK), 0, s, S, P, kb[1]);
+    // one launch per level (lg_pq_level); a level's tiles number at most tb + its ranges (<= 2^lv),
+    // taken by at most 512 workgroups (more when a workgroup would hold more than PQ_OWN tiles)
+    // (level 0 always runs: with no level to cut it queues the whole index_vector as a leaf)
     const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
-    hipLaunchKernelGGL(lg_pq_split, dim3(tb), dim3(CG_BLOCK), 0, s, S, kb[1], 0u);
+    levels = std::max<uint32_t>(levels, 1);
     for (uint32_t lv = 0; lv < levels; lv++) {
         uint64_t* const Ein = lv % 2 ? kb[0] : kb[1];
         uint64_t* const Eout = lv % 2 ? kb[1] : kb[0];
-        const uint32_t grid = tb + (1u << lv);
-        if (lv) hipLaunchKernelGGL(lg_pq_split, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, lv);
-        hipLaunchKernelGGL(lg_pq_swap, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
+        const uint32_t tiles = tb + (1u << lv);
+        const uint32_t grid = std::min(tiles, std::max<uint32_t>(512, (tiles + PQ_OWN - 1) / PQ_OWN));
+        hipLaunchKernelGGL(lg_pq_level, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
     }
     hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S, kb[1],
-                       kb[0], kb[0], vb2[0]);
+                       kb[0], kb[0], vb2[0], ((levels - 1) & 1u) + 1u);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
                        kb[0], vb2[0]);
     hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, nmax / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s, S,
@@ -1982,24 +2687,13 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     const uint32_t VB = bits_of(nmax);
     const uint32_t vb = blocks_of(nmax), wb = lg_wave_blocks(nmax);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
-    hipLaunchKernelGGL(lg_dgrid_scan, dim3(gt), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_dgrid_fill, dim3(vb), dim3(CG_BLOCK), 0, s, S);
+    hipLaunchKernelGGL(lg_dgrid_scan_fill, dim3(gt), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
     hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
-    hipLaunchKernelGGL(lg_find, dim3(vb), dim3(CG_BLOCK), 0, s, S);
-    scan_emit(S, nmax, LG_V, KeepRoot{S.lab, S.cnt, P.min_cl, P.max_cl}, KeepEmit{S.cnt, S.droot, S.dsz}, LG_C, s);
-    hipLaunchKernelGGL(lg_order, dim3(1), dim3(CG_BLOCK), 0, s, S);
-    hipLaunchKernelGGL(lg_labels, dim3(vb), dim3(CG_BLOCK), 0, s, Lh, S, f, VB);
-    // the CSR: a stable sort of the rank bits; passes past the device-side cluster count skip
-    const uint32_t cmax = P.min_cl > 1 ? nmax / P.min_cl : nmax;
-    const uint32_t hi = VB + bits_of(std::max<uint32_t>(cmax, 1)) + 1;
-    radix_sort(S, nmax, std::min(hi, VB + 8), s, VB, S.meta + LG_V, S.meta + LG_SORT_LIM, true);
-    if (hi > VB + 8) hipLaunchKernelGGL(lg_rs_rest, dim3(1), dim3(CG_BLOCK), 0, s, S, VB + 8, hi, S.meta + LG_V,
-                                        S.meta + LG_SORT_LIM);
-    const uint32_t cb = blocks_of((uint64_t)nmax + 1);
-    hipLaunchKernelGGL(lg_csr_centroids, dim3(cb + wb), dim3(CG_BLOCK), 0, s, Lh, P, S, f, VB, -1, CG_K_FROM_META,
-                       CG_K_FROM_META, cb, hi);
+    // roots, sizes, the size filter, PCL's cluster order, labels, CSR, centroids, header: one
+    // workgroup (lg_cluster_tail)
+    hipLaunchKernelGGL(lg_cluster_tail, dim3(1), dim3(CG_BLOCK), 0, s, Lh, P, S, f);
     // (left out after a large frame: the fold then hands every frame to the launches above)
     return small ? cg_launch_lg_back_small(Lh, P, S, f, CG_K_FROM_META, 0u, s) : hipGetLastError();
 }
@@ -2141,6 +2835,7 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
 // Scratch layout (one frame at a time).
 namespace {
 
+uint64_t lg_pq_tmax(uint64_t n) { return (n + PQ_T - 1) / PQ_T + PQ_MAXR; }
 template <class F>
 uint64_t lg_walk(uint32_t n, F place) {
     const uint64_t N = std::max<uint32_t>(n, 1), nch = (N + LG_CHUNK - 1) / LG_CHUNK, nt = tiles_of(N);
@@ -2162,7 +2857,8 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(28, take((uint64_t)(LG_DCELLS_MAX + 2) * 4));
     place(29, take(nch * LG_CS_WORDS * 4));
     place(30, take((LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP) * 4));   // PCL sort range lists
-    place(31, take((2 + (N + PQ_T - 1) / PQ_T + PQ_MAXR + 2) * 8));   // their look-back words
+    // their look-back words: two sets (tickets, finished, one per tile) and the range counts
+    place(31, take((2 * (2 + lg_pq_tmax(N)) + 2 * PQ_MAXR) * 8));
     return off;
 }
 }  // namespace
@@ -2190,7 +2886,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 28: S.cstart = (uint32_t*)p; break;
             case 29: S.cstat = (uint32_t*)p; break;
             case 30: S.pq = (uint32_t*)p; S.pq_cap = LG_PQ_CAP; break;
-            case 31: S.pqst = (uint64_t*)p; break;
+            case 31: S.pqst = (uint64_t*)p; S.pq_tmax = (uint32_t)lg_pq_tmax(std::max<uint32_t>(n, 1)); break;
 
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
