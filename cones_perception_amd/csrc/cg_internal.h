@@ -183,7 +183,6 @@ enum {
     LG_KHDR,                   //   K for the header
     LG_SMALL,                  //   1: the LDS backend (one workgroup) takes the frame
     LG_PQ_TIMEOUT,             // a partition level's wait for its range gave up (never expected)
-    LG_SW_DONE,                // lg_surv_write's finished workgroups (its last one folds the chunks)
     LG_META_WORDS = 64
 };
 struct LgScratch {

@@ -49,6 +49,25 @@ __device__ __forceinline__ void lg_init_meta(const LgScratch& S, const CgDevPara
 }
 __global__ void lg_init(LgScratch S, CgDevParams P) { lg_init_meta(S, P, threadIdx.x); }
 
+// The launch's last workgroup to arrive (thread 0, after every storing thread of its workgroup
+// has waited for its stores), with the arrivals spread over eight counters: one word takes ~88
+// atomics per us (MI355X_MICROARCH.md, "dequeue"), so a 1,024-workgroup launch would queue ~12
+// us on one. A workgroup adds to counter blockIdx % 8, the last of each counter to the top one,
+// and the last there is the launch's last: it resets the nine words (every other arrival has
+// happened). Each arrival is an agent-scope atomic after the arriving workgroup's sc1 stores
+// completed, so the last sees every workgroup's stores through sc1 loads.
+__device__ __forceinline__ bool lg_last_arrival(uint32_t* cnt) {
+    const uint32_t G = gridDim.x, sh = blockIdx.x & 7u;
+    const uint32_t in_shard = (G - sh + 7u) / 8u, shards = min(G, 8u);
+    if (__hip_atomic_fetch_add(&cnt[sh], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != in_shard - 1u) return false;
+    if (__hip_atomic_fetch_add(&cnt[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != shards - 1u) return false;
+    for (int i = 0; i < 9; i++) st_rlx(&cnt[i], 0u);
+    return true;
+}
+// Arrival counters of the launches that hand over to their last workgroup (zeroed scratch, and
+// left zeroed by their last arrival): 0 lg_surv_write
+__device__ __forceinline__ uint32_t* lg_arrivals(const LgScratch& S, uint32_t k);
+
 // Bounds of finite points, merged into the frame's meta words (order-preserving keys).
 struct Bounds {
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -331,7 +350,7 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams
 // fold_what != 0 (the device-sized path): the launch's last workgroup to finish folds the chunk
 // statistics (lg_reduce_chunks' work, what = fold_what) instead of a launch after it. The words
 // this launch writes go out with sc1 stores, every thread waits for its stores, then one count
-// per workgroup (meta[LG_SW_DONE], zeroed with the meta words by lg_front); the last reads the
+// per workgroup (lg_last_arrival); the last reads the
 // words with sc1 loads (MI355X_MICROARCH.md's hand-off table, row 1).
 template <int LAYOUT>
 __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch S, uint32_t f, uint32_t fold_what = 0,
@@ -400,8 +419,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_surv_write(CgLaunch L, LgScratch 
     __shared__ uint32_t last;
     __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): this thread's words are stored
     __syncthreads();
-    if (tid == 0)
-        last = __hip_atomic_fetch_add(&S.meta[LG_SW_DONE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    if (tid == 0) last = lg_last_arrival(lg_arrivals(S, 0));
     __syncthreads();
     if (last) lg_fold_chunks(S, gridDim.x, fold_what, N, szfl, true);
 }
@@ -830,7 +848,10 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
 // PCL order's partition levels (lg_pq_*, below): sizes and the range lists' header words
 #define LG_PCL_LEAF 4096       // the longest leaf sorted in LDS
 #ifndef LG_PCL_CUT
-#define LG_PCL_CUT LG_PCL_LEAF   // the levels cut ranges longer than this
+// the levels cut ranges longer than this; the leaves take up to LG_PCL_LEAF, so a range an
+// uneven last cut leaves between the two still sorts in LDS (4,096 against 2,048 on C5:
+// 271 / 268 us per frame, profiles/r5_c5_cut_ab.txt)
+#define LG_PCL_CUT 2048
 #endif
 #define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
                                // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
@@ -1066,6 +1087,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
     __shared__ uint32_t m[LG_META_WORDS];
     const uint32_t tid = threadIdx.x;
     const uint32_t* in = S.meta;
+    if (blockIdx.x == 1) CG_HOOK_LG_STAMP(S, 58);
     const uint32_t Mtot = in[LG_MTOT], npad = in[LG_NPAD];
     if (tid == 0) {
         lg_grid_setup(in, m, P, npad, Mtot);
@@ -1077,6 +1099,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
         }
     }
     __syncthreads();
+    if (blockIdx.x == 1) CG_HOOK_LG_STAMP(S, 59);
     {
         const uint32_t nc = m[LG_NCELL] + 1;
         for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
@@ -1084,18 +1107,25 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
     const uint32_t active = Mtot ? (Mtot + LG_TILE - 1) / LG_TILE : 1u;
     if (blockIdx.x >= active) return;
     const uint32_t t = lg_tile_ticket(S.sstat);
+    if (t == 1) CG_HOOK_LG_STAMP(S, 60);
     const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)tid * 8;
     const uint32_t Ms = in[LG_MS];
     const bool pass = m[LG_PASS] != 0;
     const float mnb0 = (float)(int)m[LG_MINB], mnb1 = (float)(int)m[LG_MINB + 1], mnb2 = (float)(int)m[LG_MINB + 2];
     const uint32_t mul1 = m[LG_MUL1], mul2 = m[LG_MUL2];
     uint32_t idx[8], c = 0;
+    float4 pt[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {   // the eight points' loads first (clamped: no branch between them)
+        const uint32_t j = (uint32_t)min(b0 + q, (uint64_t)(Mtot ? Mtot - 1 : 0));
+        pt[q] = j < Ms ? S.surv_p[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         const uint64_t j = b0 + q;
         idx[q] = 0xffffffffu;
         if (j < Mtot) {
-            const float4 p = lg_point(S, (uint32_t)j, Ms);
+            const float4 p = pt[q];
             uint64_t key = 0ull;   // passthrough: frame-index order (nothing listed)
             if (!pass) {
                 if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
@@ -1113,11 +1143,14 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
             c += idx[q] != 0xffffffffu ? 1u : 0u;
         }
     }
+    if (t == 1) CG_HOOK_LG_STAMP(S, 61);
     uint32_t pos = lg_tile_scan(S.sstat, t, active, c, S.meta + LG_PCL_N);
+    if (t == 1) CG_HOOK_LG_STAMP(S, 62);
 #pragma unroll
     for (int q = 0; q < 8; q++)
         if (idx[q] != 0xffffffffu) Eout[pos++] = ((uint64_t)idx[q] << 32) | (uint32_t)(b0 + q);
     lg_tile_done(S.sstat, active);
+    if (t == 1) CG_HOOK_LG_STAMP(S, 63);
 }
 
 __device__ __forceinline__ uint32_t pq_key(const uint64_t* E, uint32_t x) {
@@ -1378,6 +1411,9 @@ __device__ __forceinline__ uint64_t* pq_set(const LgScratch& S, uint32_t par) {
 __device__ __forceinline__ uint64_t* pq_done(const LgScratch& S, uint32_t par) {
     return S.pqst + 2ull * (S.pq_tmax + 2u) + (uint64_t)par * PQ_MAXR;
 }
+__device__ __forceinline__ uint32_t* lg_arrivals(const LgScratch& S, uint32_t k) {
+    return (uint32_t*)(S.pqst + 2ull * (S.pq_tmax + 2u) + 2ull * PQ_MAXR) + 16u * k;
+}
 // the set of parity par as no level has used it: ticket counter, look-back words of the tiles
 // that took tickets, range words (every thread of the block)
 __device__ __forceinline__ void pq_clear_set(const LgScratch& S, uint32_t par) {
@@ -1392,6 +1428,7 @@ __device__ __forceinline__ void pq_clear_set(const LgScratch& S, uint32_t par) {
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint64_t* E, uint64_t* Eo, uint32_t level,
                                                         uint32_t last_level, uint32_t out_buf) {
     __shared__ uint32_t tp[PQ_MAXR + 1];
+    __shared__ uint32_t rf_[CG_BLOCK], re_[CG_BLOCK], rd_[CG_BLOCK];   // the first CG_BLOCK ranges
     __shared__ uint32_t red[8 * WAVES];
     __shared__ uint32_t tk, cg[WAVES], cl[WAVES], nown;
     __shared__ uint32_t own[PQ_OWN];
@@ -1401,6 +1438,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
     uint64_t* const st = pq_set(S, par);
     uint64_t* const done = pq_done(S, par);
     const uint32_t n = S.meta[LG_PCL_N];
+    // range tid's entry (level > 0), loaded with the counts: entries past the count are stale
+    // and unused
+    uint32_t pf = 0, pe = 0, pd = 0;
+    if (level > 0) {
+        const uint32_t* Lr = pq_list(S, level % 3u) + PQ_EW * tid;
+        pf = Lr[0]; pe = Lr[1]; pd = Lr[2];
+    }
     if (blockIdx.x == 0) {
         pq_clear_set(S, par ^ 1u);   // for level + 1
         if (tid == 0) {
@@ -1423,8 +1467,18 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         tk = (uint32_t)__hip_atomic_fetch_add(&st[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         nown = 0;
     }
-    uint32_t nr;
-    const uint32_t active = pq_tiles(S, level, tp, red, nr);   // ends with a barrier
+    uint32_t nr, active;
+    const bool pre = level > 0 && min(S.pq[level % 3u], (uint32_t)PQ_MAXR) <= CG_BLOCK;
+    if (pre) {   // pq_tiles from the entries loaded above, kept in LDS for pq_range
+        nr = min(S.pq[level % 3u], (uint32_t)PQ_MAXR);
+        rf_[tid] = pf; re_[tid] = pe; rd_[tid] = pd;
+        active = block_scan(nr, [&](uint32_t r) -> uint32_t { return (pe - pf - 1 + PQ_T - 1) / PQ_T; },
+                            [&](uint32_t r, uint32_t e) { tp[r] = e; }, red);
+        if (tid == 0) tp[nr] = active;
+        __syncthreads();
+    } else {
+        active = pq_tiles(S, level, tp, red, nr);   // ends with a barrier
+    }
     if (tk == 0 && level < 7) CG_HOOK_LG_STAMP(S, 16 + 6 * level);
     // tickets per workgroup: ceil(active / grid) of them take every tile
     const uint32_t kmax = min((active + gridDim.x - 1) / gridDim.x, (uint32_t)PQ_OWN + 1u);
@@ -1440,7 +1494,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         if (t >= active) break;
         const uint32_t r = pq_find(tp, nr, t), q = t - tp[r];
         uint32_t f, e, d;
-        pq_range(S, level, r, f, e, d);
+        if (pre) { f = rf_[r]; e = re_[r]; d = rd_[r]; }
+        else pq_range(S, level, r, f, e, d);
         // the median of three and this element's record in one batch of loads: x > f, and x's
         // virtual record is E[f] when x is the median (__move_median_to_first's swap)
         const uint32_t x = f + 1 + q * PQ_T + tid;
@@ -1448,7 +1503,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
         const uint32_t ka = pq_key(E, a), kb = pq_key(E, b), kc = pq_key(E, c);
         const uint64_t rf = E[f];
-        const uint64_t rx = valid ? E[x] : 0ull;
+        const uint64_t rx = E[valid ? x : f];   // (clamped: no branch between the loads)
         const uint32_t m = pb_median(a, b, c, ka, kb, kc);
         const uint32_t p = m == a ? ka : (m == b ? kb : kc);
         const uint32_t k = valid ? (x == m ? pcl_key(rf) : pcl_key(rx)) : 0u;
@@ -2536,7 +2591,7 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
     const uint32_t npad = (kmode == CG_KMODE_PIPELINE && P.zero_pass) ? N - K : 0u;
     const uint32_t Mtot = Ms + npad;
     // PCL's order keeps at most PQ_MAXR ranges per partition level: a detector input beyond
-    // PQ_MAXR * LG_PCL_CUT / 2 records (4M) is summed in point order instead, and flagged
+    // PQ_MAXR * LG_PCL_CUT / 2 records (2M at LG_PCL_CUT = 2,048) is summed in point order instead, and flagged
     // (CG_F_VOXEL_POINT_ORDER): same voxels and clusters, last bits of some coordinates
     if ((uint64_t)Mtot > (uint64_t)PQ_MAXR * LG_PCL_CUT / 2) P.voxel_order = CG_VOXEL_ORDER_POINT;
     CgLaunch Lh = L;
@@ -2688,6 +2743,8 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     const uint32_t vb = blocks_of(nmax), wb = lg_wave_blocks(nmax);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
     hipLaunchKernelGGL(lg_dgrid_scan_fill, dim3(gt), dim3(CG_BLOCK), 0, s, S);
+    // (the flattening in lg_forest's last workgroup instead: 19.8 against 7.1 + 5.9 us, the
+    // last-arrival counting and sc1 parents costing more than the launch)
     hipLaunchKernelGGL(lg_forest, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
     hipLaunchKernelGGL(lg_flatten, dim3(1), dim3(CG_BLOCK), 0, s, S);
     hipLaunchKernelGGL(lg_cross, dim3(wb), dim3(CG_BLOCK), 0, s, S, P);
@@ -2858,7 +2915,7 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(29, take(nch * LG_CS_WORDS * 4));
     place(30, take((LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP) * 4));   // PCL sort range lists
     // their look-back words: two sets (tickets, finished, one per tile) and the range counts
-    place(31, take((2 * (2 + lg_pq_tmax(N)) + 2 * PQ_MAXR) * 8));
+    place(31, take((2 * (2 + lg_pq_tmax(N)) + 2 * PQ_MAXR + 16) * 8));   // + lg_arrivals' words
     return off;
 }
 }  // namespace

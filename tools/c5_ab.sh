@@ -1,20 +1,21 @@
 #!/bin/bash
-# GPU: C5 per-frame time (tools/c5_run.py) for the default library and variant builds
-# (lib_variants/<name>), interleaved, two rounds; then the default library's kernel trace
-# (tools/c5_profile.sh) and the C2 phase stamps (tools/c2_stamps.py).
-#   tools/c5_ab.sh variant1 variant2 ...
+# GPU: C5 frame time (tools/c5_run.py), the default library against variants (lib_variants/<name>),
+# interleaved; with CHECK=1 each variant first runs the large-path suites against the oracle.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-mkdir -p "$R/gpurun_out"
-out=$R/gpurun_out/c5_ab.txt
-: > "$out"
-for round in 1 2; do
+cd "$R" || exit 1
+for v in "$@"; do
+  if [ "${CHECK:-0}" = 1 ]; then
+    CONES_GPU_LIB=$R/lib_variants/$v/libcones_gpu.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
+      --timeout 300 --timeout-method thread -k "large or pcl_order" > gpurun_out/ab_$v.log 2>&1 \
+      || { echo "$v: tests failed"; grep -E "^E |FAILED" gpurun_out/ab_$v.log | head; exit 1; }
+    echo "$v: $(tail -1 gpurun_out/ab_$v.log)"
+  fi
+done
+for r in 1 2 3; do
   for v in default "$@"; do
-    if [ "$v" = default ]; then L=""; else L=$R/lib_variants/$v/libcones_gpu.so; fi
-    echo -n "$v round $round: " >> "$out"
-    CONES_GPU_LIB=$L timeout -k 10 120 python3 "$R/tools/c5_run.py" 100 >> "$out" 2>&1 || exit 1
+    if [ $v = default ]; then L=""; else L=$R/lib_variants/$v/libcones_gpu.so; fi
+    echo -n "run $r $v: "
+    CONES_GPU_LIB=$L timeout -k 10 120 python tools/c5_run.py 200 || exit 1
   done
 done
-cat "$out"
-bash "$R/tools/c5_profile.sh" > /dev/null || exit 1
-timeout -k 10 120 python3 "$R/tools/c2_stamps.py" 200 > "$R/gpurun_out/c2_stamps.txt" 2>&1 || exit 1

@@ -49,3 +49,6 @@ for lv in range(7):
     print(f"  level {lv}: lookback {med(st_[1] - st_[0]):6.2f}  lists {med(st_[2] - st_[1]):6.2f}  "
           f"count {med(st_[3] - st_[2]):6.2f}  wait {med(st_[4] - st_[3]):6.2f}  swaps {med(st_[5] - st_[4]):6.2f}  "
           f"to next {med(nxt - st_[5]):6.2f}")
+print("lg_pcl_index (workgroup 1 / tile 1), us: grid setup, cstart zero + ticket, keys, look-back scan, emit + done")
+for nm, i0, i1 in (("setup", 58, 59), ("zero+ticket", 59, 60), ("keys", 60, 61), ("scan", 61, 62), ("emit+done", 62, 63)):
+    print(f"  {nm:12s} {float(np.median(a[:, i1] - a[:, i0])) / 100.0:7.2f}")
