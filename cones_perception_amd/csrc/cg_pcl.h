@@ -49,7 +49,11 @@ __device__ unsigned int g_pcl_probe_n;
             if (s_ < 64) g_pcl_probe[s_] = __builtin_amdgcn_s_memrealtime();             \
         }                                                                                \
     } while (0)
+#ifdef CG_PCL_PROBE_NOSTEP   // (the whole sort's time only)
+#define PCL_STEP() ((void)0)
+#else
 #define PCL_STEP() PCL_STAMP()
+#endif
 #else
 #define PCL_STAMP() ((void)0)
 #define PCL_STEP() ((void)0)
