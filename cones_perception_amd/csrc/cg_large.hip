@@ -2770,14 +2770,18 @@ static int large_frame_dev(const CgLaunch& L, const CgDevParams& P, int kmode, L
 }
 
 // Captured frames: one hipGraph per (launch arguments, frame), instantiated once and replayed:
-// the frame's ~40 launches cost the host one graph launch instead of one call each. Captured on
-// a private stream (nothing runs there); at most LG_GRAPHS entries, then frames run eagerly.
+// the frame's ~25 launches cost the host one graph launch instead of one call each. Captured on
+// a private stream (nothing runs there); at most LG_GRAPHS entries, the least recently used one
+// replaced when a new key arrives (a caller rotating input buffers keys a graph per buffer;
+// graphs of freed buffers age out instead of pinning the cache).
 #define LG_GRAPHS 32
 struct LgGraphs {
     hipStream_t cap = nullptr;
+    uint64_t clock = 0;
     struct Entry {
         std::vector<unsigned char> key;
         hipGraphExec_t exec;
+        uint64_t used;
     };
     std::vector<Entry> e;
 };
@@ -2801,9 +2805,20 @@ static std::vector<unsigned char> lg_graph_key(const CgLaunch& L, const CgDevPar
 static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& P, int kmode, const LgScratch& S,
                              hipStream_t s, uint32_t f, uint32_t levels, bool small) {
     std::vector<unsigned char> key = lg_graph_key(L, P, kmode, S, f, levels, small);
+    g->clock++;
     for (auto& x : g->e)
-        if (x.key == key) return hipGraphLaunch(x.exec, s);
-    if (g->e.size() >= LG_GRAPHS) return large_frame_dev(L, P, kmode, S, s, f, levels, small);
+        if (x.key == key) {
+            x.used = g->clock;
+            return hipGraphLaunch(x.exec, s);
+        }
+    if (g->e.size() >= LG_GRAPHS) {   // the least recently used entry makes room
+        size_t lru = 0;
+        for (size_t i = 1; i < g->e.size(); i++)
+            if (g->e[i].used < g->e[lru].used) lru = i;
+        (void)hipDeviceSynchronize();   // (it may still be queued on some stream; eviction is rare)
+        (void)hipGraphExecDestroy(g->e[lru].exec);
+        g->e.erase(g->e.begin() + (long)lru);
+    }
     hipError_t e;
     if (!g->cap && (e = hipStreamCreateWithFlags(&g->cap, hipStreamNonBlocking)) != hipSuccess) return e;
     if ((e = hipStreamBeginCapture(g->cap, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
@@ -2819,7 +2834,7 @@ static int large_frame_graph(LgGraphs* g, const CgLaunch& L, const CgDevParams& 
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     if (e != hipSuccess) return e;
-    g->e.push_back({std::move(key), exec});
+    g->e.push_back({std::move(key), exec, g->clock});
     return hipGraphLaunch(exec, s);
 }
 

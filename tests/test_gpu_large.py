@@ -213,3 +213,20 @@ def test_hint_sequence_small_large_medium(params):
         ms.append(int(hdr[2]))
         assert_same_detection(got, ref, f"sequence frame {i} (M {ms[-1]})")
     assert ms[0] <= 1024 and ms[1] > 8 * 4096, ms
+
+
+def test_graph_cache_rotating_buffers(params):
+    """The device-sized path keys one captured graph per (arguments, frame): a caller rotating
+    more input buffers than the cache holds (32) evicts the least recently used graph and
+    captures again; every frame stays bit-exact, including buffers whose graph was evicted."""
+    import torch
+    raw = cp.synth_frames(1, first_frame=4, rings=128, cols=1024, clutter=0, cones_per_row=8)
+    n = 128 * 1024
+    ref, _ = O.run(params, cp.frame_cloud(raw[0]), O.MODE_PIPELINE)
+    copies = 36
+    d = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(raw, (copies,) + raw.shape[1:]))).cuda()
+    eng = cp.BatchEngine(params)
+    for rep in range(2):
+        for k in list(range(copies)) + [0, 1, 35]:
+            eng.run(d[k].data_ptr(), 1, n, 16, mode=cp.CG_MODE_PIPELINE)
+            assert_same_detection(eng.fetch(0), ref, f"rotation {rep} buffer {k}")
