@@ -516,11 +516,12 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
     CgLaunch L{};
     // a frame alone on the GPU: pass 1 over one workgroup per 4,096-point chunk (route 3:
     // the one-workgroup frame kernel, for comparisons)
-    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS && (h->route == 0 || h->route == 4 || h->route == 6) &&
-                       !(retry & RETRY_ONE_WG);
+    const bool split = kmode != CG_KMODE_GROUND && n <= CG_MAX_POINTS &&
+                       (h->route == 0 || h->route == 4 || h->route == 6 || h->route == 9) && !(retry & RETRY_ONE_WG);
     bool staged_later = false;
     // route 4: split, input by DMA; route 6 (tests): zero-copy with no chunk ever published
-    const bool zero_copy = split && (h->route == 0 || h->route == 6) && !dma_retry;
+    // route 9 (tests): zero-copy with chunk workgroup 0 giving up on the others at once
+    const bool zero_copy = split && (h->route == 0 || h->route == 6 || h->route == 9) && !dma_retry;
     rc = stage_frame(h, in, L, zero_copy, &staged_later);
     if (rc) return rc;
     fill_launch_outputs(h, L);
@@ -553,6 +554,7 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         L.pack = h->h_pack_dev;   // the kernel packs the results itself, into pinned host memory
         h->pack_seq = h->pack_seq + 1 ? h->pack_seq + 1 : 1;
         L.pack_seq = h->pack_seq;
+        L.split_give_up = h->route == 9 ? 1u : 0u;
     }
     h->packed = L.pack != nullptr;
     rc = launch_frames(h, L, kmode, h->stream);
@@ -1345,7 +1347,7 @@ int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || route > 6) return fail(CG_E_INVALID, "bad route %d", route);
+    if (route < 0 || (route > 6 && route != 9)) return fail(CG_E_INVALID, "bad route %d", route);   // (7, 8: retired experiments)
     h->route = route;
     return CG_OK;
 }

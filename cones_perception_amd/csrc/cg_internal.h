@@ -98,6 +98,9 @@ struct CgLaunch {
     // split launch with pack: the last workgroup stores pack_seq to pack[CG_PACK_DONE] once
     // every packed word is in host memory (the host returns on it; 0: no done word)
     uint32_t pack_seq;
+    // split launch, tests (cg_debug_route 9): chunk workgroup 0 gives up at once instead of
+    // waiting for the others, as after a CG_SPLIT_TIMEOUT
+    uint32_t split_give_up;
 };
 #define CG_STAGE_ERR 63               // in_flags word set by a chunk workgroup that timed out
 #define CG_STAGE_TIMEOUT 20000000ull  // s_memrealtime ticks (100 MHz): 200 ms

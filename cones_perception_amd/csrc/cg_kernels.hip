@@ -183,7 +183,11 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
             // the bound the frame is flagged and the host runs it again in one workgroup
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             uint32_t ok = 1;
-            while (ld_rlx(L.split + SP_ARRIVE) < gridDim.x) {
+            if (L.split_give_up && blockIdx.x == 0) {
+                st_rlx(L.split + SP_ERR, 1u);
+                ok = 0;
+            }
+            while (ok && ld_rlx(L.split + SP_ARRIVE) < gridDim.x) {
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > CG_SPLIT_TIMEOUT) {
                     st_rlx(L.split + SP_ERR, 1u);

@@ -99,6 +99,23 @@ def test_staging_timeout_reruns_by_dma(params):
     assert_same_detection(pipe.cloud_handler(msg), ref, "zero-copy again")
 
 
+def test_split_give_up_reruns_in_one_workgroup(params):
+    """Route 9: chunk workgroup 0 of the split launch gives up waiting for the other chunks at
+    once (as after CG_SPLIT_TIMEOUT), so the frame's counts are void (header word 7) and the
+    call re-runs it in one workgroup: the result is exact (a void frame would have no
+    survivors), and the state words the last chunk reset leave the next split call clean."""
+    pipe = cp.ConePipeline(params)
+    for frame in (22, 23):
+        raw = cp.synth_frames(1, first_frame=frame, rings=64, cols=1024)
+        msg = cp.frame_cloud(raw[0])
+        ref, _ = O.run(params, msg, O.MODE_PIPELINE)
+        assert ref.n_filtered > 0 and len(ref.centroids) > 0
+        pipe.debug_route(9)
+        assert_same_detection(pipe.cloud_handler(msg), ref, f"frame {frame} after the give-up")
+        pipe.debug_route(0)
+        assert_same_detection(pipe.cloud_handler(msg), ref, f"frame {frame} split again")
+
+
 def test_tile_backend_keeps_route5(params):
     """cg_tile_backend_own under route 5 (global backend, PCL sort cut after one partition
     level): the route reaches the tile protocol, and the result is exact."""
