@@ -287,34 +287,19 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_front(CgLaunch L, CgDevParams 
 }
 
 // Decide: thresholds, pass 2 per chunk, survivors = ground-kept & filter bits (from lg_front).
-// fold_nch > 0 (the device-sized path): every workgroup folds the front's nch chunk keys itself
-// (no lg_reduce_chunks launch between); workgroup 0 stores them in the meta words
+// (The device-sized pipeline frame: lg_decide_write.)
 template <int LAYOUT, int KMODE>
-__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
-                                                        uint32_t fold_nch) {
+__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
     constexpr int PPT = LG_CHUNK / CG_BLOCK;
     constexpr int NW = (PPT + 63) / 64;
     __shared__ float thr[CG_NUM_BINS + 1];
     __shared__ uint32_t tkey[CG_NUM_BINS + 1], band[2], kcount;
-    __shared__ uint32_t fk[CG_NUM_BINS + 2];
     const uint32_t c = blockIdx.x, tid = threadIdx.x, l = lane_id();
     const uint64_t base = (uint64_t)c * LG_CHUNK;
     const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
     const uint32_t* keys = S.meta + LG_SECKEY;
-    uint32_t touched;
-    if (fold_nch) {
-        __shared__ uint32_t part[16][LG_CS_WORDS];
-        const uint32_t a = lg_fold_core(S, fold_nch, LG_WM_KEYS | LG_WM_TOUCHED, part);
-        if (tid <= CG_NUM_BINS + 1) fk[tid] = a;   // (LG_CS_KEYS = 0, LG_CS_TOUCHED = CG_NUM_BINS + 1)
-        if (c == 0 && tid <= CG_NUM_BINS) S.meta[LG_SECKEY + tid] = a;
-        if (c == 0 && tid == LG_CS_TOUCHED) S.meta[LG_TOUCHED] = a;
-        __syncthreads();
-        keys = fk;
-        touched = fk[LG_CS_TOUCHED];
-    } else {
-        touched = S.meta[LG_TOUCHED];
-    }
+    const uint32_t touched = S.meta[LG_TOUCHED];
     if (tid < 64) sector_thresholds(keys, touched, P, thr, tkey, &band[0], &band[1]);
     // the frame's sector keys to the caller's per-frame output (the pipeline's re-crop reads them)
     if (KMODE == CG_KMODE_PIPELINE && c == 0 && tid <= CG_NUM_BINS && L.seckeys)
@@ -562,23 +547,126 @@ __device__ __forceinline__ uint32_t lg_tile_scan(uint32_t* st, uint32_t t, uint3
 }
 
 // Exclusive scan of flag(i) over i < n (count from meta[n_word] when n_word >= 0), calling
-// emit(i, position) for every flagged i; the total goes to meta[total_word]. One launch.
-template <class FLAG, class EMIT>
+// emit(i, position) for every flagged i; the total goes to meta[total_word]. One launch, tiles
+// of PER * CG_BLOCK elements (fewer per tile spread a short scan's loads over more CUs).
+template <class FLAG, class EMIT, int PER = 8>
 __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word, uint32_t* meta, FLAG flag,
                                                          EMIT emit, uint32_t* st, int total_word) {
+    constexpr uint32_t TILE = PER * CG_BLOCK;
     if (n_word >= 0) n = meta[n_word];
-    const uint32_t active = n ? (n + LG_TILE - 1) / LG_TILE : 1u;
+    const uint32_t active = n ? (n + TILE - 1) / TILE : 1u;
     if (blockIdx.x >= active) return;
     const uint32_t t = lg_tile_ticket(st);
-    const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)threadIdx.x * 8;
-    uint32_t fl[8], c = 0;
+    const uint64_t b0 = (uint64_t)t * TILE + (uint64_t)threadIdx.x * PER;
+    uint32_t fl[PER], c = 0;
 #pragma unroll
-    for (int q = 0; q < 8; q++) { fl[q] = (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u; c += fl[q]; }
+    for (int q = 0; q < PER; q++) { fl[q] = (b0 + q < n) ? flag((uint32_t)(b0 + q)) : 0u; c += fl[q]; }
     uint32_t pos = lg_tile_scan(st, t, active, c, meta + total_word);
 #pragma unroll
-    for (int q = 0; q < 8; q++)
+    for (int q = 0; q < PER; q++)
         if (fl[q]) emit((uint32_t)(b0 + q), pos++);
     lg_tile_done(st, active);
+}
+
+// The device-sized pipeline frame's decisions and survivors in one launch (lg_decide with the
+// front's keys folded, then lg_surv_write): a workgroup takes its chunk by ticket (so the chunk
+// look-back below only waits on chunks already running), decides the chunk's points, and the
+// chunk's survivor count goes through a decoupled look-back over the chunks (S.sstat) for its
+// base in frame-index order, instead of a launch boundary and a prefix over the chunk counts.
+// The chunk's K, survivor count and bounds leave with sc1 stores; the last workgroup to arrive
+// (lg_last_arrival, after each workgroup's storing thread waited for its stores) resets the
+// look-back words and folds the chunks into the meta words, sizing the backend.
+template <int LAYOUT>
+__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide_write(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
+                                                              uint32_t nch, uint32_t N, uint32_t szfl) {
+    constexpr int PPT = LG_CHUNK / CG_BLOCK;
+    constexpr int NW = (PPT + 63) / 64;
+    __shared__ float thr[CG_NUM_BINS + 1];
+    __shared__ uint32_t tkey[CG_NUM_BINS + 1], band[2], kw[WAVES], tk, cbase, last;
+    __shared__ uint32_t fk[CG_NUM_BINS + 2];
+    __shared__ uint32_t part[16][LG_CS_WORDS];
+    __shared__ uint32_t cnt[PPT * WAVES];
+    __shared__ uint32_t red[8 * WAVES];
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    // the ticket from the last wave, so that the other waves' fold loads overlap its latency
+    if (tid == CG_BLOCK - 1) tk = __hip_atomic_fetch_add(&S.sstat[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    {
+        const uint32_t a = lg_fold_core(S, nch, LG_WM_KEYS | LG_WM_TOUCHED, part);   // (ends with a barrier)
+        if (tid <= CG_NUM_BINS + 1) fk[tid] = a;   // (LG_CS_KEYS = 0, LG_CS_TOUCHED = CG_NUM_BINS + 1)
+    }
+    __syncthreads();
+    const uint32_t c = tk;
+    if (c == 0 && tid <= CG_NUM_BINS) S.meta[LG_SECKEY + tid] = fk[tid];
+    if (c == 0 && tid == LG_CS_TOUCHED) S.meta[LG_TOUCHED] = fk[LG_CS_TOUCHED];
+    if (tid < 64) sector_thresholds(fk, fk[LG_CS_TOUCHED], P, thr, tkey, &band[0], &band[1]);
+    if (c == 0 && tid <= CG_NUM_BINS && L.seckeys) L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = fk[tid];
+    __syncthreads();
+    const uint64_t base = (uint64_t)c * LG_CHUNK;
+    const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
+    const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
+    const uint2* codes = (const uint2*)S.codes + (uint64_t)c * (LG_CHUNK / 8);
+    LaneBits<NW> keep;
+    pass2_keep<PPT, LAYOUT>(fb, Nc, L, P, band[0], band[1], tkey, [&](int g) { return codes[g * CG_BLOCK + tid]; },
+                            keep);
+    const uint32_t kc = wave_sum(keep.count());
+    LaneBits<NW> m;   // kept by the ground filter and by the position filter
+#pragma unroll
+    for (int wi = 0; wi < NW; wi++) m.w[wi] = keep.w[wi] & S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const uint64_t bb = __ballot(m.get(k));
+        if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(bb);
+    }
+    if (l == 0) kw[w] = kc;
+    __syncthreads();
+    const uint32_t tot = block_scan(PPT * WAVES, [&](uint32_t i) -> uint32_t { return cnt[i]; },
+                                    [&](uint32_t i, uint32_t e) { cnt[i] = e; }, red);
+    if (w == 0) {   // the chunks before this one (their survivor counts), then this chunk's words
+        const uint32_t b = lg_lookback(S.sstat, c, tot);
+        if (l == 0) {
+            cbase = b;
+            uint32_t k = 0;
+            for (int q = 0; q < WAVES; q++) k += kw[q];
+            st_rlx(S.cstat + (uint64_t)c * LG_CS_WORDS + LG_CS_K, k);
+            st_rlx(S.cstat + (uint64_t)c * LG_CS_WORDS + LG_CS_MS, tot);
+        }
+    }
+    __syncthreads();
+    const uint32_t b0 = cbase;
+    const uint64_t lt = (1ull << l) - 1ull;
+    const uint32_t pidx0 = S.pidx_base + (uint32_t)base;
+    Bounds bd;
+#pragma unroll
+    for (int k0 = 0; k0 < PPT; k0 += 4) {   // four loads in flight
+        bool has[4];
+        uint32_t pos[4];
+        float4 pt[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = k0 + q;
+            has[q] = m.get(k);
+            const uint64_t bb = __ballot(has[q]);
+            pos[q] = b0 + cnt[k * WAVES + w] + (uint32_t)__popcll(bb & lt);
+            if (has[q]) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)k * CG_BLOCK + tid, L);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (!has[q]) continue;
+            S.surv_p[pos[q]] = pt[q];
+            S.surv_i[pos[q]] = pidx0 + (uint32_t)(k0 + q) * CG_BLOCK + tid;
+            bd.add(pt[q]);
+        }
+    }
+    __shared__ uint32_t bpart[7 * WAVES];
+    bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, bpart, true);   // (thread 0 stores)
+    if (tid == 0) {
+        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): its words and status are stored
+        last = lg_last_arrival(lg_arrivals(S, 0));
+    }
+    __syncthreads();
+    if (!last) return;
+    for (uint32_t i = tid; i < nch + 2; i += CG_BLOCK) st_rlx(&S.sstat[i], 0u);   // (lg_tile_done's reset)
+    lg_fold_chunks(S, nch, 2u | 4u | LG_FOLD_SIZE, N, szfl, true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -784,11 +872,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_rs_rest(LgScratch S, uint32_t lo,
 }
 
 namespace {
-template <class FLAG, class EMIT>
+template <int PER = 8, class FLAG, class EMIT>
 void scan_emit(LgScratch& S, uint32_t n_max, int n_word, FLAG flag, EMIT emit, int total_word, hipStream_t s) {
-    const uint32_t nt = std::max<uint32_t>(1, tiles_of(n_max));
-    hipLaunchKernelGGL((lg_scan_emit<FLAG, EMIT>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag, emit,
-                       S.sstat, total_word);
+    const uint32_t nt = std::max<uint32_t>(1, (uint32_t)((n_max + PER * CG_BLOCK - 1) / (PER * CG_BLOCK)));
+    hipLaunchKernelGGL((lg_scan_emit<FLAG, EMIT, PER>), dim3(nt), dim3(CG_BLOCK), 0, s, n_max, n_word, S.meta, flag,
+                       emit, S.sstat, total_word);
 }
 
 }  // namespace
@@ -1076,13 +1164,17 @@ struct PclCompactEmit {
 };
 
 // The device-sized path's index_vector in one launch (lg_voxel_keys + lg_scan_emit with
-// PclCompact*): each tile of LG_TILE survivors computes its points' voxel keys, lists the finite
+// PclCompact*): each tile of LG_IDX_TILE survivors computes its points' voxel keys, lists the finite
 // ones in frame-index order through the decoupled look-back and writes their (idx << 32 | slot)
 // records to Eout; the count goes to meta[LG_PCL_N]. The keys and slots also go to key0 / val0
 // (a passthrough frame keeps them as its order). Workgroup 0 writes the grid words to the meta
 // words and empties the partition lists; every workgroup zeroes its share of the neighbour
 // grid's cell counts (lg_voxel_centroids counts into them). Survivors arrive in frame-index
 // order (lg_surv_write), so the keys carry no frame-index bits (PB = 0).
+#ifndef LG_IDX_PER
+#define LG_IDX_PER 2   // records per thread of lg_pcl_index and the voxel-run scan after the sort
+#endif
+#define LG_IDX_TILE (LG_IDX_PER * CG_BLOCK)
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParams P, uint64_t* Eout) {
     __shared__ uint32_t m[LG_META_WORDS];
     const uint32_t tid = threadIdx.x;
@@ -1104,24 +1196,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
         const uint32_t nc = m[LG_NCELL] + 1;
         for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < nc; i += gridDim.x * CG_BLOCK) S.cstart[i] = 0;
     }
-    const uint32_t active = Mtot ? (Mtot + LG_TILE - 1) / LG_TILE : 1u;
+    const uint32_t active = Mtot ? (Mtot + LG_IDX_TILE - 1) / LG_IDX_TILE : 1u;
     if (blockIdx.x >= active) return;
     const uint32_t t = lg_tile_ticket(S.sstat);
     if (t == 1) CG_HOOK_LG_STAMP(S, 60);
-    const uint64_t b0 = (uint64_t)t * LG_TILE + (uint64_t)tid * 8;
+    const uint64_t b0 = (uint64_t)t * LG_IDX_TILE + (uint64_t)tid * LG_IDX_PER;
     const uint32_t Ms = in[LG_MS];
     const bool pass = m[LG_PASS] != 0;
     const float mnb0 = (float)(int)m[LG_MINB], mnb1 = (float)(int)m[LG_MINB + 1], mnb2 = (float)(int)m[LG_MINB + 2];
     const uint32_t mul1 = m[LG_MUL1], mul2 = m[LG_MUL2];
-    uint32_t idx[8], c = 0;
-    float4 pt[8];
+    uint32_t idx[LG_IDX_PER], c = 0;
+    float4 pt[LG_IDX_PER];
 #pragma unroll
-    for (int q = 0; q < 8; q++) {   // the eight points' loads first (clamped: no branch between them)
+    for (int q = 0; q < LG_IDX_PER; q++) {   // the points' loads first (clamped: no branch between them)
         const uint32_t j = (uint32_t)min(b0 + q, (uint64_t)(Mtot ? Mtot - 1 : 0));
         pt[q] = j < Ms ? S.surv_p[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
+    for (int q = 0; q < LG_IDX_PER; q++) {
         const uint64_t j = b0 + q;
         idx[q] = 0xffffffffu;
         if (j < Mtot) {
@@ -1147,7 +1239,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
     uint32_t pos = lg_tile_scan(S.sstat, t, active, c, S.meta + LG_PCL_N);
     if (t == 1) CG_HOOK_LG_STAMP(S, 62);
 #pragma unroll
-    for (int q = 0; q < 8; q++)
+    for (int q = 0; q < LG_IDX_PER; q++)
         if (idx[q] != 0xffffffffu) Eout[pos++] = ((uint64_t)idx[q] << 32) | (uint32_t)(b0 + q);
     lg_tile_done(S.sstat, active);
     if (t == 1) CG_HOOK_LG_STAMP(S, 63);
@@ -1415,14 +1507,16 @@ __device__ __forceinline__ uint32_t* lg_arrivals(const LgScratch& S, uint32_t k)
     return (uint32_t*)(S.pqst + 2ull * (S.pq_tmax + 2u) + 2ull * PQ_MAXR) + 16u * k;
 }
 // the set of parity par as no level has used it: ticket counter, look-back words of the tiles
-// that took tickets, range words (every thread of the block)
-__device__ __forceinline__ void pq_clear_set(const LgScratch& S, uint32_t par) {
+// that took tickets, the range words of the nd ranges the set's level had (every thread of
+// the block; nothing to clear when that level handed out no ticket)
+__device__ __forceinline__ void pq_clear_set(const LgScratch& S, uint32_t par, uint32_t nd = PQ_MAXR) {
     uint64_t* const st = pq_set(S, par);
     const uint32_t used = (uint32_t)min(st[0], (uint64_t)S.pq_tmax);   // tickets handed out
     __syncthreads();
+    if (used == 0) return;   // (uniform) no tile took a ticket: no word was written
     for (uint32_t i = threadIdx.x; i < used + 2u; i += CG_BLOCK) st[i] = 0ull;
     uint64_t* const dn = pq_done(S, par);
-    for (uint32_t i = threadIdx.x; i < PQ_MAXR; i += CG_BLOCK) dn[i] = 0ull;
+    for (uint32_t i = threadIdx.x; i < nd; i += CG_BLOCK) dn[i] = 0ull;
 }
 #define PQ_WAIT_TICKS 20000000ull   // s_memrealtime (100 MHz): 200 ms, then LG_PQ_TIMEOUT
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint64_t* E, uint64_t* Eo, uint32_t level,
@@ -1446,7 +1540,12 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         pf = Lr[0]; pe = Lr[1]; pd = Lr[2];
     }
     if (blockIdx.x == 0) {
-        pq_clear_set(S, par ^ 1u);   // for level + 1
+        // for level + 1: the set level - 1 used, with the ranges level - 1 had (level 0: the
+        // whole index_vector; later levels: their list's count, read before the barrier in
+        // pq_clear_set, and that list is emptied below). Level 0 finds both sets clean: the
+        // levels and lg_pcl_leaf of the previous frame (or the allocation) left them so.
+        const uint32_t nprev = level == 1 ? 1u : (level ? min(S.pq[(level + 2u) % 3u], (uint32_t)PQ_MAXR) : 0u);
+        pq_clear_set(S, par ^ 1u, nprev);
         if (tid == 0) {
             if (level == 0) {   // (the lists' counts were zeroed by lg_pcl_index: this level pushes)
                 if (n <= LG_PCL_CUT) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
@@ -1660,9 +1759,9 @@ struct PqDefer {
         }
     }
 };
-#define LG_PCL_LDS (8 * LG_PCL_LEAF + 6 * 4 * (LG_PCL_LEAF + 4))
+#define LG_PCL_LDS (8 * LG_PCL_LEAF + 4 * 4 * (LG_PCL_LEAF + 4))
 // The rest of each leaf range (cg_pcl.h pcl_block_sort with the depth left on its path) from
-// the buffer its last level wrote: in LDS (8 B of record and 24 B of scratch per element),
+// the buffer its last level wrote: in LDS (8 B of record and 16 B of scratch per element),
 // else in HBM (ranges are disjoint, so each uses its own span of the scratch arrays).
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
                                                         uint32_t* vout, uint32_t clear_set) {
@@ -1684,8 +1783,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
         if (size <= LG_PCL_LEAF) {
             lds_u64* const El = (lds_u64*)(uint64_t*)smem;
             lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * LG_PCL_LEAF);
-            const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4),
-                                      w0 + 4 * (LG_PCL_LEAF + 4), w0 + 5 * (LG_PCL_LEAF + 4)};
+            const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4)};
             lds_u32* const Rl = (lds_u32*)red;
             const PqLeafOut out{kout, vout, first};
             const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ent[3], S.droot, S.pq + PQ_WAVES};
@@ -1716,7 +1814,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
 
 // The leaves' ranges of 65-512 records (S.dsz), one workgroup each, in LDS; their ranges of
 // 17-64 records go on to lg_pcl_waves.
-#define LG_MID_LDS (8 * PQ_MID + 6 * 4 * (PQ_MID + 4))
+#define LG_MID_LDS (8 * PQ_MID + 4 * 4 * (PQ_MID + 4))
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
                                                        uint32_t* vout) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LG_MID_LDS];
@@ -1724,8 +1822,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
     const uint32_t n = S.pq[PQ_MIDS];
     lds_u64* const El = (lds_u64*)(uint64_t*)smem;
     lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * PQ_MID);
-    const PbScratch<PbLds> PS{w0, w0 + (PQ_MID + 4), w0 + 2 * (PQ_MID + 4), w0 + 3 * (PQ_MID + 4),
-                              w0 + 4 * (PQ_MID + 4), w0 + 5 * (PQ_MID + 4)};
+    const PbScratch<PbLds> PS{w0, w0 + (PQ_MID + 4), w0 + 2 * (PQ_MID + 4), w0 + 3 * (PQ_MID + 4)};
     lds_u32* const Rl = (lds_u32*)red;
     for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
         const uint32_t first = S.dsz[2 * b], w1 = S.dsz[2 * b + 1];
@@ -2322,9 +2419,14 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
         typename K::P32 cw = D + w * C;
         for (uint32_t k = l; k < C; k += 64) cw[k] = 0u;
         const uint32_t cbits = cg_bits_of(C);
-        for (uint32_t v = wb0 + l; v < wb1; v += 64) {
-            const uint32_t rr = B[v];
-            if (rr != 0xffffffffu) lg_add(&cw[rr], 1u);
+        // (the counters are the wave's own: one plain add per distinct cluster of a 64-voxel
+        // chunk, by its lowest lane, instead of an LDS atomic per member)
+        for (uint32_t vb = wb0; vb < wb1; vb += 64) {
+            const uint32_t v = vb + l;
+            const uint32_t rr = v < wb1 ? B[v] : 0xffffffffu;
+            const bool in = rr != 0xffffffffu;
+            const uint64_t same = lg_match(rr, cbits, __ballot(in));
+            if (in && (same & lt) == 0ull) cw[rr] += (uint32_t)__popcll(same);
         }
         __syncthreads();
         for (uint32_t k = tid; k < C; k += CG_BLOCK) {   // counts -> each wave's start per cluster
@@ -2516,7 +2618,7 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
         return hipGetLastError();
     }
     const uint32_t fi = init ? 1u : 0u;   // lg_front's workgroup 0 resets the meta words
-    // the device-sized path: lg_decide folds the chunks' keys (no lg_reduce_chunks launch after
+    // the device-sized path: lg_decide_write folds the chunks' keys (no lg_reduce_chunks launch after
     // the pipeline front); the counts' fold also sizes the detector input (LG_FOLD_SIZE)
     const bool dev = (szfl & LG_SZ_ON) != 0;
     const dim3 g(nch), b(CG_BLOCK);
@@ -2531,7 +2633,7 @@ int cg_large_front(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch
     } else {                                                                                      \
         hipLaunchKernelGGL((lg_front<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, fi);             \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 1u, 0u, 0u);                      \
-        hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f, 0u);        \
+        hipLaunchKernelGGL((lg_decide<LAY, CG_KMODE_GROUND>), g, b, 0, s, L, P, S, f);            \
         hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u, 0u, 0u);                      \
         hipLaunchKernelGGL(lg_ground_out<LAY>, g, b, 0, s, L, P, S, f);                           \
     }
@@ -2549,20 +2651,26 @@ int cg_large_decide(const CgLaunch& L, const CgDevParams& P, LgScratch S, hipStr
     if (nch == 0) return hipSuccess;
     const bool xyzi16 = L.point_step == 16 && L.off_x == 0 && L.off_y == 4 && L.off_z == 8 && L.off_i == 12;
     const dim3 g(nch), b(CG_BLOCK);
-    const bool dev = (szfl & LG_SZ_ON) != 0;   // (lg_decide folds the front's chunk keys)
-    // the decisions' counts and bounds folded by one workgroup: the device-sized path folds them
-    // in lg_surv_write's last workgroup, otherwise a launch after it (folded in every
-    // lg_voxel_keys workgroup instead, 2,048 of them on C5 each reading the 256 chunk records:
-    // 15.6 against 5.0 + 5.0 us, profiles/r4_c5_fold_ab.txt)
-    const uint32_t fw = dev ? 2u | 4u | LG_FOLD_SIZE : 0u;
-    if (xyzi16) {
-        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
-        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f, fw, L.n_points, szfl);
-    } else {
-        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f, dev ? nch : 0u);
-        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f, fw, L.n_points, szfl);
+    // the device-sized path: decisions and survivors in one launch, the counts and bounds
+    // folded by its last workgroup (lg_decide_write; round 4's lg_decide + lg_surv_write pair
+    // 9.2 + 11.6 us on C5). Otherwise the decisions, the survivors, then one workgroup folds
+    // (folded in every lg_voxel_keys workgroup instead, 2,048 of them on C5 each reading the
+    // 256 chunk records: 15.6 against 5.0 + 5.0 us, profiles/r4_c5_fold_ab.txt).
+    if (szfl & LG_SZ_ON) {
+        if (xyzi16)
+            hipLaunchKernelGGL(lg_decide_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, P, S, f, nch, L.n_points, szfl);
+        else
+            hipLaunchKernelGGL(lg_decide_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, P, S, f, nch, L.n_points, szfl);
+        return hipGetLastError();
     }
-    if (!dev) hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u, L.n_points, szfl);
+    if (xyzi16) {
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_XYZI16, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_XYZI16>, g, b, 0, s, L, S, f, 0u, L.n_points, szfl);
+    } else {
+        hipLaunchKernelGGL((lg_decide<CG_LAYOUT_GENERIC, CG_KMODE_PIPELINE>), g, b, 0, s, L, P, S, f);
+        hipLaunchKernelGGL(lg_surv_write<CG_LAYOUT_GENERIC>, g, b, 0, s, L, S, f, 0u, L.n_points, szfl);
+    }
+    hipLaunchKernelGGL(lg_reduce_chunks, dim3(1), b, 0, s, S, nch, 2u | 4u, L.n_points, szfl);
     return hipGetLastError();
 }
 
@@ -2717,7 +2825,8 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     // index_vector (finite points in frame-index order) as (idx, slot) records, with the voxel
     // keys computed on the way (lg_pcl_index), then std::sort's permutation of it: levels for the
     // frame's N (levels with no range return at once)
-    hipLaunchKernelGGL(lg_pcl_index, dim3(std::max<uint32_t>(1, tiles_of(nmax))), dim3(CG_BLOCK), 0, s, S, P, kb[1]);
+    hipLaunchKernelGGL(lg_pcl_index, dim3(std::max<uint32_t>(1, (nmax + LG_IDX_TILE - 1) / LG_IDX_TILE)), dim3(CG_BLOCK), 0,
+                       s, S, P, kb[1]);
     // one launch per level (lg_pq_level); a level's tiles number at most tb + its ranges (<= 2^lv),
     // taken by at most 512 workgroups (more when a workgroup would hold more than PQ_OWN tiles)
     // (level 0 always runs: with no level to cut it queues the whole index_vector as a leaf)
@@ -2737,10 +2846,9 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, nmax / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s, S,
                        kb[1], kb[0], kb[0], vb2[0]);
     // voxel runs over the finite points (LG_SCAN_N; every point if passthrough), centroids
-    scan_emit(S, nmax, LG_SCAN_N, VoxelHead{S.key0, S.meta, 0u}, VoxelEmit{S.run}, LG_V, s);
+    scan_emit<LG_IDX_PER>(S, nmax, LG_SCAN_N, VoxelHead{S.key0, S.meta, 0u}, VoxelEmit{S.run}, LG_V, s);
     hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(nmax)), dim3(CG_BLOCK), 0, s, Lh, S, f, nmax, 0);
-    const uint32_t VB = bits_of(nmax);
-    const uint32_t vb = blocks_of(nmax), wb = lg_wave_blocks(nmax);
+    const uint32_t wb = lg_wave_blocks(nmax);
     const uint32_t gt = LG_DCELLS_MAX / LG_TILE + 1;
     hipLaunchKernelGGL(lg_dgrid_scan_fill, dim3(gt), dim3(CG_BLOCK), 0, s, S);
     // (the flattening in lg_forest's last workgroup instead: 19.8 against 7.1 + 5.9 us, the
@@ -2910,7 +3018,7 @@ namespace {
 uint64_t lg_pq_tmax(uint64_t n) { return (n + PQ_T - 1) / PQ_T + PQ_MAXR; }
 template <class F>
 uint64_t lg_walk(uint32_t n, F place) {
-    const uint64_t N = std::max<uint32_t>(n, 1), nch = (N + LG_CHUNK - 1) / LG_CHUNK, nt = tiles_of(N);
+    const uint64_t N = std::max<uint32_t>(n, 1), nch = (N + LG_CHUNK - 1) / LG_CHUNK;
     uint64_t off = 0;
     auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~255ull; return o; };
     place(0, take(LG_META_WORDS * 4));
@@ -2922,7 +3030,7 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(10, take(N * 4)); place(11, take(N * 4));
     const uint64_t nrs = (N + LG_RS_TILE - 1) / LG_RS_TILE;
     place(12, take((std::max<uint64_t>(256 * nrs, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
-    place(13, take((std::max<uint64_t>(nt, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));
+    place(13, take((std::max<uint64_t>(N / CG_BLOCK + 1, LG_DCELLS_MAX / LG_TILE + 1) + 2) * 4));   // (tiles of >= 512)
     place(14, take(N * 16));
     place(15, take((N + 2) * 4));
     for (int a = 0; a < 12; a++) place(16 + a, take((N + 2) * 4));

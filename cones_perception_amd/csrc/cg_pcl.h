@@ -125,36 +125,36 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 // ------------------------------------------------------------------------------------------
 // The whole workgroup sorts n <= CG_BLOCK * PER elements, every partition of a level of
 // __introsort_loop at once. Element x = tid + CG_BLOCK * k (k < PER); each thread keeps the
-// range [f, e) of its elements in registers and follows the cut after every level. Per level
-// (a barrier after each step):
-//   S1. >= / <= pivot against the range's pivot; per (chunk, wave) counts;
+// range [f, e) of its elements and the range's depth budget in registers and follows the cut
+// after every level. Per level (a barrier after each step):
+//   S1. every element of a range to partition (longer than WMAX, budget left) reads the range's
+//       median of three itself (__move_median_to_first's swap stays virtual: position m holds
+//       E[f]'s record, position f the median's) and compares with the pivot; per (chunk, wave)
+//       counts; the barrier's OR ends the levels when no range is left to partition;
 //   S2. the counts scanned: every position's inclusive >= / <= counts over the whole array
 //       (RLO); the >= elements listed at their exclusive count in PL, the <= ones in PR, so
 //       a range's L list is the stretch of PL from RLO[f] and its R list the stretch of PR
-//       below RLO[e - 1], read from the right; heads reset the swap count;
+//       below RLO[e - 1], read from the right;
 //   S4. the swaps (L_k, R_k) while L_k < R_k: every partner is read, then every element
-//       written (or the records go out of place to E2); the last swap of a range records the
-//       swap count s;
-//   S5. each head: the cut (L_0 if s = 0, else min(L_s, R_{s-1})), then both children set up
-//       as __introsort_loop does (heapsort when the depth budget is spent, a wave task when at
-//       most 64 long, else the median of three moved to first and the pivot);
-//   S0. every element follows the cut into its child range.
-// Then the ranges of 17-64 records, one wave each (pw_range64), and the final insertion
-// passes of the rest: a stable rank inside each range of at most 16; heapsorted ranges are
-// sorted already. A (wave, k) slot whose elements are all in final ranges skips every step
-// of the later levels. Scratch: INFO (act | final | wave | budget at heads), PIV, RLO, PL,
-// PR, CUT (swap count, then cut), n + 1 words each; cnt: 8 * PER words. E is permuted in place.
-#define PB_ACT 0x100u
-#define PB_FIN 0x200u
-#define PB_WAVE 0x400u   // a range of at most PW_MAX records with budget left: one wave sorts it
+//       written (or the records go out of place to E2) with V of its partner; the range's
+//       cutter stores the cut: the element holding the last swap's L (min(L_s, R_{s-1})), or
+//       L_0 when there is no swap;
+//   S0. every element follows the cut into its child range, budget - 1.
+// Then a range longer than 16 with its budget spent is heapsorted by its first element's
+// thread (__partial_sort); the ranges of 17-WMAX records go one wave each (pw_range64, or a
+// deferring functor); the rest get the final insertion passes: a stable rank inside each range
+// of at most 16. A (wave, k) slot whose elements are all in final ranges skips every step of
+// the later levels. Scratch: RLO, PL, PR, CUT, n + 1 words each; cnt: 8 * PER words. E is
+// permuted in place. (Round 4's form set each range up in a fourth step by its first element's
+// thread; the three-step form takes 8.4-8.8 against 9.4-9.6 us for C3's 243 records,
+// profiles/r5_pb3_ab.txt.)
 #define PW_MAX 64
-#define PB_BUDGET 0xffu
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 // Pointer kinds: LDS (ds_* instructions) when the arrays live in LDS, generic otherwise.
 struct PbLds { typedef lds_u32* P32; typedef lds_u64* P64; };
 struct PbGen { typedef uint32_t* P32; typedef uint64_t* P64; };
-template <class K> struct PbScratch { typename K::P32 INFO, PIV, RLO, PL, PR, CUT; };
+template <class K> struct PbScratch { typename K::P32 RLO, PL, PR, CUT; };
 struct PwLess {   // a functor, not a function: a function pointer could become an indirect call
     __device__ __forceinline__ bool operator()(uint64_t a, uint64_t b) const { return pcl_key(a) < pcl_key(b); }
 };
@@ -165,49 +165,6 @@ __device__ __forceinline__ uint32_t pb_median(uint32_t a, uint32_t b, uint32_t c
     if (ka < kb) return kb < kc ? b : (ka < kc ? c : a);
     if (ka < kc) return a;
     return kb < kc ? c : b;
-}
-
-// A head sets up the two children [f, cut) and [cut, e) of a partitioned range, children's
-// budget d (the body of __introsort_loop): a child longer than 16 is heapsorted when d == 0
-// (final), else its median of three is moved to its first and its pivot noted (partitioned in
-// the next level). The eight elements are read in one batch, then written. Returns whether a
-// child is partitioned next.
-template <class K, uint32_t WMAX>
-__device__ __forceinline__ bool pb_children(typename K::P64 E, const PbScratch<K>& S, uint32_t f, uint32_t cut,
-                                            uint32_t e, uint32_t d) {
-    const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
-    bool med[2];
-    uint32_t ia[2], ib[2], ic[2];
-    uint64_t v0[2], va[2], vb[2], vc[2];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-        med[c] = hi[c] - lo[c] > WMAX && d > 0;
-        ia[c] = lo[c] + 1; ib[c] = lo[c] + (hi[c] - lo[c]) / 2; ic[c] = hi[c] - 1;
-        if (med[c]) { v0[c] = E[lo[c]]; va[c] = E[ia[c]]; vb[c] = E[ib[c]]; vc[c] = E[ic[c]]; }
-    }
-    bool act = false;
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-        uint32_t info = d;
-        if (hi[c] - lo[c] > CG_SORT_THRESHOLD) {
-            if (d == 0) {   // __partial_sort(first, last, last): final
-                cg_heap_sort_range((uint64_t*)(E + lo[c]), (long)(hi[c] - lo[c]), PwLess{});
-                info |= PB_FIN;
-            } else if (hi[c] - lo[c] <= WMAX) {   // the rest of it as a task (one wave: pw_range64)
-                info |= PB_WAVE;
-            } else {
-                const uint32_t m = pb_median(ia[c], ib[c], ic[c], pcl_key(va[c]), pcl_key(vb[c]), pcl_key(vc[c]));
-                const uint64_t vm = m == ia[c] ? va[c] : (m == ib[c] ? vb[c] : vc[c]);
-                E[lo[c]] = vm;
-                E[m] = v0[c];
-                S.PIV[lo[c]] = pcl_key(vm);
-                info |= PB_ACT;
-                act = true;
-            }
-        }
-        S.INFO[lo[c]] = info;
-    }
-    return act;
 }
 
 // Always inlined: an out-of-line call takes its arguments through scratch memory (and
@@ -324,6 +281,14 @@ struct PwInline {
 // per-slot counts). S.RLO holds n + 1 words.
 // WMAX: ranges of at most WMAX records (with budget left) leave the levels as tasks for wt;
 // PwInline takes at most PW_MAX.
+// Three barrier-separated steps per level. Each thread keeps, for each of its elements, the
+// element's range [f, e) and the range's depth budget in registers, so a range's set-up needs
+// no heads step: in S1 every element of a range longer than WMAX (budget left) reads the
+// range's median of three itself (__move_median_to_first's swap stays virtual: position m
+// holds E[f]'s record, position f the median's), in S4 the swaps write V(partner) and the
+// range's cutter -- the element holding the last swap's L (cut = min(L_s, R_{s-1})), or L_0
+// when there is no swap (cut = L_0) -- stores the cut, and S0 follows it. (tests/pb_model.py
+// block_sort models it thread by thread against std::sort.)
 template <int PER, class K, class OUT = PbStore<typename K::P64>, bool OOP = false, class WT = PwInline,
           uint32_t WMAX = PW_MAX>
 __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint32_t n, uint32_t depth0,
@@ -332,49 +297,50 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     constexpr uint32_t GE = 1u << 24, LE = 1u << 25, IN = 1u << 26, PART = 1u << 27;
     constexpr uint32_t NS = PER * WAVES;   // (chunk, wave) slots: position x is in slot x / 64
-    uint32_t fe[PER];
+    uint32_t fe[PER], dp[PER];
 #pragma unroll
-    for (int k = 0; k < PER; k++) fe[k] = n << 16;
-    bool act = false;
-    if (tid == 0 && n) {   // the whole array as the right child of an empty range
-        act = pb_children<K, WMAX>(E, S, 0, 0, n, depth0);
-    }
-    bool any = __syncthreads_or(act);
+    for (int k = 0; k < PER; k++) { fe[k] = n << 16; dp[k] = depth0; }
     // (wave, k) slots with an element in a partitioned range; a slot without one has nothing
     // to do in any later level (ranges only shrink, and a final range stays final)
     uint32_t live = (1u << PER) - 1u;
-    while (any) {
-        uint32_t st[PER], nn[PER];
-        // S1: compare with the range's pivot; per-slot counts
+    const uint32_t top = n ? n - 1 : 0u;
+    for (;;) {
+        uint32_t st[PER], mm[PER];
+        bool mine = false;
+        // S1: the range's median of three and pivot, >= / <= against it; per-slot counts
 #pragma unroll
         for (int k = 0; k < PER; k++) {
+            mm[k] = 0u;
             if (!((live >> k) & 1u)) {
                 if (l == 0) cnt[k * WAVES + w] = 0u;
                 st[k] = 0u;
                 continue;
             }
-            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
-            uint32_t info = 0, p = 0, kx = 0;
-            if (x < n) {
-                info = S.INFO[f];
-                p = S.PIV[f];
-                kx = pcl_key(E[x]);
-            }
-            const bool part = (info & PB_ACT) != 0, in = part && x > f;
+            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+            const bool part = x < n && e - f > CG_SORT_THRESHOLD && e - f > WMAX && dp[k] > 0;
+            // the five keys in one batch (indices clamped: no branch between the loads)
+            const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
+            const uint32_t ka = pcl_key(E[part ? a : 0u]), kb = pcl_key(E[part ? b : 0u]), kc = pcl_key(E[part ? c : 0u]);
+            const uint32_t kf = pcl_key(E[part ? f : 0u]), kx0 = pcl_key(E[min(x, top)]);
+            const uint32_t m = pb_median(a, b, c, ka, kb, kc);
+            const uint32_t p = m == a ? ka : (m == b ? kb : kc);
+            const uint32_t kx = x == m ? kf : kx0;
+            const bool in = part && x > f;
             const bool ge = in && kx >= p, le = in && kx <= p;
             const uint64_t gm = __ballot(ge), lm = __ballot(le);
             if (l == 0) cnt[k * WAVES + w] = (uint32_t)__popcll(gm) | ((uint32_t)__popcll(lm) << 16);
             st[k] = mbcnt(gm) | (mbcnt(lm) << 12) | (ge ? GE : 0u) | (le ? LE : 0u) | (in ? IN : 0u) | (part ? PART : 0u);
+            mm[k] = m;
+            mine |= part;
             if (!__ballot(part)) live &= ~(1u << k);
         }
-        __syncthreads();
+        if (!__syncthreads_or(mine)) break;   // (uniform) no range left to partition
         PCL_STEP();
         // S2: lane j of every wave scans the slot counts; every position's >= / <= counts over
         // the whole array, inclusive, go to RLO, and the >= elements are listed in position
         // order at their exclusive >= count in PL, the <= elements at theirs in PR: a range's
-        // L list is then a contiguous stretch of PL from RLO[f] (the head counts for nothing),
-        // its R list the stretch of PR below RLO[e - 1], read from the right. Both words lie
-        // in live slots.
+        // L list is then a contiguous stretch of PL from RLO[f] (the first position counts for
+        // nothing), its R list the stretch of PR below RLO[e - 1], read from the right.
         {
             // both counts in one scan of the packed word (totals <= n <= 4,096: no carry
             // between the halves)
@@ -384,21 +350,20 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
 #pragma unroll
             for (int k = 0; k < PER; k++) {
                 if (!((live >> k) & 1u)) continue;
-                const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
+                const uint32_t x = tid + CG_BLOCK * k;
                 const uint32_t src = (uint32_t)k * WAVES + w;
                 const uint32_t gx = (uint32_t)__builtin_amdgcn_readlane((int)gex, (int)src) + (st[k] & 0xfffu);
                 const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)hex, (int)src) + ((st[k] >> 12) & 0xfffu);
                 if (x < n) S.RLO[x] = (gx + ((st[k] & GE) ? 1u : 0u)) | ((lx + ((st[k] & LE) ? 1u : 0u)) << 16);
                 if (st[k] & GE) S.PL[gx] = x;
                 if (st[k] & LE) S.PR[lx] = x;
-                if ((st[k] & PART) && x == f) S.CUT[f] = 0u;
                 st[k] = (gx & 0xfffu) | ((lx & 0xfffu) << 12) | (st[k] & (GE | LE | IN | PART));
             }
         }
         __syncthreads();
         PCL_STEP();
-        // S4: the range's list bounds, the partners and the next pair in one batch, then the
-        // partners' records
+        // S4: the range's list bounds, the partners and the next pair in one batch, then V of
+        // the partner; the cutter stores the cut
         uint64_t val[PER];
         uint32_t sw = 0;
         uint32_t bf[PER], be[PER];
@@ -413,29 +378,34 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         for (int k = 0; k < PER; k++) {
             if (!OOP && !((live >> k) & 1u)) continue;   // out of place, every record moves
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
-            const bool in = (st[k] & IN) != 0;
+            const bool in = (st[k] & IN) != 0, part = (st[k] & PART) != 0;
             const uint32_t gf = bf[k] & 0xffffu, lend = be[k] >> 16;
             const uint32_t nL = (be[k] & 0xffffu) - gf, nR = lend - (bf[k] >> 16);
-            nn[k] = nL | (nR << 16);
             const uint32_t li = in ? (st[k] & 0xfffu) - gf : 0u, ri = in ? lend - 1u - ((st[k] >> 12) & 0xfffu) : 0u;
             const bool hasL = in && (st[k] & GE) && li < nR, hasR = in && (st[k] & LE) && ri < nL;
             const bool nxt = hasL && li + 1 < min(nL, nR);
-            const uint32_t top = n ? n - 1 : 0u;
-            const uint32_t j = S.PR[hasL ? lend - 1u - li : 0u];        // R_li
-            const uint32_t i = S.PL[hasR ? gf + ri : 0u];                // L_ri
-            const uint32_t pl2 = S.PL[min(nxt ? gf + li + 1u : 0u, top)];          // L_li+1
-            const uint32_t pr2 = S.PR[nxt ? lend - 2u - li : 0u];        // R_li+1
+            const uint32_t j = S.PR[hasL ? lend - 1u - li : 0u];                     // R_li
+            const uint32_t i = S.PL[hasR ? gf + ri : 0u];                             // L_ri
+            const uint32_t pl2 = S.PL[min(hasL && li + 1 < nL ? gf + li + 1u : 0u, top)];   // L_li+1
+            const uint32_t pr2 = S.PR[nxt ? lend - 2u - li : 0u];                    // R_li+1
             uint32_t partner = x;
-            if (hasL && x < j) {
-                partner = j;
-                if (!nxt || !(pl2 < pr2)) S.CUT[f] = li + 1;
+            if (hasL) {
+                if (x < j) {
+                    partner = j;
+                    if (!nxt || !(pl2 < pr2)) S.CUT[f] = min(li + 1 < nL ? pl2 : 0xffffffffu, j);   // the last swap
+                } else if (li == 0) {
+                    S.CUT[f] = x;   // no swap: the left scan stops at L_0
+                }
             }
             if (hasR && i < x) partner = i;
             if (x < n) {
+                // V(partner): position m holds E[f]'s record, position f the median's
+                uint32_t src = partner;
+                if (part) src = x == f ? mm[k] : (partner == mm[k] ? f : partner);
                 if (OOP) {
-                    val[k] = E[partner];
-                } else if (partner != x) {
-                    val[k] = E[partner];
+                    val[k] = E[src];
+                } else if (src != x) {
+                    val[k] = E[src];
                     sw |= 1u << k;
                 }
             }
@@ -455,46 +425,33 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         }
         __syncthreads();
         PCL_STEP();
-        // S5: heads
-        act = false;
-#pragma unroll
-        for (int k = 0; k < PER; k++) {
-            const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
-            if ((st[k] & PART) && x == f) {
-                const uint32_t s = S.CUT[f], info = S.INFO[f];
-                const uint32_t gf = S.RLO[f] & 0xffffu, lend = S.RLO[e - 1] >> 16, nL = nn[k] & 0xffffu;
-                const uint32_t pl1 = S.PL[gf];
-                const uint32_t pls = s < nL ? S.PL[gf + s] : 0xffffffffu, prs = s ? S.PR[lend - s] : 0u;
-                const uint32_t cut = s == 0 ? pl1 : min(pls, prs);
-                act |= pb_children<K, WMAX>(E, S, f, cut, e, (info & PB_BUDGET) - 1u);
-                S.CUT[f] = cut;
-            }
-        }
-        any = __syncthreads_or(act);
-        PCL_STEP();
-        // S0
+        // S0: every element follows the cut into its child range
 #pragma unroll
         for (int k = 0; k < PER; k++) {
             const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
             if (st[k] & PART) {
                 const uint32_t c = S.CUT[f];
                 fe[k] = x < c ? (f | (c << 16)) : (c | (e << 16));
+                dp[k] -= 1u;
             }
         }
     }
-    // ranges of at most WMAX records with budget left: one wave each (wt), listed
-    // in PL (first | last << 16) and PR (budget), the count in cnt[0]
+    // the ranges left longer than 16: a spent budget is heapsorted (__partial_sort) and stored
+    // by its first element's thread; the others (at most WMAX records) go to one wave each (wt),
+    // listed in PL (first | last << 16) and PR (budget), the count in cnt[0]
     if (tid == 0) cnt[0] = 0u;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PER; k++) {
-        const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu;
-        if (x < n && x == f) {
-            const uint32_t info = S.INFO[f];
-            if (info & PB_WAVE) {
+        const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
+        if (x < n && x == f && e - f > CG_SORT_THRESHOLD) {
+            if (dp[k] == 0) {
+                cg_heap_sort_range((uint64_t*)(E + f), (long)(e - f), PwLess{});
+                for (uint32_t y = f; y < e; y++) out(y, E[y]);
+            } else {
                 const uint32_t q = atomicAdd((uint32_t*)(cnt + 0), 1u);
                 S.PL[q] = fe[k];
-                S.PR[q] = info & PB_BUDGET;
+                S.PR[q] = dp[k];
             }
         }
     }
@@ -507,33 +464,28 @@ __device__ __forceinline__ void pcl_block_sort(typename K::P64 E, OUT out, uint3
         }
     }
     PCL_STEP();
-    // the final insertion passes of the other ranges
+    // the final insertion passes of the ranges of at most 16
 #pragma unroll
     for (int k = 0; k < PER; k++) {
         const uint32_t x = tid + CG_BLOCK * k, f = fe[k] & 0xffffu, e = fe[k] >> 16;
-        if (x < n && !(S.INFO[f] & PB_WAVE)) {
+        if (x < n && e - f <= CG_SORT_THRESHOLD) {
             const uint64_t r = E[x];
-            const uint32_t info = S.INFO[f];
             uint32_t kj[CG_SORT_THRESHOLD];
 #pragma unroll
             for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++) kj[j] = f + j < e ? pcl_key(E[f + j]) : 0u;
-            if (info & PB_FIN) {
-                out(x, r);
-            } else {
-                const uint32_t kx = pcl_key(r);
-                uint32_t rank = 0;
+            const uint32_t kx = pcl_key(r);
+            uint32_t rank = 0;
 #pragma unroll
-                for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++)
-                    rank += f + j < e && ((kj[j] < kx) || (kj[j] == kx && f + j < x));
-                out(f + rank, r);
-            }
+            for (uint32_t j = 0; j < CG_SORT_THRESHOLD; j++)
+                rank += f + j < e && ((kj[j] < kx) || (kj[j] == kx && f + j < x));
+            out(f + rank, r);
         }
     }
     __syncthreads();
 }
 
 // std::sort(E, E + n) by key (E in W.VOX) into KEY, libstdc++'s permutation. Up to
-// PCL_BLOCK_MAX elements: pcl_block_sort (scratch W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD; red
+// PCL_BLOCK_MAX elements: pcl_block_sort (scratch W.A, W.PAR, W.CNT, W.ORD; red
 // for the counts). Longer arrays (the HBM-scratch backend, large-frame leaves in HBM): block
 // levels over W.A (prefix, n + 1), W.PAR / W.CNT (L and R lists), W.UK (range of each
 // position), W.ORD (flags), W.LAB (size | depth << 26 at each range's first), W.OFF (pivot,
@@ -559,8 +511,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
     const uint32_t d0 = (uint32_t)(depth0 >= 0 ? depth0 : 2 * cg_lg((long)n));
     PCL_STAMP();
     if constexpr (LDS) {
-        const PbScratch<PbLds> PS{(lds_u32*)(uint32_t*)W.LAB, (lds_u32*)W.OFF, (lds_u32*)W.A, (lds_u32*)W.PAR,
-                                  (lds_u32*)W.CNT, (lds_u32*)W.ORD};
+        const PbScratch<PbLds> PS{(lds_u32*)W.A, (lds_u32*)W.PAR, (lds_u32*)W.CNT, (lds_u32*)W.ORD};
         lds_u64* const El = (lds_u64*)E;
         lds_u64* const Ko = (lds_u64*)W.KEY;
         lds_u32* const Rl = (lds_u32*)red;
@@ -579,7 +530,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         PCL_STAMP();
         return;
     }
-    const PbScratch<PbGen> PS{(uint32_t*)W.LAB, W.OFF, W.A, W.PAR, W.CNT, W.ORD};
+    const PbScratch<PbGen> PS{W.A, W.PAR, W.CNT, W.ORD};
     if (n <= PMAX * CG_BLOCK) {
         pcl_block_sort<PMAX, PbGen>(E, PbStore<uint64_t*>{W.KEY}, n, d0, PS, red);
         PCL_STAMP();
@@ -744,8 +695,7 @@ __device__ __forceinline__ void pcl_sort(const Work& W, uint64_t* E, uint32_t n,
         const uint32_t size = INFO[first] & ISZ, depth = INFO[first] >> 26;
         __syncthreads();   // every thread has the range before pcl_block_sort rewrites INFO[first]
         pcl_block_sort<PMAX, PbGen>(E + first, PbStore<uint64_t*>{KEY + first}, size, depth,
-                                    PbScratch<PbGen>{(uint32_t*)W.LAB + first, W.OFF + first, W.A + first,
-                                                     W.PAR + first, W.CNT + first, W.ORD + first},
+                                    PbScratch<PbGen>{W.A + first, W.PAR + first, W.CNT + first, W.ORD + first},
                                     red);
     }
     __syncthreads();

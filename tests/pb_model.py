@@ -129,184 +129,12 @@ def std_sort(a, depth0=None):
 
 # ---- the block model ------------------------------------------------------------------------
 BLOCK, WAVES = 512, 8
-ACT, FINB, WAVEB, BUDGET = 0x100, 0x200, 0x400, 0xFF
+
 PW_MAX = 64
 
 
 def _popc(m):
     return bin(m).count("1")
-
-
-def _setup(E, S, cf, ce, d, wmax):
-    info, act = d, False
-    if ce - cf > THRESH:
-        if d == 0:
-            heap_sort_range(E, cf, ce - cf)
-            info |= FINB
-        elif ce - cf <= wmax:
-            info |= WAVEB
-        else:
-            move_median_to_first(E, cf, cf + 1, cf + (ce - cf) // 2, ce - 1)
-            S["PIV"][cf] = key(E[cf])
-            info |= ACT
-            act = True
-    S["INFO"][cf] = info
-    return act
-
-
-def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False):
-    """cg_pcl.h pcl_block_sort, thread by thread: element x = tid + 512 k (oop: the swaps go
-    to a second buffer, as in the frame kernel). Ranges of 17..wmax records with budget left
-    leave the levels as tasks: sorted by wave_sort (PwInline), or, with defer, returned as
-    (first, size, budget, records) with their output positions left None (PqDefer)."""
-    n = len(E_in)
-    if PER is None:
-        PER = 1 if n <= 512 else 2 if n <= 1024 else 4 if n <= 2048 else 8
-    assert n <= BLOCK * PER
-    if depth0 is None:
-        depth0 = 2 * _lg(n) if n else 0
-    E = Arr(n)
-    E.v = list(E_in)
-    out = Arr(n, None)
-    S = {k: Arr(n + 1) for k in ("INFO", "PIV", "RLO", "PL", "PR", "CUT")}
-    cnt = Arr(8 * PER)
-    T = range(BLOCK)
-    fe = [[n << 16] * PER for _ in T]
-    anyact = _setup(E, S, 0, n, depth0, wmax) if n else False
-    live = [[True] * PER for _ in range(WAVES)]       # (wave, k) slots with a partitioned range
-    while anyact:
-        st = [[0] * PER for _ in T]
-        nn = [[0] * PER for _ in T]
-        S["RLO"] = Arr(n + 1, None)                  # a read of a word not written this level fails
-        for k in range(PER):                         # S1
-            ge = [False] * BLOCK
-            le = [False] * BLOCK
-            dead = [not live[w][k] for w in range(WAVES)]
-            for t in T:
-                if dead[t // 64]:                    # a dead slot: nothing to do in any step
-                    st[t][k] = dict(part=False, inn=False)
-                    continue
-                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
-                info = p = kx = 0
-                if x < n:
-                    info, p, kx = S["INFO"][f], S["PIV"][f], key(E[x])
-                part = bool(info & ACT)
-                inn = part and x > f
-                ge[t], le[t] = inn and kx >= p, inn and kx <= p
-                st[t][k] = dict(part=part, inn=inn)
-            for w in range(WAVES):
-                if dead[w]:
-                    cnt[k * WAVES + w] = 0
-                    continue
-                gm = sum(1 << l for l in range(64) if ge[64 * w + l])
-                lm = sum(1 << l for l in range(64) if le[64 * w + l])
-                cnt[k * WAVES + w] = _popc(gm) | (_popc(lm) << 16)
-                if not any(st[64 * w + l][k]["part"] for l in range(64)):
-                    live[w][k] = False               # ranges only shrink: dead for good
-                for l in range(64):
-                    t = 64 * w + l
-                    st[t][k].update(ge=ge[t], le=le[t], mg=_popc(gm & ((1 << l) - 1)), ml=_popc(lm & ((1 << l) - 1)))
-        NS = PER * WAVES                             # S2: global ranks, lists at those ranks
-        c = [cnt[j] for j in range(NS)]
-        gex = [sum(c[i] & 0xFFFF for i in range(j)) for j in range(NS)]
-        hex_ = [sum(c[i] >> 16 for i in range(j)) for j in range(NS)]
-        for t in T:
-            w = t // 64
-            for k in range(PER):
-                x, f = t + BLOCK * k, fe[t][k] & 0xFFFF
-                q = st[t][k]
-                if "ge" not in q:                    # dead slot (it was dead in S1 already)
-                    continue
-                gx, lx = gex[k * WAVES + w] + q["mg"], hex_[k * WAVES + w] + q["ml"]
-                assert gx < 4096 and lx < 4096
-                q.update(gx=gx, lx=lx)
-                if x < n:   # inclusive counts: a range's words are at its first and last position
-                    S["RLO"][x] = (gx + q["ge"]) | ((lx + q["le"]) << 16)
-                if q["ge"]:
-                    S["PL"][gx] = x
-                if q["le"]:
-                    S["PR"][lx] = x
-                if q["part"] and x == f:
-                    S["CUT"][f] = 0
-        val = {}
-        for t in T:                                  # S4: a range's bounds from RLO
-            for k in range(PER):
-                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-                q = st[t][k]
-                if not q["part"]:
-                    continue
-                bf, be = S["RLO"][f], S["RLO"][e - 1]
-                gf, lend = bf & 0xFFFF, be >> 16
-                nL, nR = (be & 0xFFFF) - gf, lend - (bf >> 16)
-                nn[t][k] = (nL, nR)
-                if not q["inn"]:
-                    continue
-                li, ri = q["gx"] - gf, lend - 1 - q["lx"]
-                partner = x
-                if q["ge"] and li < nR:
-                    j = S["PR"][lend - 1 - li]            # R_li
-                    if x < j:
-                        partner = j
-                        if li + 1 >= min(nL, nR) or not S["PL"][gf + li + 1] < S["PR"][lend - 2 - li]:
-                            S["CUT"][f] = li + 1
-                if q["le"] and ri < nL:
-                    i = S["PL"][gf + ri]                 # L_ri
-                    if i < x:
-                        assert partner == x, "an element swapped twice"
-                        partner = i
-                if partner != x:
-                    val[x] = E[partner]
-        if oop:   # every record to the other buffer, then the buffers trade places
-            E2 = Arr(n)
-            E2.v = list(E.v)
-            for x, v in val.items():
-                E2[x] = v
-            E = E2
-        else:
-            for x, v in val.items():
-                E[x] = v
-        anyact = False                               # S5
-        for t in T:
-            for k in range(PER):
-                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-                if st[t][k]["part"] and x == f:
-                    s, nL = S["CUT"][f], nn[t][k][0]
-                    gf, lend = S["RLO"][f] & 0xFFFF, S["RLO"][e - 1] >> 16
-                    cut = S["PL"][gf] if s == 0 else min(S["PL"][gf + s] if s < nL else 0xFFFFFFFF, S["PR"][lend - s])
-                    d = (S["INFO"][f] & BUDGET) - 1
-                    anyact |= _setup(E, S, f, cut, d, wmax)
-                    anyact |= _setup(E, S, cut, e, d, wmax)
-                    S["CUT"][f] = cut
-        for t in T:                                  # S0
-            for k in range(PER):
-                x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-                if st[t][k]["part"]:
-                    cc = S["CUT"][f]
-                    fe[t][k] = (f | (cc << 16)) if x < cc else (cc | (e << 16))
-    tasks = []                                       # ranges of 17..wmax: tasks
-    for t in T:
-        for k in range(PER):
-            x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-            if x < n and x == f and S["INFO"][f] & WAVEB:
-                tasks.append((f, e - f, S["INFO"][f] & BUDGET, [E[j] for j in range(f, e)]))
-    for (f, m, d, recs) in tasks:
-        if not defer:
-            assert m <= PW_MAX
-            for i, r in enumerate(wave_sort(recs, d)):
-                out[f + i] = r
-    for t in T:                                      # final insertion passes of the rest
-        for k in range(PER):
-            x, f, e = t + BLOCK * k, fe[t][k] & 0xFFFF, fe[t][k] >> 16
-            if x < n and not S["INFO"][f] & WAVEB:
-                r = E[x]
-                if S["INFO"][f] & FINB:
-                    out[x] = r
-                else:
-                    assert e - f <= THRESH
-                    kx = key(r)
-                    rank = sum(1 for j in range(f, e) if key(E[j]) < kx or (key(E[j]) == kx and j < x))
-                    out[f + rank] = r
-    return (out.v, tasks) if defer else out.v
 
 
 # ---- the large path's partition levels (cg_large.hip lg_pq_split / lg_pq_swap / lg_pcl_leaf) ----
@@ -499,3 +327,153 @@ def wave_sort(recs, depth):
             rank = sum(1 for j in range(hd[l], en[l]) if key(v[j]) < kx or (key(v[j]) == kx and j < l))
         out[hd[l] + rank] = v[l]
     return out
+
+
+def block_sort(E_in, PER=None, depth0=None, oop=False, wmax=PW_MAX, defer=False):
+    """cg_pcl.h pcl_block_sort, thread by thread (element x = tid + 512 k; oop: the swaps go to a
+    second buffer, as in the frame kernel), three barrier steps per level: each element's range carries its own
+    bounds and budget (registers), S1 computes the range's median of three itself (the swap
+    with the first stays virtual: V(m) = E[f], V(f) = E[m]), S4's swaps write V of the partner
+    and the range's cutter (the last swap's L element, or L_0 when there is none) stores the
+    cut, S0 follows it. No heads step: a range's set-up (median, budget, task or heapsort) is
+    read off its bounds by every element. Ranges of 17..wmax records with budget left leave
+    the levels as tasks: sorted by wave_sort (PwInline), or, with defer, returned as (first,
+    size, budget, records) with their output positions left None (PqDefer)."""
+    n = len(E_in)
+    if PER is None:
+        PER = 1 if n <= 512 else 2 if n <= 1024 else 4 if n <= 2048 else 8
+    assert n <= BLOCK * PER
+    if depth0 is None:
+        depth0 = 2 * _lg(n) if n else 0
+    E = Arr(n)
+    E.v = list(E_in)
+    out = Arr(n, None)
+    S = {k: Arr(n + 1) for k in ("RLO", "PL", "PR", "CUT")}
+    T = range(BLOCK)
+    rg = [[(0, n, depth0)] * PER for _ in T]   # each element's range (first, last, budget)
+
+    def part_of(f, e, d):
+        return e - f > THRESH and d > 0 and e - f > wmax
+
+    while True:
+        st = [[None] * PER for _ in T]
+        anyp = False
+        cnt = {}
+        for k in range(PER):                         # S1: the range's pivot, >= / <=, counts
+            ge = [False] * BLOCK
+            le = [False] * BLOCK
+            for t in T:
+                x = t + BLOCK * k
+                f, e, d = rg[t][k]
+                part = x < n and part_of(f, e, d)
+                m = p = kx = None
+                if part:
+                    a, b, c = f + 1, f + (e - f) // 2, e - 1
+                    m = _pb_median(a, b, c, key(E[a]), key(E[b]), key(E[c]))
+                    p = key(E[m])
+                    kx = key(E[f]) if x == m else key(E[x])
+                inn = part and x > f
+                ge[t], le[t] = inn and kx >= p, inn and kx <= p
+                st[t][k] = dict(part=part, inn=inn, m=m)
+                anyp |= part
+            for w in range(WAVES):
+                gm = sum(1 << l for l in range(64) if ge[64 * w + l])
+                lm = sum(1 << l for l in range(64) if le[64 * w + l])
+                cnt[k * WAVES + w] = _popc(gm) | (_popc(lm) << 16)
+                for l in range(64):
+                    t = 64 * w + l
+                    st[t][k].update(ge=ge[t], le=le[t], mg=_popc(gm & ((1 << l) - 1)), ml=_popc(lm & ((1 << l) - 1)))
+        if not anyp:                                 # (the S1 barrier's OR)
+            break
+        NS = PER * WAVES                             # S2
+        c = [cnt[j] for j in range(NS)]
+        gex = [sum(c[i] & 0xFFFF for i in range(j)) for j in range(NS)]
+        hex_ = [sum(c[i] >> 16 for i in range(j)) for j in range(NS)]
+        S["RLO"] = Arr(n + 1, None)
+        for t in T:
+            w = t // 64
+            for k in range(PER):
+                x = t + BLOCK * k
+                q = st[t][k]
+                gx, lx = gex[k * WAVES + w] + q["mg"], hex_[k * WAVES + w] + q["ml"]
+                q.update(gx=gx, lx=lx)
+                if x < n:
+                    S["RLO"][x] = (gx + q["ge"]) | ((lx + q["le"]) << 16)
+                if q["ge"]:
+                    S["PL"][gx] = x
+                if q["le"]:
+                    S["PR"][lx] = x
+        S["CUT"] = Arr(n + 1, None)
+        val = {}
+        for t in T:                                  # S4: partners, V of the partner, the cut
+            for k in range(PER):
+                x = t + BLOCK * k
+                f, e, d = rg[t][k]
+                q = st[t][k]
+                if not q["part"]:
+                    continue
+                m = q["m"]
+                if not q["inn"]:                     # the first position takes the median's record
+                    val[x] = E[m]
+                    continue
+                bf, be = S["RLO"][f], S["RLO"][e - 1]
+                gf, lend = bf & 0xFFFF, be >> 16
+                nL, nR = (be & 0xFFFF) - gf, lend - (bf >> 16)
+                li, ri = q["gx"] - gf, lend - 1 - q["lx"]
+                partner = x
+                if q["ge"] and li < nR:
+                    j = S["PR"][lend - 1 - li]       # R_li
+                    if x < j:
+                        partner = j
+                        if li + 1 >= min(nL, nR) or not S["PL"][gf + li + 1] < S["PR"][lend - 2 - li]:
+                            S["CUT"][f] = min(S["PL"][gf + li + 1] if li + 1 < nL else 0xFFFFFFFF, j)
+                    elif li == 0:                    # no swap at all: the left scan stops at L_0
+                        S["CUT"][f] = x
+                if q["le"] and ri < nL:
+                    i = S["PL"][gf + ri]             # L_ri
+                    if i < x:
+                        assert partner == x, "an element swapped twice"
+                        partner = i
+                val[x] = E[f] if partner == m else E[partner]
+        if oop:
+            E2 = Arr(n)
+            E2.v = list(E.v)
+            for x, v in val.items():
+                E2[x] = v
+            E = E2
+        else:
+            for x, v in val.items():
+                E[x] = v
+        for t in T:                                  # S0
+            for k in range(PER):
+                if st[t][k]["part"]:
+                    x = t + BLOCK * k
+                    f, e, d = rg[t][k]
+                    cc = S["CUT"][f]
+                    rg[t][k] = (f, cc, d - 1) if x < cc else (cc, e, d - 1)
+    tasks = []
+    for t in T:                                      # heads: tasks and heapsorts
+        for k in range(PER):
+            x = t + BLOCK * k
+            f, e, d = rg[t][k]
+            if x < n and x == f and e - f > THRESH:
+                if d == 0:
+                    heap_sort_range(E, f, e - f)
+                    for j in range(f, e):
+                        out[j] = E[j]
+                else:
+                    assert e - f <= wmax
+                    tasks.append((f, e - f, d, [E[j] for j in range(f, e)]))
+    for (f, m, d, recs) in tasks:
+        if not defer:
+            for i, r in enumerate(wave_sort(recs, d)):
+                out[f + i] = r
+    for t in T:                                      # final insertion passes
+        for k in range(PER):
+            x = t + BLOCK * k
+            f, e, d = rg[t][k]
+            if x < n and e - f <= THRESH:
+                kx = key(E[x])
+                rank = sum(1 for j in range(f, e) if key(E[j]) < kx or (key(E[j]) == kx and j < x))
+                out[f + rank] = E[x]
+    return (out.v, tasks) if defer else out.v

@@ -19,7 +19,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "cones_perception_amd", "lib", "libcones_gpu.so")
+LIB = os.environ.get("CONES_GPU_LIB") or os.path.join(ROOT, "cones_perception_amd", "lib", "libcones_gpu.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 

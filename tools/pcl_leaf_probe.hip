@@ -15,7 +15,7 @@
 #include "../cones_perception_amd/csrc/cg_pcl.h"
 
 #define LEAF 4096
-#define LDSB (8 * LEAF + 6 * 4 * (LEAF + 4))
+#define LDSB (8 * LEAF + 4 * 4 * (LEAF + 4))
 struct ProbeOut {
     uint64_t* o;
     __device__ __forceinline__ void operator()(uint32_t i, uint64_t r) const { o[i] = r; }
@@ -27,8 +27,7 @@ __global__ __launch_bounds__(CG_BLOCK) void probe(const uint64_t* in, uint64_t* 
     const uint32_t o = offs[blockIdx.x], n = offs[blockIdx.x + 1] - o;
     lds_u64* const El = (lds_u64*)(uint64_t*)smem;
     lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * LEAF);
-    const PbScratch<PbLds> PS{w0, w0 + (LEAF + 4), w0 + 2 * (LEAF + 4), w0 + 3 * (LEAF + 4), w0 + 4 * (LEAF + 4),
-                              w0 + 5 * (LEAF + 4)};
+    const PbScratch<PbLds> PS{w0, w0 + (LEAF + 4), w0 + 2 * (LEAF + 4), w0 + 3 * (LEAF + 4)};
     lds_u32* const Rl = (lds_u32*)red;
     for (uint32_t i = threadIdx.x; i < n; i += CG_BLOCK) El[i] = in[o + i];
     if (stamp && threadIdx.x == 0) g_pcl_probe_n = 0;
