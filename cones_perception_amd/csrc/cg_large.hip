@@ -1927,6 +1927,18 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_dgrid_fill(LgScratch S) {
     const uint32_t v = blockIdx.x * CG_BLOCK + threadIdx.x, V = S.meta[LG_V];
     if (v < V) S.ord[S.cstart[S.uk[v]] + S.ca[v]] = v;
 }
+// The lanes of the wave whose value v (< 2^nb) equals this lane's, among the lanes of `act`:
+// one ballot per bit (a constant cost, where a loop over the distinct values of a wave costs a
+// round per value).
+__device__ __forceinline__ uint64_t lg_match(uint32_t v, uint32_t nb, uint64_t act) {
+    uint64_t m = act;
+    for (uint32_t b = 0; b < nb; b++) {
+        const bool bit = (v >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
 // The voxels of the 27 cells around voxel q, visited by one wave: lanes 0-8 look up the nine
 // (z, y) rows, whose cells x-1..x+1 are consecutive in ord; then the 64 lanes stride each row.
 template <class F>
@@ -2011,25 +2023,35 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_flatten(LgScratch S) {
         for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = lpar[x];
 }
 // cross-tree edges (v < o): united unless both ends already share a parent
-__device__ __forceinline__ void lg_cross_one(const LgScratch& S, const CgDevParams& P, uint32_t v) {
+__device__ __forceinline__ void lg_cross_one(const LgScratch& S, const CgDevParams& P, uint32_t v, uint32_t vb) {
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
     const uint32_t pv = S.par[v];
+    const uint64_t lt = (1ull << lane_id()) - 1ull;
     lg_neighbours(S, g, q, [&](uint32_t o) {
         // each edge once, from its lower end: the higher neighbours only are loaded. Plain loads,
         // issued together: a stale pair of equal parents still lies in one tree (trees only
         // merge); different ones go through uf_union, which re-reads
-        if (o <= v) return;
-        const float4 p = S.vox[o];
-        const uint32_t po = S.par[o];
+        const bool hi = o > v;
+        float4 p = q;
+        uint32_t po = pv;
+        if (hi) { p = S.vox[o]; po = S.par[o]; }
         // pv / po (the flattened parents) lie on v's / o's paths to their roots (unions only
-        // hook roots under roots), so the finds start there
-        if (po != pv && lg_adjacent(q, p, P.r2)) uf_union(S.par, pv, po);
+        // hook roots under roots), so the finds start there. The lanes whose edges join v's tree
+        // to the same parent po make one union, by the lowest of them: the others' would only
+        // race it for the same root (a failed CAS and a second find each)
+        const bool cut = hi && po != pv && lg_adjacent(q, p, P.r2);
+        const uint64_t need = __ballot(cut);
+        if (need) {
+            const uint64_t same = lg_match(po, vb, need);
+            if (cut && (same & lt) == 0ull) uf_union(S.par, pv, po);
+        }
     });
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_cross(LgScratch S, CgDevParams P) {
-    for (uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V]; v < V; v += gridDim.x * WAVES)
-        lg_cross_one(S, P, v);
+    const uint32_t V = S.meta[LG_V], vb = V ? 32u - (uint32_t)__builtin_clz(V) : 1u;   // (parents < V)
+    for (uint32_t v = blockIdx.x * WAVES + wave_id(); v < V; v += gridDim.x * WAVES)
+        lg_cross_one(S, P, v, vb);
 }
 // roots and component sizes: the lanes of a wave that share a root add their count with one
 // atomic (a component's voxels are mostly neighbours in idx order; same-address atomics from
@@ -2241,18 +2263,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
 // wave per cluster collects them by ballots over the rank array, so the cost is C * V / 64
 // ballots (C5: 36 clusters, 5,363 voxels).
 #define LG_TAIL_LDS 7168
-// The lanes of the wave whose value v (< 2^nb) equals this lane's, among the lanes of `act`:
-// one ballot per bit (a constant cost, where a loop over the distinct values of a wave costs a
-// round per value).
-__device__ __forceinline__ uint64_t lg_match(uint32_t v, uint32_t nb, uint64_t act) {
-    uint64_t m = act;
-    for (uint32_t b = 0; b < nb; b++) {
-        const bool bit = (v >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        m &= bit ? bb : ~bb;
-    }
-    return m;
-}
 // LDS word add (ds_add_u32) or global atomic add, by pointer kind
 __device__ __forceinline__ void lg_add(lds_u32* p, uint32_t v) { __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
 __device__ __forceinline__ void lg_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
@@ -2419,14 +2429,9 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
         typename K::P32 cw = D + w * C;
         for (uint32_t k = l; k < C; k += 64) cw[k] = 0u;
         const uint32_t cbits = cg_bits_of(C);
-        // (the counters are the wave's own: one plain add per distinct cluster of a 64-voxel
-        // chunk, by its lowest lane, instead of an LDS atomic per member)
-        for (uint32_t vb = wb0; vb < wb1; vb += 64) {
-            const uint32_t v = vb + l;
-            const uint32_t rr = v < wb1 ? B[v] : 0xffffffffu;
-            const bool in = rr != 0xffffffffu;
-            const uint64_t same = lg_match(rr, cbits, __ballot(in));
-            if (in && (same & lt) == 0ull) cw[rr] += (uint32_t)__popcll(same);
+        for (uint32_t v = wb0 + l; v < wb1; v += 64) {
+            const uint32_t rr = B[v];
+            if (rr != 0xffffffffu) lg_add(&cw[rr], 1u);
         }
         __syncthreads();
         for (uint32_t k = tid; k < C; k += CG_BLOCK) {   // counts -> each wave's start per cluster
