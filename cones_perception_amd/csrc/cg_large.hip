@@ -1494,6 +1494,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_swap(LgScratch S, const uint64
 // A workgroup's first tile keeps its state in registers; further tiles (only when the level has
 // more tiles than the grid) leave theirs in the tile table (S.ca) and their ranks in S.vox.
 #define PQ_OWN 16   // tiles per workgroup and level beyond the first (the host sizes the grid)
+#ifndef LG_PQ_GRID
+// the levels' smallest grid (more when a workgroup would hold > PQ_OWN + 1 tiles); 128 and 256
+// measured the same on C5, a level with no range included (4.6 us, profiles/r5_c5_grid_ab.txt)
+#define LG_PQ_GRID 512
+#endif
 #define PQ_RW_TILE (1ull << 46)
 #define PQ_RW_N ((1ull << 23) - 1ull)
 static_assert(LG_DEV_MAX_POINTS < (1u << 23), "range totals fit 23 bits");
@@ -2841,7 +2846,7 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
         uint64_t* const Ein = lv % 2 ? kb[0] : kb[1];
         uint64_t* const Eout = lv % 2 ? kb[1] : kb[0];
         const uint32_t tiles = tb + (1u << lv);
-        const uint32_t grid = std::min(tiles, std::max<uint32_t>(512, (tiles + PQ_OWN - 1) / PQ_OWN));
+        const uint32_t grid = std::min(tiles, std::max<uint32_t>(LG_PQ_GRID, (tiles + PQ_OWN - 1) / PQ_OWN));
         hipLaunchKernelGGL(lg_pq_level, dim3(grid), dim3(CG_BLOCK), 0, s, S, Ein, Eout, lv, levels - 1, (lv + 1) % 2);
     }
     hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S, kb[1],
