@@ -577,7 +577,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_scan_emit(uint32_t n, int n_word,
 // (lg_last_arrival, after each workgroup's storing thread waited for its stores) resets the
 // look-back words and folds the chunks into the meta words, sizing the backend.
 template <int LAYOUT>
-__global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide_write(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
+__global__ __launch_bounds__(CG_BLOCK, 2) void lg_decide_write(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f,
                                                               uint32_t nch, uint32_t N, uint32_t szfl) {
     constexpr int PPT = LG_CHUNK / CG_BLOCK;
     constexpr int NW = (PPT + 63) / 64;
@@ -612,6 +612,12 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide_write(CgLaunch L, CgDev
     LaneBits<NW> m;   // kept by the ground filter and by the position filter
 #pragma unroll
     for (int wi = 0; wi < NW; wi++) m.w[wi] = keep.w[wi] & S.keep[((uint64_t)c * CG_BLOCK + tid) * NW + wi];
+    // the survivors' points: loaded now, so that their latency overlaps the scans below (only
+    // their stores wait for the chunk's base), and their bounds taken before it
+    float4 pt[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++)
+        if (m.get(k)) pt[k] = load_xyzi<LAYOUT>(fb, (uint32_t)k * CG_BLOCK + tid, L);
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         const uint64_t bb = __ballot(m.get(k));
@@ -631,34 +637,24 @@ __global__ __launch_bounds__(CG_BLOCK, 4) void lg_decide_write(CgLaunch L, CgDev
             st_rlx(S.cstat + (uint64_t)c * LG_CS_WORDS + LG_CS_MS, tot);
         }
     }
-    __syncthreads();
+    Bounds bd;
+#pragma unroll
+    for (int k = 0; k < PPT; k++)
+        if (m.get(k)) bd.add(pt[k]);
+    __shared__ uint32_t bpart[7 * WAVES];
+    bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, bpart, true);   // (thread 0 stores; ends after a barrier)
     const uint32_t b0 = cbase;
     const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t pidx0 = S.pidx_base + (uint32_t)base;
-    Bounds bd;
 #pragma unroll
-    for (int k0 = 0; k0 < PPT; k0 += 4) {   // four loads in flight
-        bool has[4];
-        uint32_t pos[4];
-        float4 pt[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int k = k0 + q;
-            has[q] = m.get(k);
-            const uint64_t bb = __ballot(has[q]);
-            pos[q] = b0 + cnt[k * WAVES + w] + (uint32_t)__popcll(bb & lt);
-            if (has[q]) pt[q] = load_xyzi<LAYOUT>(fb, (uint32_t)k * CG_BLOCK + tid, L);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (!has[q]) continue;
-            S.surv_p[pos[q]] = pt[q];
-            S.surv_i[pos[q]] = pidx0 + (uint32_t)(k0 + q) * CG_BLOCK + tid;
-            bd.add(pt[q]);
-        }
+    for (int k = 0; k < PPT; k++) {
+        const bool has = m.get(k);
+        const uint64_t bb = __ballot(has);
+        if (!has) continue;
+        const uint32_t pos = b0 + cnt[k * WAVES + w] + (uint32_t)__popcll(bb & lt);
+        S.surv_p[pos] = pt[k];
+        S.surv_i[pos] = pidx0 + (uint32_t)k * CG_BLOCK + tid;
     }
-    __shared__ uint32_t bpart[7 * WAVES];
-    bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, bpart, true);   // (thread 0 stores)
     if (tid == 0) {
         __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): its words and status are stored
         last = lg_last_arrival(lg_arrivals(S, 0));
