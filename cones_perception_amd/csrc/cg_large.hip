@@ -14,7 +14,7 @@
 //   backend     M <= CG_MMAX: one workgroup from LDS (cg_kernels.hip, cg_launch_lg_back_small);
 //               otherwise the global backend below: PCL's index_vector as (idx, slot) records
 //               and std::sort's permutation of it (partition levels lg_pq_split / lg_pq_swap,
-//               then lg_pcl_leaf, lg_pcl_mid, lg_pcl_waves; point order instead: a stable LSD
+//               then lg_pcl_leaf and lg_pcl_mid; point order instead: a stable LSD
 //               radix sort), voxel runs + centroids in that order, a dense neighbour grid, a
 //               lowest-neighbour forest, pointer jumping and cross-tree unions (roots = lowest
 //               voxel index = PCL's seed), size filter, PCL's cluster order, CSR by a sort of
@@ -938,8 +938,7 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
 #define LG_PCL_CUT 2048
 #endif
 #define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
-                               // [6] wave tasks (lg_pcl_waves), [7] mid tasks (lg_pcl_mid)
-#define PQ_WAVES 6
+                               // [6] (unused), [7] mid tasks (lg_pcl_mid)
 #define PQ_MIDS 7
 #define PQ_TILES 8             // S.ca: [0] a level's tile count; from word 8, eight words per tile
                                // (range, median, pivot, budget, range index, tile in range):
@@ -1181,7 +1180,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParam
         lg_grid_setup(in, m, P, npad, Mtot);
         if (Mtot == 0) m[LG_NCELL] = 0;
         if (blockIdx.x == 0) {
-            S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0; S.pq[PQ_MIDS] = 0;
+            S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_MIDS] = 0;
             lg_grid_setup(in, S.meta, P, npad, Mtot);
             if (Mtot == 0) S.meta[LG_NFIN_ALL] = S.meta[LG_SCAN_N] = S.meta[LG_NCELL] = 0;
         }
@@ -1335,7 +1334,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_split(LgScratch S, const uint6
     __shared__ uint64_t tbase;
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     if (level == 0 && blockIdx.x == 0 && tid == 0) {
-        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_WAVES] = 0; S.pq[PQ_MIDS] = 0;
+        S.pq[1] = 0; S.pq[2] = 0; S.pq[PQ_LEAFLIST] = 0; S.pq[PQ_MIDS] = 0;
         const uint32_t n = S.meta[LG_PCL_N];
         if (n <= LG_PCL_CUT) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
     }
@@ -1734,29 +1733,33 @@ struct PqLeafOut {
         v[base + i] = (uint32_t)r;
     }
 };
-// Ranges handed on to a chip-wide launch: their records go back to the HBM buffer the range
-// was loaded from and onto a task list (first, size | budget << 16 | buffer << 24):
-//   lg_pcl_leaf's ranges of 65-512 records -> S.dsz, for lg_pcl_mid (one workgroup each);
-//   ranges of 17-64 records (of the leaves and of lg_pcl_mid) -> S.droot, for lg_pcl_waves
-//   (one wave each).
-// (S.dsz and S.droot are free until the clustering.) The leaf and mid workgroups then only
-// run the levels of their longer ranges, on a few CUs; the tasks spread over the chip.
+// The ranges a leaf's levels leave (cg_pcl.h pcl_block_sort's wave tasks, 17-PQ_MID records):
+//   17-64 records: the wave finishes the range itself (pw_range64 from LDS, results straight to
+//   the outputs);
+//   65-PQ_MID records (lg_pcl_leaf's): handed on to a chip-wide launch, lg_pcl_mid (one
+//   workgroup each): the records go back to the HBM buffer the range was loaded from and onto
+//   a task list in S.dsz (first, size | budget << 16 | buffer << 24; free until the
+//   clustering). The leaf workgroups then only run the levels of their longer ranges, on a few
+//   CUs; the tasks spread over the chip.
+// (Round 5 handed the 17-64-record ranges on too, to a third launch of one wave each: 24.6 +
+// 20.7 + 6.5 us against 26.4 + 21.2 us inline, profiles/r5_c5_waves_ab.txt.)
 #ifndef PQ_MID
 #define PQ_MID 512
 #endif
 struct PqDefer {
     uint64_t* Eh; uint32_t* list; uint32_t* count; uint32_t base, buf;
-    uint32_t* wlist = nullptr; uint32_t* wcount = nullptr;   // ranges of <= 64 straight to the waves
     template <class P64, class OUT>
-    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT) const {
+    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
+        if (m <= PW_MAX) {
+            pw_range64(E, f, m, d, out);
+            return;
+        }
         const uint32_t l = lane_id();
         for (uint32_t i = l; i < m; i += 64) Eh[base + f + i] = E[f + i];
         if (l == 0) {
-            const bool w = wlist && m <= PW_MAX;
-            const uint32_t q = atomicAdd(w ? wcount : count, 1u);
-            uint32_t* const e = (w ? wlist : list) + 2 * q;
-            e[0] = base + f;
-            e[1] = m | (d << 16) | (buf << 24);
+            const uint32_t q = atomicAdd(count, 1u);
+            list[2 * q] = base + f;
+            list[2 * q + 1] = m | (d << 16) | (buf << 24);
         }
     }
 };
@@ -1787,7 +1790,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
             const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4)};
             lds_u32* const Rl = (lds_u32*)red;
             const PqLeafOut out{kout, vout, first};
-            const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ent[3], S.droot, S.pq + PQ_WAVES};
+            const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ent[3]};
             for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
             __syncthreads();
             if (size <= CG_BLOCK)
@@ -1813,8 +1816,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
     }
 }
 
-// The leaves' ranges of 65-512 records (S.dsz), one workgroup each, in LDS; their ranges of
-// 17-64 records go on to lg_pcl_waves.
+// The leaves' ranges of 65-512 records (S.dsz), one workgroup each, in LDS (their ranges of
+// 17-64 records one wave each, in LDS too).
 #define LG_MID_LDS (8 * PQ_MID + 4 * 4 * (PQ_MID + 4))
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
                                                        uint32_t* vout) {
@@ -1831,7 +1834,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
         uint64_t* const E = buf ? E1 : E0;
         for (uint32_t i = threadIdx.x; i < size; i += CG_BLOCK) El[i] = E[first + i];
         __syncthreads();
-        const PqDefer wt{E, S.droot, S.pq + PQ_WAVES, first, buf};
+        const PqDefer wt{E, nullptr, nullptr, first, buf};   // (every task here is <= 64 records)
         if constexpr (PQ_MID > CG_BLOCK) {
             if (size > CG_BLOCK) {
                 pcl_block_sort<2, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS,
@@ -1843,18 +1846,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
                                                             nullptr, wt);
     }
 }
-// The ranges of 17-64 records (S.droot), one wave each: pw_range64 from the HBM buffer,
-// results straight to the outputs.
-__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_waves(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
-                                                         uint32_t* vout) {
-    const uint32_t n = S.pq[PQ_WAVES];
-    const PqLeafOut out{kout, vout, 0u};
-    for (uint32_t q = blockIdx.x * WAVES + wave_id(); q < n; q += gridDim.x * WAVES) {
-        const uint32_t first = S.droot[2 * q], w1 = S.droot[2 * q + 1];
-        pw_range64((w1 >> 24) ? E1 : E0, first, w1 & 0xffffu, (w1 >> 16) & 0xffu, out);
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // Euclidean clustering over the V voxels (FLANN L2_Simple predicate, PCL's seed = the lowest
 // index of each component):
@@ -2766,11 +2757,9 @@ static int large_backend_from(const CgLaunch& L, const CgDevParams& P0, int kmod
         }
         hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S,
                            kb[buf ^ 1], kb[buf], kb[buf], vb2[buf], 0u);
-        // ranges of 65-512 records, then of 17-64 records: at most Mtot / 65 and Mtot / 17
+        // ranges of 65-512 records: at most Mtot / 65
         hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, Mtot / 65 + 1)), dim3(CG_BLOCK), 0, s, S,
                            kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
-        hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, Mtot / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s,
-                           S, kb[buf ^ 1], kb[buf], kb[buf], vb2[buf]);
         run_pb = 0;   // sorted keys are the idx alone
     }
     const uint64_t* vkey = buf ? S.key1 : S.key0;
@@ -2849,8 +2838,6 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
                        kb[0], kb[0], vb2[0], ((levels - 1) & 1u) + 1u);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
                        kb[0], vb2[0]);
-    hipLaunchKernelGGL(lg_pcl_waves, dim3(std::min<uint32_t>(1024, nmax / (17 * WAVES) + 1)), dim3(CG_BLOCK), 0, s, S,
-                       kb[1], kb[0], kb[0], vb2[0]);
     // voxel runs over the finite points (LG_SCAN_N; every point if passthrough), centroids
     scan_emit<LG_IDX_PER>(S, nmax, LG_SCAN_N, VoxelHead{S.key0, S.meta, 0u}, VoxelEmit{S.run}, LG_V, s);
     hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(nmax)), dim3(CG_BLOCK), 0, s, Lh, S, f, nmax, 0);

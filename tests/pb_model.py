@@ -211,7 +211,7 @@ def levels_sort(E_in, leaf=4096, levels=None):
         cur = nxt
     assert not cur
     out = [None] * n
-    for (f, e, d, b) in leaves:   # lg_pcl_leaf -> lg_pcl_mid -> lg_pcl_waves
+    for (f, e, d, b) in leaves:   # lg_pcl_leaf -> lg_pcl_mid (17-64 records: one wave each)
         seg = bufs[b][f:e]
         if e - f > min(leaf, 4096):
             out[f:e] = std_sort(seg, depth0=d)

@@ -113,7 +113,7 @@ def test_wave_model_matches_std_sort():
 
 def test_chip_wide_leaf_stages_model():
     """cg_large.hip's leaf stages: a leaf's levels stop at 512-record ranges (lg_pcl_leaf), those
-    stop at 64 (lg_pcl_mid), the rest one wave each (lg_pcl_waves); against std::sort."""
+    stop at 64 (lg_pcl_mid), the rest one wave each (pw_range64); against std::sort."""
     rng = random.Random(12)
     for it in range(4):
         n = rng.choice([1500, 3000, 4096])
