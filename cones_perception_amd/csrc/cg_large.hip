@@ -1744,7 +1744,7 @@ struct PqLeafOut {
 // (Round 5 handed the 17-64-record ranges on too, to a third launch of one wave each: 24.6 +
 // 20.7 + 6.5 us against 26.4 + 21.2 us inline, profiles/r5_c5_waves_ab.txt.)
 #ifndef PQ_MID
-#define PQ_MID 512
+#define PQ_MID 512   // (256: 34.3 + 16.2 us, 1,024: 20.1 + 32.6 us against 26.6 + 21.4, profiles/r5_c5_mid_ab.txt)
 #endif
 struct PqDefer {
     uint64_t* Eh; uint32_t* list; uint32_t* count; uint32_t base, buf;
