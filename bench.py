@@ -215,11 +215,19 @@ def main():
         avg_event_ms = sum(kern_ms) / len(kern_ms)
     step_span_ms = float((sp[:, 1] - sp[:, 0]).mean()) * 1e-5 if spans_ok else avg_event_ms   # 100 MHz ticks
     # the launch's duration as rocprofv3 reports it (dispatch to completion, which includes a
-    # queued launch's wait for CU room behind the other streams' launches): the HIP events of
-    # the identical untimed pass; the in-kernel span (first workgroup start to last end) is
-    # reported beside it. (Round 5: 122.7 us events and 118.2 us span against rocprofv3's
-    # 126.3 us over the same 20 timed launches, profiles/r5_timing_check.json.)
-    avg_kernel_ms = avg_event_ms if avg_event_ms is not None else step_span_ms
+    # queued launch's wait for CU room behind the other streams' launches): each timed launch
+    # from the end of the launch before it on its stream (a stream runs its launches in order,
+    # so that is when the queue dispatches it; a stream's first launch from the first workgroup
+    # start of the region) to its own last workgroup's end, from the timed launches' own in-kernel
+    # stamps (no event in the timed region). The in-kernel span (first workgroup start to last
+    # end) and the HIP events of the untimed pass are reported beside it. (Round 5 before this:
+    # events 120.6 us and rocprofv3 124.9 us over the 20 timed launches, -3.4%.)
+    queue_ms = None
+    if spans_ok:
+        t_first = int(sp[:, 0].min())   # (every stream's first launch is queued at the region's start)
+        prev = np.array([sp[i - S, 1] if i >= S else t_first for i in range(args.steps)], np.int64)
+        queue_ms = float((sp[:, 1] - prev).mean()) * 1e-5
+    avg_kernel_ms = queue_ms if queue_ms is not None else (avg_event_ms if avg_event_ms is not None else step_span_ms)
     sustained = None
     if args.sustained_steps > 0:
         sustained = sustained_pass(args, world, dev, engines, queue, S, F, N)
@@ -328,9 +336,12 @@ def main():
                          "traffic_source": traffic_source(),
                          "kernel": "cg_frame_kernel",
                          "avg_kernel_ms": avg_kernel_ms,
-                         "avg_kernel_ms_source": ("HIP events on the launch streams, identical untimed pass (dispatch "
-                                                  "to completion, as rocprofv3)" if avg_event_ms is not None
-                                                  else "in-kernel span (s_memrealtime) of the timed launches"),
+                         "avg_kernel_ms_source": ("timed launches, each from the end of the launch before it on its "
+                                                  "stream to its last workgroup's end (s_memrealtime stamps): dispatch "
+                                                  "to completion, as rocprofv3" if queue_ms is not None else
+                                                  "HIP events on the launch streams, identical untimed pass"
+                                                  if avg_event_ms is not None else
+                                                  "in-kernel span (s_memrealtime) of the timed launches"),
                          "step_span_ms": step_span_ms,
                          "step_span_ms_max": float((sp[:, 1] - sp[:, 0]).max()) * 1e-5 if spans_ok else None,
                          "step_span_frac": bytes_per_launch / (step_span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
