@@ -222,11 +222,7 @@ def main():
     # stamps (no event in the timed region). The in-kernel span (first workgroup start to last
     # end) and the HIP events of the untimed pass are reported beside it. (Round 5 before this:
     # events 120.6 us and rocprofv3 124.9 us over the 20 timed launches, -3.4%.)
-    queue_ms = None
-    if spans_ok:
-        t_first = int(sp[:, 0].min())   # (every stream's first launch is queued at the region's start)
-        prev = np.array([sp[i - S, 1] if i >= S else t_first for i in range(args.steps)], np.int64)
-        queue_ms = float((sp[:, 1] - prev).mean()) * 1e-5
+    queue_ms = float(queued_durations(sp, S).mean()) * 1e-5 if spans_ok else None
     avg_kernel_ms = queue_ms if queue_ms is not None else (avg_event_ms if avg_event_ms is not None else step_span_ms)
     sustained = None
     if args.sustained_steps > 0:
@@ -398,6 +394,18 @@ def rank_census(world, local):
     devs = {i for i in ids if not i.startswith("none")}
     return {"ranks_seen": len(ids), "world_size_env": world, "distinct_devices": len(devs),
             "backend": backend, "devices": ids[:16]}
+
+
+def queued_durations(sp, S):
+    """Dispatch-to-completion ticks of launches rotated over S in-order streams, from their
+    in-kernel [first workgroup start, last workgroup end] stamps sp (launch i on stream i % S):
+    launch i from the end of launch i - S (its stream's previous launch), a stream's first
+    launch from the first start of all (every stream's first launch is queued then)."""
+    import numpy as np
+    sp = np.asarray(sp, np.int64)
+    t_first = int(sp[:, 0].min())
+    prev = np.array([sp[i - S, 1] if i >= S else t_first for i in range(len(sp))], np.int64)
+    return sp[:, 1] - prev
 
 
 def sustained_pass(args, world, dev, engines, queue, S, F, N):
