@@ -590,6 +590,7 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void lg_decide_write(CgLaunch L, CgDev
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     // the ticket from the last wave, so that the other waves' fold loads overlap its latency
     if (tid == CG_BLOCK - 1) tk = __hip_atomic_fetch_add(&S.sstat[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0) CG_HOOK_LG_STAMP(S, 0);
     {
         const uint32_t a = lg_fold_core(S, nch, LG_WM_KEYS | LG_WM_TOUCHED, part);   // (ends with a barrier)
         if (tid <= CG_NUM_BINS + 1) fk[tid] = a;   // (LG_CS_KEYS = 0, LG_CS_TOUCHED = CG_NUM_BINS + 1)
@@ -601,6 +602,7 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void lg_decide_write(CgLaunch L, CgDev
     if (tid < 64) sector_thresholds(fk, fk[LG_CS_TOUCHED], P, thr, tkey, &band[0], &band[1]);
     if (c == 0 && tid <= CG_NUM_BINS && L.seckeys) L.seckeys[(uint64_t)f * (CG_NUM_BINS + 1) + tid] = fk[tid];
     __syncthreads();
+    if (blockIdx.x == 0) CG_HOOK_LG_STAMP(S, 13);
     const uint64_t base = (uint64_t)c * LG_CHUNK;
     const uint32_t Nc = (uint32_t)min((uint64_t)LG_CHUNK, (uint64_t)L.n_points - base);
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride + base * L.point_step;
@@ -643,6 +645,7 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void lg_decide_write(CgLaunch L, CgDev
         if (m.get(k)) bd.add(pt[k]);
     __shared__ uint32_t bpart[7 * WAVES];
     bd.merge_block(S.cstat + (uint64_t)c * LG_CS_WORDS, bpart, true);   // (thread 0 stores; ends after a barrier)
+    if (blockIdx.x == 0) CG_HOOK_LG_STAMP(S, 14);
     const uint32_t b0 = cbase;
     const uint64_t lt = (1ull << l) - 1ull;
     const uint32_t pidx0 = S.pidx_base + (uint32_t)base;
@@ -663,6 +666,7 @@ __global__ __launch_bounds__(CG_BLOCK, 2) void lg_decide_write(CgLaunch L, CgDev
     if (!last) return;
     for (uint32_t i = tid; i < nch + 2; i += CG_BLOCK) st_rlx(&S.sstat[i], 0u);   // (lg_tile_done's reset)
     lg_fold_chunks(S, nch, 2u | 4u | LG_FOLD_SIZE, N, szfl, true);
+    CG_HOOK_LG_STAMP(S, 15);
 }
 
 // ------------------------------------------------------------------------------------------
