@@ -230,3 +230,16 @@ def test_graph_cache_rotating_buffers(params):
         for k in list(range(copies)) + [0, 1, 35]:
             eng.run(d[k].data_ptr(), 1, n, 16, mode=cp.CG_MODE_PIPELINE)
             assert_same_detection(eng.fetch(0), ref, f"rotation {rep} buffer {k}")
+
+
+@pytest.mark.parametrize("rings,cols", [(256, 16384), (257, 16384)])
+def test_largest_device_sized_frame(params, rings, cols):
+    """The device-sized path's largest frame (LG_DEV_MAX_POINTS = 4,194,304 points: 1,024 chunks
+    taken by ticket in lg_decide_write, their look-back and fold) and one ring more, which takes
+    the host-sized path; both bit-exact. (The 4M frame's 7,510 voxels also put lg_cluster_tail on
+    its HBM form, past LG_TAIL_LDS.)"""
+    msg = _frame(rings, cols, frame=2, clutter=60, cpr=12)
+    got = cp.ConePipeline(params).cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_PIPELINE)
+    assert got.n_points == rings * cols
+    assert_same_detection(got, ref, f"{rings}x{cols}")
