@@ -722,7 +722,9 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
         peak = XGMI_LINK_GBS * min(world - 1, 7)
         out["roofline"] = {"bound": "xgmi", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
                            "bytes_per_step": egress,
-                           "peak_basis": f"root egress over {min(world - 1, 7)} direct xGMI links x {XGMI_LINK_GBS} GB/s"}
+                           "peak_basis": f"root egress over {min(world - 1, 7)} direct xGMI links x {XGMI_LINK_GBS} GB/s "
+                                         "(assumed: a direct link to every peer, the fully connected 8-GPU "
+                                         "xGMI node; the topology is not probed)"}
     else:   # one rank: the scatter is the root's own share, a device-local copy through RCCL
         out["roofline"] = None
         out["note"] = "world size 1 with collectives forced on: RCCL scatter/gather executed, no xGMI traffic"
