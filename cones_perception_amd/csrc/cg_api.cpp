@@ -269,6 +269,7 @@ LgScratch route_scratch(cg_handle* h, bool second = false) {
     LgScratch S = second ? h->lg2 : h->lg;
     S.force_global = (h->route == 2 || h->route == 5) ? 1u : 0u;
     S.pcl_levels_cap = h->route == 5 ? 1u : 0u;
+    S.force_wait_fail = h->route == 10 ? 1u : 0u;
     return S;
 }
 
@@ -423,6 +424,8 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
         const uint32_t V = p[CG_HDR_V], C = p[CG_HDR_C];
         if (V <= CG_PACK_MAX && C <= CG_PACK_MAX && (C == 0 || p[CG_PACK_OFFS + C] <= CG_PACK_MAX)) {
             std::memcpy(h->h_hdr, p, CG_HDR_WORDS * 4);
+            if (p[CG_HDR_WORDS - 1] == CG_HDR_E_WAIT)
+                return fail(CG_E_DEVICE, "frame %u: a device-side wait of the large-frame path gave up; results void", frame);
             out->n_points = p[CG_HDR_N];
             out->n_kept = p[CG_HDR_K];
             out->n_filtered = p[CG_HDR_M];
@@ -440,6 +443,8 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
     HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, CG_HDR_WORDS * 4,
                           hipMemcpyDeviceToHost, s));
     HIPCHK(cg_stream_wait(s));
+    if (h->h_hdr[CG_HDR_WORDS - 1] == CG_HDR_E_WAIT)
+        return fail(CG_E_DEVICE, "frame %u: a device-side wait of the large-frame path gave up; results void", frame);
     const uint32_t V = h->h_hdr[CG_HDR_V], C = h->h_hdr[CG_HDR_C];
     h->h_vox.resize((size_t)V * 4 + 4);
     h->h_lab.resize((size_t)V + 1);
@@ -1347,7 +1352,7 @@ int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches) {
 
 int cg_debug_route(cg_handle* h, int route) {
     if (!h) return fail(CG_E_INVALID, "null handle");
-    if (route < 0 || (route > 6 && route != 9)) return fail(CG_E_INVALID, "bad route %d", route);   // (7, 8: retired experiments)
+    if (route < 0 || (route > 6 && route != 9 && route != 10)) return fail(CG_E_INVALID, "bad route %d", route);   // (7, 8: retired experiments)
     h->route = route;
     return CG_OK;
 }

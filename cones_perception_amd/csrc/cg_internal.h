@@ -215,6 +215,8 @@ struct LgScratch {
     uint32_t pq_tmax;         //   tiles a level can have (lg_pq_level)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
+    uint32_t force_wait_fail; // diagnostics (cg_debug_route 10): the first partition level reports
+                              // a timed-out wait, as if its range never completed
     uint32_t pidx_base;       // frame index of the first point at L.in (a tile of a larger frame)
 };
 // Bytes of the large-frame scratch for frames of n points, and its layout at base.
@@ -296,6 +298,9 @@ int cg_launch_recrop(const CgLaunch& L, const CgDevParams& P, bool pipeline, con
 // CG_PACK_MAX are fetched separately).
 #define CG_PACK_MAX 1024
 #define CG_PACK_VOX CG_HDR_WORDS
+// header word CG_HDR_WORDS - 1 of a large frame whose device-side wait gave up (LG_PQ_TIMEOUT):
+// its results are void and the fetch fails with CG_E_DEVICE
+#define CG_HDR_E_WAIT 0x57414954u
 #define CG_PACK_LAB (CG_PACK_VOX + 4 * CG_PACK_MAX)
 #define CG_PACK_OFFS (CG_PACK_LAB + CG_PACK_MAX)
 #define CG_PACK_IDX (CG_PACK_OFFS + CG_PACK_MAX + 1)

@@ -1543,6 +1543,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         const uint32_t* Lr = pq_list(S, level % 3u) + PQ_EW * tid;
         pf = Lr[0]; pe = Lr[1]; pd = Lr[2];
     }
+    if (level == 0 && blockIdx.x == 0 && tid == 0 && S.force_wait_fail) S.meta[LG_PQ_TIMEOUT] = 1u;   // (route 10)
     if (blockIdx.x == 0) {
         // for level + 1: the set level - 1 used, with the ranges level - 1 had (level 0: the
         // whole index_vector; later levels: their list's count, read before the barrier in
@@ -2179,6 +2180,7 @@ __device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const CgDevParams&
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
                           (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
+        h[CG_HDR_WORDS - 1] = 0u;
     }
 }
 __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S,
@@ -2551,6 +2553,7 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
                           (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
+        h[CG_HDR_WORDS - 1] = m[LG_PQ_TIMEOUT] ? CG_HDR_E_WAIT : 0u;   // (the fetch fails on it)
     }
     CG_HOOK_LG_STAMP(S, 12);
 }

@@ -390,7 +390,8 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * published, so every chunk workgroup times out and the call re-runs the frame by DMA (6,
  * tests of that retry); single-frame split calls whose chunk workgroup 0 gives up waiting for
  * the other chunks at once, so the call re-runs the frame in one workgroup (9, tests of that
- * retry); 0 = automatic. */
+ * retry); large frames whose first partition level reports a timed-out device-side wait, so the
+ * fetch fails with CG_E_DEVICE (10, tests of that failure); 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

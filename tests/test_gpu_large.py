@@ -243,3 +243,18 @@ def test_largest_device_sized_frame(params, rings, cols):
     ref, _ = O.run(params, msg, O.MODE_PIPELINE)
     assert got.n_points == rings * cols
     assert_same_detection(got, ref, f"{rings}x{cols}")
+
+
+def test_device_wait_timeout_fails_loudly(params):
+    """A large frame whose device-side wait gives up (LG_PQ_TIMEOUT; forced by cg_debug_route 10
+    at its first partition level) fails its fetch with CG_E_DEVICE instead of returning void
+    results; the handle serves the next frame exactly."""
+    msg = _frame(128, 4096, frame=5, clutter=60, cpr=12)   # (M past the LDS backend: the levels run)
+    ref, hdr = O.run(params, msg, O.MODE_PIPELINE)
+    assert int(hdr[2]) > 4096
+    pipe = cp.ConePipeline(params)
+    pipe.debug_route(10)
+    with pytest.raises(Exception, match="gave up"):
+        pipe.cloud_handler(msg)
+    pipe.debug_route(0)
+    assert_same_detection(pipe.cloud_handler(msg), ref, "after the failed frame")
