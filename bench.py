@@ -919,11 +919,17 @@ def single_frame_latency(cp, params, raw, device, reps=200, order=None):
     msg = cp.frame_cloud(raw[0])
     for _ in range(10):
         pipe.cloud_handler(msg)
-    t0 = time.perf_counter()
+    each = []
+    t0 = ti = time.perf_counter()
     for _ in range(reps):
         pipe.cloud_handler(msg)
-    dt = (time.perf_counter() - t0) / reps
-    return {"latency_ms": dt * 1e3, "frames_per_s": 1.0 / dt,
+        tj = time.perf_counter()
+        each.append(tj - ti)
+        ti = tj
+    dt = (ti - t0) / reps
+    each.sort()
+    return {"latency_ms": dt * 1e3, "latency_p50_ms": each[reps // 2] * 1e3, "latency_p90_ms": each[reps * 9 // 10] * 1e3,
+            "frames_per_s": 1.0 / dt,
             "includes": "C2: one 64k-point PointCloud2 in pageable host memory through the synchronous "
                         "ConePipeline.cloud_handler (the split kernel launched first; the host copies the message into "
                         "pinned memory chunk by chunk, publishing each chunk to the workgroup reading "

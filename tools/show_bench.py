@@ -20,8 +20,10 @@ for line in open(path):
             print("C5", {k: c5.get(k) for k in ("ms_per_frame", "point_order_ms_per_frame", "error")})
         sf = d.get("single_frame")
         if sf:
-            print("C2 python %.4f ms, cpp %s" % (sf.get("latency_ms", float("nan")),
-                                                  (sf.get("cpp_node") or {}).get("latency_ms")))
+            c = sf.get("cpp_node") or {}
+            print("C2 python %.4f ms (p50 %s), cpp %s (p50 %s, p90 %s)" % (
+                sf.get("latency_ms", float("nan")), sf.get("latency_p50_ms"), c.get("latency_ms"),
+                c.get("latency_p50_ms"), c.get("latency_p90_ms")))
         if "ranks" in d:
             print("RANKS", d["ranks"])
         if "c5_tiled" in d:
