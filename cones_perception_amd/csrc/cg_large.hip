@@ -1172,6 +1172,7 @@ struct PclCompactEmit {
 // order (lg_surv_write), so the keys carry no frame-index bits (PB = 0).
 #ifndef LG_IDX_PER
 #define LG_IDX_PER 2   // records per thread of lg_pcl_index and the voxel-run scan after the sort
+                       // (1, 4 and round 5's first 8 measured slower, profiles/r5_c5_idx_ab.txt)
 #endif
 #define LG_IDX_TILE (LG_IDX_PER * CG_BLOCK)
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_index(LgScratch S, CgDevParams P, uint64_t* Eout) {
