@@ -1322,7 +1322,7 @@ int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words) {
 int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
     if (!h || !out) return fail(CG_E_INVALID, "null argument");
     if (!h->d_large) return fail(CG_E_INVALID, "no large frame has run on this handle");
-    // 4: the first 512 bytes of the radix histogram area (phase stamps of variant builds,
+    // 4: the first 1024 bytes of the radix histogram area (phase stamps of variant builds,
     // tools/variants/lg_stamps.h)
     const void* src = which == 0   ? (const void*)h->lg.meta
                       : which == 1 ? (const void*)h->lg.codes
@@ -1333,7 +1333,7 @@ int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
     const uint64_t cap = which == 0   ? LG_META_WORDS * 4
                          : which == 1 ? nch * LG_CHUNK
                          : which == 2 ? nch * CG_BLOCK * 16
-                         : which == 4 ? 512
+                         : which == 4 ? 1024
                                       : (uint64_t)cg_large_pq_words() * 4;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, src, std::min(bytes, cap), hipMemcpyDeviceToHost));

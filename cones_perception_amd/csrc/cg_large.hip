@@ -1937,6 +1937,25 @@ __device__ __forceinline__ uint64_t lg_match(uint32_t v, uint32_t nb, uint64_t a
     }
     return m;
 }
+// lg_match for waves that hold few distinct values (a chunk of voxels in PCL order meets a few
+// clusters): one round per distinct value, the leader's value broadcast and compared, for at
+// most nb rounds; the lanes still unmatched then take lg_match's nb ballots. (Active lanes
+// only: the result of a lane outside `act` is 0.)
+__device__ __forceinline__ uint64_t lg_match_few(uint32_t v, uint32_t nb, uint64_t act) {
+    const uint32_t l = lane_id();
+    uint64_t rem = act, same = 0ull;
+    for (uint32_t r = 0; r < nb && rem; r++) {
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(rem));
+        const uint64_t m = __ballot(v == v0) & rem;
+        if ((m >> l) & 1ull) same = m;
+        rem &= ~m;
+    }
+    if (rem) {
+        const uint64_t m = lg_match(v, nb, rem);
+        if ((rem >> l) & 1ull) same = m;
+    }
+    return same;
+}
 // The voxels of the 27 cells around voxel q, visited by one wave: lanes 0-8 look up the nine
 // (z, y) rows, whose cells x-1..x+1 are consecutive in ord; then the 64 lanes stride each row.
 template <class F>
@@ -2041,7 +2060,7 @@ __device__ __forceinline__ void lg_cross_one(const LgScratch& S, const CgDevPara
         const bool cut = hi && po != pv && lg_adjacent(q, p, P.r2);
         const uint64_t need = __ballot(cut);
         if (need) {
-            const uint64_t same = lg_match(po, vb, need);
+            const uint64_t same = lg_match_few(po, vb, need);
             if (cut && (same & lt) == 0ull) uf_union(S.par, pv, po);
         }
     });
@@ -2256,11 +2275,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_csr_centroids(CgLaunch L, CgDevPa
 //   A: parents, then the kept roots (droot, ascending = PCL's discovery order), then the
 //      cluster offsets; B: each voxel's root, then its cluster rank (or ~0);
 //   Cc: component sizes by root, then each root's cluster rank; D: kept sizes (dsz);
-//   Ef: the cluster order (fin), then the CSR member list; B and Cc hold the voxels' x, y for
-//   the centroid sums at the end (LDS form).
-// The CSR lists cluster k's members in ascending voxel index (PCL's extract sorts them): one
-// wave per cluster collects them by ballots over the rank array, so the cost is C * V / 64
-// ballots (C5: 36 clusters, 5,363 voxels).
+//   Ef: the cluster order (fin), then the CSR member list; B and Cc hold the members' x, y in
+//   CSR order for the centroid sums at the end (LDS form).
+// The CSR lists cluster k's members in ascending voxel index (PCL's extract sorts them): each
+// wave places a block of consecutive voxels at per-(wave, cluster) starts (C5: 36 clusters,
+// 5,363 voxels).
 #define LG_TAIL_LDS 7168
 // LDS word add (ds_add_u32) or global atomic add, by pointer kind
 __device__ __forceinline__ void lg_add(lds_u32* p, uint32_t v) { __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
@@ -2419,8 +2438,8 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     // 8. the CSR: every cluster's members in ascending voxel index. Each wave takes a block of
     //    consecutive voxels: it counts its members per cluster (D as WAVES x C counters, free
     //    now), the counts become each wave's start per cluster, and the wave writes its members
-    //    there in voxel order, one round per distinct cluster in a 64-voxel chunk. (More than
-    //    (V + 2) / WAVES clusters: one wave per cluster collects them by ballots instead.)
+    //    there in voxel order, each 64-voxel chunk's same-cluster lanes found by lg_match. (More
+    //    than (V + 2) / WAVES clusters: one wave per cluster collects them by ballots instead.)
     int32_t* const idx_out = L.idx + (uint64_t)f * L.cap;
     if ((uint64_t)WAVES * C <= V + 2) {
         const uint32_t blk = ((V + WAVES * 64 - 1) / (WAVES * 64)) * 64;   // voxels per wave
@@ -2428,31 +2447,74 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
         typename K::P32 cw = D + w * C;
         for (uint32_t k = l; k < C; k += 64) cw[k] = 0u;
         const uint32_t cbits = cg_bits_of(C);
-        for (uint32_t v = wb0 + l; v < wb1; v += 64) {
-            const uint32_t rr = B[v];
-            if (rr != 0xffffffffu) lg_add(&cw[rr], 1u);
-        }
-        __syncthreads();
-        for (uint32_t k = tid; k < C; k += CG_BLOCK) {   // counts -> each wave's start per cluster
-            uint32_t run = A[k];
-            for (uint32_t q = 0; q < WAVES; q++) {
-                const uint32_t c = D[q * C + k];
-                D[q * C + k] = run;
-                run += c;
+        auto to_starts = [&]() {   // counts -> each wave's start per cluster
+            for (uint32_t k = tid; k < C; k += CG_BLOCK) {
+                uint32_t run = A[k];
+                for (uint32_t q = 0; q < WAVES; q++) {
+                    const uint32_t c = D[q * C + k];
+                    D[q * C + k] = run;
+                    run += c;
+                }
             }
-        }
-        __syncthreads();
-        for (uint32_t vb = wb0; vb < wb1; vb += 64) {
-            const uint32_t v = vb + l;
-            const uint32_t rr = v < wb1 ? B[v] : 0xffffffffu;
-            const bool in = rr != 0xffffffffu;
-            const uint64_t same = lg_match(rr, cbits, __ballot(in));
-            if (in) {
-                const uint32_t o = cw[rr];   // (every lane of the group reads before its first writes)
-                const uint32_t pos = o + (uint32_t)__popcll(same & lt);
-                Ef[pos] = v;
-                idx_out[pos] = (int32_t)v;
-                if ((same & lt) == 0ull) cw[rr] = o + (uint32_t)__popcll(same);
+        };
+        if constexpr (K::in_lds) {
+            // LDS form (at most NCH chunks per wave): the chunks' ranks and same-rank lane masks
+            // stay in registers between the count and the placement, and each group's leader
+            // adds its group's size (distinct addresses: no same-address atomics to serialise)
+            constexpr int NCH = (LG_TAIL_LDS + WAVES * 64 - 1) / (WAVES * 64);
+            uint32_t rr[NCH];
+            uint64_t same[NCH];
+#pragma unroll
+            for (int j = 0; j < NCH; j++) {
+                const uint32_t v = wb0 + 64u * j + l;
+                rr[j] = v < wb1 ? B[v] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int j = 0; j < NCH; j++) {
+                same[j] = 0ull;
+                if (wb0 + 64u * j >= wb1) continue;   // (wave-uniform)
+                const bool in = rr[j] != 0xffffffffu;
+                same[j] = lg_match(rr[j], cbits, __ballot(in));
+                if (in && (same[j] & lt) == 0ull) lg_add(&cw[rr[j]], (uint32_t)__popcll(same[j]));
+            }
+            __syncthreads();
+            CG_HOOK_LG_STAMP(S, 64);
+            to_starts();
+            __syncthreads();
+            CG_HOOK_LG_STAMP(S, 65);
+#pragma unroll
+            for (int j = 0; j < NCH; j++) {
+                const uint32_t v = wb0 + 64u * j + l;
+                if (rr[j] != 0xffffffffu) {
+                    const uint32_t o = cw[rr[j]];   // (every lane of the group reads before its leader writes)
+                    const uint32_t pos = o + (uint32_t)__popcll(same[j] & lt);
+                    Ef[pos] = v;
+                    idx_out[pos] = (int32_t)v;
+                    if ((same[j] & lt) == 0ull) cw[rr[j]] = o + (uint32_t)__popcll(same[j]);
+                }
+            }
+        } else {
+            for (uint32_t v = wb0 + l; v < wb1; v += 64) {
+                const uint32_t rr = B[v];
+                if (rr != 0xffffffffu) lg_add(&cw[rr], 1u);
+            }
+            __syncthreads();
+            CG_HOOK_LG_STAMP(S, 64);
+            to_starts();
+            __syncthreads();
+            CG_HOOK_LG_STAMP(S, 65);
+            for (uint32_t vb = wb0; vb < wb1; vb += 64) {
+                const uint32_t v = vb + l;
+                const uint32_t rr = v < wb1 ? B[v] : 0xffffffffu;
+                const bool in = rr != 0xffffffffu;
+                const uint64_t same = lg_match(rr, cbits, __ballot(in));
+                if (in) {
+                    const uint32_t o = cw[rr];   // (every lane of the group reads before its first writes)
+                    const uint32_t pos = o + (uint32_t)__popcll(same & lt);
+                    Ef[pos] = v;
+                    idx_out[pos] = (int32_t)v;
+                    if ((same & lt) == 0ull) cw[rr] = o + (uint32_t)__popcll(same);
+                }
             }
         }
     } else {
@@ -2474,60 +2536,81 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     }
     __syncthreads();
     CG_HOOK_LG_STAMP(S, 9);
-    // 9. the voxels' x, y next to each other (LDS form: over B and Cc, which are used up)
-    typename K::P32 XY = B;   // (two words per voxel: B and Cc are adjacent)
-    if (lds) {
-        for (uint32_t vb = 0; vb < V; vb += 16 * CG_BLOCK) {   // sixteen loads in flight per thread
+    // 9. the members' x, y in CSR order, next to each other (LDS form: over B and Cc, which are
+    //    used up), so each cluster's sum below reads one contiguous run
+    typename K::P32 XY = B;   // (two words per slot: B and Cc are adjacent)
+    const uint32_t nmem = A[C];
+    if (K::in_lds && nmem) {
+        for (uint32_t pb = 0; pb < nmem; pb += 16 * CG_BLOCK) {   // sixteen loads in flight per thread
             float cx[16], cy[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) {   // (clamped: no branch between the loads)
-                const float4 c = S.vox[min(vb + (uint32_t)q * CG_BLOCK + tid, V - 1)];
+                const float4 c = S.vox[Ef[min(pb + (uint32_t)q * CG_BLOCK + tid, nmem - 1)]];
                 cx[q] = c.x;
                 cy[q] = c.y;
             }
 #pragma unroll
             for (int q = 0; q < 16; q++) {
-                const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
-                if (v < V) {
-                    XY[2 * v] = __float_as_uint(cx[q]);
-                    XY[2 * v + 1] = __float_as_uint(cy[q]);
+                const uint32_t p = pb + (uint32_t)q * CG_BLOCK + tid;
+                if (p < nmem) {
+                    XY[2 * p] = __float_as_uint(cx[q]);
+                    XY[2 * p + 1] = __float_as_uint(cy[q]);
                 }
             }
         }
-        __syncthreads();
     }
+    __syncthreads();
     CG_HOOK_LG_STAMP(S, 10);
     // 10. per-cluster centroid + radial push (src/cone_detection.cpp:261-279): float sums in
     //     ascending member order (lg_centroids_one's arithmetic), one lane per cluster: each sum
-    //     is a sequential chain, kept in the lane's registers while its loads run ahead
+    //     is a sequential chain, kept in the lane's registers while its loads run ahead (LDS
+    //     form: 16-byte reads of the contiguous x, y pairs, two members each)
     float2* const cen_out = L.cen + (uint64_t)f * L.cap;
     for (uint32_t k = tid; k < C; k += CG_BLOCK) {
         const uint32_t s0 = A[k], e0 = A[k + 1];
         float x = 0.0f, y = 0.0f;
-        auto xy = [&](uint32_t i, float& px, float& py) {
-            const uint32_t m = Ef[i];
-            if (lds) {
-                px = __uint_as_float(XY[2 * m]);
-                py = __uint_as_float(XY[2 * m + 1]);
-            } else {
-                const float4 c = S.vox[m];
-                px = c.x;
-                py = c.y;
-            }
-        };
         uint32_t i = s0;
-        for (; i + 8 <= e0; i += 8) {
-            float px[8], py[8];
+        if constexpr (K::in_lds) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+            if ((i & 1u) && i < e0) {   // to an even slot: 16-byte aligned pairs from there
+                x += __uint_as_float(XY[2 * i]);
+                y += __uint_as_float(XY[2 * i + 1]);
+                i++;
+            }
+            for (; i + 16 <= e0; i += 16) {
+                u32x4 q[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) xy(i + u, px[u], py[u]);
+                for (int u = 0; u < 8; u++) q[u] = ((const lds_u32x4*)(XY + 2 * i))[u];
 #pragma unroll
-            for (int u = 0; u < 8; u++) { x += px[u]; y += py[u]; }
-        }
-        for (; i < e0; i++) {
-            float px, py;
-            xy(i, px, py);
-            x += px;
-            y += py;
+                for (int u = 0; u < 8; u++) {
+                    x += __uint_as_float(q[u].x);
+                    y += __uint_as_float(q[u].y);
+                    x += __uint_as_float(q[u].z);
+                    y += __uint_as_float(q[u].w);
+                }
+            }
+            for (; i < e0; i++) {
+                x += __uint_as_float(XY[2 * i]);
+                y += __uint_as_float(XY[2 * i + 1]);
+            }
+        } else {
+            for (; i + 8 <= e0; i += 8) {
+                float px[8], py[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const float4 c = S.vox[Ef[i + u]];
+                    px[u] = c.x;
+                    py[u] = c.y;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) { x += px[u]; y += py[u]; }
+            }
+            for (; i < e0; i++) {
+                const float4 c = S.vox[Ef[i]];
+                x += c.x;
+                y += c.y;
+            }
         }
         {
             const int j = (int)(e0 - s0);
@@ -2559,7 +2642,7 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     CG_HOOK_LG_STAMP(S, 12);
 }
 __global__ __launch_bounds__(CG_BLOCK) void lg_cluster_tail(CgLaunch L, CgDevParams P, LgScratch S, uint32_t f) {
-    __shared__ uint32_t lds[5 * LG_TAIL_LDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[5 * LG_TAIL_LDS];   // (16-byte reads in stage 10)
     __shared__ uint32_t red[8 * WAVES];
     __shared__ int32_t stk[3 * CG_SORT_STACK];
     const uint32_t V = S.meta[LG_V];

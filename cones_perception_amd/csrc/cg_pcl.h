@@ -152,8 +152,8 @@ __device__ __forceinline__ void pcl_index_vector(const Work& W, uint32_t M, uint
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 // Pointer kinds: LDS (ds_* instructions) when the arrays live in LDS, generic otherwise.
-struct PbLds { typedef lds_u32* P32; typedef lds_u64* P64; };
-struct PbGen { typedef uint32_t* P32; typedef uint64_t* P64; };
+struct PbLds { typedef lds_u32* P32; typedef lds_u64* P64; static constexpr bool in_lds = true; };
+struct PbGen { typedef uint32_t* P32; typedef uint64_t* P64; static constexpr bool in_lds = false; };
 template <class K> struct PbScratch { typename K::P32 RLO, PL, PR, CUT; };
 struct PwLess {   // a functor, not a function: a function pointer could become an indirect call
     __device__ __forceinline__ bool operator()(uint64_t a, uint64_t b) const { return pcl_key(a) < pcl_key(b); }

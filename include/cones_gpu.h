@@ -398,7 +398,8 @@ int cg_debug_route(cg_handle* h, int route);
 int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words);
 /* Diagnostics: raw large-frame scratch of the last frame: 0 = meta words, 1 = z codes
  * ([chunk][group][lane] words of 8 codes), 2 = ground-mode kept bits, 3 = the PCL voxel sort's
- * range lists (8 header words: level counts, leaf count; then 4 lists of 5-word entries). */
+ * range lists (8 header words: level counts, leaf count; then 4 lists of 5-word entries),
+ * 4 = the first 1024 bytes of the radix histogram area (phase stamps of variant builds). */
 int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes);
 
 /* Exported library version string. */

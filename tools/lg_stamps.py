@@ -21,15 +21,18 @@ rows = []
 for it in range(40):
     eng.run(d.data_ptr(), 1, raw.shape[1] // 16, 16)
     torch.cuda.synchronize()
-    st = np.zeros(64, np.uint64)
-    _abi.check(_abi.lib().cg_debug_large_buffer(eng.handle, 4, st.ctypes.data, 512))
+    st = np.zeros(66, np.uint64)
+    _abi.check(_abi.lib().cg_debug_large_buffer(eng.handle, 4, st.ctypes.data, 528))
     if it >= 5:
-        rows.append(st[:13].astype(np.int64))
+        rows.append(st.astype(np.int64))
 t = np.array(rows)
 print("lg_cluster_tail phases, us (median of %d frames):" % len(rows))
 for i in range(2, 13):
     print(f"  {names[i - 1]:12s} {statistics.median((t[:, i] - t[:, i - 1]) / 100.0):7.2f}")
 print(f"  total        {statistics.median((t[:, 12] - t[:, 1]) / 100.0):7.2f}")
+if (t[:, 64] > t[:, 8]).all():   # the CSR's three parts (stamps 64, 65)
+    for nm, a0, a1 in (("csr counts", 8, 64), ("csr starts", 64, 65), ("csr place", 65, 9)):
+        print(f"  {nm:12s} {statistics.median((t[:, a1] - t[:, a0]) / 100.0):7.2f}")
 # lg_pq_level, workgroup 0: split phase, wait for the range, swaps; gap from the previous level
 allr = []
 for it in range(20):
