@@ -2293,7 +2293,8 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     const uint64_t lt = (1ull << l) - 1ull;
     CG_HOOK_LG_STAMP(S, 1);
     // 1. parents (flattened by lg_flatten, then united across trees by lg_cross), sixteen
-    //    loads in flight per thread (one round trip for C5's 5,363 voxels)
+    //    loads in flight per thread (one round trip for C5's 5,363 voxels); the size counters
+    //    zeroed
     if (lds) {
         for (uint32_t vb = 0; vb < V; vb += 16 * CG_BLOCK) {
             uint32_t pv[16];
@@ -2305,13 +2306,17 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
 #pragma unroll
             for (int q = 0; q < 16; q++) {
                 const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
-                if (v < V) A[v] = pv[q];
+                if (v < V) { A[v] = pv[q]; Cc[v] = 0u; }
             }
         }
-        __syncthreads();
+    } else {
+        for (uint32_t v = tid; v < V; v += CG_BLOCK) Cc[v] = 0u;
     }
+    __syncthreads();
     CG_HOOK_LG_STAMP(S, 2);
-    // 2. roots (the forest's roots are the components' lowest indices = PCL's seeds)
+    // 2. roots (the forest's roots are the components' lowest indices = PCL's seeds) and the
+    //    component sizes (LDS atomics: the LDS unit takes a wave's same-address adds in turn,
+    //    cheaper than matching the lanes' roots first)
     for (uint32_t vb = 0; vb < V; vb += 4 * CG_BLOCK) {   // four chases interleaved
         uint32_t r[4], p[4];
         bool go = true;
@@ -2330,18 +2335,19 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
-            if (v < V) { B[v] = r[q]; Cc[v] = 0u; }
+            if (v < V) {
+                B[v] = r[q];
+                lg_add(&Cc[r[q]], 1u);
+            }
         }
     }
     __syncthreads();
-    CG_HOOK_LG_STAMP(S, 3);
-    // 3. component sizes (LDS atomics: the LDS unit takes a wave's same-address adds in turn,
-    //    cheaper than matching the lanes' roots first)
-    for (uint32_t v = tid; v < V; v += CG_BLOCK) lg_add(&Cc[B[v]], 1u);
-    __syncthreads();
+    CG_HOOK_LG_STAMP(S, 3);   // (stage 3, the sizes, is part of stage 2)
     CG_HOOK_LG_STAMP(S, 4);
     // 4. the size filter over the seeds in ascending order (PCL's discovery order): droot in A,
-    //    sizes in D; each thread scans `per` consecutive voxels
+    //    sizes in D; each thread scans `per` consecutive voxels (a ballot form over 64-voxel
+    //    chunks measured no faster, profiles/r5_c5_tail_csr_ab.txt)
+    uint32_t C = 0;
     const uint32_t per = (V + CG_BLOCK - 1) / CG_BLOCK;
     const uint32_t v0 = min(V, tid * per), v1 = min(V, v0 + per);
     uint32_t mine = 0;
@@ -2352,7 +2358,7 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     const uint32_t inc = wave_incl_scan(mine);
     if (l == 63) red[w] = inc;
     __syncthreads();
-    uint32_t base = inc - mine, C = 0;
+    uint32_t base = inc - mine;
     for (uint32_t q = 0; q < WAVES; q++) {
         base += q < w ? red[q] : 0u;
         C += red[q];
@@ -2441,6 +2447,9 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     //    there in voxel order, each 64-voxel chunk's same-cluster lanes found by lg_match. (More
     //    than (V + 2) / WAVES clusters: one wave per cluster collects them by ballots instead.)
     int32_t* const idx_out = L.idx + (uint64_t)f * L.cap;
+    typename K::P32 XY = B;   // LDS form: the members' x, y in CSR order (two words per slot:
+                              // B and Cc are adjacent), for stage 10
+    bool xy_ready = false;
     if ((uint64_t)WAVES * C <= V + 2) {
         const uint32_t blk = ((V + WAVES * 64 - 1) / (WAVES * 64)) * 64;   // voxels per wave
         const uint32_t wb0 = min(V, w * blk), wb1 = min(V, wb0 + blk);
@@ -2464,10 +2473,14 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
             constexpr int NCH = (LG_TAIL_LDS + WAVES * 64 - 1) / (WAVES * 64);
             uint32_t rr[NCH];
             uint64_t same[NCH];
+            float cx[NCH], cy[NCH];   // the voxels' x, y, for stage 10 (loads in flight meanwhile)
 #pragma unroll
             for (int j = 0; j < NCH; j++) {
                 const uint32_t v = wb0 + 64u * j + l;
                 rr[j] = v < wb1 ? B[v] : 0xffffffffu;
+                const float4 c = v < wb1 ? S.vox[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+                cx[j] = c.x;
+                cy[j] = c.y;
             }
 #pragma unroll
             for (int j = 0; j < NCH; j++) {
@@ -2488,11 +2501,13 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
                 if (rr[j] != 0xffffffffu) {
                     const uint32_t o = cw[rr[j]];   // (every lane of the group reads before its leader writes)
                     const uint32_t pos = o + (uint32_t)__popcll(same[j] & lt);
-                    Ef[pos] = v;
                     idx_out[pos] = (int32_t)v;
+                    XY[2 * pos] = __float_as_uint(cx[j]);   // (B is in registers, Cc used up)
+                    XY[2 * pos + 1] = __float_as_uint(cy[j]);
                     if ((same[j] & lt) == 0ull) cw[rr[j]] = o + (uint32_t)__popcll(same[j]);
                 }
             }
+            xy_ready = true;
         } else {
             for (uint32_t v = wb0 + l; v < wb1; v += 64) {
                 const uint32_t rr = B[v];
@@ -2536,11 +2551,10 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
     }
     __syncthreads();
     CG_HOOK_LG_STAMP(S, 9);
-    // 9. the members' x, y in CSR order, next to each other (LDS form: over B and Cc, which are
-    //    used up), so each cluster's sum below reads one contiguous run
-    typename K::P32 XY = B;   // (two words per slot: B and Cc are adjacent)
+    // 9. (LDS form, when the ballot form above has not placed them) the members' x, y in CSR
+    //    order, next to each other, so each cluster's sum below reads one contiguous run
     const uint32_t nmem = A[C];
-    if (K::in_lds && nmem) {
+    if (K::in_lds && !xy_ready && nmem) {
         for (uint32_t pb = 0; pb < nmem; pb += 16 * CG_BLOCK) {   // sixteen loads in flight per thread
             float cx[16], cy[16];
 #pragma unroll
