@@ -2011,33 +2011,63 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_forest(LgScratch S, CgDevParams P
     for (uint32_t v = blockIdx.x * WAVES + wave_id(), V = S.meta[LG_V]; v < V; v += gridDim.x * WAVES)
         lg_forest_one(S, P, v);
 }
-// flatten: rounds of par[x] = par[par[x]] until nothing changes, in LDS when V <= LG_FLAT_LDS
-// (else on the HBM array, still one workgroup: its barriers order the rounds)
+// flatten: every voxel's parent replaced by its forest root. Each thread chases its voxels' paths
+// to the root, four chases interleaved, and writes the root in place: a path read meanwhile
+// sees either the old parent or the root, both ancestors on its way to the same root, so the
+// chases need no rounds or barriers (the pointer-jumping rounds this replaces took two
+// barriers each). In LDS when V <= LG_FLAT_LDS, else on the HBM array (one workgroup).
 #define LG_FLAT_LDS 32768
+template <class P32>
+__device__ __forceinline__ void lg_roots_in_place(P32 par, uint32_t V) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t vb = 0; vb < V; vb += 4 * CG_BLOCK) {
+        uint32_t r[4], p[4];
+        bool go = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) r[q] = min(vb + (uint32_t)q * CG_BLOCK + tid, V - 1);
+        while (go) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) p[q] = par[r[q]];
+            go = false;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                go |= p[q] != r[q];
+                r[q] = p[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+            if (v < V) par[v] = r[q];
+        }
+    }
+}
 __global__ __launch_bounds__(CG_BLOCK) void lg_flatten(LgScratch S) {
     __shared__ uint32_t lpar[LG_FLAT_LDS];
-    __shared__ uint32_t changed[2];
     const uint32_t tid = threadIdx.x, V = S.meta[LG_V];
-    uint32_t* const par = V <= LG_FLAT_LDS ? lpar : S.par;
-    if (V <= LG_FLAT_LDS)
-        for (uint32_t x = tid; x < V; x += CG_BLOCK) lpar[x] = S.par[x];
-    if (tid < 2) changed[tid] = 0;
-    __syncthreads();
-    for (uint32_t r = 0;; r++) {
-        bool ch = false;
-        for (uint32_t x = tid; x < V; x += CG_BLOCK) {
-            const uint32_t p = par[x], pp = par[p];
-            if (pp != p) { par[x] = pp; ch = true; }
+    if (V == 0) return;
+    if (V <= LG_FLAT_LDS) {
+        lds_u32* const lp = (lds_u32*)(uint32_t*)lpar;
+        for (uint32_t vb = 0; vb < V; vb += 16 * CG_BLOCK) {   // sixteen loads in flight per thread
+            uint32_t pv[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+                pv[q] = v < V ? S.par[v] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t v = vb + (uint32_t)q * CG_BLOCK + tid;
+                if (v < V) lp[v] = pv[q];
+            }
         }
-        if (__ballot(ch) && lane_id() == 0) changed[r & 1] = 1;
         __syncthreads();
-        const bool any = changed[r & 1] != 0;
-        if (tid == 0) changed[(r + 1) & 1] = 0;
+        lg_roots_in_place(lp, V);
         __syncthreads();
-        if (!any) break;
+        for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = lp[x];
+    } else {
+        lg_roots_in_place(S.par, V);
     }
-    if (V <= LG_FLAT_LDS)
-        for (uint32_t x = tid; x < V; x += CG_BLOCK) S.par[x] = lpar[x];
 }
 // cross-tree edges (v < o): united unless both ends already share a parent
 __device__ __forceinline__ void lg_cross_one(const LgScratch& S, const CgDevParams& P, uint32_t v, uint32_t vb) {
