@@ -1981,12 +1981,21 @@ __device__ __forceinline__ void lg_neighbours(const LgScratch& S, const LgGrid& 
         rx[r] = tot;
         tot += (uint32_t)__builtin_amdgcn_readlane((int)e, r) - rb[r];
     }
-    for (uint32_t t = l; t < tot; t += 64) {
-        uint32_t j = 0;
+    // two rounds' neighbour indices loaded together, then visited
+    for (uint32_t t0 = l; t0 < tot; t0 += 128) {
+        uint32_t o[2];
 #pragma unroll
-        for (int r = 0; r < 9; r++)
-            if (t >= rx[r]) j = rb[r] + (t - rx[r]);   // the last row starting at or before t
-        visit(S.ord[j]);
+        for (int u = 0; u < 2; u++) {
+            const uint32_t t = t0 + 64u * u;
+            uint32_t j = 0;
+#pragma unroll
+            for (int r = 0; r < 9; r++)
+                if (t >= rx[r]) j = rb[r] + (t - rx[r]);   // the last row starting at or before t
+            o[u] = t < tot ? S.ord[j] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            if (o[u] != 0xffffffffu) visit(o[u]);
     }
 }
 __device__ __forceinline__ bool lg_adjacent(const float4& q, const float4& p, float r2) {
@@ -2001,8 +2010,11 @@ __device__ __forceinline__ void lg_forest_one(const LgScratch& S, const CgDevPar
     const LgGrid g(S.meta);
     const float4 q = S.vox[v];
     uint32_t lo = v;
-    lg_neighbours(S, g, q, [&](uint32_t o) {
-        if (o < lo && lg_adjacent(q, S.vox[o], P.r2)) lo = o;
+    lg_neighbours(S, g, q, [&](uint32_t o) {   // (the load depends on o < v only: the visits' loads go together)
+        if (o < v) {
+            const float4 p = S.vox[o];
+            if (o < lo && lg_adjacent(q, p, P.r2)) lo = o;
+        }
     });
     lo = wave_umin(lo);
     if (lane_id() == 0) S.par[v] = lo;
