@@ -688,6 +688,9 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
     if rank == 0:
         allf = torch.from_numpy(cp.synth_frames(F * world, first_frame=0, rings=64, cols=N // 64)).to(dev)
     hdr = torch.empty((F, 8), dtype=torch.int32, device=dev)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")   # (once, outside the timed loop)
+    hip.hipMemcpyDtoDAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
 
     def one():
         mine = cd.scatter_frames(allf, F, raw.shape[1], dev)
@@ -696,9 +699,6 @@ def scatter_composition(cp, cd, eng, stream, raw, F, N, dev, rank, world, steps)
             eng.run(mine.data_ptr(), F, N, 16, stream=stream.cuda_stream)
         torch.cuda.current_stream(dev).wait_stream(stream)
         # header words: copy out of the engine's device buffer (int32 view)
-        import ctypes
-        hip = ctypes.CDLL("libamdhip64.so")
-        hip.hipMemcpyDtoDAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         hip.hipMemcpyDtoDAsync(hdr.data_ptr(), eng.results().d_header, F * 32,
                                ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
         return cd.gather_headers(hdr)

@@ -15,7 +15,8 @@ CG_OK, CG_E_INVALID, CG_E_DEVICE, CG_E_OOM, CG_E_CAPACITY = 0, 1, 2, 3, 4
 CG_F_VOXEL_PASSTHROUGH, CG_F_GLOBAL_SCRATCH, CG_F_ORDER_CANONICAL, CG_F_VOXEL_POINT_ORDER = 0x1, 0x2, 0x4, 0x8
 CG_VOXEL_ORDER_POINT, CG_VOXEL_ORDER_PCL = 0, 1
 CG_MODE_PIPELINE, CG_MODE_DETECT = 0, 1
-CG_HDR_N, CG_HDR_K, CG_HDR_M, CG_HDR_V, CG_HDR_C, CG_HDR_FLAGS, CG_HDR_WORDS = 0, 1, 2, 3, 4, 5, 8
+CG_HDR_N, CG_HDR_K, CG_HDR_M, CG_HDR_V, CG_HDR_C, CG_HDR_FLAGS, CG_HDR_ERR, CG_HDR_WORDS = 0, 1, 2, 3, 4, 5, 7, 8
+CG_HDR_E_WAIT = 0x57414954
 
 
 class cg_params(C.Structure):

@@ -12,7 +12,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
-#include "../../include/cones_gpu.h"
+#include "../../include/cones_gpu_debug.h"
 #include "cg_internal.h"
 #include "cg_math.h"
 #include "cg_host.h"
@@ -424,7 +424,7 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
         const uint32_t V = p[CG_HDR_V], C = p[CG_HDR_C];
         if (V <= CG_PACK_MAX && C <= CG_PACK_MAX && (C == 0 || p[CG_PACK_OFFS + C] <= CG_PACK_MAX)) {
             std::memcpy(h->h_hdr, p, CG_HDR_WORDS * 4);
-            if (p[CG_HDR_WORDS - 1] == CG_HDR_E_WAIT)
+            if (p[CG_HDR_ERR] == CG_HDR_E_WAIT)
                 return fail(CG_E_DEVICE, "frame %u: a device-side wait of the large-frame path gave up; results void", frame);
             out->n_points = p[CG_HDR_N];
             out->n_kept = p[CG_HDR_K];
@@ -443,7 +443,7 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
     HIPCHK(hipMemcpyAsync(h->h_hdr, h->d_hdr + (uint64_t)frame * CG_HDR_WORDS, CG_HDR_WORDS * 4,
                           hipMemcpyDeviceToHost, s));
     HIPCHK(cg_stream_wait(s));
-    if (h->h_hdr[CG_HDR_WORDS - 1] == CG_HDR_E_WAIT)
+    if (h->h_hdr[CG_HDR_ERR] == CG_HDR_E_WAIT)
         return fail(CG_E_DEVICE, "frame %u: a device-side wait of the large-frame path gave up; results void", frame);
     const uint32_t V = h->h_hdr[CG_HDR_V], C = h->h_hdr[CG_HDR_C];
     h->h_vox.resize((size_t)V * 4 + 4);
@@ -593,7 +593,7 @@ int run_single(cg_handle* h, const cg_cloud_view* in, int kmode, cg_detect_resul
         h->retries++;
         return run_single(h, in, kmode, dres, gres, retry | RETRY_DMA);
     }
-    if (split && h->h_hdr[CG_HDR_WORDS - 1]) {   // (the kernel's own flag: header word 7)
+    if (split && h->h_hdr[CG_HDR_ERR]) {   // (the kernel's own flag: header word 7)
         h->retries++;
         return run_single(h, in, kmode, dres, gres, retry | RETRY_ONE_WG);
     }
@@ -620,7 +620,7 @@ extern "C" {
 
 // 0.2.0: cg_run_batch_split, cg_debug_front_span and CG_F_PAIR_TIMEOUT removed (round 4;
 // INTEGRATION.md, ABI history)
-const char* cg_version(void) { return "cones_gpu 0.2.0 (gfx950)"; }
+const char* cg_version(void) { return "cones_gpu 0.2.1 (gfx950)"; }
 
 void cg_params_init(cg_params* p) {
     if (!p) return;
@@ -930,7 +930,10 @@ int cg_batch_fetch(cg_handle* h, uint32_t frame, cg_detect_result* out) {
     if (!h || !out) return fail(CG_E_INVALID, "null argument");
     if (frame >= h->last_frames) return fail(CG_E_INVALID, "frame %u >= %u", frame, h->last_frames);
     HIPCHK(hipSetDevice(h->device));
-    return fetch_frame(h, h->last_stream, frame, out);
+    const int rc = fetch_frame(h, h->last_stream, frame, out);
+    if (rc == CG_OK && h->h_hdr[CG_HDR_ERR] != 0u)   // (include/cones_gpu.h CG_HDR_ERR)
+        return fail(CG_E_DEVICE, "frame %u: header error word %#x; results void", frame, h->h_hdr[CG_HDR_ERR]);
+    return rc;
 }
 
 // ---- tiled frames (C5) ----------------------------------------------------------------------

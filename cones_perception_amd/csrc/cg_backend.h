@@ -581,6 +581,7 @@ __device__ __forceinline__ void backend(const Work& W, uint32_t M, FrontShared* 
         h[CG_HDR_V] = V;
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = flags;
+        h[CG_HDR_ERR] = 0u;   // (a split launch overwrites it after the backend)
     }
     STAMP(20);
 }

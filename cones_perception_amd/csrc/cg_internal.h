@@ -298,9 +298,8 @@ int cg_launch_recrop(const CgLaunch& L, const CgDevParams& P, bool pipeline, con
 // CG_PACK_MAX are fetched separately).
 #define CG_PACK_MAX 1024
 #define CG_PACK_VOX CG_HDR_WORDS
-// header word CG_HDR_WORDS - 1 of a large frame whose device-side wait gave up (LG_PQ_TIMEOUT):
-// its results are void and the fetch fails with CG_E_DEVICE
-#define CG_HDR_E_WAIT 0x57414954u
+// (header word CG_HDR_ERR of a large frame whose device-side wait gave up, LG_PQ_TIMEOUT:
+// CG_HDR_E_WAIT, include/cones_gpu.h)
 #define CG_PACK_LAB (CG_PACK_VOX + 4 * CG_PACK_MAX)
 #define CG_PACK_OFFS (CG_PACK_LAB + CG_PACK_MAX)
 #define CG_PACK_IDX (CG_PACK_OFFS + CG_PACK_MAX + 1)

@@ -559,7 +559,7 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     }
     if constexpr (SPLIT) {   // the results packed for the host's one copy (fetch_frame)
         // header word 7: a chunk gave up waiting for the others (the host runs the frame again)
-        if (tid == 0) L.hdr[CG_HDR_WORDS - 1] = fs->scal[S_ERR];
+        if (tid == 0) L.hdr[CG_HDR_ERR] = fs->scal[S_ERR];
         if (L.pack) {
             __threadfence();
             __syncthreads();

@@ -1544,7 +1544,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         const uint32_t* Lr = pq_list(S, level % 3u) + PQ_EW * tid;
         pf = Lr[0]; pe = Lr[1]; pd = Lr[2];
     }
-    if (level == 0 && blockIdx.x == 0 && tid == 0 && S.force_wait_fail) S.meta[LG_PQ_TIMEOUT] = 1u;   // (route 10)
     if (blockIdx.x == 0) {
         // for level + 1: the set level - 1 used, with the ranges level - 1 had (level 0: the
         // whole index_vector; later levels: their list's count, read before the barrier in
@@ -1667,24 +1666,35 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
         }
         // every tile of the range has stored its lists: the range's word counts them all, and
         // then holds the totals
+        const uint64_t need = (uint64_t)(tp[r + 1] - tp[r]);
         if (tid == 0) {
-            const uint64_t need = (uint64_t)(tp[r + 1] - tp[r]);
             const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
-            uint64_t wv;
-            while (((wv = ld64(&done[r])) >> 46) < need) {
+            uint64_t wv = 0;
+            // route 10 (tests) takes the expired path itself at level 0: no wait at all
+            while (!(level == 0 && S.force_wait_fail) && ((wv = ld64(&done[r])) >> 46) < need) {
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t_0 > PQ_WAIT_TICKS) {   // (never expected)
-                    S.meta[LG_PQ_TIMEOUT] = 1u;
-                    break;
-                }
+                if (__builtin_amdgcn_s_memrealtime() - t_0 > PQ_WAIT_TICKS) break;   // (never expected)
             }
+            if ((wv >> 46) < need) S.meta[LG_PQ_TIMEOUT] = 1u;   // (the frame's fetch fails on it)
             rword = wv;
         }
         if (t0 == 0 && j == 0 && level < 7) CG_HOOK_LG_STAMP(S, 20 + 6 * level);   // (the tile-0 holder)
         __syncthreads();
         const uint64_t rw = rword;
-        const uint32_t nL = (uint32_t)(rw >> 23) & (uint32_t)PQ_RW_N, nR = (uint32_t)rw & (uint32_t)PQ_RW_N;
         const uint32_t x = f + 1 + q * PQ_T + tid;
+        if ((rw >> 46) < need) {   // (uniform) the wait gave up: the range's totals and lists are
+            // partial, so no list entry is read. The tile's records go out unchanged, and the
+            // range's first tile queues the whole range as one leaf: every later index stays
+            // inside [f, e). The frame's results are void (LG_PQ_TIMEOUT), never a wild access.
+            if (x < e) Eo[x] = rx;
+            if (q == 0 && tid == 0) {
+                Eo[f] = rf;
+                pq_push(S, PQ_LEAFLIST, f, e, d > 0 ? d - 1u : 0u, out_buf);
+            }
+            __syncthreads();
+            continue;
+        }
+        const uint32_t nL = (uint32_t)(rw >> 23) & (uint32_t)PQ_RW_N, nR = (uint32_t)rw & (uint32_t)PQ_RW_N;
         if (q == 0 && tid == 0) Eo[f] = E[m];
         if (x < e) {
             const uint64_t vx = x == m ? rf : rx;
@@ -2242,7 +2252,7 @@ __device__ __forceinline__ void lg_csr_one(const CgLaunch& L, const CgDevParams&
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
                           (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
-        h[CG_HDR_WORDS - 1] = 0u;
+        h[CG_HDR_ERR] = 0u;
     }
 }
 __device__ __forceinline__ void lg_centroids_one(const CgLaunch& L, const CgDevParams& P, const LgScratch& S,
@@ -2693,7 +2703,7 @@ __device__ __forceinline__ void lg_tail_body(const CgLaunch& L, const CgDevParam
         h[CG_HDR_C] = C;
         h[CG_HDR_FLAGS] = CG_F_GLOBAL_SCRATCH | (m[LG_PASS] ? CG_F_VOXEL_PASSTHROUGH : 0u) |
                           (P.voxel_order == CG_VOXEL_ORDER_PCL ? 0u : CG_F_VOXEL_POINT_ORDER);
-        h[CG_HDR_WORDS - 1] = m[LG_PQ_TIMEOUT] ? CG_HDR_E_WAIT : 0u;   // (the fetch fails on it)
+        h[CG_HDR_ERR] = m[LG_PQ_TIMEOUT] ? CG_HDR_E_WAIT : 0u;   // (the fetch fails on it)
     }
     CG_HOOK_LG_STAMP(S, 12);
 }

@@ -179,7 +179,12 @@ int cg_run_batches(cg_handle* const* handles, const cg_batch* batches, uint32_t 
 #define CG_HDR_V      3
 #define CG_HDR_C      4
 #define CG_HDR_FLAGS  5
+#define CG_HDR_ERR    7   /* 0 for a good frame. Nonzero: the frame's results are void and
+                             cg_batch_fetch fails with CG_E_DEVICE; a caller reading d_header
+                             directly must drop such a frame. CG_HDR_E_WAIT: a large frame's
+                             device-side wait gave up (never expected; ABI 0.2.0+) */
 #define CG_HDR_WORDS  8
+#define CG_HDR_E_WAIT 0x57414954u
 
 typedef struct cg_batch_results {
     uint32_t n_frames;
@@ -359,48 +364,6 @@ int  cg_tracker_set_params(cg_tracker* t, const cg_track_params* p);
 int  cg_tracker_match(cg_tracker* t, const float* centroids_xy, uint32_t n, int32_t* status, uint32_t* n_need);
 int  cg_tracker_commit(cg_tracker* t, const int32_t* colors, uint32_t n_colors);
 int  cg_tracker_cloud(const cg_tracker* t, int color, const float** xy, uint32_t* n);
-
-/* ---- device self-checks (tests) ------------------------------------------------------ */
-/* Evaluate the device atan2f / sector / sqrt restatements on n host inputs (device round
- * trip), for comparison with the host libm in tests. atan2f: out[2i] = the exact restatement,
- * out[2i+1] = sector + 32 * (angle filter at ang_hi = 1.3 removes it), both through the
- * certified fast classification. */
-int cg_selftest_atan2f(cg_handle* h, const float* y, const float* x, float* out, uint32_t n);
-int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
-
-/* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz; 32 slots per frame) for the
- * next batch calls; enable = 0 frees the buffer. Fetch synchronises the batch stream. */
-int cg_debug_stamps(cg_handle* h, int enable);
-/* Timing: the next cg_run_batch launch of the frame kernel records its execution span in
- * d_span (device memory, 2 x uint64 the caller sets to {UINT64_MAX, 0}): the first workgroup's
- * start and the last workgroup's end, s_memrealtime ticks (100 MHz). One atomic per workgroup
- * at each end; frames of more than 65,536 points (large-frame path) do not record. */
-int cg_debug_launch_span(cg_handle* h, void* d_span);
-/* The same for the handle's next n_launches batch launches, launch k into d_spans[2k, 2k + 1]
- * (no host call between the launches). */
-int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches);
-int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
-
-/* Diagnostics: route every frame through the large-frame path (1), and also through its
- * global HBM backend even when the detector input fits the LDS backend (2); run single-frame
- * calls in one workgroup instead of the per-chunk split launch (3), or split with the input
- * copied by DMA instead of read by the kernel from pinned memory (4); the global backend with
- * the PCL voxel sort cut after one partition level, so its leaves longer than the LDS leaf
- * are finished in HBM side by side (5); single-frame calls whose staged chunks are never
- * published, so every chunk workgroup times out and the call re-runs the frame by DMA (6,
- * tests of that retry); single-frame split calls whose chunk workgroup 0 gives up waiting for
- * the other chunks at once, so the call re-runs the frame in one workgroup (9, tests of that
- * retry); large frames whose first partition level reports a timed-out device-side wait, so the
- * fetch fails with CG_E_DEVICE (10, tests of that failure); 0 = automatic. */
-int cg_debug_route(cg_handle* h, int route);
-/* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
- * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */
-int cg_debug_large_meta(cg_handle* h, uint32_t* out, uint32_t n_words);
-/* Diagnostics: raw large-frame scratch of the last frame: 0 = meta words, 1 = z codes
- * ([chunk][group][lane] words of 8 codes), 2 = ground-mode kept bits, 3 = the PCL voxel sort's
- * range lists (8 header words: level counts, leaf count; then 4 lists of 5-word entries),
- * 4 = the first 1024 bytes of the radix histogram area (phase stamps of variant builds). */
-int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes);
 
 /* Exported library version string. */
 /* "cones_gpu MAJOR.MINOR.PATCH (gfx950)"; INTEGRATION.md, ABI history */

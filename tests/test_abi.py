@@ -14,12 +14,24 @@ from cones_perception_amd import _abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "cones_gpu.h")
+DEBUG_HEADER = os.path.join(ROOT, "include", "cones_gpu_debug.h")   # tests and tools only
 
 
-def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(cg_[a-z0-9_]+)\s*\(", text)))
+def declared_functions(headers=(HEADER, DEBUG_HEADER)):
+    names = set()
+    for h in headers:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(cg_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
+
+
+def test_product_header_has_no_debug_entry_points():
+    """A ROS integrator sees only the product calls: self-tests, stamps, forced routes and
+    scratch dumps live in cones_gpu_debug.h, which cones_gpu.h does not include."""
+    prod = declared_functions((HEADER,))
+    assert not [n for n in prod if n.startswith(("cg_debug_", "cg_selftest_"))], prod
+    assert "cones_gpu_debug.h" not in open(HEADER).read()
+    assert "cg_debug_route" in declared_functions((DEBUG_HEADER,))
 
 
 def test_header_symbols_exported():
@@ -33,7 +45,7 @@ def test_header_symbols_exported():
 
 def test_header_compiles_as_c_and_cpp(tmp_path):
     src = tmp_path / "h.c"
-    src.write_text('#include "cones_gpu.h"\nint main(void){cg_params p; cg_params_init(&p); return 0;}\n')
+    src.write_text('#include "cones_gpu_debug.h"\nint main(void){cg_params p; cg_params_init(&p); return 0;}\n')
     for cc in (["gcc", "-std=c99"], ["g++", "-x", "c++"]):
         r = subprocess.run(cc + ["-fsyntax-only", "-I", os.path.join(ROOT, "include"), str(src)],
                            capture_output=True, text=True)

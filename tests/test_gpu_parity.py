@@ -2,9 +2,10 @@
 
 Integer/index outputs (K, M, V, C, cluster index sets, labels) must be identical, and every
 float output (voxel centroids, cluster centroids) bit-identical: the device restates the
-reference's float/double arithmetic exactly (cg_math.h) and sums voxels in ascending point
-order, the oracle's ORDER_STABLE mode. The north star's 1e-5 m centroid tolerance is therefore
-met with 0 error. Sizes: C1 (16 rings x 1024) and C2 (64 x 1024) synthetic frames.
+reference's float/double arithmetic exactly (cg_math.h) and sums each voxel in PCL's std::sort
+permutation of index_vector (the default CG_VOXEL_ORDER_PCL), compared with the oracle's
+ORDER_PCL mode (tests/oracle_py.py's default). The north star's 1e-5 m centroid tolerance is
+therefore met with 0 error. Sizes: C1 (16 rings x 1024) and C2 (64 x 1024) synthetic frames.
 """
 import ctypes as C
 
