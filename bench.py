@@ -800,9 +800,13 @@ def c5_cpu(cp, params, det, budget_s):
         exact = True
     except AssertionError:
         exact = False
+    fl = O.flann_check(params, msg, O.MODE_PIPELINE)
     return {"ms_per_frame": el / n * 1e3, "frames_per_s": n / el, "cores": 1, "kind": "port",
             "sample": f"{n} C5 frames (1,048,576 points, sequential), {el:.1f} s, oracle/cg_oracle.cpp",
-            "gpu_bit_exact_vs_oracle_pcl_order": exact}
+            "gpu_bit_exact_vs_oracle_pcl_order": exact,
+            "near_tolerance_pairs": fl["near_tolerance_pairs"],
+            "flann_check": {k: fl[k] for k in ("voxels", "queries_differ", "clusters_equal", "near_tolerance_pairs",
+                                               "near_tolerance_inside", "closest_inside_ulps")}}
 
 
 def c5_tiled(cp, cd, params, device, rank, world, reps=20, halo=False):
@@ -1027,7 +1031,21 @@ def cpu_baseline(cp, params, raw, budget_s, eng, threads, order=None):
             exact += (same_sets and g.n_kept == r.n_kept and g.n_filtered == r.n_filtered
                       and same_bits(g.voxels, r.voxels) and np.array_equal(g.labels, r.labels)
                       and same_bits(g.centroids, r.centroids))
+    # FLANN's own search (restated, oracle SEARCH_FLANN) against the exact radius predicate the
+    # device implements, on the same sample (tests/test_flann.py)
+    fl = {"frames": 0, "voxels": 0, "queries_differ": 0, "clusters_differ": 0, "near_tolerance_pairs": 0,
+          "near_tolerance_inside": 0}
+    for i in ref:
+        f = O.flann_check(params, msgs[i], O.MODE_PIPELINE)
+        fl["frames"] += 1
+        fl["clusters_differ"] += int(not f["clusters_equal"])
+        for k in ("voxels", "queries_differ", "near_tolerance_pairs", "near_tolerance_inside"):
+            fl[k] += f[k]
     out["parity"] = {"frames": len(ref), "reference": "oracle ORDER_PCL (PCL 1.10 VoxelGrid std::sort order)",
+                     "near_tolerance_pairs": fl["near_tolerance_pairs"],
+                     "near_tolerance_note": "voxel pairs whose float L2_Simple sum lies within 4 ulp of r2 (the "
+                                            "only pairs FLANN's float pruning could drop)",
+                     "flann_check": fl,
                      "cluster_sets_identical_vs_pcl": int(sets), "max_centroid_abs_err_vs_pcl_m": maxerr,
                      "bit_exact": int(exact),
                      "bit_exact_against": "ORDER_STABLE (point-order mode)" if point else "ORDER_PCL",

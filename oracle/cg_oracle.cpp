@@ -14,6 +14,8 @@
 //   distance          perception_handling::euclidan_dist              src/perception_handling/utils.cpp:32-34
 //   voxel grid        pcl::VoxelGrid<PointXYZI>::applyFilter (1.10)   called src/cone_detection.cpp:240-249
 //   clustering        pcl::extractEuclideanClusters + KdTreeFLANN     called src/cone_detection.cpp:206-220
+//                     (default: the exact L2_Simple radius predicate; checker mode SEARCH_FLANN:
+//                     FLANN 1.9.1's own KDTreeSingleIndex and float-pruned search, FlannIndex)
 //   cluster order     std::sort(clusters.rbegin(), rend(), size<)     (EuclideanClusterExtraction::extract)
 //   centroid          ConeDetector::get_centroid_clouds (centroid)    src/cone_detection.cpp:261-279
 //   re-crop           ConeDetector::get_reconstructed_cone            src/cone_detection.cpp:222-238
@@ -278,13 +280,215 @@ struct KdTree {
     }
 };
 
+// ---------------- checker mode: FLANN 1.9.1's own tree and search ----------------
+// The exact predicate above assumes FLANN returns every point with acc < r2. FLANN prunes with
+// a float lower bound that it updates incrementally, which could in principle overshoot by an
+// ulp and drop a neighbour within a few ulps of r2. This restates the search PCL 1.10 actually
+// runs, so the assumption can be checked frame by frame (tests/test_flann.py, bench parity):
+//   pcl::search::KdTree<PointXYZI>(sorted = true) -> pcl::KdTreeFLANN<PointXYZI,
+//   flann::L2_Simple<float>>::setInputCloud: x, y, z of every valid point, in cloud order,
+//   flann::KDTreeSingleIndex with KDTreeSingleIndexParams(15) (leaf_max_size 15, reorder true);
+//   radiusSearch: r2 = float(radius * radius) (radius a double), SearchParams(checks -1,
+//   eps 0, sorted true), max_neighbors -1: RadiusResultSet, KDTreeSingleIndex::findNeighbors.
+// FLANN 1.9.1 (flann/algorithms/kdtree_single_index.h, flann/util/result_set.h) is not in this
+// image or in the reference; restated from its published source:
+//   buildIndex: vind = 0..N-1, root bbox = per-dim min / max over all points, divideTree;
+//   divideTree(left, right, bbox&): a leaf when right - left <= leaf_max_size (bbox := its
+//     points' bounds); else middleSplit_ on the CELL bbox it was given, child1 over
+//     [left, left + idx) with bbox[cutfeat].high = cutval, child2 over the rest with
+//     bbox[cutfeat].low = cutval; divlow / divhigh = the children's actual bounds in cutfeat;
+//     bbox := the union of the children's actual bounds;
+//   middleSplit_: max_span over the cell's dims; among dims with span > (1 - 1e-5f) * max_span
+//     the one of largest actual spread of the points (first on ties); split_val = the cell's
+//     middle, clamped to the points' [min, max]; planeSplit gives lim1 (< cutval first), lim2
+//     (<= cutval); index = lim1 if lim1 > count / 2, else lim2 if lim2 < count / 2, else count / 2;
+//   findNeighbors: epsError = 1 + eps = 1; dists[] = 0 and distsq = 0 for a query inside the
+//     root bbox (computeInitialDistances); searchLevel: leaf -> every point with
+//     L2_Simple acc < worstDist() (= r2) is added; inner node -> diff1 = val - divlow,
+//     diff2 = val - divhigh, the nearer child first (diff1 + diff2 < 0: child1), then
+//     mindistsq = mindistsq + cut_dist - dists[idx] (float), the other child only if
+//     mindistsq * epsError <= r2;
+//   copy(sorted): std::sort of (dist, index) pairs, DistIndex::operator< (dist, then index).
+// All of it in float (DistanceType = ElementType = float), no contraction (-ffp-contract=off).
+struct FlannIndex {
+    struct Node { int left = 0, right = 0, divfeat = 0; float divlow = 0.f, divhigh = 0.f; int child1 = -1, child2 = -1; };
+    struct Iv { float low, high; };
+    static constexpr int kLeafMax = 15;
+    std::vector<float> pts;    // points_: N x 3 (the KdTreeFLANN array)
+    std::vector<int> vind;
+    std::vector<Node> nodes;
+    std::vector<Iv> root_bbox;
+    int root = -1;
+
+    float at(int i, int d) const { return pts[3 * (size_t)i + d]; }
+    void compute_min_max(const int* ind, int count, int dim, float& mn, float& mx) const {
+        mn = at(ind[0], dim);
+        mx = at(ind[0], dim);
+        for (int i = 1; i < count; ++i) {
+            const float v = at(ind[i], dim);
+            if (v < mn) mn = v;
+            if (v > mx) mx = v;
+        }
+    }
+    void plane_split(int* ind, int count, int cutfeat, float cutval, int& lim1, int& lim2) const {
+        int left = 0, right = count - 1;
+        for (;;) {
+            while (left <= right && at(ind[left], cutfeat) < cutval) ++left;
+            while (left <= right && at(ind[right], cutfeat) >= cutval) --right;
+            if (left > right) break;
+            std::swap(ind[left], ind[right]); ++left; --right;
+        }
+        lim1 = left;
+        right = count - 1;
+        for (;;) {
+            while (left <= right && at(ind[left], cutfeat) <= cutval) ++left;
+            while (left <= right && at(ind[right], cutfeat) > cutval) --right;
+            if (left > right) break;
+            std::swap(ind[left], ind[right]); ++left; --right;
+        }
+        lim2 = left;
+    }
+    void middle_split(int* ind, int count, int& index, int& cutfeat, float& cutval, const std::vector<Iv>& bbox) const {
+        const float EPS = 0.00001f;
+        float max_span = bbox[0].high - bbox[0].low;
+        for (int i = 1; i < 3; ++i) {
+            const float span = bbox[i].high - bbox[i].low;
+            if (span > max_span) max_span = span;
+        }
+        float max_spread = -1;
+        cutfeat = 0;
+        for (int i = 0; i < 3; ++i) {
+            const float span = bbox[i].high - bbox[i].low;
+            if (span > (1 - EPS) * max_span) {
+                float mn, mx;
+                compute_min_max(ind, count, i, mn, mx);
+                const float spread = mx - mn;
+                if (spread > max_spread) { cutfeat = i; max_spread = spread; }
+            }
+        }
+        const float split_val = (bbox[cutfeat].low + bbox[cutfeat].high) / 2;
+        float mn, mx;
+        compute_min_max(ind, count, cutfeat, mn, mx);
+        if (split_val < mn) cutval = mn;
+        else if (split_val > mx) cutval = mx;
+        else cutval = split_val;
+        int lim1, lim2;
+        plane_split(ind, count, cutfeat, cutval, lim1, lim2);
+        if (lim1 > count / 2) index = lim1;
+        else if (lim2 < count / 2) index = lim2;
+        else index = count / 2;
+    }
+    int divide(int left, int right, std::vector<Iv>& bbox) {
+        const int me = (int)nodes.size();
+        nodes.emplace_back();
+        if (right - left <= kLeafMax) {
+            nodes[me].left = left; nodes[me].right = right;
+            for (int i = 0; i < 3; ++i) bbox[i].low = bbox[i].high = at(vind[left], i);
+            for (int k = left + 1; k < right; ++k)
+                for (int i = 0; i < 3; ++i) {
+                    if (bbox[i].low > at(vind[k], i)) bbox[i].low = at(vind[k], i);
+                    if (bbox[i].high < at(vind[k], i)) bbox[i].high = at(vind[k], i);
+                }
+            return me;
+        }
+        int idx, cutfeat;
+        float cutval;
+        middle_split(&vind[0] + left, right - left, idx, cutfeat, cutval, bbox);
+        nodes[me].divfeat = cutfeat;
+        std::vector<Iv> left_bbox(bbox);
+        left_bbox[cutfeat].high = cutval;
+        const int c1 = divide(left, left + idx, left_bbox);
+        std::vector<Iv> right_bbox(bbox);
+        right_bbox[cutfeat].low = cutval;
+        const int c2 = divide(left + idx, right, right_bbox);
+        nodes[me].child1 = c1; nodes[me].child2 = c2;
+        nodes[me].divlow = left_bbox[cutfeat].high;
+        nodes[me].divhigh = right_bbox[cutfeat].low;
+        for (int i = 0; i < 3; ++i) {
+            bbox[i].low = std::min(left_bbox[i].low, right_bbox[i].low);
+            bbox[i].high = std::max(left_bbox[i].high, right_bbox[i].high);
+        }
+        return me;
+    }
+    void build(const std::vector<Pt>& cloud) {
+        pts.clear();
+        for (const Pt& p : cloud) pts.insert(pts.end(), {p.x, p.y, p.z});
+        const int n = (int)cloud.size();
+        vind.resize(n);
+        for (int i = 0; i < n; i++) vind[i] = i;
+        nodes.clear();
+        root = -1;
+        if (n == 0) return;
+        root_bbox.assign(3, Iv{0.f, 0.f});
+        for (int i = 0; i < 3; ++i) root_bbox[i].low = root_bbox[i].high = at(0, i);
+        for (int k = 1; k < n; ++k)
+            for (int i = 0; i < 3; ++i) {
+                if (at(k, i) < root_bbox[i].low) root_bbox[i].low = at(k, i);
+                if (at(k, i) > root_bbox[i].high) root_bbox[i].high = at(k, i);
+            }
+        root = divide(0, n, root_bbox);
+    }
+    void search_level(std::vector<std::pair<float, int>>& res, const float* vec, int node, float mindistsq,
+                      float* dists, float r2) const {
+        const Node& nd = nodes[node];
+        if (nd.child1 < 0 && nd.child2 < 0) {
+            const float worst_dist = r2;
+            for (int i = nd.left; i < nd.right; ++i) {
+                const int j = vind[i];   // data_[i] (reordered) holds points_[vind_[i]]
+                float result = 0.f, diff;
+                for (int d = 0; d < 3; ++d) {
+                    diff = vec[d] - at(j, d);
+                    result += diff * diff;
+                }
+                if (result < worst_dist) res.push_back({result, j});   // (RadiusResultSet: dist < radius)
+            }
+            return;
+        }
+        const int idx = nd.divfeat;
+        const float val = vec[idx];
+        const float diff1 = val - nd.divlow, diff2 = val - nd.divhigh;
+        int best, other;
+        float cut_dist;
+        if ((diff1 + diff2) < 0) {
+            best = nd.child1; other = nd.child2;
+            cut_dist = (val - nd.divhigh) * (val - nd.divhigh);
+        } else {
+            best = nd.child2; other = nd.child1;
+            cut_dist = (val - nd.divlow) * (val - nd.divlow);
+        }
+        search_level(res, vec, best, mindistsq, dists, r2);
+        const float dst = dists[idx];
+        mindistsq = mindistsq + cut_dist - dst;
+        dists[idx] = cut_dist;
+        if (mindistsq * 1.0f <= r2) search_level(res, vec, other, mindistsq, dists, r2);
+        dists[idx] = dst;
+    }
+    void radius(const Pt& q, float r2, std::vector<std::pair<float, int>>& res) const {
+        res.clear();
+        if (root < 0) return;
+        const float vec[3] = {q.x, q.y, q.z};
+        float dists[3] = {0.f, 0.f, 0.f};
+        float distsq = 0.f;
+        for (int i = 0; i < 3; ++i) {   // computeInitialDistances
+            if (vec[i] < root_bbox[i].low) { dists[i] = (vec[i] - root_bbox[i].low) * (vec[i] - root_bbox[i].low); distsq += dists[i]; }
+            if (vec[i] > root_bbox[i].high) { dists[i] = (vec[i] - root_bbox[i].high) * (vec[i] - root_bbox[i].high); distsq += dists[i]; }
+        }
+        search_level(res, vec, root, distsq, dists, r2);
+        std::sort(res.begin(), res.end());   // DistIndex: (dist, index)
+    }
+};
+
+enum { SEARCH_EXACT = 0, SEARCH_FLANN = 1 };
+
 // pcl::extractEuclideanClusters (PCL 1.10) + EuclideanClusterExtraction::extract ordering.
 std::vector<std::vector<int>> euclidean_clusters(const std::vector<Pt>& cloud, float tolerance,
-                                                 unsigned min_pts, unsigned max_pts) {
+                                                 unsigned min_pts, unsigned max_pts, int search = SEARCH_EXACT) {
     std::vector<std::vector<int>> clusters;
     if (cloud.empty()) return clusters;
     KdTree tree;
-    tree.init(cloud);
+    FlannIndex flann;
+    if (search == SEARCH_FLANN) flann.build(cloud);
+    else tree.init(cloud);
     const float r2 = (float)((double)tolerance * (double)tolerance);   // KdTreeFLANN::radiusSearch
     const size_t nn_start_idx = 1;                                     // sorted results
     std::vector<bool> processed(cloud.size(), false);
@@ -294,7 +498,8 @@ std::vector<std::vector<int>> euclidean_clusters(const std::vector<Pt>& cloud, f
         std::vector<int> seed_queue{(int)i};
         processed[i] = true;
         for (size_t sq = 0; sq < seed_queue.size(); sq++) {
-            tree.radius(cloud[seed_queue[sq]], r2, nn);
+            if (search == SEARCH_FLANN) flann.radius(cloud[seed_queue[sq]], r2, nn);
+            else tree.radius(cloud[seed_queue[sq]], r2, nn);
             for (size_t j = nn_start_idx; j < nn.size(); j++) {
                 int k = nn[j].second;
                 if (processed[k]) continue;
@@ -323,18 +528,22 @@ struct Out {
     float* centroids;   // C x 2
 };
 
-void detect(std::vector<Pt>& cloud, bool is_dense, const Params& prm, int order, Out& o) {
+// ConeDetector constants (src/cone_detection.cpp:22-23) and the tolerance (line 212): the double
+// sqrt, passed to setClusterTolerance (double) and on to extractEuclideanClusters as a float.
+float cluster_tolerance() {
+    const float CONE_WIDTH = 0.228, CONE_HEIGHT = 0.325;
+    return (float)std::sqrt(std::pow(CONE_HEIGHT, 2) + std::pow(CONE_WIDTH, 2));
+}
+
+void detect(std::vector<Pt>& cloud, bool is_dense, const Params& prm, int order, Out& o, int search = SEARCH_EXACT) {
     filter_points_position(cloud, prm);
     o.hdr[2] = (uint32_t)cloud.size();
     std::vector<Pt> vox;
     bool passthrough = voxel_grid(cloud, is_dense, prm, order, vox);
     o.hdr[3] = (uint32_t)vox.size();
     o.hdr[5] = passthrough ? 1u : 0u;
-    // ConeDetector constants (src/cone_detection.cpp:22-23) and tolerance (line 212)
-    const float CONE_WIDTH = 0.228, CONE_HEIGHT = 0.325;
-    const double tol = std::sqrt(std::pow(CONE_HEIGHT, 2) + std::pow(CONE_WIDTH, 2));
-    auto clusters = euclidean_clusters(vox, (float)tol, (unsigned)prm.min_cluster_size,
-                                       (unsigned)prm.max_cluster_size);
+    auto clusters = euclidean_clusters(vox, cluster_tolerance(), (unsigned)prm.min_cluster_size,
+                                       (unsigned)prm.max_cluster_size, search);
     o.hdr[4] = (uint32_t)clusters.size();
     // duplicate (bit-identical) voxel points break the nn_start_idx = 1 assumption (rule E2)
     {
@@ -544,10 +753,11 @@ int oracle_node_step(void* node, const void* params, const void* view, int mode,
 
 // mode: 0 = pipeline (ground removal then detector), 1 = detector only, 2 = ground only.
 // order: 0 = stable voxel sums (device order), 1 = PCL std::sort order.
+// search: 0 = the exact radius predicate (the default), 1 = FLANN 1.9.1's own tree and search.
 // All output arrays must hold N entries (N+1 for offsets; 8N floats for ground).
-int oracle_run(const void* params, const void* view, int mode, int order, uint32_t* hdr,
-               float* ground, float* voxels, int32_t* labels, int32_t* offsets, int32_t* indices,
-               float* centroids) {
+int oracle_run_search(const void* params, const void* view, int mode, int order, int search, uint32_t* hdr,
+                      float* ground, float* voxels, int32_t* labels, int32_t* offsets, int32_t* indices,
+                      float* centroids) {
     const Params& prm = *(const Params*)params;
     const View& v = *(const View*)view;
     std::vector<Pt> cloud = decode(v);
@@ -560,8 +770,103 @@ int oracle_run(const void* params, const void* view, int mode, int order, uint32
         return 0;
     }
     Out o{hdr, ground, voxels, labels, offsets, indices, centroids};
-    detect(cloud, v.is_dense != 0, prm, order, o);
+    detect(cloud, v.is_dense != 0, prm, order, o, search);
     return 0;
+}
+int oracle_run(const void* params, const void* view, int mode, int order, uint32_t* hdr,
+               float* ground, float* voxels, int32_t* labels, int32_t* offsets, int32_t* indices,
+               float* centroids) {
+    return oracle_run_search(params, view, mode, order, SEARCH_EXACT, hdr, ground, voxels, labels, offsets, indices,
+                             centroids);
+}
+
+// The FLANN check of one frame (mode 0 / 1, voxel order as oracle_run): the voxel cloud the
+// clustering sees, every voxel as a query through both searches, and both clusterings.
+// stats (ORACLE_FLANN_WORDS words):
+//   [0] V voxels                       [1] queries whose neighbour sets differ
+//   [2] pairs the exact predicate has and FLANN's search misses (ordered: query, neighbour)
+//   [3] pairs FLANN returns that the exact predicate lacks (ordered)
+//   [4] near-tolerance pairs: unordered pairs whose float L2_Simple acc lies within 4 ulp of r2
+//       (either side), the only pairs a float pruning error could drop
+//   [5] of them, the pairs inside (acc < r2)
+//   [6] 1 when both clusterings are identical (index sets and order)
+//   [7] C exact                        [8] C FLANN
+//   [9] ulps from r2 of the closest in-tolerance pair (acc < r2), 0xffffffff when none
+int oracle_flann_check(const void* params, const void* view, int mode, int order, uint32_t* stats) {
+    const Params& prm = *(const Params*)params;
+    const View& v = *(const View*)view;
+    std::memset(stats, 0, 10 * sizeof(uint32_t));
+    stats[9] = 0xffffffffu;
+    std::vector<Pt> cloud = decode(v);
+    if (mode == 0) ground_remove(cloud, prm);
+    filter_points_position(cloud, prm);
+    std::vector<Pt> vox;
+    voxel_grid(cloud, v.is_dense != 0, prm, order, vox);
+    stats[0] = (uint32_t)vox.size();
+    if (vox.empty()) { stats[6] = 1; return 0; }
+    const float tol = cluster_tolerance();
+    const float r2 = (float)((double)tol * (double)tol);
+    KdTree tree;
+    tree.init(vox);
+    FlannIndex flann;
+    flann.build(vox);
+    uint32_t r2b;
+    std::memcpy(&r2b, &r2, 4);
+    std::vector<std::pair<float, int>> a, b, wide;
+    const float wide_r2 = std::nextafter(r2, INFINITY) * 1.0001f;
+    for (size_t i = 0; i < vox.size(); i++) {
+        tree.radius(vox[i], r2, a);
+        flann.radius(vox[i], r2, b);
+        if (a != b) stats[1]++;
+        size_t x = 0, y = 0;   // both sorted by (dist, index)
+        while (x < a.size() || y < b.size()) {
+            if (y == b.size() || (x < a.size() && a[x] < b[y])) { stats[2]++; x++; }
+            else if (x == a.size() || b[y] < a[x]) { stats[3]++; y++; }
+            else { x++; y++; }
+        }
+        tree.radius(vox[i], wide_r2, wide);   // candidates just past r2 too
+        for (const auto& pr : wide) {
+            if ((size_t)pr.second <= i) continue;   // unordered pairs, no self pair
+            uint32_t ab;
+            std::memcpy(&ab, &pr.first, 4);
+            const uint32_t ulps = ab > r2b ? ab - r2b : r2b - ab;   // (both positive floats)
+            if (ulps <= 4) {
+                stats[4]++;
+                if (pr.first < r2) stats[5]++;
+            }
+            if (pr.first < r2 && ulps < stats[9]) stats[9] = ulps;
+        }
+    }
+    const auto ce = euclidean_clusters(vox, tol, (unsigned)prm.min_cluster_size, (unsigned)prm.max_cluster_size,
+                                       SEARCH_EXACT);
+    const auto cf = euclidean_clusters(vox, tol, (unsigned)prm.min_cluster_size, (unsigned)prm.max_cluster_size,
+                                       SEARCH_FLANN);
+    stats[6] = ce == cf ? 1u : 0u;
+    stats[7] = (uint32_t)ce.size();
+    stats[8] = (uint32_t)cf.size();
+    return 0;
+}
+
+// FLANN's radius search alone on n points (xyz float triples) for every point as the query:
+// out_counts[i] = its neighbour count, out_idx the neighbours (sorted by (dist, index)) up to
+// cap in all. Returns the total. (tests: the restatement against brute force.)
+uint32_t oracle_flann_radius_all(const float* xyz, uint32_t n, float r2, uint32_t* out_counts, int32_t* out_idx,
+                                 uint32_t cap) {
+    std::vector<Pt> c(n);
+    for (uint32_t i = 0; i < n; i++) { c[i].x = xyz[3 * i]; c[i].y = xyz[3 * i + 1]; c[i].z = xyz[3 * i + 2]; }
+    FlannIndex flann;
+    flann.build(c);
+    std::vector<std::pair<float, int>> res;
+    uint32_t tot = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        flann.radius(c[i], r2, res);
+        out_counts[i] = (uint32_t)res.size();
+        for (const auto& pr : res) {
+            if (tot < cap) out_idx[tot] = pr.second;
+            tot++;
+        }
+    }
+    return tot;
 }
 
 // Host libm probes for the device-restatement checks.

@@ -22,6 +22,13 @@ def lib():
         _lib = C.CDLL(ORACLE_SO)
         _lib.oracle_run.restype = C.c_int
         _lib.oracle_run.argtypes = [C.c_void_p] * 2 + [C.c_int, C.c_int] + [C.c_void_p] * 7
+        _lib.oracle_run_search.restype = C.c_int
+        _lib.oracle_run_search.argtypes = [C.c_void_p] * 2 + [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 7
+        _lib.oracle_flann_check.restype = C.c_int
+        _lib.oracle_flann_check.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        _lib.oracle_flann_radius_all.restype = C.c_uint32
+        _lib.oracle_flann_radius_all.argtypes = [C.c_void_p, C.c_uint32, C.c_float, C.c_void_p, C.c_void_p,
+                                                 C.c_uint32]
         _lib.oracle_atan2f.restype = C.c_float
         _lib.oracle_atan2f.argtypes = [C.c_float, C.c_float]
         _lib.oracle_sector.restype = C.c_int
@@ -112,10 +119,43 @@ def server(crops, classify):
     return [int(classify(c)) for c in crops if len(c)]
 
 
-def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_PCL, intensity_offset=None):
+SEARCH_EXACT, SEARCH_FLANN = 0, 1
+FLANN_STATS = ("voxels", "queries_differ", "pairs_missed", "pairs_extra", "near_tolerance_pairs",
+               "near_tolerance_inside", "clusters_equal", "clusters_exact", "clusters_flann", "closest_inside_ulps")
+
+
+def flann_check(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_PCL, intensity_offset=None) -> dict:
+    """oracle_flann_check on one cloud: FLANN 1.9.1's own tree and search (restated) against the
+    exact radius predicate, for every voxel as a query, and both clusterings."""
+    v = msg.view(intensity_offset=intensity_offset)
+    st = np.zeros(10, np.uint32)
+    lib().oracle_flann_check(C.addressof(params), C.addressof(v), mode, order, st.ctypes.data)
+    return dict(zip(FLANN_STATS, (int(x) for x in st)))
+
+
+def flann_radius_all(xyz, r2):
+    """FLANN's radius search (restated) with every point of xyz (n, 3) as the query: a list of
+    neighbour index arrays, each sorted by (distance, index)."""
+    xyz = np.ascontiguousarray(np.asarray(xyz, np.float32).reshape(-1, 3))
+    n = xyz.shape[0]
+    counts = np.zeros(max(n, 1), np.uint32)
+    cap = max(64 * n, 1)
+    while True:
+        idx = np.zeros(cap, np.int32)
+        tot = lib().oracle_flann_radius_all(xyz.ctypes.data, n, float(r2), counts.ctypes.data, idx.ctypes.data, cap)
+        if tot <= cap:
+            break
+        cap = int(tot)
+    offs = np.concatenate([[0], np.cumsum(counts[:n])]).astype(np.int64)
+    return [idx[offs[i]:offs[i + 1]].copy() for i in range(n)]
+
+
+def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_PCL, intensity_offset=None, search=SEARCH_EXACT):
     """Run the restatement on one cloud; returns (Detection or ground bytes, header). order:
     ORDER_PCL (default) sums each voxel in PCL's std::sort order, as the reference and the device
-    do; ORDER_STABLE in ascending point order (the numpy restatement's and the halo form's)."""
+    do; ORDER_STABLE in ascending point order (the numpy restatement's and the halo form's).
+    search: SEARCH_EXACT (default) clusters with the exact L2_Simple radius predicate,
+    SEARCH_FLANN with FLANN 1.9.1's own tree and pruning (restated)."""
     n = msg.width * msg.height
     v = msg.view(intensity_offset=intensity_offset)
     cap = max(n, 1)
@@ -126,9 +166,9 @@ def run(params, msg: PointCloud2, mode=MODE_PIPELINE, order=ORDER_PCL, intensity
     offs = np.zeros(cap + 1, np.int32)
     idx = np.zeros(cap, np.int32)
     cen = np.zeros(cap * 2, np.float32)
-    lib().oracle_run(C.addressof(params), C.addressof(v), mode, order, hdr.ctypes.data,
-                     ground.ctypes.data, vox.ctypes.data, lab.ctypes.data, offs.ctypes.data,
-                     idx.ctypes.data, cen.ctypes.data)
+    lib().oracle_run_search(C.addressof(params), C.addressof(v), mode, order, search, hdr.ctypes.data,
+                            ground.ctypes.data, vox.ctypes.data, lab.ctypes.data, offs.ctypes.data,
+                            idx.ctypes.data, cen.ctypes.data)
     if mode == MODE_GROUND:
         return ground[: n * 8].view(np.uint8).copy(), hdr
     V, Cn = int(hdr[3]), int(hdr[4])
