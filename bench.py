@@ -171,10 +171,10 @@ def main():
     timed = queue(args.steps)
     # each timed launch stamps its own execution span (first workgroup start, last workgroup
     # end: what rocprofv3's kernel trace reports); armed per engine before the region
-    spans = torch.zeros((args.steps, 2), dtype=torch.int64, device=dev)
+    spans = torch.zeros((args.steps, SPAN_WORDS), dtype=torch.int64, device=dev)
     spans[:, 0] = 2 ** 63 - 1
     per_eng = [list(range(k, args.steps, S)) for k in range(S)]
-    span_bufs = [torch.zeros((max(1, len(ix)), 2), dtype=torch.int64, device=dev) for ix in per_eng]
+    span_bufs = [torch.zeros((max(1, len(ix)), SPAN_WORDS), dtype=torch.int64, device=dev) for ix in per_eng]
     for k in range(S):
         span_bufs[k][:, 0] = 2 ** 63 - 1
     torch.cuda.synchronize(dev)
@@ -291,6 +291,10 @@ def main():
             pcie = pcie_inclusive(raw, d_ins, engines, streams, F, N, dev)
         except Exception as e:  # noqa: BLE001
             pcie = {"error": repr(e)}
+    elif world > 1 and not args.no_scatter:
+        # C4's ingest that scales: every rank copies its own pinned host batch over its own
+        # PCIe link (no root), processes it, max over ranks
+        pcie = per_rank_ingest(cd, raw, d_ins, engines, streams, F, N, dev, rank, world)
     colornet = None
     if args.colornet and rank == 0:
         colornet = colornet_service(cp, params, raw, local)
@@ -339,6 +343,7 @@ def main():
                                                   if avg_event_ms is not None else
                                                   "in-kernel span (s_memrealtime) of the timed launches"),
                          "step_span_ms": step_span_ms,
+                         "shader_clock_mhz": shader_clock_mhz(sp) if spans_ok else None,
                          "step_span_ms_max": float((sp[:, 1] - sp[:, 0]).max()) * 1e-5 if spans_ok else None,
                          "step_span_frac": bytes_per_launch / (step_span_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                          "avg_launch_ms_events": avg_event_ms,
@@ -361,7 +366,7 @@ def main():
         if colornet is not None:
             line["colornet"] = colornet
         if pcie is not None:
-            line["pcie_inclusive"] = pcie
+            line["pcie_inclusive" if world == 1 else "c4_per_rank_ingest"] = pcie
         if c5 is not None:
             line["c5_single_gpu"] = {k: v for k, v in c5.items() if not k.startswith("_")}
         if c5t is not None:
@@ -421,7 +426,7 @@ def sustained_pass(args, world, dev, engines, queue, S, F, N):
     K = args.sustained_steps
     q = queue(K)
     per_eng = [list(range(k, K, S)) for k in range(S)]
-    bufs = [torch.zeros((max(1, len(ix)), 2), dtype=torch.int64, device=dev) for ix in per_eng]
+    bufs = [torch.zeros((max(1, len(ix)), SPAN_WORDS), dtype=torch.int64, device=dev) for ix in per_eng]
     for b in bufs:
         b[:, 0] = 2 ** 63 - 1
     torch.cuda.synchronize(dev)
@@ -436,7 +441,7 @@ def sustained_pass(args, world, dev, engines, queue, S, F, N):
     if world > 1:
         dist.barrier()
     el = cd.max_over_ranks(time.perf_counter() - t0, dev)
-    sp = np.zeros((K, 2), np.int64)
+    sp = np.zeros((K, SPAN_WORDS), np.int64)
     for k in range(S):
         if per_eng[k]:
             sp[per_eng[k]] = bufs[k][: len(per_eng[k])].cpu().numpy()
@@ -454,17 +459,25 @@ def sustained_pass(args, world, dev, engines, queue, S, F, N):
         ext = (sp[ix, 1].max() - sp[ix, 0].min()) * 1e-5
         quarters.append({"launches": [int(ix[0]), int(ix[-1])],
                          "span_ms_mean": float(dur[ix].mean()),
+                         "shader_clock_mhz": shader_clock_mhz(sp[ix]),
                          "overlap_depth": float(dur[ix].sum() / ext),
                          "ms_per_step": float(ext / ix.size),
                          "aggregate_frac": B * ix.size / (ext * 1e-3) / 1e9 / HBM_PEAK_GBS})
     d0, d3 = quarters[0], quarters[-1]
     drift = d3["span_ms_mean"] / d0["span_ms_mean"] - 1.0
+    clk = (d3["shader_clock_mhz"] / d0["shader_clock_mhz"] - 1.0) if d0["shader_clock_mhz"] else None
     deeper = d3["overlap_depth"] / d0["overlap_depth"] - 1.0
     pace = d3["ms_per_step"] / d0["ms_per_step"] - 1.0
     if abs(pace) < 0.03:
         finding = "steady: last quarter's step time within 3% of the first's"
+    elif clk is not None and clk < -0.02 and drift > 0.02:
+        finding = (f"the shader clock falls {-clk * 100:.1f}% from the first quarter to the last "
+                   f"({d0['shader_clock_mhz']:.0f} -> {d3['shader_clock_mhz']:.0f} MHz, s_memtime / s_memrealtime "
+                   f"of every workgroup) while per-launch spans grow {drift * 100:.1f}%")
     elif drift > 0.03 and abs(deeper) < 0.03:
-        finding = "per-launch duration drifts upward at equal overlap (clock / power)"
+        finding = ("per-launch duration drifts upward at equal overlap and the shader clock holds "
+                   f"({clk * 100:+.1f}%): not the clock" if clk is not None else
+                   "per-launch duration drifts upward at equal overlap")
     elif deeper > 0.03:
         finding = "overlap depth grows (launches queue behind each other)"
     else:
@@ -475,9 +488,20 @@ def sustained_pass(args, world, dev, engines, queue, S, F, N):
             "span_ms_max": float(dur.max()),
             "span_frac": B / (float(dur.mean()) * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "quarters": quarters, "span_drift_last_vs_first": drift, "overlap_growth_last_vs_first": deeper,
-            "step_time_change_last_vs_first": pace, "finding": finding,
+            "step_time_change_last_vs_first": pace, "shader_clock_change_last_vs_first": clk,
+            "shader_clock_mhz": shader_clock_mhz(sp), "finding": finding,
             "includes": f"one more cg_run_batches call of {K} steps after the timed region (same engines, "
                         "inputs and stream rotation), in-kernel spans of every launch"}
+
+
+SPAN_WORDS = 4   # cg_debug_launch_spans (include/cones_gpu_debug.h CG_SPAN_WORDS)
+
+
+def shader_clock_mhz(sp):
+    """The shader clock of launches from their span records: every workgroup's s_memtime cycles
+    over its s_memrealtime ticks (100 MHz), summed over the launches' workgroups."""
+    ticks = float(sp[:, 3].sum())
+    return float(sp[:, 2].sum()) / ticks * 100.0 if ticks > 0 else None
 
 
 def free_port():
@@ -882,6 +906,39 @@ def pcie_inclusive(raw, d_ins, engines, streams, F, N, dev, steps=12):
     dt = (time.perf_counter() - t0) / steps
     return {"frames_per_s": F / dt, "ms_per_step": dt * 1e3, "h2d_GBs": raw.nbytes / dt / 1e9,
             "includes": "pinned host batch -> device copy (PCIe) + processing per step, 3 streams"}
+
+
+def per_rank_ingest(cd, raw, d_ins, engines, streams, F, N, dev, rank, world, steps=12):
+    """C4 with the frames arriving on every rank's host (each GPU's own sensor feed): each rank
+    copies its own pinned batch over its own PCIe link and processes it, pcie_inclusive's loop
+    on every rank at once. Timed like the main loop (barrier + sync, max over ranks). The root
+    scatter (c4_scatter_gather) sends (N - 1) batches out of one GPU per step; this leg moves no
+    frame between GPUs, so it scales with the ranks' PCIe links."""
+    import torch
+    import torch.distributed as dist
+    host = torch.from_numpy(raw).pin_memory()
+    S = len(streams)
+
+    def step(i):
+        with torch.cuda.stream(streams[i % S]):
+            d_ins[i % S].copy_(host, non_blocking=True)
+        engines[i % S].run(d_ins[i % S].data_ptr(), F, N, 16, stream=streams[i % S].cuda_stream)
+
+    for i in range(2 * S):
+        step(i)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    el = cd.max_over_ranks(time.perf_counter() - t0, dev)
+    dt = el / steps
+    return {"frames_per_s": F * world / dt, "ms_per_step": dt * 1e3, "ranks": world,
+            "h2d_GBs_per_rank": raw.nbytes / dt / 1e9, "h2d_GBs_total": raw.nbytes * world / dt / 1e9,
+            "includes": "every rank: its own pinned host batch -> its device (PCIe) + processing per step, "
+                        f"{S} streams; max over ranks; no frame crosses GPUs"}
 
 
 def colornet_service(cp, params, raw, device, frames=16, reps=50):

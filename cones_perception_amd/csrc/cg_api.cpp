@@ -10,8 +10,14 @@
 #include <cstdio>
 #include <chrono>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+#include <immintrin.h>
 #include "../../include/cones_gpu_debug.h"
 #include "cg_internal.h"
 #include "cg_math.h"
@@ -40,6 +46,73 @@ int prepare(const cg_params& p, CgDevParams& d) { return cg_prepare_params(p, d)
 
 }  // namespace
 
+// Host helper threads for the single-frame staging copy (C2). The split launch's chunk
+// workgroups each wait for their chunk of the message to be copied into pinned memory and
+// published; one thread publishing 16 chunks of 64 KiB one after another took 15.5 us, and the
+// GPU's PCIe reads of the last chunks waited for it (profiles/r5_c2_stamps.txt). The pool's
+// threads copy and publish interleaved chunks beside the calling thread (chunk c by part
+// c % parts; the caller is part 0), so every chunk is published within a few us of the launch.
+// Between calls a helper spins for CG_STAGE_SPIN_US (the node's next frame usually comes within
+// it when frames queue), then sleeps on a condition variable. CG_STAGE_THREADS sets the helper
+// count (default 3; 0: the caller copies every chunk, as before).
+struct StagePool {
+    std::vector<std::thread> th;
+    std::atomic<uint32_t> job{0};       // the current job's number (helpers start when it changes)
+    std::atomic<uint32_t> left{0};      // helpers still copying the current job
+    std::atomic<int> sleepers{0};
+    std::atomic<bool> quit{false};
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t spin_ns = 2000000;
+    // the current job (written before `job` is released)
+    const uint8_t* src = nullptr;
+    uint8_t* dst = nullptr;
+    uint32_t* flags = nullptr;
+    uint32_t seq = 0, n = 0, step = 0, nch = 0, parts = 1;
+    bool copy = true;
+
+    void chunks(uint32_t part) const {
+        for (uint32_t c = part; c < nch; c += parts) {
+            if (copy && (uint64_t)c * CG_SPLIT_CHUNK < n) {
+                const size_t b0 = (size_t)c * CG_SPLIT_CHUNK * step;
+                const size_t nb = (size_t)std::min<uint32_t>(CG_SPLIT_CHUNK, n - c * CG_SPLIT_CHUNK) * step;
+                std::memcpy(dst + b0, src + b0, nb);
+            }
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);   // also orders a memcpy's non-temporal stores
+            __atomic_store_n(&flags[c], seq, __ATOMIC_RELEASE);
+        }
+    }
+    void worker(uint32_t part) {
+        uint32_t seen = 0;
+        for (;;) {
+            auto t0 = std::chrono::steady_clock::now();
+            while (job.load(std::memory_order_acquire) == seen && !quit.load(std::memory_order_relaxed)) {
+                _mm_pause();
+                if ((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                        .count() > spin_ns) {
+                    std::unique_lock<std::mutex> lk(mu);
+                    sleepers++;
+                    cv.wait(lk, [&] { return job.load(std::memory_order_acquire) != seen || quit.load(); });
+                    sleepers--;
+                    t0 = std::chrono::steady_clock::now();
+                }
+            }
+            if (quit.load()) return;
+            seen = job.load(std::memory_order_acquire);
+            chunks(part);
+            left.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    ~StagePool() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit.store(true);
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
 struct cg_handle {
     int device = 0;
     cg_params params{};
@@ -64,6 +137,8 @@ struct cg_handle {
     uint32_t* h_flags_dev = nullptr;
     uint32_t stage_seq = 0;
     size_t h_stage_bytes = 0;
+    StagePool* pool = nullptr;       // staging helper threads (created with the first split call)
+    bool pool_tried = false;
     // last batch
     uint32_t last_frames = 0, last_points = 0;
     int last_mode = -1;
@@ -333,7 +408,7 @@ int use_stream(cg_handle* h, hipStream_t s) {
 unsigned long long* take_span(cg_handle* h) {
     if (!h->spans_left) return nullptr;
     unsigned long long* p = h->next_span;
-    h->next_span += 2;
+    h->next_span += CG_SPAN_WORDS;
     h->spans_left--;
     return p;
 }
@@ -483,10 +558,44 @@ int fetch_frame(cg_handle* h, hipStream_t s, uint32_t frame, cg_detect_result* o
 // The staging buffer's chunks (CG_SPLIT_CHUNK points each): copied from the message (unless
 // `only_flags`: already staged) and published to the split kernel's chunk workgroups one by
 // one (release: the chunk's bytes before its word).
+StagePool* stage_pool(cg_handle* h) {
+    if (h->pool || h->pool_tried) return h->pool;
+    h->pool_tried = true;
+    const char* e = std::getenv("CG_STAGE_THREADS");
+    const int k = e ? std::atoi(e) : 3;
+    if (k <= 0) return nullptr;
+    StagePool* p = new StagePool();
+    p->parts = (uint32_t)std::min(k, 15) + 1u;
+    if (const char* sp = std::getenv("CG_STAGE_SPIN_US")) p->spin_ns = (uint64_t)std::atoll(sp) * 1000ull;
+    try {
+        for (uint32_t t = 1; t < p->parts; t++) p->th.emplace_back([p, t] { p->worker(t); });
+    } catch (...) {   // (no threads: the caller copies alone)
+        delete p;
+        return nullptr;
+    }
+    h->pool = p;
+    return p;
+}
+
 void publish_chunks(cg_handle* h, const cg_cloud_view* v, uint32_t n, uint32_t step, bool only_flags) {
     // every workgroup of the launch waits for its word: one even for an empty frame
     const uint32_t nch = std::max<uint32_t>(1, (n + CG_SPLIT_CHUNK - 1) / CG_SPLIT_CHUNK);
     const uint8_t* src = (const uint8_t*)v->data;
+    StagePool* pool = nch > 1 ? stage_pool(h) : nullptr;
+    if (pool) {   // interleaved chunks: helpers take parts 1.., the caller part 0
+        pool->src = src; pool->dst = h->h_stage; pool->flags = h->h_flags;
+        pool->seq = h->stage_seq; pool->n = n; pool->step = step; pool->nch = nch; pool->copy = !only_flags;
+        pool->left.store(pool->parts - 1, std::memory_order_relaxed);
+        pool->job.store(pool->job.load(std::memory_order_relaxed) + 1u, std::memory_order_release);
+        if (pool->sleepers.load() > 0) {
+            std::lock_guard<std::mutex> lk(pool->mu);
+            pool->cv.notify_all();
+        }
+        pool->chunks(0);
+        // the message is the caller's until the call returns: the helpers finish with it first
+        while (pool->left.load(std::memory_order_acquire)) _mm_pause();
+        return;
+    }
     for (uint32_t c = 0; c < nch; c++) {
         if (!only_flags && (uint64_t)c * CG_SPLIT_CHUNK < n) {
             const size_t b0 = (size_t)c * CG_SPLIT_CHUNK * step;
@@ -688,6 +797,7 @@ int cg_destroy(cg_handle* h) {
     if (h->d_boxes) (void)hipFree(h->d_boxes);
     if (h->d_rc_cnt) (void)hipFree(h->d_rc_cnt);
     if (h->d_rc_out) (void)hipFree(h->d_rc_out);
+    delete h->pool;   // (joins the helpers; none is copying: every call waits for its helpers)
     if (h->h_stage) (void)hipHostFree(h->h_stage);
     if (h->h_flags) (void)hipHostFree(h->h_flags);
     if (h->h_ground) (void)hipHostFree(h->h_ground);

@@ -91,7 +91,15 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
     const uint8_t* fb = L.in + (uint64_t)f * L.frame_stride;
     const uint32_t N = L.n_points;
     STAMP(0);
-    if (L.span && tid == 0) atomicMin(&L.span[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    // launch spans (cg_debug_launch_spans, CG_SPAN_WORDS per launch): the first workgroup's
+    // start, the last one's end, and every workgroup's shader cycles and real time, whose ratio
+    // is the clock the CUs held (s_memtime counts shader cycles, s_memrealtime 100 MHz ticks)
+    uint64_t span_c0 = 0, span_r0 = 0;
+    if (L.span && tid == 0) {
+        span_r0 = __builtin_amdgcn_s_memrealtime();
+        span_c0 = __builtin_amdgcn_s_memtime();
+        atomicMin(&L.span[0], (unsigned long long)span_r0);
+    }
 
     if (tid <= CG_NUM_BINS) fs->sec_key[tid] = cg_fkey(P.default_low);
     init_rays<FILTER>(P, fs->rays, tid);
@@ -580,7 +588,12 @@ __device__ __forceinline__ void frame_body(const CgLaunch& L, const CgDevParams&
             }
         }
     }
-    if (L.span && tid == 0) atomicMax(&L.span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (L.span && tid == 0) {
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        atomicMax(&L.span[1], (unsigned long long)r1);
+        atomicAdd(&L.span[2], (unsigned long long)(c1 - span_c0));
+        atomicAdd(&L.span[3], (unsigned long long)(r1 - span_r0));
+    }
 }
 
 // The kernels: the batch frame kernel (two workgroups per CU: <= 128 VGPRs); the single-frame

@@ -1257,6 +1257,8 @@ __device__ __forceinline__ void pq_push(const LgScratch& S, uint32_t which, uint
     if (i < LG_PQ_CAP) {
         uint32_t* e = pq_list(S, which) + PQ_EW * i;
         e[0] = first; e[1] = last; e[2] = depth; e[3] = w3;
+    } else {
+        S.meta[LG_PQ_TIMEOUT] = 1u;   // (a list overflowed: the frame's results are void, never expected)
     }
 }
 // The ranges of a level (level 0: the whole index_vector when it needs partitioning) and the
@@ -1741,6 +1743,67 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
     if (t0 == 0 && level < 7) CG_HOOK_LG_STAMP(S, 21 + 6 * level);
 }
 
+// ------------------------------------------------------------------------------------------
+// The device-sized frame's partition as ONE dataflow launch (lg_pq_flow), in place of one
+// lg_pq_level launch per level. Each range's split and swaps are the level kernel's (the same
+// median of three, >= / <= lists from a look-back segmented by range, swaps once a per-range
+// word shows every tile's lists); what changes is how ranges reach workgroups:
+//   - one queue of tickets for the whole sort. Tickets [0, T0) are the tiles of range 0 (the
+//     whole index_vector, implicit); every later ticket's entry is published by the workgroup
+//     that finished the range it belongs to, as soon as that range's swaps are stored. A range
+//     starts when its parent ends, not when the slowest range of a level ends, and there are no
+//     empty levels: the sort takes as many dependent range steps as its deepest range needs;
+//   - entries are 16 bytes, (first, last) and (budget | kind | depth | tile, first ticket of the
+//     range), both halves nonzero once written (last >= 1, budget >= 2), stored by two sc1
+//     stores and polled by two sc1 loads (a half not yet written reads 0);
+//   - a tile's workgroup keeps its split state in registers and runs the tile's swaps itself
+//     when every ticket of its range has been handed out (the ticket counter has passed them:
+//     every tile of the range is held by a running workgroup, which never waits on a later
+//     ticket). Otherwise it leaves its state in HBM (S.vox) and queues a swap entry for the
+//     tile at the end of the queue, whose holder waits for the range word instead;
+//   - a range's last tile to finish its swaps (one agent-scope count per range) reads the cut
+//     the cutter or'ed into the range's cut word and queues the children: ranges longer than
+//     LG_PCL_CUT with budget left as new tickets, the others on lg_pcl_leaf's list;
+//   - the launch ends when every range is finished: `pend` = ranges finished - ranges queued
+//     reaches 1 (range 0 is not queued; a range counts its end and its children in one add
+//     before the children are published). A workgroup whose ticket has no entry yet polls the
+//     entry and `pend` together and exits at 1.
+// Forward progress: a tile waits only on tickets below its own (look-back), or on a range all
+// of whose tickets are held; a workgroup without an entry waits on workgroups with lower
+// tickets. So the launch drains whatever the grid size and residency.
+// Visibility: every cross-workgroup byte (records, lists, swap state, entries, words) is stored
+// sc1 (st_rlx / st64 / agent-scope atomics) after which the storing waves wait vmcnt(0) before
+// the barrier and the one signalling add or entry store, and loaded sc1 (ld_rlx / ld64):
+// MI355X_MICROARCH.md's hand-off table, row 1. lg_pcl_leaf clears the used words and lg_pcl_mid
+// the counters, so the next frame finds them zero.
+#ifndef LG_FLOW_GRID
+#define LG_FLOW_GRID 512   // workgroups of the launch (two per CU)
+#endif
+#define LG_CLEAR_FLOW 0x100u   // lg_pcl_leaf's clear_set for lg_pq_flow's words
+#define PQF_HDR 8          // u64 words: [0] tickets handed out, [1] tickets queued past range 0's, [2] pend
+#define PQF_KIND_SWAP (1u << 7)
+struct PqfView {
+    uint64_t* hdr; uint64_t* ent; uint64_t* lb; uint64_t* rw; uint32_t* sd; uint32_t* cw; uint32_t cap;
+};
+__device__ __forceinline__ PqfView pqf_view(const LgScratch& S) {
+    PqfView v;
+    v.cap = S.pqf_cap;
+    v.hdr = S.pqf;
+    v.ent = S.pqf + PQF_HDR;      // two words per ticket
+    v.lb = v.ent + 2ull * v.cap;  // look-back status per ticket
+    v.rw = v.lb + v.cap;          // range word, by the range's first ticket
+    v.sd = (uint32_t*)(v.rw + v.cap);   // tiles whose swaps are stored, by first ticket
+    v.cw = v.sd + v.cap;          // cut + 1 (bit 31: a wait gave up), by first ticket
+    return v;
+}
+__device__ __forceinline__ uint32_t pqf_tiles(uint32_t f, uint32_t e) { return (e - f - 1 + PQ_T - 1) / PQ_T; }
+__device__ __forceinline__ uint32_t pqf_key(const uint64_t* E, uint32_t x) {
+    return ld_rlx((uint32_t*)E + 2ull * x + 1);
+}
+__device__ __forceinline__ void pqf_entry(const PqfView& Q, uint64_t k, uint32_t f, uint32_t e, uint32_t w2, uint32_t tb) {
+    st64(Q.ent + 2 * k, ((uint64_t)e << 32) | f);
+    st64(Q.ent + 2 * k + 1, ((uint64_t)tb << 32) | w2);
+}
 // A leaf's results straight to the outputs: idx in the key array, slot in the value array.
 struct PqLeafOut {
     uint64_t* k; uint32_t* v; uint32_t base;
@@ -1790,9 +1853,18 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
     const uint32_t n = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
     const uint32_t tid = threadIdx.x;
     // the split's ticket counter, also when no level followed the level-0 split (no swap);
-    // lg_pq_level's levels: the last level's set (clear_set = its parity + 1)
+    // lg_pq_level's levels: the last level's set (clear_set = its parity + 1); lg_pq_flow
+    // (clear_set = LG_CLEAR_FLOW): the words of every ticket it handed out, across the grid
+    // (lg_pcl_mid clears its counters after this launch)
     if (blockIdx.x == 0 && tid == 0 && !clear_set) S.pqst[0] = 0;
-    if (blockIdx.x == 0 && clear_set) {
+    if (clear_set == LG_CLEAR_FLOW) {
+        const PqfView Q = pqf_view(S);
+        const uint32_t used = (uint32_t)min(Q.hdr[0], (uint64_t)Q.cap);
+        for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < used; i += gridDim.x * CG_BLOCK) {
+            Q.ent[2ull * i] = 0ull; Q.ent[2ull * i + 1] = 0ull;
+            Q.lb[i] = 0ull; Q.rw[i] = 0ull; Q.sd[i] = 0u; Q.cw[i] = 0u;
+        }
+    } else if (blockIdx.x == 0 && clear_set) {
         pq_clear_set(S, clear_set - 1u);
         __syncthreads();
     }
@@ -1836,10 +1908,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
 // 17-64 records one wave each, in LDS too).
 #define LG_MID_LDS (8 * PQ_MID + 4 * 4 * (PQ_MID + 4))
 __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
-                                                       uint32_t* vout) {
+                                                       uint32_t* vout, uint32_t clear_flow = 0u) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[LG_MID_LDS];
     __shared__ uint32_t red[8 * WAVES];
     const uint32_t n = S.pq[PQ_MIDS];
+    if (clear_flow && blockIdx.x == 0 && threadIdx.x < PQF_HDR) S.pqf[threadIdx.x] = 0ull;   // (lg_pq_flow's counters)
     lds_u64* const El = (lds_u64*)(uint64_t*)smem;
     lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * PQ_MID);
     const PbScratch<PbLds> PS{w0, w0 + (PQ_MID + 4), w0 + 2 * (PQ_MID + 4), w0 + 3 * (PQ_MID + 4)};
@@ -1862,6 +1935,314 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
                                                             nullptr, wt);
     }
 }
+#define PQF_WAIT_TICKS PQ_WAIT_TICKS
+// (LEAVES) entry word 1's high half for a task: bit 31 a leaf or mid range, bit 30 a mid range
+// (first tickets are < 2^30)
+#define PQF_TASK 0x80000000u
+#define PQF_MID 0x40000000u
+// A leaf's ranges of 65-PQ_MID records as tasks of the same launch (lg_pcl_leaf's PqDefer
+// hands them to lg_pcl_mid instead): the wave writes the range's records back to the buffer
+// (sc1), counts the task into `pend` before publishing it, and queues its entry.
+struct PqfDefer {
+    uint64_t* Eh; PqfView Q; uint32_t base, w2, T0;
+    template <class P64, class OUT>
+    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
+        if (m <= PW_MAX) {
+            pw_range64(E, f, m, d, out);
+            return;
+        }
+        const uint32_t l = lane_id();
+        for (uint32_t i = l; i < m; i += 64) st64(Eh + base + f + i, E[f + i]);
+        __builtin_amdgcn_s_waitcnt(0x0070);
+        if (l == 0) {
+            __hip_atomic_fetch_add(&Q.hdr[2], (uint64_t)(int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t k = T0 + __hip_atomic_fetch_add(&Q.hdr[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(0x0070);   // (the count is performed before the entry)
+            if (k < Q.cap) pqf_entry(Q, k, base + f, base + f + m, (w2 & ~0x7fu) | d, PQF_TASK | PQF_MID);
+        }
+    }
+};
+// A leaf (at most LG_PCL_LEAF records) or a mid range (at most PQ_MID) of the flow: its records
+// from the buffer of its depth (sc1: written by this launch's swaps or a leaf's hand-back) into
+// LDS, pcl_block_sort to the end, results straight to the outputs (as lg_pcl_leaf and
+// lg_pcl_mid); then the task's end into `pend` (its mid tasks were counted when queued).
+__device__ __forceinline__ void pqf_leaf_task(const LgScratch& S, const PqfView& Q, unsigned char* pqf_smem, uint64_t* E,
+                                              uint32_t first, uint32_t size, uint32_t depth, uint32_t dpt, bool mid,
+                                              uint64_t* kout, uint32_t* vout) {
+    const uint32_t tid = threadIdx.x;
+    lds_u64* const El = (lds_u64*)(uint64_t*)pqf_smem;
+    const uint32_t cap = mid ? PQ_MID : LG_PCL_LEAF;
+    lds_u32* const w0 = (lds_u32*)(uint32_t*)(pqf_smem + 8 * LG_PCL_LEAF);
+    const PbScratch<PbLds> PS{w0, w0 + (cap + 4), w0 + 2 * (cap + 4), w0 + 3 * (cap + 4)};
+    lds_u32* const Rl = (lds_u32*)(uint32_t*)(pqf_smem + LG_PCL_LDS);
+    for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = ld64(E + first + i);
+    __syncthreads();
+    const PqLeafOut out{kout, vout, first};
+    if (mid) {
+        if (size <= CG_BLOCK) pcl_block_sort<1, PbLds, PqLeafOut>(El, out, size, depth, PS, Rl);
+        else pcl_block_sort<2, PbLds, PqLeafOut>(El, out, size, depth, PS, Rl);
+    } else {
+        const PqfDefer wt{E, Q, first, dpt << 8, pqf_tiles(0, S.meta[LG_PCL_N])};
+        if (size <= CG_BLOCK)
+            pcl_block_sort<1, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
+        else if (size <= 2 * CG_BLOCK)
+            pcl_block_sort<2, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
+        else if (size <= 4 * CG_BLOCK)
+            pcl_block_sort<4, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
+        else pcl_block_sort<8, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&Q.hdr[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool LEAVES>
+__global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap,
+                                                       uint64_t* kout, uint32_t* vout) {
+    __shared__ uint32_t cg[WAVES], cl[WAVES];
+    __shared__ uint64_t tbase;
+    __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the tile's decisions
+    __shared__ uint32_t ch[8];   // children: count, first ticket, their (first, last) and tiles
+    __shared__ __attribute__((aligned(16))) unsigned char smem[LEAVES ? LG_PCL_LDS + 8 * WAVES * 4 : 16];
+    const PqfView Q = pqf_view(S);
+    const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
+    const uint32_t n = S.meta[LG_PCL_N];
+    if (n <= LG_PCL_CUT) {   // nothing to cut: index_vector is one leaf
+        if (blockIdx.x == 0 && tid == 0) pq_push(S, PQ_LEAFLIST, 0, n, (uint32_t)(2 * cg_lg((long)n)), 0u);
+        return;
+    }
+    const uint32_t T0 = pqf_tiles(0, n);
+    const uint32_t d0 = (uint32_t)(2 * cg_lg((long)n));
+    uint64_t* const vst = (uint64_t*)S.vox;   // a deferred tile's per-element state: gi << 32 | li
+    for (;;) {
+        if (tid == 0) {   // the next ticket and its entry
+            const uint32_t t = (uint32_t)__hip_atomic_fetch_add(&Q.hdr[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t ok = 1, f = 0, e = n, w2 = d0 | (t << 16), tb = 0;   // (range 0: budget d0, depth 0, tile t)
+            if (t >= T0) {
+                if (t >= Q.cap) {
+                    ok = 0;   // (past every ticket the sort can queue: nothing will be published here)
+                } else {
+                    const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+                    for (;;) {
+                        const uint64_t a = ld64(Q.ent + 2ull * t), b = ld64(Q.ent + 2ull * t + 1);
+                        const int64_t pend = (int64_t)ld64(&Q.hdr[2]);
+                        if (a && b) {
+                            f = (uint32_t)a; e = (uint32_t)(a >> 32); w2 = (uint32_t)b; tb = (uint32_t)(b >> 32);
+                            break;
+                        }
+                        if (pend == 1) { ok = 0; break; }   // every range finished
+                        if (__builtin_amdgcn_s_memrealtime() - t_0 > PQF_WAIT_TICKS) {   // (never expected)
+                            S.meta[LG_PQ_TIMEOUT] = 1u;
+                            ok = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+            }
+            es[0] = ok; es[1] = f; es[2] = e; es[3] = w2; es[4] = tb; es[5] = t;
+        }
+        __syncthreads();
+        if (!es[0]) return;
+        const uint32_t f = es[1], e = es[2], w2 = es[3], tb = es[4], t = es[5];
+        const uint32_t d = w2 & 0x7fu, depth = (w2 >> 8) & 0xffu;
+        if constexpr (LEAVES) {
+            if (tb & PQF_TASK) {   // (uniform) a leaf or a mid range: sorted to the end here
+                pqf_leaf_task(S, Q, smem, (depth & 1u) ? E1 : E0, f, e - f, d, depth, (tb & PQF_MID) != 0, kout, vout);
+                continue;
+            }
+        }
+        const bool swap_entry = (w2 & PQF_KIND_SWAP) != 0;
+        const uint32_t q = swap_entry ? (w2 >> 16) : t - tb;
+        const uint32_t T = pqf_tiles(f, e);
+        const uint64_t* const E = (depth & 1u) ? E1 : E0;
+        uint64_t* const Eo = (depth & 1u) ? E0 : E1;
+        // the median of three and this element's record in one batch of loads: x > f, and x's
+        // virtual record is E[f] when x is the median (__move_median_to_first's swap)
+        const uint32_t x = f + 1 + q * PQ_T + tid;
+        const bool valid = x < e;
+        const uint32_t a = f + 1, b = f + (e - f) / 2, c = e - 1;
+        const uint32_t ka = pqf_key(E, a), kb = pqf_key(E, b), kc = pqf_key(E, c);
+        const uint64_t rf = ld64((uint64_t*)E + f);
+        const uint64_t rx = ld64((uint64_t*)E + (valid ? x : f));   // (clamped: no branch between the loads)
+        const uint32_t m = pb_median(a, b, c, ka, kb, kc);
+        const uint32_t p = m == a ? ka : (m == b ? kb : kc);
+        uint32_t gi = 0, li = 0;
+        if (!swap_entry) {
+            // split: >= / <= counts, the range's look-back over its tiles' tickets, the lists
+            const uint32_t k = valid ? (x == m ? pcl_key(rf) : pcl_key(rx)) : 0u;
+            const bool ge = valid && k >= p, le = valid && k <= p;
+            const uint64_t gm = __ballot(ge), lm = __ballot(le);
+            if (l == 0) { cg[w] = (uint32_t)__popcll(gm); cl[w] = (uint32_t)__popcll(lm); }
+            __syncthreads();
+            uint32_t tg = 0, tl = 0;
+            for (uint32_t v = 0; v < WAVES; v++) { tg += cg[v]; tl += cl[v]; }
+            if (w == 0) {
+                const uint64_t bs = pq_lookback(Q.lb, tb, t, ((uint64_t)tg << 32) | tl);
+                if (l == 0) tbase = bs;
+            }
+            __syncthreads();
+            gi = (uint32_t)(tbase >> 32) + mbcnt(gm);
+            li = (uint32_t)tbase + mbcnt(lm);
+            for (uint32_t v = 0; v < w; v++) { gi += cg[v]; li += cl[v]; }
+            if (ge) st_rlx(S.par + f + 1 + gi, x);
+            if (le) st_rlx(S.cnt + f + 1 + li, x);
+            __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): the lists are stored
+            __syncthreads();
+            if (tid == 0) {
+                __hip_atomic_fetch_add(&Q.rw[tb], PQ_RW_TILE | ((uint64_t)tg << 23) | tl, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                // the swaps here only when every ticket of the range is held (or done)
+                es[6] = ld64(&Q.hdr[0]) >= (uint64_t)tb + T ? 1u : 0u;
+            }
+            __syncthreads();
+            if (!es[6]) {   // defer: the state to HBM, a swap entry at the end of the queue
+                if (valid) st64(vst + x, ((uint64_t)gi << 32) | li);
+                __builtin_amdgcn_s_waitcnt(0x0070);
+                __syncthreads();
+                if (tid == 0) {
+                    const uint64_t kq = T0 + __hip_atomic_fetch_add(&Q.hdr[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (kq < Q.cap) pqf_entry(Q, kq, f, e, (w2 & 0xffffu) | PQF_KIND_SWAP | (q << 16), tb);
+                    else S.meta[LG_PQ_TIMEOUT] = 1u;   // (the capacity bounds every queue: never expected)
+                }
+                __syncthreads();
+                continue;
+            }
+        } else if (valid) {   // a deferred tile: its split state
+            const uint64_t rk = ld64(vst + x);
+            gi = (uint32_t)(rk >> 32);
+            li = (uint32_t)rk;
+        }
+        // swaps: once the range word counts every tile, it holds the range's totals
+        if (tid == 0) {
+            const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+            uint64_t wv = 0;
+            // route 10 (tests) takes the expired path itself on range 0: no wait at all
+            while (!(tb == 0 && S.force_wait_fail) && ((wv = ld64(&Q.rw[tb])) >> 46) < T) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t_0 > PQF_WAIT_TICKS) break;   // (never expected)
+            }
+            if ((wv >> 46) < T) S.meta[LG_PQ_TIMEOUT] = 1u;   // (the frame's fetch fails on it)
+            tbase = wv;
+        }
+        __syncthreads();
+        const uint64_t rw = tbase;
+        if ((rw >> 46) < T) {   // (uniform) the wait gave up: the range's totals and lists are
+            // partial, so no list entry is read. The tile's records go out unchanged, the range's
+            // first tile queues the whole range as one leaf and the range queues no children:
+            // every later index stays inside [f, e); the frame's results are void.
+            if (valid) st64(Eo + x, rx);
+            if (q == 0 && tid == 0) {
+                st64(Eo + f, rf);
+                pq_push(S, PQ_LEAFLIST, f, e, d - 1u, (depth + 1u) & 1u);
+            }
+            if (tid == 0) atomicOr(&Q.cw[tb], 0x80000000u);
+        } else {
+            const uint32_t nL = (uint32_t)(rw >> 23) & (uint32_t)PQ_RW_N, nR = (uint32_t)rw & (uint32_t)PQ_RW_N;
+            if (q == 0 && tid == 0) st64(Eo + f, ld64((uint64_t*)E + m));
+            if (valid) {
+                const uint64_t vx = x == m ? rf : rx;
+                const uint32_t k = pcl_key(vx);
+                const bool ge = k >= p, le = k <= p;
+                // the partners and the next pair in one batch of loads (indices clamped when unused)
+                const bool hasL = ge && gi < nR;
+                const bool nx = hasL && gi + 1 < min(nL, nR);
+                const uint32_t ri = nR - 1 - li;
+                const bool hasR = le && ri < nL;
+                const uint32_t jj = ld_rlx(S.cnt + f + 1 + (hasL ? nR - 1 - gi : 0u));   // R_gi
+                const uint32_t l2 = ld_rlx(S.par + f + 1 + (gi + 1 < nL ? gi + 1 : 0u));  // L_gi+1
+                const uint32_t r2 = ld_rlx(S.cnt + f + 1 + (nx ? nR - 2 - gi : 0u));      // R_gi+1
+                const uint32_t il = ld_rlx(S.par + f + 1 + (hasR ? ri : 0u));             // L_ri
+                uint32_t partner = x;
+                bool cutter = false;
+                uint32_t cut = 0;
+                if (hasL) {
+                    if (x < jj) {
+                        partner = jj;
+                        if (!nx || !(l2 < r2)) {   // swap gi is the last: s = gi + 1
+                            cutter = true;
+                            cut = min(gi + 1 < nL ? l2 : 0xffffffffu, jj);
+                        }
+                    } else if (gi == 0) {   // no swap at all: the left scan stops at L_0
+                        cutter = true;
+                        cut = x;
+                    }
+                }
+                if (hasR && il < x) partner = il;
+                partner = min(max(partner, f), e - 1u);   // (defensive: list entries lie in (f, e))
+                st64(Eo + x, partner == x ? vx : (partner == m ? rf : ld64((uint64_t*)E + partner)));
+                if (cutter) atomicOr(&Q.cw[tb], min(max(cut, f), e) + 1u);
+            }
+        }
+        // the tile's swaps are stored; the range's last tile queues the children
+        __builtin_amdgcn_s_waitcnt(0x0070);
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t done = __hip_atomic_fetch_add(&Q.sd[tb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t nch = 0, nt = 0, first = 0;
+            if (done == T - 1u) {
+                const uint32_t cw = ld_rlx(&Q.cw[tb]);
+                const uint32_t cut = (cw & 0x7fffffffu) - 1u;
+                if (!(cw >> 31) && (cw & 0x7fffffffu)) {
+                    const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
+                    uint32_t tc[2] = {0, 0};
+                    bool rng[2];
+                    bool lf[2] = {false, false};
+                    for (int cc = 0; cc < 2; cc++) {
+                        rng[cc] = hi[cc] - lo[cc] > LG_PCL_CUT && d > 1 && !(depth_cap && depth + 1u >= depth_cap);
+                        if (rng[cc]) tc[cc] = pqf_tiles(lo[cc], hi[cc]);
+                        // (LEAVES) a leaf that fits LDS becomes a task of this launch: one ticket
+                        lf[cc] = LEAVES && !rng[cc] && hi[cc] > lo[cc] && hi[cc] - lo[cc] <= LG_PCL_LEAF;
+                        if (lf[cc]) tc[cc] = 1u;
+                    }
+                    if (tc[0] + tc[1]) {
+                        first = T0 + (uint32_t)__hip_atomic_fetch_add(&Q.hdr[1], (uint64_t)(tc[0] + tc[1]), __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT);
+                        if ((uint64_t)first + tc[0] + tc[1] > Q.cap) {   // (never expected) the leaves finish them in HBM
+                            rng[0] = rng[1] = lf[0] = lf[1] = false;
+                            tc[0] = tc[1] = 0;
+                        }
+                    }
+                    for (int cc = 0; cc < 2; cc++) {
+                        if (rng[cc] || lf[cc]) {
+                            ch[2 + 2 * nch] = lo[cc]; ch[3 + 2 * nch] = hi[cc] | (lf[cc] ? 0x80000000u : 0u);
+                            ch[6 + nch] = tc[cc];
+                            nch++;
+                        } else {
+                            pq_push(S, PQ_LEAFLIST, lo[cc], hi[cc], d - 1u, (depth + 1u) & 1u);
+                        }
+                    }
+                    nt = tc[0] + tc[1];
+                } else if (!(cw >> 31)) {
+                    S.meta[LG_PQ_TIMEOUT] = 1u;   // (no cut stored: never expected)
+                }
+                // the range's end and its queued children in one count, performed before any
+                // child is published: `pend` cannot read 1 while a child is outstanding (a child
+                // that finished before this count would otherwise let waiting workgroups leave
+                // with tickets the grandchildren are then queued on)
+                __hip_atomic_fetch_add(&Q.hdr[2], (uint64_t)(int64_t)(1 - (int)nch), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_waitcnt(0x0070);
+            }
+            ch[0] = nch; ch[1] = first; es[7] = nt;
+            if (done == T - 1u) ch[5] = 1u; else ch[5] = 0u;
+        }
+        __syncthreads();
+        if (ch[5]) {   // (uniform) this workgroup finished the range
+            const uint32_t nch = ch[0], first = ch[1], nt = es[7];
+            const uint32_t w2c = (d - 1u) | ((depth + 1u) << 8);
+            for (uint32_t i = tid; i < nt; i += CG_BLOCK) {
+                const uint32_t cc = (nch == 2 && i >= ch[6]) ? 1u : 0u;
+                const uint32_t fb = first + (cc ? ch[6] : 0u);   // the child's first ticket
+                const uint32_t hi = ch[3 + 2 * cc];
+                if (hi >> 31)   // a leaf task (its budget and depth; the buffer is the depth's)
+                    pqf_entry(Q, first + i, ch[2 + 2 * cc], hi & 0x7fffffffu, w2c, PQF_TASK);
+                else
+                    pqf_entry(Q, first + i, ch[2 + 2 * cc], hi, w2c | ((first + i - fb) << 16), fb);
+            }
+        }
+        __syncthreads();   // (es and ch are rewritten for the next ticket)
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Euclidean clustering over the V voxels (FLANN L2_Simple predicate, PCL's seed = the lowest
 // index of each component):
@@ -2979,10 +3360,31 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     // frame's N (levels with no range return at once)
     hipLaunchKernelGGL(lg_pcl_index, dim3(std::max<uint32_t>(1, (nmax + LG_IDX_TILE - 1) / LG_IDX_TILE)), dim3(CG_BLOCK), 0,
                        s, S, P, kb[1]);
-    // one launch per level (lg_pq_level); a level's tiles number at most tb + its ranges (<= 2^lv),
-    // taken by at most 512 workgroups (more when a workgroup would hold more than PQ_OWN tiles)
-    // (level 0 always runs: with no level to cut it queues the whole index_vector as a leaf)
     const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
+#ifndef LG_PQ_MODE
+#define LG_PQ_MODE 0   // 0: one launch per partition level; 1: lg_pq_flow; 2: lg_pq_flow with the leaves
+#endif
+#if LG_PQ_MODE != 0
+    // the partition as one dataflow launch (lg_pq_flow): depth-0 records in kb[1], parity 1 in
+    // kb[0]; route 5's level cap as a depth cap
+    (void)levels;
+#if LG_PQ_MODE == 2
+    // (leaves and mid ranges sorted inside the launch: one workgroup per CU for the leaves' LDS)
+    hipLaunchKernelGGL(lg_pq_flow<true>, dim3(std::min<uint32_t>(256, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
+                       S.pcl_levels_cap, kb[0], vb2[0]);
+#else
+    hipLaunchKernelGGL(lg_pq_flow<false>, dim3(std::min<uint32_t>(LG_FLOW_GRID, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1],
+                       kb[0], S.pcl_levels_cap, kb[0], vb2[0]);
+#endif
+    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0, s, S,
+                       kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
+    hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
+                       kb[0], vb2[0], 1u);
+#else
+    // one launch per level (lg_pq_level); a level's tiles
+    // number at most tb + its ranges (<= 2^lv), taken by at most 512 workgroups (more when a
+    // workgroup would hold more than PQ_OWN tiles) (level 0 always runs: with no level to cut
+    // it queues the whole index_vector as a leaf)
     levels = std::max<uint32_t>(levels, 1);
     for (uint32_t lv = 0; lv < levels; lv++) {
         uint64_t* const Ein = lv % 2 ? kb[0] : kb[1];
@@ -2994,7 +3396,8 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, (2u << levels) + 1)), dim3(CG_BLOCK), 0, s, S, kb[1],
                        kb[0], kb[0], vb2[0], ((levels - 1) & 1u) + 1u);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
-                       kb[0], vb2[0]);
+                       kb[0], vb2[0], 0u);
+#endif
     // voxel runs over the finite points (LG_SCAN_N; every point if passthrough), centroids
     scan_emit<LG_IDX_PER>(S, nmax, LG_SCAN_N, VoxelHead{S.key0, S.meta, 0u}, VoxelEmit{S.run}, LG_V, s);
     hipLaunchKernelGGL(lg_voxel_centroids, dim3(lg_wave_blocks(nmax)), dim3(CG_BLOCK), 0, s, Lh, S, f, nmax, 0);
@@ -3166,6 +3569,14 @@ int cg_run_large(const CgLaunch& L, const CgDevParams& P, int kmode, LgScratch S
 namespace {
 
 uint64_t lg_pq_tmax(uint64_t n) { return (n + PQ_T - 1) / PQ_T + PQ_MAXR; }
+// lg_pq_flow's tickets for index_vectors of up to n records: ranges of one depth are disjoint and
+// longer than LG_PCL_CUT, so a depth holds at most n / PQ_T + n / LG_PCL_CUT + 1 tiles; the
+// budget bounds the depth by 2 lg n; every tile at most twice (split, and a deferred swap)
+uint64_t lg_pqf_cap(uint64_t n) {
+    uint64_t lg = 0;
+    while ((2ull << lg) <= n) lg++;
+    return 2 * (2 * lg + 2) * (n / PQ_T + n / LG_PCL_CUT + 2) + 1024;
+}
 template <class F>
 uint64_t lg_walk(uint32_t n, F place) {
     const uint64_t N = std::max<uint32_t>(n, 1), nch = (N + LG_CHUNK - 1) / LG_CHUNK;
@@ -3189,6 +3600,7 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(30, take((LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP) * 4));   // PCL sort range lists
     // their look-back words: two sets (tickets, finished, one per tile) and the range counts
     place(31, take((2 * (2 + lg_pq_tmax(N)) + 2 * PQ_MAXR + 16) * 8));   // + lg_arrivals' words
+    place(32, take(PQF_HDR * 8 + lg_pqf_cap(N) * 40));   // lg_pq_flow: 16 + 8 + 8 + 4 + 4 B per ticket
     return off;
 }
 }  // namespace
@@ -3217,6 +3629,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 29: S.cstat = (uint32_t*)p; break;
             case 30: S.pq = (uint32_t*)p; S.pq_cap = LG_PQ_CAP; break;
             case 31: S.pqst = (uint64_t*)p; S.pq_tmax = (uint32_t)lg_pq_tmax(std::max<uint32_t>(n, 1)); break;
+            case 32: S.pqf = (uint64_t*)p; S.pqf_cap = (uint32_t)lg_pqf_cap(std::max<uint32_t>(n, 1)); break;
 
             default: *arr[k - 16] = (uint32_t*)p; break;
         }

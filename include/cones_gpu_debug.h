@@ -26,12 +26,16 @@ int cg_selftest_sqrt(cg_handle* h, const double* s, double* out, uint32_t n);
  * next batch calls; enable = 0 frees the buffer. Fetch synchronises the batch stream. */
 int cg_debug_stamps(cg_handle* h, int enable);
 /* Timing: the next cg_run_batch launch of the frame kernel records its execution span in
- * d_span (device memory, 2 x uint64 the caller sets to {UINT64_MAX, 0}): the first workgroup's
- * start and the last workgroup's end, s_memrealtime ticks (100 MHz). One atomic per workgroup
- * at each end; frames of more than 65,536 points (large-frame path) do not record. */
+ * d_span (device memory, CG_SPAN_WORDS x uint64 the caller sets to {UINT64_MAX, 0, 0, 0}):
+ * [0] the first workgroup's start and [1] the last workgroup's end, s_memrealtime ticks
+ * (100 MHz); [2] the sum over workgroups of their shader cycles (s_memtime) and [3] of their
+ * s_memrealtime ticks, so [2] / [3] x 100 MHz is the shader clock the launch ran at. Atomics by
+ * one lane per workgroup at each end; frames of more than 65,536 points (large-frame path) do
+ * not record. */
+#define CG_SPAN_WORDS 4
 int cg_debug_launch_span(cg_handle* h, void* d_span);
-/* The same for the handle's next n_launches batch launches, launch k into d_spans[2k, 2k + 1]
- * (no host call between the launches). */
+/* The same for the handle's next n_launches batch launches, launch k into
+ * d_spans[CG_SPAN_WORDS k, CG_SPAN_WORDS (k + 1)) (no host call between the launches). */
 int cg_debug_launch_spans(cg_handle* h, void* d_spans, uint32_t n_launches);
 int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
 
@@ -44,8 +48,12 @@ int cg_debug_stamps_fetch(cg_handle* h, uint64_t* out, uint32_t n_frames);
  * published, so every chunk workgroup times out and the call re-runs the frame by DMA (6,
  * tests of that retry); single-frame split calls whose chunk workgroup 0 gives up waiting for
  * the other chunks at once, so the call re-runs the frame in one workgroup (9, tests of that
- * retry); large frames whose first partition level reports a timed-out device-side wait, so the
- * fetch fails with CG_E_DEVICE (10, tests of that failure); 0 = automatic. */
+ * retry); large frames whose PCL-order partition gives up waiting on its first range (10, tests
+ * of that failure: the range's tiles take the expired-wait path itself, store their records
+ * unchanged and queue the range whole as a leaf, and the fetch fails with CG_E_DEVICE). Route 10
+ * acts only where that partition runs: device-sized frames (65,536 < N <= 2^22 points, pipeline
+ * or detect mode, PCL voxel order) whose index_vector holds more than 2,048 records; the flag is
+ * read by the clustering tail of that path, which every such frame runs; 0 = automatic. */
 int cg_debug_route(cg_handle* h, int route);
 /* Diagnostics: the meta words of the last large frame (sector minimum keys 0-17, touched
  * bins 18, K 19, candidates 20, survivors 21, ...; cg_internal.h LG_*). */

@@ -25,3 +25,11 @@ def test_queued_durations_follow_each_stream():
 def test_queued_durations_one_stream_is_back_to_back():
     sp = np.array([[0, 5], [6, 11], [12, 20]])
     assert bench.queued_durations(sp, 1).tolist() == [5, 6, 9]
+
+
+def test_shader_clock_from_span_records():
+    # [start, end, shader cycles summed over workgroups, real-time ticks summed over them]:
+    # 21,000 cycles over 1,000 ticks (10 us at 100 MHz) = 2,100 MHz
+    sp = np.array([[0, 10, 10_000, 500], [5, 15, 11_000, 500]])
+    assert abs(bench.shader_clock_mhz(sp) - 2100.0) < 1e-9
+    assert bench.shader_clock_mhz(np.zeros((2, 4), np.int64)) is None
