@@ -2000,7 +2000,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
     __shared__ uint32_t cg[WAVES], cl[WAVES];
     __shared__ uint64_t tbase;
     __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the tile's decisions
-    __shared__ uint32_t ch[8];   // children: count, first ticket, their (first, last) and tiles
+    __shared__ uint32_t ch[9];   // children: [0] count, [1] first ticket, [2..5] their (first, last),
+                                 // [6..7] their tickets, [8] this workgroup finished the range
     __shared__ __attribute__((aligned(16))) unsigned char smem[LEAVES ? LG_PCL_LDS + 8 * WAVES * 4 : 16];
     const PqfView Q = pqf_view(S);
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
@@ -2026,6 +2027,14 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                         const int64_t pend = (int64_t)ld64(&Q.hdr[2]);
                         if (a && b) {
                             f = (uint32_t)a; e = (uint32_t)(a >> 32); w2 = (uint32_t)b; tb = (uint32_t)(b >> 32);
+                            // (never expected) an entry that does not describe a range or task of
+                            // this index_vector: the frame fails, no index is formed from it
+                            const uint32_t tbr = tb & ~(PQF_TASK | PQF_MID);
+                            if (!(f < e && e <= n && tbr < Q.cap && e - f <= ((tb & PQF_TASK) ? (uint32_t)LG_PCL_LEAF : n) &&
+                                  ((tb & PQF_TASK) || ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tbr) < pqf_tiles(f, e)))) {
+                                S.meta[LG_PQ_TIMEOUT] = 1u;
+                                ok = 0;
+                            }
                             break;
                         }
                         if (pend == 1) { ok = 0; break; }   // every range finished
@@ -2223,10 +2232,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 __builtin_amdgcn_s_waitcnt(0x0070);
             }
             ch[0] = nch; ch[1] = first; es[7] = nt;
-            if (done == T - 1u) ch[5] = 1u; else ch[5] = 0u;
+            ch[8] = done == T - 1u ? 1u : 0u;
         }
         __syncthreads();
-        if (ch[5]) {   // (uniform) this workgroup finished the range
+        if (ch[8]) {   // (uniform) this workgroup finished the range
             const uint32_t nch = ch[0], first = ch[1], nt = es[7];
             const uint32_t w2c = (d - 1u) | ((depth + 1u) << 8);
             for (uint32_t i = tid; i < nt; i += CG_BLOCK) {

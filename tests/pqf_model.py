@@ -1,0 +1,249 @@
+"""Tile-by-tile model of cg_large.hip lg_pq_flow (the device-sized PCL partition as one dataflow
+launch) for tests/test_pq_flow_model.py: the same ticket queue, 16-byte entries (both halves'
+bit layouts), look-back counts, range words, inline / deferred swaps, cut word, the children's
+shared slots (ch[]), the `pend` count and the leaf tasks, with every array access bounds-checked
+(pb_model.Arr). Workgroups are modelled as a pool that takes tickets in order; a random
+scheduler interleaves their steps (split, wait, swap, push) so that ranges of different depths
+run side by side as on the device. The leaves then go through std::sort's restatement with
+their budgets (their in-LDS sort is modelled in pb_model.block_sort). Returns the records and
+the statistics the kernel's design relies on (every ticket served, pend never 1 early)."""
+import random
+
+from pb_model import Arr, _lg, _pb_median, key, std_sort
+
+PQ_T = 512
+CUT = 2048            # LG_PCL_CUT
+LEAF = 4096           # LG_PCL_LEAF
+TILE = 1 << 46        # PQ_RW_TILE
+RW_N = (1 << 23) - 1  # PQ_RW_N
+KIND_SWAP = 1 << 7
+TASK, MID = 0x80000000, 0x40000000
+M32 = 0xFFFFFFFF
+
+
+def tiles(f, e):
+    return (e - f - 1 + PQ_T - 1) // PQ_T
+
+
+def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0.3):
+    rng = random.Random(seed)
+    n = len(E_in)
+    d0 = 2 * _lg(n)
+    bufs = [Arr(n), Arr(n)]
+    for i, r in enumerate(E_in):
+        bufs[0][i] = r
+    leaflist = []          # pq_push(PQ_LEAFLIST): (first, last, budget, buffer)
+    tasks_done = []        # (LEAVES) leaf tasks run in the launch: (first, last, budget, buffer)
+    if n <= CUT:
+        leaflist.append((0, n, d0, 0))
+        return finish(n, bufs, leaflist, tasks_done), {"tickets": 0}
+    T0 = tiles(0, n)
+    cap = 2 * (2 * _lg(n) + 2) * (n // PQ_T + n // CUT + 2) + 1024
+    ent = Arr(2 * cap)
+    lb = Arr(cap)
+    rw = Arr(cap)
+    sd = Arr(cap)
+    cw = Arr(cap)
+    par = Arr(n + 2)
+    cnt = Arr(n + 2)
+    vst = Arr(n)
+    hdr = [0, 0, 0]        # tickets handed out, queued past T0, pend
+    st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0}
+
+    def entry(k, f, e, w2, tb):
+        assert 0 <= k < cap
+        ent[2 * k] = (e << 32) | f
+        ent[2 * k + 1] = (tb << 32) | w2
+
+    # a workgroup is a generator: it yields when it waits (for an entry or a range word)
+    def workgroup():
+        while True:
+            t = hdr[0]
+            hdr[0] += 1
+            st["tickets"] = max(st["tickets"], hdr[0])
+            f, e, w2, tb = 0, n, d0 | (t << 16), 0
+            if t >= T0:
+                if t >= cap:
+                    return
+                while True:
+                    a, b = ent[2 * t], ent[2 * t + 1]
+                    if a and b:
+                        f, e, w2, tb = a & M32, a >> 32, b & M32, b >> 32
+                        break
+                    if hdr[2] == 1:
+                        return
+                    yield "entry"
+            d, depth = w2 & 0x7F, (w2 >> 8) & 0xFF
+            assert f < e <= n, (f, e)
+            if tb & TASK:
+                size = e - f
+                assert size <= (512 if tb & MID else LEAF)
+                tasks_done.append((f, e, d, depth & 1))
+                hdr[2] += 1
+                yield "task"
+                continue
+            swap_entry = (w2 & KIND_SWAP) != 0
+            q = (w2 >> 16) if swap_entry else t - tb
+            T = tiles(f, e)
+            assert 0 <= q < T
+            E, Eo = bufs[depth & 1], bufs[(depth + 1) & 1]
+            a_, b_, c_ = f + 1, f + (e - f) // 2, e - 1
+            m = _pb_median(a_, b_, c_, key(E[a_]), key(E[b_]), key(E[c_]))
+            p = key(E[a_]) if m == a_ else (key(E[b_]) if m == b_ else key(E[c_]))
+            rf = E[f]
+            xs = [f + 1 + q * PQ_T + tid for tid in range(PQ_T)]
+            valid = [x < e for x in xs]
+            rx = [E[x] if v else E[f] for x, v in zip(xs, valid)]
+            gi = [0] * PQ_T
+            li = [0] * PQ_T
+            if not swap_entry:
+                k_ = [(key(rf) if x == m else key(r)) if v else 0 for x, r, v in zip(xs, rx, valid)]
+                ge = [v and k >= p for k, v in zip(k_, valid)]
+                le = [v and k <= p for k, v in zip(k_, valid)]
+                tg, tl = sum(ge), sum(le)
+                # look-back: counts of the range's earlier tiles (their status words)
+                while any(lb[j] == 0 for j in range(tb, t)):
+                    yield "lookback"
+                bg = sum((lb[j] >> 32) & 0x3FFFFFFF for j in range(tb, t))   # (PQ_ST_V: flags off)
+                bl = sum(lb[j] & M32 for j in range(tb, t))
+                lb[t] = (tg << 32) | tl | (1 << 62)   # (published; the model's flag bit)
+                rg = rl = 0
+                for i in range(PQ_T):
+                    gi[i], li[i] = bg + rg, bl + rl
+                    if ge[i]:
+                        par[f + 1 + gi[i]] = xs[i]
+                        rg += 1
+                    if le[i]:
+                        cnt[f + 1 + li[i]] = xs[i]
+                        rl += 1
+                rw[tb] = rw[tb] + (TILE | (tg << 23) | tl)
+                yield "split"
+                inline = hdr[0] >= tb + T and rng.random() >= defer_p
+                if not inline:
+                    for i in range(PQ_T):
+                        if valid[i]:
+                            vst[xs[i]] = (gi[i] << 32) | li[i]
+                    kq = T0 + hdr[1]
+                    hdr[1] += 1
+                    entry(kq, f, e, (w2 & 0xFFFF) | KIND_SWAP | (q << 16), tb)
+                    st["deferred"] += 1
+                    continue
+                st["inline"] += 1
+            else:
+                for i in range(PQ_T):
+                    if valid[i]:
+                        rk = vst[xs[i]]
+                        gi[i], li[i] = rk >> 32, rk & M32
+            while (rw[tb] >> 46) < T:
+                yield "rangeword"
+            w_ = rw[tb]
+            nL, nR = (w_ >> 23) & RW_N, w_ & RW_N
+            if q == 0:
+                Eo[f] = E[m]
+            for i in range(PQ_T):
+                x = xs[i]
+                if not valid[i]:
+                    continue
+                vx = rf if x == m else rx[i]
+                k = key(vx)
+                ge, le = k >= p, k <= p
+                hasL = ge and gi[i] < nR
+                nx = hasL and gi[i] + 1 < min(nL, nR)
+                ri = (nR - 1 - li[i]) & M32
+                hasR = le and ri < nL
+                jj = cnt[f + 1 + (nR - 1 - gi[i] if hasL else 0)]
+                l2 = par[f + 1 + (gi[i] + 1 if gi[i] + 1 < nL else 0)]
+                r2 = cnt[f + 1 + (nR - 2 - gi[i] if nx else 0)]
+                il = par[f + 1 + (ri if hasR else 0)]
+                partner, cutter, cut = x, False, 0
+                if hasL:
+                    if x < jj:
+                        partner = jj
+                        if not nx or not l2 < r2:
+                            cutter, cut = True, min(l2 if gi[i] + 1 < nL else M32, jj)
+                    elif gi[i] == 0:
+                        cutter, cut = True, x
+                if hasR and il < x:
+                    partner = il
+                partner = min(max(partner, f), e - 1)
+                Eo[x] = vx if partner == x else (rf if partner == m else E[partner])
+                if cutter:
+                    assert cw[tb] == 0, "two cutters"
+                    cw[tb] = cw[tb] | (min(max(cut, f), e) + 1)
+            yield "swap"
+            done = sd[tb]
+            sd[tb] = done + 1
+            ch = [None] * 9
+            nch = nt = first = 0
+            if done == T - 1:
+                c = cw[tb]
+                assert c and not (c >> 31)
+                cut = (c & 0x7FFFFFFF) - 1
+                lo, hi = (f, cut), (cut, e)
+                tc = [0, 0]
+                rg_ = [False, False]
+                lf = [False, False]
+                for cc in range(2):
+                    rg_[cc] = hi[cc] - lo[cc] > CUT and d > 1 and not (depth_cap and depth + 1 >= depth_cap)
+                    if rg_[cc]:
+                        tc[cc] = tiles(lo[cc], hi[cc])
+                    lf[cc] = leaves_in_flow and not rg_[cc] and hi[cc] > lo[cc] and hi[cc] - lo[cc] <= LEAF
+                    if lf[cc]:
+                        tc[cc] = 1
+                if tc[0] + tc[1]:
+                    first = T0 + hdr[1]
+                    hdr[1] += tc[0] + tc[1]
+                    assert first + tc[0] + tc[1] <= cap
+                for cc in range(2):
+                    if rg_[cc] or lf[cc]:
+                        ch[2 + 2 * nch] = lo[cc]
+                        ch[3 + 2 * nch] = hi[cc] | (0x80000000 if lf[cc] else 0)
+                        ch[6 + nch] = tc[cc]
+                        nch += 1
+                        st["ranges"] += rg_[cc]
+                    else:
+                        leaflist.append((lo[cc], hi[cc], d - 1, (depth + 1) & 1))
+                nt = tc[0] + tc[1]
+                hdr[2] += 1 - nch   # before any child is published
+                st["max_depth"] = max(st["max_depth"], depth + 1)
+            ch[0], ch[1], ch[8] = nch, first, 1 if done == T - 1 else 0
+            if ch[8]:
+                w2c = (d - 1) | ((depth + 1) << 8)
+                for i in range(nt):
+                    cc = 1 if (nch == 2 and i >= ch[6]) else 0
+                    fb = first + (ch[6] if cc else 0)
+                    hi_ = ch[3 + 2 * cc]
+                    if hi_ >> 31:
+                        entry(first + i, ch[2 + 2 * cc], hi_ & 0x7FFFFFFF, w2c, TASK)
+                    else:
+                        entry(first + i, ch[2 + 2 * cc], hi_, w2c | ((first + i - fb) << 16), fb)
+            yield "push"
+
+    pool = [workgroup() for _ in range(grid)]
+    live = list(pool)
+    steps = 0
+    while live:
+        g = rng.choice(live)
+        try:
+            next(g)
+        except StopIteration:
+            live.remove(g)
+        steps += 1
+        assert steps < 50_000_000, "no progress"
+    assert hdr[2] == 1, hdr
+    st["pend"] = hdr[2]
+    return finish(n, bufs, leaflist, tasks_done), st
+
+
+def finish(n, bufs, leaflist, tasks):
+    """Every leaf (list or task) sorted with its budget from the buffer its depth left it in;
+    the leaves must tile [0, n) exactly."""
+    out = [None] * n
+    for (f, e, d, b) in leaflist + tasks:
+        seg = [bufs[b][i] for i in range(f, e)]
+        srt = std_sort(seg, depth0=d)
+        for i in range(f, e):
+            assert out[i] is None, "overlapping leaves"
+            out[i] = srt[i - f]
+    assert None not in out, "a position no leaf covers"
+    return out
