@@ -9,7 +9,7 @@ their budgets (their in-LDS sort is modelled in pb_model.block_sort). Returns th
 the statistics the kernel's design relies on (every ticket served, pend never 1 early)."""
 import random
 
-from pb_model import Arr, _lg, _pb_median, key, std_sort
+from pb_model import Arr, _lg, _pb_median, block_sort, key, std_sort, wave_sort
 
 PQ_T = 512
 CUT = 2048            # LG_PCL_CUT
@@ -25,7 +25,7 @@ def tiles(f, e):
     return (e - f - 1 + PQ_T - 1) // PQ_T
 
 
-def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0.3):
+def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0.3, model_mids=False):
     rng = random.Random(seed)
     n = len(E_in)
     d0 = 2 * _lg(n)
@@ -48,6 +48,7 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
     cnt = Arr(n + 2)
     vst = Arr(n)
     hdr = [0, 0, 0]        # tickets handed out, queued past T0, pend
+    outk = [None] * n      # (model_mids) the in-launch leaves' and mid ranges' outputs
     st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0}
 
     def entry(k, f, e, w2, tb):
@@ -78,7 +79,37 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
             if tb & TASK:
                 size = e - f
                 assert size <= (512 if tb & MID else LEAF)
-                tasks_done.append((f, e, d, depth & 1))
+                if not model_mids:
+                    tasks_done.append((f, e, d, depth & 1))
+                    hdr[2] += 1
+                    yield "task"
+                    continue
+                # pqf_leaf_task: the records of the depth's buffer, sorted in LDS (pb_model's
+                # thread model), ranges of 65-512 records queued as mid tasks (PqfDefer: the
+                # records back to the buffer, pend - 1, then the entry), outputs straight out
+                buf = bufs[depth & 1]
+                seg = [buf[i] for i in range(f, e)]
+                if tb & MID:
+                    mo, waves = block_sort(seg, depth0=d, defer=True)
+                    for (wf, wm, wd, wrecs) in waves:
+                        mo[wf:wf + wm] = wave_sort(wrecs, wd)
+                    for i in range(size):
+                        assert outk[f + i] is None, "output written twice"
+                        outk[f + i] = mo[i]
+                else:
+                    lo_, mids = block_sort(seg, depth0=d, wmax=512, defer=True)
+                    for i in range(size):
+                        if lo_[i] is not None:
+                            assert outk[f + i] is None, "output written twice"
+                            outk[f + i] = lo_[i]
+                    for (mf, mm, md, mrecs) in mids:
+                        for i in range(mm):
+                            buf[f + mf + i] = mrecs[i]
+                        hdr[2] -= 1
+                        kq = T0 + hdr[1]
+                        hdr[1] += 1
+                        entry(kq, f + mf, f + mf + mm, ((depth & 0xFF) << 8) | md, TASK | MID)
+                        yield "mid queued"
                 hdr[2] += 1
                 yield "task"
                 continue
@@ -232,13 +263,14 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
         assert steps < 50_000_000, "no progress"
     assert hdr[2] == 1, hdr
     st["pend"] = hdr[2]
-    return finish(n, bufs, leaflist, tasks_done), st
+    res = finish(n, bufs, leaflist, tasks_done, outk if model_mids else None)
+    return res, st
 
 
-def finish(n, bufs, leaflist, tasks):
+def finish(n, bufs, leaflist, tasks, outk=None):
     """Every leaf (list or task) sorted with its budget from the buffer its depth left it in;
-    the leaves must tile [0, n) exactly."""
-    out = [None] * n
+    the leaves must tile [0, n) exactly (with the in-launch outputs outk, when modelled)."""
+    out = list(outk) if outk is not None else [None] * n
     for (f, e, d, b) in leaflist + tasks:
         seg = [bufs[b][i] for i in range(f, e)]
         srt = std_sort(seg, depth0=d)

@@ -43,3 +43,13 @@ def test_flow_model_depth_cap_route5():
     recs = _records(30000, 3000, 11)
     got, st = flow_sort(recs, grid=8, seed=11, depth_cap=1)
     assert got == std_sort(recs) and st["ranges"] == 1
+
+
+@pytest.mark.parametrize("n,keys,seed", [(6000, 900, 21), (14000, 1500, 22)])
+def test_flow_model_leaf_and_mid_tasks(n, keys, seed):
+    """LG_PQ_MODE 2: leaves sorted inside the launch (pb_model's thread model of the LDS sort),
+    their 65-512-record ranges queued as mid tasks with the records handed back through the
+    buffer; every output written once, the launch drains with pend at 1."""
+    recs = _records(n, keys, seed)
+    got, st = flow_sort(recs, grid=6, seed=seed, leaves_in_flow=True, model_mids=True)
+    assert got == std_sort(recs) and st["pend"] == 1
