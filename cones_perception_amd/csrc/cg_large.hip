@@ -1777,13 +1777,20 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
 // MI355X_MICROARCH.md's hand-off table, row 1. lg_pcl_leaf clears the used words and lg_pcl_mid
 // the counters, so the next frame finds them zero.
 #ifndef LG_FLOW_GRID
-#define LG_FLOW_GRID 512   // workgroups of the launch (two per CU)
+// workgroups of the launch: 192 measured best on C5 (235-238 us per frame against 237-241 at 128
+// and 256, 266-270 at 512 before the counters had lines of their own, profiles/r6_c5_flow_ab.txt)
+#define LG_FLOW_GRID 192
 #endif
 #define LG_CLEAR_FLOW 0x100u   // lg_pcl_leaf's clear_set for lg_pq_flow's words
-#define PQF_HDR 8          // u64 words: [0] tickets handed out, [1] tickets queued past range 0's, [2] pend
+#define PQF_HDR 48         // u64 words, the counters on lines of their own (they take every
+                           // workgroup's atomics and polls): [PQF_TK] tickets handed out,
+                           // [PQF_TAIL] tickets queued past range 0's, [PQF_PEND] pend
+#define PQF_TK 0
+#define PQF_TAIL 16
+#define PQF_PEND 32
 #define PQF_KIND_SWAP (1u << 7)
 struct PqfView {
-    uint64_t* hdr; uint64_t* ent; uint64_t* lb; uint64_t* rw; uint32_t* sd; uint32_t* cw; uint32_t cap;
+    uint64_t* hdr; uint64_t* ent; uint64_t* lb; uint64_t* rw; uint64_t* sd; uint32_t cap;
 };
 __device__ __forceinline__ PqfView pqf_view(const LgScratch& S) {
     PqfView v;
@@ -1792,8 +1799,9 @@ __device__ __forceinline__ PqfView pqf_view(const LgScratch& S) {
     v.ent = S.pqf + PQF_HDR;      // two words per ticket
     v.lb = v.ent + 2ull * v.cap;  // look-back status per ticket
     v.rw = v.lb + v.cap;          // range word, by the range's first ticket
-    v.sd = (uint32_t*)(v.rw + v.cap);   // tiles whose swaps are stored, by first ticket
-    v.cw = v.sd + v.cap;          // cut + 1 (bit 31: a wait gave up), by first ticket
+    v.sd = v.rw + v.cap;          // by first ticket: tiles whose swaps are stored (bits 0-15), the
+                                  // cut + 1 (16-39, added by the cutter's tile), tiles whose wait
+                                  // gave up (40-63): one add per tile, the last one reads it all
     return v;
 }
 __device__ __forceinline__ uint32_t pqf_tiles(uint32_t f, uint32_t e) { return (e - f - 1 + PQ_T - 1) / PQ_T; }
@@ -1859,10 +1867,10 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
     if (blockIdx.x == 0 && tid == 0 && !clear_set) S.pqst[0] = 0;
     if (clear_set == LG_CLEAR_FLOW) {
         const PqfView Q = pqf_view(S);
-        const uint32_t used = (uint32_t)min(Q.hdr[0], (uint64_t)Q.cap);
+        const uint32_t used = (uint32_t)min(Q.hdr[PQF_TK], (uint64_t)Q.cap);
         for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < used; i += gridDim.x * CG_BLOCK) {
             Q.ent[2ull * i] = 0ull; Q.ent[2ull * i + 1] = 0ull;
-            Q.lb[i] = 0ull; Q.rw[i] = 0ull; Q.sd[i] = 0u; Q.cw[i] = 0u;
+            Q.lb[i] = 0ull; Q.rw[i] = 0ull; Q.sd[i] = 0ull;
         }
     } else if (blockIdx.x == 0 && clear_set) {
         pq_clear_set(S, clear_set - 1u);
@@ -1938,6 +1946,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
 #define PQF_WAIT_TICKS PQ_WAIT_TICKS
 // (LEAVES) entry word 1's high half for a task: bit 31 a leaf or mid range, bit 30 a mid range
 // (first tickets are < 2^30)
+#define PQF_SD_BAD 0xffffffffu
 #define PQF_TASK 0x80000000u
 #define PQF_MID 0x40000000u
 // A leaf's ranges of 65-PQ_MID records as tasks of the same launch (lg_pcl_leaf's PqDefer
@@ -1955,8 +1964,8 @@ struct PqfDefer {
         for (uint32_t i = l; i < m; i += 64) st64(Eh + base + f + i, E[f + i]);
         __builtin_amdgcn_s_waitcnt(0x0070);
         if (l == 0) {
-            __hip_atomic_fetch_add(&Q.hdr[2], (uint64_t)(int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t k = T0 + __hip_atomic_fetch_add(&Q.hdr[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&Q.hdr[PQF_PEND], (uint64_t)(int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t k = T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_s_waitcnt(0x0070);   // (the count is performed before the entry)
             if (k < Q.cap) pqf_entry(Q, k, base + f, base + f + m, (w2 & ~0x7fu) | d, PQF_TASK | PQF_MID);
         }
@@ -1992,7 +2001,7 @@ __device__ __forceinline__ void pqf_leaf_task(const LgScratch& S, const PqfView&
         else pcl_block_sort<8, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
     }
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&Q.hdr[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(&Q.hdr[PQF_PEND], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <bool LEAVES>
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap,
@@ -2000,6 +2009,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
     __shared__ uint32_t cg[WAVES], cl[WAVES];
     __shared__ uint64_t tbase;
     __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the tile's decisions
+    __shared__ uint32_t tcut;    // the tile's cut + 1 (its cutter), PQF_SD_BAD, or 0
     __shared__ uint32_t ch[9];   // children: [0] count, [1] first ticket, [2..5] their (first, last),
                                  // [6..7] their tickets, [8] this workgroup finished the range
     __shared__ __attribute__((aligned(16))) unsigned char smem[LEAVES ? LG_PCL_LDS + 8 * WAVES * 4 : 16];
@@ -2015,16 +2025,17 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
     uint64_t* const vst = (uint64_t*)S.vox;   // a deferred tile's per-element state: gi << 32 | li
     for (;;) {
         if (tid == 0) {   // the next ticket and its entry
-            const uint32_t t = (uint32_t)__hip_atomic_fetch_add(&Q.hdr[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t t = (uint32_t)__hip_atomic_fetch_add(&Q.hdr[PQF_TK], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint32_t ok = 1, f = 0, e = n, w2 = d0 | (t << 16), tb = 0;   // (range 0: budget d0, depth 0, tile t)
             if (t >= T0) {
                 if (t >= Q.cap) {
                     ok = 0;   // (past every ticket the sort can queue: nothing will be published here)
                 } else {
                     const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
-                    for (;;) {
+                    for (uint32_t it = 0;; it++) {
                         const uint64_t a = ld64(Q.ent + 2ull * t), b = ld64(Q.ent + 2ull * t + 1);
-                        const int64_t pend = (int64_t)ld64(&Q.hdr[2]);
+                        // (every fourth poll: one line that every waiting workgroup reads)
+                        const int64_t pend = (it & 3u) == 3u ? (int64_t)ld64(&Q.hdr[PQF_PEND]) : 0;
                         if (a && b) {
                             f = (uint32_t)a; e = (uint32_t)(a >> 32); w2 = (uint32_t)b; tb = (uint32_t)(b >> 32);
                             // (never expected) an entry that does not describe a range or task of
@@ -2072,6 +2083,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
         const uint32_t ka = pqf_key(E, a), kb = pqf_key(E, b), kc = pqf_key(E, c);
         const uint64_t rf = ld64((uint64_t*)E + f);
         const uint64_t rx = ld64((uint64_t*)E + (valid ? x : f));   // (clamped: no branch between the loads)
+        // the ticket count for the inline-swap decision, in the same batch: it only grows, so a
+        // count read now that covers the range still covers it after the split
+        const uint64_t handed = (!swap_entry && tid == 0) ? ld64(&Q.hdr[PQF_TK]) : 0ull;
         const uint32_t m = pb_median(a, b, c, ka, kb, kc);
         const uint32_t p = m == a ? ka : (m == b ? kb : kc);
         uint32_t gi = 0, li = 0;
@@ -2100,7 +2114,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 __hip_atomic_fetch_add(&Q.rw[tb], PQ_RW_TILE | ((uint64_t)tg << 23) | tl, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 // the swaps here only when every ticket of the range is held (or done)
-                es[6] = ld64(&Q.hdr[0]) >= (uint64_t)tb + T ? 1u : 0u;
+                es[6] = handed >= (uint64_t)tb + T ? 1u : 0u;
             }
             __syncthreads();
             if (!es[6]) {   // defer: the state to HBM, a swap entry at the end of the queue
@@ -2108,7 +2122,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 __builtin_amdgcn_s_waitcnt(0x0070);
                 __syncthreads();
                 if (tid == 0) {
-                    const uint64_t kq = T0 + __hip_atomic_fetch_add(&Q.hdr[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t kq = T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (kq < Q.cap) pqf_entry(Q, kq, f, e, (w2 & 0xffffu) | PQF_KIND_SWAP | (q << 16), tb);
                     else S.meta[LG_PQ_TIMEOUT] = 1u;   // (the capacity bounds every queue: never expected)
                 }
@@ -2131,6 +2145,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             }
             if ((wv >> 46) < T) S.meta[LG_PQ_TIMEOUT] = 1u;   // (the frame's fetch fails on it)
             tbase = wv;
+            tcut = 0u;
         }
         __syncthreads();
         const uint64_t rw = tbase;
@@ -2143,7 +2158,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 st64(Eo + f, rf);
                 pq_push(S, PQ_LEAFLIST, f, e, d - 1u, (depth + 1u) & 1u);
             }
-            if (tid == 0) atomicOr(&Q.cw[tb], 0x80000000u);
+            if (tid == 0) tcut = PQF_SD_BAD;
         } else {
             const uint32_t nL = (uint32_t)(rw >> 23) & (uint32_t)PQ_RW_N, nR = (uint32_t)rw & (uint32_t)PQ_RW_N;
             if (q == 0 && tid == 0) st64(Eo + f, ld64((uint64_t*)E + m));
@@ -2178,19 +2193,23 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 if (hasR && il < x) partner = il;
                 partner = min(max(partner, f), e - 1u);   // (defensive: list entries lie in (f, e))
                 st64(Eo + x, partner == x ? vx : (partner == m ? rf : ld64((uint64_t*)E + partner)));
-                if (cutter) atomicOr(&Q.cw[tb], min(max(cut, f), e) + 1u);
+                if (cutter) tcut = min(max(cut, f), e) + 1u;
             }
         }
         // the tile's swaps are stored; the range's last tile queues the children
         __builtin_amdgcn_s_waitcnt(0x0070);
         __syncthreads();
         if (tid == 0) {
-            const uint32_t done = __hip_atomic_fetch_add(&Q.sd[tb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // one add per tile: its count, the cut if the cutter is here, a wait that gave up
+            const uint64_t add = 1ull | (tcut == PQF_SD_BAD ? (1ull << 40) : ((uint64_t)tcut << 16));
+            const uint64_t tot = __hip_atomic_fetch_add(&Q.sd[tb], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+            const uint32_t done = (uint32_t)(tot & 0xffffull) - 1u;
             uint32_t nch = 0, nt = 0, first = 0;
             if (done == T - 1u) {
-                const uint32_t cw = ld_rlx(&Q.cw[tb]);
-                const uint32_t cut = (cw & 0x7fffffffu) - 1u;
-                if (!(cw >> 31) && (cw & 0x7fffffffu)) {
+                const uint32_t cw = (uint32_t)((tot >> 16) & 0xffffffull);
+                const uint32_t cut = cw - 1u;
+                const bool bad = (tot >> 40) != 0ull;
+                if (!bad && cw) {
                     const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
                     uint32_t tc[2] = {0, 0};
                     bool rng[2];
@@ -2203,7 +2222,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                         if (lf[cc]) tc[cc] = 1u;
                     }
                     if (tc[0] + tc[1]) {
-                        first = T0 + (uint32_t)__hip_atomic_fetch_add(&Q.hdr[1], (uint64_t)(tc[0] + tc[1]), __ATOMIC_RELAXED,
+                        first = T0 + (uint32_t)__hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], (uint64_t)(tc[0] + tc[1]), __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_AGENT);
                         if ((uint64_t)first + tc[0] + tc[1] > Q.cap) {   // (never expected) the leaves finish them in HBM
                             rng[0] = rng[1] = lf[0] = lf[1] = false;
@@ -2220,14 +2239,14 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                         }
                     }
                     nt = tc[0] + tc[1];
-                } else if (!(cw >> 31)) {
+                } else if (!bad) {
                     S.meta[LG_PQ_TIMEOUT] = 1u;   // (no cut stored: never expected)
                 }
                 // the range's end and its queued children in one count, performed before any
                 // child is published: `pend` cannot read 1 while a child is outstanding (a child
                 // that finished before this count would otherwise let waiting workgroups leave
                 // with tickets the grandchildren are then queued on)
-                __hip_atomic_fetch_add(&Q.hdr[2], (uint64_t)(int64_t)(1 - (int)nch), __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&Q.hdr[PQF_PEND], (uint64_t)(int64_t)(1 - (int)nch), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 __builtin_amdgcn_s_waitcnt(0x0070);
             }
@@ -3371,7 +3390,10 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
                        s, S, P, kb[1]);
     const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
 #ifndef LG_PQ_MODE
-#define LG_PQ_MODE 0   // 0: one launch per partition level; 1: lg_pq_flow; 2: lg_pq_flow with the leaves
+// 1: lg_pq_flow (round 6); 0: one lg_pq_level launch per partition level (round 5); 2: lg_pq_flow
+// with the leaves and mid ranges as tasks of the same launch (hangs on a 131k-point detector
+// frame on the GPU, cause not found: not used)
+#define LG_PQ_MODE 1
 #endif
 #if LG_PQ_MODE != 0
     // the partition as one dataflow launch (lg_pq_flow): depth-0 records in kb[1], parity 1 in
