@@ -1944,75 +1944,14 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
     }
 }
 #define PQF_WAIT_TICKS PQ_WAIT_TICKS
-// (LEAVES) entry word 1's high half for a task: bit 31 a leaf or mid range, bit 30 a mid range
-// (first tickets are < 2^30)
-#define PQF_SD_BAD 0xffffffffu
-#define PQF_TASK 0x80000000u
-#define PQF_MID 0x40000000u
-// A leaf's ranges of 65-PQ_MID records as tasks of the same launch (lg_pcl_leaf's PqDefer
-// hands them to lg_pcl_mid instead): the wave writes the range's records back to the buffer
-// (sc1), counts the task into `pend` before publishing it, and queues its entry.
-struct PqfDefer {
-    uint64_t* Eh; PqfView Q; uint32_t base, w2, T0;
-    template <class P64, class OUT>
-    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
-        if (m <= PW_MAX) {
-            pw_range64(E, f, m, d, out);
-            return;
-        }
-        const uint32_t l = lane_id();
-        for (uint32_t i = l; i < m; i += 64) st64(Eh + base + f + i, E[f + i]);
-        __builtin_amdgcn_s_waitcnt(0x0070);
-        if (l == 0) {
-            __hip_atomic_fetch_add(&Q.hdr[PQF_PEND], (uint64_t)(int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t k = T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_s_waitcnt(0x0070);   // (the count is performed before the entry)
-            if (k < Q.cap) pqf_entry(Q, k, base + f, base + f + m, (w2 & ~0x7fu) | d, PQF_TASK | PQF_MID);
-        }
-    }
-};
-// A leaf (at most LG_PCL_LEAF records) or a mid range (at most PQ_MID) of the flow: its records
-// from the buffer of its depth (sc1: written by this launch's swaps or a leaf's hand-back) into
-// LDS, pcl_block_sort to the end, results straight to the outputs (as lg_pcl_leaf and
-// lg_pcl_mid); then the task's end into `pend` (its mid tasks were counted when queued).
-__device__ __forceinline__ void pqf_leaf_task(const LgScratch& S, const PqfView& Q, unsigned char* pqf_smem, uint64_t* E,
-                                              uint32_t first, uint32_t size, uint32_t depth, uint32_t dpt, bool mid,
-                                              uint64_t* kout, uint32_t* vout) {
-    const uint32_t tid = threadIdx.x;
-    lds_u64* const El = (lds_u64*)(uint64_t*)pqf_smem;
-    const uint32_t cap = mid ? PQ_MID : LG_PCL_LEAF;
-    lds_u32* const w0 = (lds_u32*)(uint32_t*)(pqf_smem + 8 * LG_PCL_LEAF);
-    const PbScratch<PbLds> PS{w0, w0 + (cap + 4), w0 + 2 * (cap + 4), w0 + 3 * (cap + 4)};
-    lds_u32* const Rl = (lds_u32*)(uint32_t*)(pqf_smem + LG_PCL_LDS);
-    for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = ld64(E + first + i);
-    __syncthreads();
-    const PqLeafOut out{kout, vout, first};
-    if (mid) {
-        if (size <= CG_BLOCK) pcl_block_sort<1, PbLds, PqLeafOut>(El, out, size, depth, PS, Rl);
-        else pcl_block_sort<2, PbLds, PqLeafOut>(El, out, size, depth, PS, Rl);
-    } else {
-        const PqfDefer wt{E, Q, first, dpt << 8, pqf_tiles(0, S.meta[LG_PCL_N])};
-        if (size <= CG_BLOCK)
-            pcl_block_sort<1, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-        else if (size <= 2 * CG_BLOCK)
-            pcl_block_sort<2, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-        else if (size <= 4 * CG_BLOCK)
-            pcl_block_sort<4, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-        else pcl_block_sort<8, PbLds, PqLeafOut, false, PqfDefer, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-    }
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(&Q.hdr[PQF_PEND], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool LEAVES>
-__global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap,
-                                                       uint64_t* kout, uint32_t* vout) {
+#define PQF_SD_BAD 0xffffffffu   // tcut of a tile whose range wait gave up
+__global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap) {
     __shared__ uint32_t cg[WAVES], cl[WAVES];
     __shared__ uint64_t tbase;
     __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the tile's decisions
     __shared__ uint32_t tcut;    // the tile's cut + 1 (its cutter), PQF_SD_BAD, or 0
     __shared__ uint32_t ch[9];   // children: [0] count, [1] first ticket, [2..5] their (first, last),
                                  // [6..7] their tickets, [8] this workgroup finished the range
-    __shared__ __attribute__((aligned(16))) unsigned char smem[LEAVES ? LG_PCL_LDS + 8 * WAVES * 4 : 16];
     const PqfView Q = pqf_view(S);
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint32_t n = S.meta[LG_PCL_N];
@@ -2040,9 +1979,8 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                             f = (uint32_t)a; e = (uint32_t)(a >> 32); w2 = (uint32_t)b; tb = (uint32_t)(b >> 32);
                             // (never expected) an entry that does not describe a range or task of
                             // this index_vector: the frame fails, no index is formed from it
-                            const uint32_t tbr = tb & ~(PQF_TASK | PQF_MID);
-                            if (!(f < e && e <= n && tbr < Q.cap && e - f <= ((tb & PQF_TASK) ? (uint32_t)LG_PCL_LEAF : n) &&
-                                  ((tb & PQF_TASK) || ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tbr) < pqf_tiles(f, e)))) {
+                            if (!(f < e && e <= n && tb < Q.cap &&
+                                  ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tb) < pqf_tiles(f, e))) {
                                 S.meta[LG_PQ_TIMEOUT] = 1u;
                                 ok = 0;
                             }
@@ -2064,12 +2002,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
         if (!es[0]) return;
         const uint32_t f = es[1], e = es[2], w2 = es[3], tb = es[4], t = es[5];
         const uint32_t d = w2 & 0x7fu, depth = (w2 >> 8) & 0xffu;
-        if constexpr (LEAVES) {
-            if (tb & PQF_TASK) {   // (uniform) a leaf or a mid range: sorted to the end here
-                pqf_leaf_task(S, Q, smem, (depth & 1u) ? E1 : E0, f, e - f, d, depth, (tb & PQF_MID) != 0, kout, vout);
-                continue;
-            }
-        }
         const bool swap_entry = (w2 & PQF_KIND_SWAP) != 0;
         const uint32_t q = swap_entry ? (w2 >> 16) : t - tb;
         const uint32_t T = pqf_tiles(f, e);
@@ -2213,25 +2145,21 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                     const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
                     uint32_t tc[2] = {0, 0};
                     bool rng[2];
-                    bool lf[2] = {false, false};
                     for (int cc = 0; cc < 2; cc++) {
                         rng[cc] = hi[cc] - lo[cc] > LG_PCL_CUT && d > 1 && !(depth_cap && depth + 1u >= depth_cap);
                         if (rng[cc]) tc[cc] = pqf_tiles(lo[cc], hi[cc]);
-                        // (LEAVES) a leaf that fits LDS becomes a task of this launch: one ticket
-                        lf[cc] = LEAVES && !rng[cc] && hi[cc] > lo[cc] && hi[cc] - lo[cc] <= LG_PCL_LEAF;
-                        if (lf[cc]) tc[cc] = 1u;
                     }
                     if (tc[0] + tc[1]) {
                         first = T0 + (uint32_t)__hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], (uint64_t)(tc[0] + tc[1]), __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_AGENT);
                         if ((uint64_t)first + tc[0] + tc[1] > Q.cap) {   // (never expected) the leaves finish them in HBM
-                            rng[0] = rng[1] = lf[0] = lf[1] = false;
+                            rng[0] = rng[1] = false;
                             tc[0] = tc[1] = 0;
                         }
                     }
                     for (int cc = 0; cc < 2; cc++) {
-                        if (rng[cc] || lf[cc]) {
-                            ch[2 + 2 * nch] = lo[cc]; ch[3 + 2 * nch] = hi[cc] | (lf[cc] ? 0x80000000u : 0u);
+                        if (rng[cc]) {
+                            ch[2 + 2 * nch] = lo[cc]; ch[3 + 2 * nch] = hi[cc];
                             ch[6 + nch] = tc[cc];
                             nch++;
                         } else {
@@ -2260,11 +2188,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             for (uint32_t i = tid; i < nt; i += CG_BLOCK) {
                 const uint32_t cc = (nch == 2 && i >= ch[6]) ? 1u : 0u;
                 const uint32_t fb = first + (cc ? ch[6] : 0u);   // the child's first ticket
-                const uint32_t hi = ch[3 + 2 * cc];
-                if (hi >> 31)   // a leaf task (its budget and depth; the buffer is the depth's)
-                    pqf_entry(Q, first + i, ch[2 + 2 * cc], hi & 0x7fffffffu, w2c, PQF_TASK);
-                else
-                    pqf_entry(Q, first + i, ch[2 + 2 * cc], hi, w2c | ((first + i - fb) << 16), fb);
+                pqf_entry(Q, first + i, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c | ((first + i - fb) << 16), fb);
             }
         }
         __syncthreads();   // (es and ch are rewritten for the next ticket)
@@ -3390,23 +3314,15 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
                        s, S, P, kb[1]);
     const uint32_t tb = (nmax + PQ_T - 1) / PQ_T;
 #ifndef LG_PQ_MODE
-// 1: lg_pq_flow (round 6); 0: one lg_pq_level launch per partition level (round 5); 2: lg_pq_flow
-// with the leaves and mid ranges as tasks of the same launch (hangs on a 131k-point detector
-// frame on the GPU, cause not found: not used)
+// 1: lg_pq_flow (round 6); 0: one lg_pq_level launch per partition level (round 5)
 #define LG_PQ_MODE 1
 #endif
 #if LG_PQ_MODE != 0
     // the partition as one dataflow launch (lg_pq_flow): depth-0 records in kb[1], parity 1 in
     // kb[0]; route 5's level cap as a depth cap
     (void)levels;
-#if LG_PQ_MODE == 2
-    // (leaves and mid ranges sorted inside the launch: one workgroup per CU for the leaves' LDS)
-    hipLaunchKernelGGL(lg_pq_flow<true>, dim3(std::min<uint32_t>(256, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
-                       S.pcl_levels_cap, kb[0], vb2[0]);
-#else
-    hipLaunchKernelGGL(lg_pq_flow<false>, dim3(std::min<uint32_t>(LG_FLOW_GRID, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1],
-                       kb[0], S.pcl_levels_cap, kb[0], vb2[0]);
-#endif
+    hipLaunchKernelGGL(lg_pq_flow, dim3(std::min<uint32_t>(LG_FLOW_GRID, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
+                       S.pcl_levels_cap);
     hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0, s, S,
                        kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],

@@ -1,7 +1,7 @@
 """Tile-by-tile model of cg_large.hip lg_pq_flow (the device-sized PCL partition as one dataflow
 launch) for tests/test_pq_flow_model.py: the same ticket queue, 16-byte entries (both halves'
 bit layouts), look-back counts, range words, inline / deferred swaps, cut word, the children's
-shared slots (ch[]), the `pend` count and the leaf tasks, with every array access bounds-checked
+shared slots (ch[]), the `pend` count and the leaf list, with every array access bounds-checked
 (pb_model.Arr). Workgroups are modelled as a pool that takes tickets in order; a random
 scheduler interleaves their steps (split, wait, swap, push) so that ranges of different depths
 run side by side as on the device. The leaves then go through std::sort's restatement with
@@ -9,7 +9,7 @@ their budgets (their in-LDS sort is modelled in pb_model.block_sort). Returns th
 the statistics the kernel's design relies on (every ticket served, pend never 1 early)."""
 import random
 
-from pb_model import Arr, _lg, _pb_median, block_sort, key, std_sort, wave_sort
+from pb_model import Arr, _lg, _pb_median, key, std_sort
 
 PQ_T = 512
 CUT = 2048            # LG_PCL_CUT
@@ -17,7 +17,6 @@ LEAF = 4096           # LG_PCL_LEAF
 TILE = 1 << 46        # PQ_RW_TILE
 RW_N = (1 << 23) - 1  # PQ_RW_N
 KIND_SWAP = 1 << 7
-TASK, MID = 0x80000000, 0x40000000
 M32 = 0xFFFFFFFF
 
 
@@ -25,7 +24,7 @@ def tiles(f, e):
     return (e - f - 1 + PQ_T - 1) // PQ_T
 
 
-def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0.3, model_mids=False):
+def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
     rng = random.Random(seed)
     n = len(E_in)
     d0 = 2 * _lg(n)
@@ -33,22 +32,19 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
     for i, r in enumerate(E_in):
         bufs[0][i] = r
     leaflist = []          # pq_push(PQ_LEAFLIST): (first, last, budget, buffer)
-    tasks_done = []        # (LEAVES) leaf tasks run in the launch: (first, last, budget, buffer)
     if n <= CUT:
         leaflist.append((0, n, d0, 0))
-        return finish(n, bufs, leaflist, tasks_done), {"tickets": 0}
+        return finish(n, bufs, leaflist), {"tickets": 0}
     T0 = tiles(0, n)
     cap = 2 * (2 * _lg(n) + 2) * (n // PQ_T + n // CUT + 2) + 1024
     ent = Arr(2 * cap)
     lb = Arr(cap)
     rw = Arr(cap)
     sd = Arr(cap)
-    cw = Arr(cap)
     par = Arr(n + 2)
     cnt = Arr(n + 2)
     vst = Arr(n)
     hdr = [0, 0, 0]        # tickets handed out, queued past T0, pend
-    outk = [None] * n      # (model_mids) the in-launch leaves' and mid ranges' outputs
     st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0}
 
     def entry(k, f, e, w2, tb):
@@ -76,43 +72,6 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
                     yield "entry"
             d, depth = w2 & 0x7F, (w2 >> 8) & 0xFF
             assert f < e <= n, (f, e)
-            if tb & TASK:
-                size = e - f
-                assert size <= (512 if tb & MID else LEAF)
-                if not model_mids:
-                    tasks_done.append((f, e, d, depth & 1))
-                    hdr[2] += 1
-                    yield "task"
-                    continue
-                # pqf_leaf_task: the records of the depth's buffer, sorted in LDS (pb_model's
-                # thread model), ranges of 65-512 records queued as mid tasks (PqfDefer: the
-                # records back to the buffer, pend - 1, then the entry), outputs straight out
-                buf = bufs[depth & 1]
-                seg = [buf[i] for i in range(f, e)]
-                if tb & MID:
-                    mo, waves = block_sort(seg, depth0=d, defer=True)
-                    for (wf, wm, wd, wrecs) in waves:
-                        mo[wf:wf + wm] = wave_sort(wrecs, wd)
-                    for i in range(size):
-                        assert outk[f + i] is None, "output written twice"
-                        outk[f + i] = mo[i]
-                else:
-                    lo_, mids = block_sort(seg, depth0=d, wmax=512, defer=True)
-                    for i in range(size):
-                        if lo_[i] is not None:
-                            assert outk[f + i] is None, "output written twice"
-                            outk[f + i] = lo_[i]
-                    for (mf, mm, md, mrecs) in mids:
-                        for i in range(mm):
-                            buf[f + mf + i] = mrecs[i]
-                        hdr[2] -= 1
-                        kq = T0 + hdr[1]
-                        hdr[1] += 1
-                        entry(kq, f + mf, f + mf + mm, ((depth & 0xFF) << 8) | md, TASK | MID)
-                        yield "mid queued"
-                hdr[2] += 1
-                yield "task"
-                continue
             swap_entry = (w2 & KIND_SWAP) != 0
             q = (w2 >> 16) if swap_entry else t - tb
             T = tiles(f, e)
@@ -169,6 +128,7 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
                 yield "rangeword"
             w_ = rw[tb]
             nL, nR = (w_ >> 23) & RW_N, w_ & RW_N
+            tcut = 0                  # the tile's cut + 1 when its cutter is here
             if q == 0:
                 Eo[f] = E[m]
             for i in range(PQ_T):
@@ -199,36 +159,36 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
                 partner = min(max(partner, f), e - 1)
                 Eo[x] = vx if partner == x else (rf if partner == m else E[partner])
                 if cutter:
-                    assert cw[tb] == 0, "two cutters"
-                    cw[tb] = cw[tb] | (min(max(cut, f), e) + 1)
+                    assert tcut == 0, "two cutters in a tile"
+                    tcut = min(max(cut, f), e) + 1
             yield "swap"
-            done = sd[tb]
-            sd[tb] = done + 1
+            # one add per tile: count (bits 0-15), cut + 1 (16-39); the last tile reads both
+            add = 1 | (tcut << 16)
+            assert not (tcut and (sd[tb] >> 16) & 0xFFFFFF), "two cutters in a range"
+            sd[tb] = sd[tb] + add
+            tot = sd[tb]
+            done = (tot & 0xFFFF) - 1
             ch = [None] * 9
             nch = nt = first = 0
             if done == T - 1:
-                c = cw[tb]
+                c = (tot >> 16) & 0xFFFFFF
                 assert c and not (c >> 31)
                 cut = (c & 0x7FFFFFFF) - 1
                 lo, hi = (f, cut), (cut, e)
                 tc = [0, 0]
                 rg_ = [False, False]
-                lf = [False, False]
                 for cc in range(2):
                     rg_[cc] = hi[cc] - lo[cc] > CUT and d > 1 and not (depth_cap and depth + 1 >= depth_cap)
                     if rg_[cc]:
                         tc[cc] = tiles(lo[cc], hi[cc])
-                    lf[cc] = leaves_in_flow and not rg_[cc] and hi[cc] > lo[cc] and hi[cc] - lo[cc] <= LEAF
-                    if lf[cc]:
-                        tc[cc] = 1
                 if tc[0] + tc[1]:
                     first = T0 + hdr[1]
                     hdr[1] += tc[0] + tc[1]
                     assert first + tc[0] + tc[1] <= cap
                 for cc in range(2):
-                    if rg_[cc] or lf[cc]:
+                    if rg_[cc]:
                         ch[2 + 2 * nch] = lo[cc]
-                        ch[3 + 2 * nch] = hi[cc] | (0x80000000 if lf[cc] else 0)
+                        ch[3 + 2 * nch] = hi[cc]
                         ch[6 + nch] = tc[cc]
                         nch += 1
                         st["ranges"] += rg_[cc]
@@ -243,11 +203,7 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
                 for i in range(nt):
                     cc = 1 if (nch == 2 and i >= ch[6]) else 0
                     fb = first + (ch[6] if cc else 0)
-                    hi_ = ch[3 + 2 * cc]
-                    if hi_ >> 31:
-                        entry(first + i, ch[2 + 2 * cc], hi_ & 0x7FFFFFFF, w2c, TASK)
-                    else:
-                        entry(first + i, ch[2 + 2 * cc], hi_, w2c | ((first + i - fb) << 16), fb)
+                    entry(first + i, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c | ((first + i - fb) << 16), fb)
             yield "push"
 
     pool = [workgroup() for _ in range(grid)]
@@ -263,15 +219,14 @@ def flow_sort(E_in, grid=8, seed=0, leaves_in_flow=False, depth_cap=0, defer_p=0
         assert steps < 50_000_000, "no progress"
     assert hdr[2] == 1, hdr
     st["pend"] = hdr[2]
-    res = finish(n, bufs, leaflist, tasks_done, outk if model_mids else None)
-    return res, st
+    return finish(n, bufs, leaflist), st
 
 
-def finish(n, bufs, leaflist, tasks, outk=None):
-    """Every leaf (list or task) sorted with its budget from the buffer its depth left it in;
-    the leaves must tile [0, n) exactly (with the in-launch outputs outk, when modelled)."""
-    out = list(outk) if outk is not None else [None] * n
-    for (f, e, d, b) in leaflist + tasks:
+def finish(n, bufs, leaflist):
+    """Every leaf sorted with its budget from the buffer its depth left it in (lg_pcl_leaf); the
+    leaves must tile [0, n) exactly."""
+    out = [None] * n
+    for (f, e, d, b) in leaflist:
         seg = [bufs[b][i] for i in range(f, e)]
         srt = std_sort(seg, depth0=d)
         for i in range(f, e):

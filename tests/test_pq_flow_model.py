@@ -1,6 +1,6 @@
 """lg_pq_flow's queue and bookkeeping, modelled tile by tile on the CPU (tests/pqf_model.py):
 entries, look-back, range words, inline and deferred swaps, the children's slots, `pend` and
-the leaf tasks, under random interleavings of the workgroups' steps and small grids (ranges with
+the leaf list, under random interleavings of the workgroups' steps and small grids (ranges with
 more tiles than workgroups take the deferred path). The result must be libstdc++'s std::sort
 permutation (pb_model.std_sort) and the launch must drain with every ticket served."""
 import random
@@ -16,17 +16,17 @@ def _records(n, keys, seed):
     return [(rng.randrange(keys) << 32) | i for i in range(n)]
 
 
-@pytest.mark.parametrize("n,keys,grid,leaves,seed", [
-    (3000, 400, 4, False, 1),        # one cut: two leaves
-    (9000, 2000, 6, False, 2),       # children ranges, one of them cut again
-    (20000, 50, 5, False, 3),        # tie-heavy: long equal runs, uneven cuts
-    (20000, 20000, 3, True, 4),      # leaves as tasks; ranges of more tiles than workgroups
-    (40000, 5000, 16, True, 5),
-    (49128, 5400, 12, False, 6),     # C5's index_vector length
+@pytest.mark.parametrize("n,keys,grid,seed", [
+    (3000, 400, 4, 1),        # one cut: two leaves
+    (9000, 2000, 6, 2),       # children ranges, one of them cut again
+    (20000, 50, 5, 3),        # tie-heavy: long equal runs, uneven cuts
+    (20000, 20000, 3, 4),     # ranges of more tiles than workgroups: deferred swaps
+    (40000, 5000, 16, 5),
+    (49128, 5400, 12, 6),     # C5's index_vector length
 ])
-def test_flow_model_equals_std_sort(n, keys, grid, leaves, seed):
+def test_flow_model_equals_std_sort(n, keys, grid, seed):
     recs = _records(n, keys, seed)
-    got, st = flow_sort(recs, grid=grid, seed=seed, leaves_in_flow=leaves)
+    got, st = flow_sort(recs, grid=grid, seed=seed)
     assert got == std_sort(recs)
     assert st["pend"] == 1 and st["ranges"] >= 1
 
@@ -43,13 +43,3 @@ def test_flow_model_depth_cap_route5():
     recs = _records(30000, 3000, 11)
     got, st = flow_sort(recs, grid=8, seed=11, depth_cap=1)
     assert got == std_sort(recs) and st["ranges"] == 1
-
-
-@pytest.mark.parametrize("n,keys,seed", [(6000, 900, 21), (14000, 1500, 22)])
-def test_flow_model_leaf_and_mid_tasks(n, keys, seed):
-    """LG_PQ_MODE 2: leaves sorted inside the launch (pb_model's thread model of the LDS sort),
-    their 65-512-record ranges queued as mid tasks with the records handed back through the
-    buffer; every output written once, the launch drains with pend at 1."""
-    recs = _records(n, keys, seed)
-    got, st = flow_sort(recs, grid=6, seed=seed, leaves_in_flow=True, model_mids=True)
-    assert got == std_sort(recs) and st["pend"] == 1

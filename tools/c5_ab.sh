@@ -15,7 +15,7 @@ done
 for r in 1 2 3; do
   for v in default "$@"; do
     if [ $v = default ]; then L=""; else L=$R/lib_variants/$v/libcones_gpu.so; fi
-    echo -n "run $r $v: " 2>/dev/null
-    CONES_GPU_LIB=$L timeout -k 10 120 python tools/c5_run.py 200 || exit 1
+    echo -n "run $r $v: "
+    CONES_GPU_LIB=$L timeout -k 10 120 python tools/c5_run.py 200 2>> gpurun_out/c5_ab.err || exit 1
   done
 done

@@ -20,6 +20,6 @@ else
   head -1 gpurun_out/c5prof_gaps.txt; tail -1 gpurun_out/c5prof_launches.txt
   CG_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu --no-c5 \
       > gpurun_out/${tag}_gloo2.json 2> gpurun_out/${tag}_gloo2.err || { tail -20 gpurun_out/${tag}_gloo2.err; exit 1; }
-  bash tools/c5_ab.sh levels 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r6_c5_final_ab.txt
+  bash tools/c5_ab.sh levels 2>&1 | tee gpurun_out/r6_c5_final_ab.txt
   timeout -k 10 300 python bench.py --no-cpu --no-c2 --steps 5 --sustained-steps 0 --c5-tiled > gpurun_out/${tag}_c5tiled.json 2> gpurun_out/${tag}_c5tiled.err || { tail -20 gpurun_out/${tag}_c5tiled.err; exit 1; }
 fi
