@@ -214,7 +214,8 @@ struct LgScratch {
                               //   two sets of pq_tmax + 2, then two sets of PQ_MAXR range counts
     uint32_t pq_tmax;         //   tiles a level can have (lg_pq_level)
     uint64_t* pqf;            //   the dataflow partition's queue (lg_pq_flow): counters, entries,
-    uint32_t pqf_cap;         //   look-back, range and cut words for pqf_cap tickets
+    uint32_t pqf_cap;         //   look-back, range and count words for pqf_cap tickets
+    uint64_t* pqr;            //   the records beside the L and R lists (2 N words)
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
     uint32_t force_wait_fail; // diagnostics (cg_debug_route 10): the first partition level reports

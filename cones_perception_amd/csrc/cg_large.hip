@@ -1306,8 +1306,10 @@ __device__ __forceinline__ uint32_t pq_find(const uint32_t* tp, uint32_t nr, uin
 #define PQ_ST_A (1ull << 62)
 #define PQ_ST_P (1ull << 63)
 #define PQ_ST_V (~(PQ_ST_A | PQ_ST_P))
-__device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint32_t t, uint64_t count) {
+__device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint32_t t, uint64_t count,
+                                                uint32_t* fail = nullptr) {
     const uint32_t l = lane_id();
+    const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
     if (t == lo) {
         if (l == 0) __hip_atomic_store(&ts[t], PQ_ST_P | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
@@ -1322,6 +1324,12 @@ __device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint3
         const uint64_t pm = __ballot((w & PQ_ST_P) != 0ull);
         const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
         if (__ballot(w == 0ull && l < first)) {   // a tile before the nearest prefix not published yet
+            // (bounded: a tile that never publishes fails the frame, never the launch's end;
+            // 200 ms, never expected)
+            if (fail && __builtin_amdgcn_s_memrealtime() - t_0 > 20000000ull) {
+                if (l == 0) *fail = 1u;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -1753,29 +1761,34 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
 //     that finished the range it belongs to, as soon as that range's swaps are stored. A range
 //     starts when its parent ends, not when the slowest range of a level ends, and there are no
 //     empty levels: the sort takes as many dependent range steps as its deepest range needs;
-//   - entries are 16 bytes, (first, last) and (budget | kind | depth | tile, first ticket of the
-//     range), both halves nonzero once written (last >= 1, budget >= 2), stored by two sc1
-//     stores and polled by two sc1 loads (a half not yet written reads 0);
+//   - a range's first tile reserves, as it starts, the block of T + 1 tickets its children will
+//     take (their tiles number at most T + 1) and adds the block's base to the range's count
+//     word; the range's last tile reads the base with the count and the cut in one atomic
+//     (PQF_SD_BASE) and publishes every slot of the block: the children's tiles, then nops. The
+//     end of a range costs no allocation;
+//   - entries are 16 bytes, (first, last) and (budget | nop | kind | depth | tile, first ticket of
+//     the range), both halves nonzero once written, stored by two sc1 stores and polled by two
+//     sc1 loads (a half not yet written reads 0);
+//   - the lists hold each element's record beside its position, so a swap loads its partner's
+//     record with the partner's position: one round of loads;
 //   - a tile's workgroup keeps its split state in registers and runs the tile's swaps itself
 //     when every ticket of its range has been handed out (the ticket counter has passed them:
 //     every tile of the range is held by a running workgroup, which never waits on a later
 //     ticket). Otherwise it leaves its state in HBM (S.vox) and queues a swap entry for the
 //     tile at the end of the queue, whose holder waits for the range word instead;
-//   - a range's last tile to finish its swaps (one agent-scope count per range) reads the cut
-//     the cutter or'ed into the range's cut word and queues the children: ranges longer than
-//     LG_PCL_CUT with budget left as new tickets, the others on lg_pcl_leaf's list;
-//   - the launch ends when every range is finished: `pend` = ranges finished - ranges queued
-//     reaches 1 (range 0 is not queued; a range counts its end and its children in one add
-//     before the children are published). A workgroup whose ticket has no entry yet polls the
-//     entry and `pend` together and exits at 1.
+//   - the launch ends when every record is in a leaf: the tile that ends a range adds its leaf
+//     children's records to PQF_DONE, and a workgroup whose ticket has no entry yet polls the
+//     entry and that count together and leaves at n (a range still queued holds records that
+//     are in no leaf, so no ordering with the entries is needed).
 // Forward progress: a tile waits only on tickets below its own (look-back), or on a range all
 // of whose tickets are held; a workgroup without an entry waits on workgroups with lower
-// tickets. So the launch drains whatever the grid size and residency.
+// tickets. So the launch drains whatever the grid size and residency; every wait is bounded
+// (200 ms, never expected: the frame then fails with CG_E_DEVICE, LG_PQ_TIMEOUT).
 // Visibility: every cross-workgroup byte (records, lists, swap state, entries, words) is stored
 // sc1 (st_rlx / st64 / agent-scope atomics) after which the storing waves wait vmcnt(0) before
 // the barrier and the one signalling add or entry store, and loaded sc1 (ld_rlx / ld64):
 // MI355X_MICROARCH.md's hand-off table, row 1. lg_pcl_leaf clears the used words and lg_pcl_mid
-// the counters, so the next frame finds them zero.
+// the counters, so the next frame finds them zero. (tests/pqf_model.py models it tile by tile.)
 #ifndef LG_FLOW_GRID
 // workgroups of the launch: 192 measured best on C5 (235-238 us per frame against 237-241 at 128
 // and 256, 266-270 at 512 before the counters had lines of their own, profiles/r6_c5_flow_ab.txt)
@@ -1784,11 +1797,12 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
 #define LG_CLEAR_FLOW 0x100u   // lg_pcl_leaf's clear_set for lg_pq_flow's words
 #define PQF_HDR 48         // u64 words, the counters on lines of their own (they take every
                            // workgroup's atomics and polls): [PQF_TK] tickets handed out,
-                           // [PQF_TAIL] tickets queued past range 0's, [PQF_PEND] pend
+                           // [PQF_TAIL] tickets queued past range 0's, [PQF_DONE] records in leaves
 #define PQF_TK 0
 #define PQF_TAIL 16
-#define PQF_PEND 32
+#define PQF_DONE 32
 #define PQF_KIND_SWAP (1u << 7)
+#define PQF_NOP (1u << 6)  // an unused slot of a children block (budgets take bits 0-5)
 struct PqfView {
     uint64_t* hdr; uint64_t* ent; uint64_t* lb; uint64_t* rw; uint64_t* sd; uint32_t cap;
 };
@@ -1799,9 +1813,7 @@ __device__ __forceinline__ PqfView pqf_view(const LgScratch& S) {
     v.ent = S.pqf + PQF_HDR;      // two words per ticket
     v.lb = v.ent + 2ull * v.cap;  // look-back status per ticket
     v.rw = v.lb + v.cap;          // range word, by the range's first ticket
-    v.sd = v.rw + v.cap;          // by first ticket: tiles whose swaps are stored (bits 0-15), the
-                                  // cut + 1 (16-39, added by the cutter's tile), tiles whose wait
-                                  // gave up (40-63): one add per tile, the last one reads it all
+    v.sd = v.rw + v.cap;          // by first ticket: the range's count word (PQF_SD_BASE)
     return v;
 }
 __device__ __forceinline__ uint32_t pqf_tiles(uint32_t f, uint32_t e) { return (e - f - 1 + PQ_T - 1) / PQ_T; }
@@ -1867,7 +1879,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leaf(LgScratch S, uint64_t* E
     if (blockIdx.x == 0 && tid == 0 && !clear_set) S.pqst[0] = 0;
     if (clear_set == LG_CLEAR_FLOW) {
         const PqfView Q = pqf_view(S);
-        const uint32_t used = (uint32_t)min(Q.hdr[PQF_TK], (uint64_t)Q.cap);
+        // every ticket handed out, and every slot allocated (nop slots published for a block
+        // the workgroups never reached before the launch ended)
+        const uint64_t n_ = S.meta[LG_PCL_N];
+        const uint64_t alloc = n_ > LG_PCL_CUT ? 2ull * ((n_ - 1 + PQ_T - 1) / PQ_T) + Q.hdr[PQF_TAIL] : 0ull;
+        const uint32_t used = (uint32_t)min(max(Q.hdr[PQF_TK], alloc), (uint64_t)Q.cap);
         for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < used; i += gridDim.x * CG_BLOCK) {
             Q.ent[2ull * i] = 0ull; Q.ent[2ull * i + 1] = 0ull;
             Q.lb[i] = 0ull; Q.rw[i] = 0ull; Q.sd[i] = 0ull;
@@ -1945,13 +1961,17 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
 }
 #define PQF_WAIT_TICKS PQ_WAIT_TICKS
 #define PQF_SD_BAD 0xffffffffu   // tcut of a tile whose range wait gave up
+// the per-range count word (Q.sd): tiles whose swaps are stored (bits 0-15), the cut + 1 (16-38,
+// from the cutter's tile), the children block's base ticket (39-62, from the first tile as it
+// starts), a wait that gave up (63): one add per tile, the last one reads it all
+#define PQF_SD_BASE 39
 __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap) {
     __shared__ uint32_t cg[WAVES], cl[WAVES];
     __shared__ uint64_t tbase;
-    __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the tile's decisions
+    __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the inline decision
     __shared__ uint32_t tcut;    // the tile's cut + 1 (its cutter), PQF_SD_BAD, or 0
-    __shared__ uint32_t ch[9];   // children: [0] count, [1] first ticket, [2..5] their (first, last),
-                                 // [6..7] their tickets, [8] this workgroup finished the range
+    __shared__ uint32_t ch[9];   // children: [0] count, [1] block base, [2..5] their (first, last),
+                                 // [6..7] their tiles, [8] this workgroup finished the range
     const PqfView Q = pqf_view(S);
     const uint32_t tid = threadIdx.x, l = lane_id(), w = wave_id();
     const uint32_t n = S.meta[LG_PCL_N];
@@ -1962,10 +1982,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
     const uint32_t T0 = pqf_tiles(0, n);
     const uint32_t d0 = (uint32_t)(2 * cg_lg((long)n));
     uint64_t* const vst = (uint64_t*)S.vox;   // a deferred tile's per-element state: gi << 32 | li
+    uint64_t* const recL = S.pqr;             // the records of the L / R lists, beside their positions
+    uint64_t* const recR = S.pqr + n;
     for (;;) {
         if (tid == 0) {   // the next ticket and its entry
             const uint32_t t = (uint32_t)__hip_atomic_fetch_add(&Q.hdr[PQF_TK], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t ok = 1, f = 0, e = n, w2 = d0 | (t << 16), tb = 0;   // (range 0: budget d0, depth 0, tile t)
+            // (range 0: budget d0, depth 0, its swap slots at [T0, 2 T0))
+            uint32_t ok = 1, f = 0, e = n, w2 = d0 | (T0 << 16), tb = 0;
             if (t >= T0) {
                 if (t >= Q.cap) {
                     ok = 0;   // (past every ticket the sort can queue: nothing will be published here)
@@ -1974,19 +1997,19 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                     for (uint32_t it = 0;; it++) {
                         const uint64_t a = ld64(Q.ent + 2ull * t), b = ld64(Q.ent + 2ull * t + 1);
                         // (every fourth poll: one line that every waiting workgroup reads)
-                        const int64_t pend = (it & 3u) == 3u ? (int64_t)ld64(&Q.hdr[PQF_PEND]) : 0;
+                        const uint64_t placed = (it & 3u) == 3u ? ld64(&Q.hdr[PQF_DONE]) : 0ull;
                         if (a && b) {
                             f = (uint32_t)a; e = (uint32_t)(a >> 32); w2 = (uint32_t)b; tb = (uint32_t)(b >> 32);
-                            // (never expected) an entry that does not describe a range or task of
-                            // this index_vector: the frame fails, no index is formed from it
+                            // (never expected) an entry that does not describe a range of this
+                            // index_vector: the frame fails, no index is formed from it
                             if (!(f < e && e <= n && tb < Q.cap &&
-                                  ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tb) < pqf_tiles(f, e))) {
+                                  ((w2 & PQF_NOP) || ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tb) < pqf_tiles(f, e)))) {
                                 S.meta[LG_PQ_TIMEOUT] = 1u;
                                 ok = 0;
                             }
                             break;
                         }
-                        if (pend == 1) { ok = 0; break; }   // every range finished
+                        if (placed >= n) { ok = 0; break; }   // every record is in a leaf: the sort is done
                         if (__builtin_amdgcn_s_memrealtime() - t_0 > PQF_WAIT_TICKS) {   // (never expected)
                             S.meta[LG_PQ_TIMEOUT] = 1u;
                             ok = 0;
@@ -2001,12 +2024,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
         __syncthreads();
         if (!es[0]) return;
         const uint32_t f = es[1], e = es[2], w2 = es[3], tb = es[4], t = es[5];
-        const uint32_t d = w2 & 0x7fu, depth = (w2 >> 8) & 0xffu;
+        if (w2 & PQF_NOP) continue;   // (uniform) an unused slot of a children block
+        const uint32_t d = w2 & 0x3fu, depth = (w2 >> 8) & 0xffu;
         const bool swap_entry = (w2 & PQF_KIND_SWAP) != 0;
         const uint32_t q = swap_entry ? (w2 >> 16) : t - tb;
+        const uint32_t off = swap_entry ? 0u : (w2 >> 16);   // a split entry: the range's swap slots at tb + off
         const uint32_t T = pqf_tiles(f, e);
         const uint64_t* const E = (depth & 1u) ? E1 : E0;
         uint64_t* const Eo = (depth & 1u) ? E0 : E1;
+        // the range's first tile reserves the block its children will be queued in as it starts
+        // (off the critical path; the base rides in the range's count word to the tile that ends
+        // the range): T + 1 slots for the children's tiles (they number at most T + 1), then T + 1
+        // for their swap slots
+        if (!swap_entry && q == 0 && tid == 0) {
+            const uint64_t base = 2ull * T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 2ull * ((uint64_t)T + 1ull),
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&Q.sd[tb], min(base, (uint64_t)Q.cap) << PQF_SD_BASE, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
         // the median of three and this element's record in one batch of loads: x > f, and x's
         // virtual record is E[f] when x is the median (__move_median_to_first's swap)
         const uint32_t x = f + 1 + q * PQ_T + tid;
@@ -2020,10 +2055,13 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
         const uint64_t handed = (!swap_entry && tid == 0) ? ld64(&Q.hdr[PQF_TK]) : 0ull;
         const uint32_t m = pb_median(a, b, c, ka, kb, kc);
         const uint32_t p = m == a ? ka : (m == b ? kb : kc);
+        const uint64_t vx = x == m ? rf : rx;
         uint32_t gi = 0, li = 0;
         if (!swap_entry) {
             // split: >= / <= counts, the range's look-back over its tiles' tickets, the lists
-            const uint32_t k = valid ? (x == m ? pcl_key(rf) : pcl_key(rx)) : 0u;
+            // (positions and, beside them, the records: a swap then reads its partner's record
+            // with the partner's position, one round of loads)
+            const uint32_t k = valid ? pcl_key(vx) : 0u;
             const bool ge = valid && k >= p, le = valid && k <= p;
             const uint64_t gm = __ballot(ge), lm = __ballot(le);
             if (l == 0) { cg[w] = (uint32_t)__popcll(gm); cl[w] = (uint32_t)__popcll(lm); }
@@ -2031,31 +2069,33 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             uint32_t tg = 0, tl = 0;
             for (uint32_t v = 0; v < WAVES; v++) { tg += cg[v]; tl += cl[v]; }
             if (w == 0) {
-                const uint64_t bs = pq_lookback(Q.lb, tb, t, ((uint64_t)tg << 32) | tl);
+                const uint64_t bs = pq_lookback(Q.lb, tb, t, ((uint64_t)tg << 32) | tl, S.meta + LG_PQ_TIMEOUT);
                 if (l == 0) tbase = bs;
             }
             __syncthreads();
             gi = (uint32_t)(tbase >> 32) + mbcnt(gm);
             li = (uint32_t)tbase + mbcnt(lm);
             for (uint32_t v = 0; v < w; v++) { gi += cg[v]; li += cl[v]; }
-            if (ge) st_rlx(S.par + f + 1 + gi, x);
-            if (le) st_rlx(S.cnt + f + 1 + li, x);
+            if (ge) { st_rlx(S.par + f + 1 + gi, x); st64(recL + f + 1 + gi, vx); }
+            if (le) { st_rlx(S.cnt + f + 1 + li, x); st64(recR + f + 1 + li, vx); }
             __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): the lists are stored
             __syncthreads();
+            const uint32_t slot = tb + off + q;   // the tile's swap slot
             if (tid == 0) {
                 __hip_atomic_fetch_add(&Q.rw[tb], PQ_RW_TILE | ((uint64_t)tg << 23) | tl, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                // the swaps here only when every ticket of the range is held (or done)
+                // the swaps here only when every ticket of the range is held (or done); the swap
+                // slot then takes a nop
                 es[6] = handed >= (uint64_t)tb + T ? 1u : 0u;
+                if (es[6] && slot < Q.cap) pqf_entry(Q, slot, 0u, 1u, PQF_NOP, 0u);
             }
             __syncthreads();
-            if (!es[6]) {   // defer: the state to HBM, a swap entry at the end of the queue
+            if (!es[6]) {   // defer: the state to HBM, a swap entry in the tile's swap slot
                 if (valid) st64(vst + x, ((uint64_t)gi << 32) | li);
                 __builtin_amdgcn_s_waitcnt(0x0070);
                 __syncthreads();
                 if (tid == 0) {
-                    const uint64_t kq = T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (kq < Q.cap) pqf_entry(Q, kq, f, e, (w2 & 0xffffu) | PQF_KIND_SWAP | (q << 16), tb);
+                    if (slot < Q.cap) pqf_entry(Q, slot, f, e, (w2 & 0xffffu) | PQF_KIND_SWAP | (q << 16), tb);
                     else S.meta[LG_PQ_TIMEOUT] = 1u;   // (the capacity bounds every queue: never expected)
                 }
                 __syncthreads();
@@ -2089,30 +2129,38 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             if (q == 0 && tid == 0) {
                 st64(Eo + f, rf);
                 pq_push(S, PQ_LEAFLIST, f, e, d - 1u, (depth + 1u) & 1u);
+                __hip_atomic_fetch_add(&Q.hdr[PQF_DONE], (uint64_t)(e - f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (tid == 0) tcut = PQF_SD_BAD;
+            if (tid == 0) {
+                tcut = PQF_SD_BAD;
+                // (before the tile's count add, same address: the range's last tile sees it)
+                __hip_atomic_fetch_or(&Q.sd[tb], 1ull << 63, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
             const uint32_t nL = (uint32_t)(rw >> 23) & (uint32_t)PQ_RW_N, nR = (uint32_t)rw & (uint32_t)PQ_RW_N;
             if (q == 0 && tid == 0) st64(Eo + f, ld64((uint64_t*)E + m));
             if (valid) {
-                const uint64_t vx = x == m ? rf : rx;
                 const uint32_t k = pcl_key(vx);
                 const bool ge = k >= p, le = k <= p;
-                // the partners and the next pair in one batch of loads (indices clamped when unused)
+                // the partners (position and record) and the next pair in one batch of loads
+                // (indices clamped when unused)
                 const bool hasL = ge && gi < nR;
                 const bool nx = hasL && gi + 1 < min(nL, nR);
                 const uint32_t ri = nR - 1 - li;
                 const bool hasR = le && ri < nL;
-                const uint32_t jj = ld_rlx(S.cnt + f + 1 + (hasL ? nR - 1 - gi : 0u));   // R_gi
-                const uint32_t l2 = ld_rlx(S.par + f + 1 + (gi + 1 < nL ? gi + 1 : 0u));  // L_gi+1
-                const uint32_t r2 = ld_rlx(S.cnt + f + 1 + (nx ? nR - 2 - gi : 0u));      // R_gi+1
-                const uint32_t il = ld_rlx(S.par + f + 1 + (hasR ? ri : 0u));             // L_ri
-                uint32_t partner = x;
+                const uint32_t iR = f + 1 + (hasL ? nR - 1 - gi : 0u), iL = f + 1 + (hasR ? ri : 0u);
+                const uint32_t jj = ld_rlx(S.cnt + iR);                                           // R_gi
+                const uint64_t rjj = ld64(recR + iR);
+                const uint32_t l2 = ld_rlx(S.par + f + 1 + (gi + 1 < nL ? gi + 1 : 0u));          // L_gi+1
+                const uint32_t r2 = ld_rlx(S.cnt + f + 1 + (nx ? nR - 2 - gi : 0u));              // R_gi+1
+                const uint32_t il = ld_rlx(S.par + iL);                                           // L_ri
+                const uint64_t ril = ld64(recL + iL);
+                uint64_t rec = vx;
                 bool cutter = false;
                 uint32_t cut = 0;
                 if (hasL) {
                     if (x < jj) {
-                        partner = jj;
+                        rec = rjj;
                         if (!nx || !(l2 < r2)) {   // swap gi is the last: s = gi + 1
                             cutter = true;
                             cut = min(gi + 1 < nL ? l2 : 0xffffffffu, jj);
@@ -2122,73 +2170,74 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                         cut = x;
                     }
                 }
-                if (hasR && il < x) partner = il;
-                partner = min(max(partner, f), e - 1u);   // (defensive: list entries lie in (f, e))
-                st64(Eo + x, partner == x ? vx : (partner == m ? rf : ld64((uint64_t*)E + partner)));
+                if (hasR && il < x) rec = ril;
+                st64(Eo + x, rec);
                 if (cutter) tcut = min(max(cut, f), e) + 1u;
             }
         }
-        // the tile's swaps are stored; the range's last tile queues the children
+        // the tile's swaps are stored; the range's last tile queues the children in the block
         __builtin_amdgcn_s_waitcnt(0x0070);
         __syncthreads();
         if (tid == 0) {
-            // one add per tile: its count, the cut if the cutter is here, a wait that gave up
-            const uint64_t add = 1ull | (tcut == PQF_SD_BAD ? (1ull << 40) : ((uint64_t)tcut << 16));
+            // one add per tile: its count, and the cut when the cutter is here; the first tile
+            // added the children block's base when it started
+            const uint64_t add = 1ull | (tcut == PQF_SD_BAD ? 0ull : ((uint64_t)tcut << 16));
             const uint64_t tot = __hip_atomic_fetch_add(&Q.sd[tb], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
             const uint32_t done = (uint32_t)(tot & 0xffffull) - 1u;
-            uint32_t nch = 0, nt = 0, first = 0;
+            const uint32_t base = (uint32_t)((tot >> PQF_SD_BASE) & 0xffffffull);
+            uint32_t nch = 0;
             if (done == T - 1u) {
-                const uint32_t cw = (uint32_t)((tot >> 16) & 0xffffffull);
-                const uint32_t cut = cw - 1u;
-                const bool bad = (tot >> 40) != 0ull;
-                if (!bad && cw) {
+                // no children after a wait that gave up (the range went to the leaves whole)
+                const uint32_t cw = (tot >> 63) ? 0u : (uint32_t)((tot >> 16) & 0x7fffffull);
+                const bool fits = (uint64_t)base + 2ull * (T + 1u) <= Q.cap;
+                uint32_t placed = 0;
+                if (cw) {
+                    const uint32_t cut = cw - 1u;
                     const uint32_t lo[2] = {f, cut}, hi[2] = {cut, e};
-                    uint32_t tc[2] = {0, 0};
-                    bool rng[2];
+                    uint32_t used = 0;
                     for (int cc = 0; cc < 2; cc++) {
-                        rng[cc] = hi[cc] - lo[cc] > LG_PCL_CUT && d > 1 && !(depth_cap && depth + 1u >= depth_cap);
-                        if (rng[cc]) tc[cc] = pqf_tiles(lo[cc], hi[cc]);
-                    }
-                    if (tc[0] + tc[1]) {
-                        first = T0 + (uint32_t)__hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], (uint64_t)(tc[0] + tc[1]), __ATOMIC_RELAXED,
-                                                                     __HIP_MEMORY_SCOPE_AGENT);
-                        if ((uint64_t)first + tc[0] + tc[1] > Q.cap) {   // (never expected) the leaves finish them in HBM
-                            rng[0] = rng[1] = false;
-                            tc[0] = tc[1] = 0;
-                        }
-                    }
-                    for (int cc = 0; cc < 2; cc++) {
-                        if (rng[cc]) {
+                        const uint32_t tcc = pqf_tiles(lo[cc], hi[cc]);
+                        const bool rng = hi[cc] - lo[cc] > LG_PCL_CUT && d > 1 && !(depth_cap && depth + 1u >= depth_cap) &&
+                                         fits;   // (a block past the capacity: the leaves finish it in HBM)
+                        if (rng) {
                             ch[2 + 2 * nch] = lo[cc]; ch[3 + 2 * nch] = hi[cc];
-                            ch[6 + nch] = tc[cc];
+                            ch[6 + nch] = tcc;
+                            used += tcc;
                             nch++;
                         } else {
                             pq_push(S, PQ_LEAFLIST, lo[cc], hi[cc], d - 1u, (depth + 1u) & 1u);
+                            placed += hi[cc] - lo[cc];
                         }
                     }
-                    nt = tc[0] + tc[1];
-                } else if (!bad) {
-                    S.meta[LG_PQ_TIMEOUT] = 1u;   // (no cut stored: never expected)
+                } else {
+                    S.meta[LG_PQ_TIMEOUT] = 1u;   // (no cut stored, or a wait gave up: never expected)
                 }
-                // the range's end and its queued children in one count, performed before any
-                // child is published: `pend` cannot read 1 while a child is outstanding (a child
-                // that finished before this count would otherwise let waiting workgroups leave
-                // with tickets the grandchildren are then queued on)
-                __hip_atomic_fetch_add(&Q.hdr[PQF_PEND], (uint64_t)(int64_t)(1 - (int)nch), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_s_waitcnt(0x0070);
+                // records now in leaves: the launch ends when every record is (no ordering with
+                // the children's entries needed: a child range holds records that are not)
+                if (placed)
+                    __hip_atomic_fetch_add(&Q.hdr[PQF_DONE], (uint64_t)placed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            ch[0] = nch; ch[1] = first; es[7] = nt;
+            ch[0] = nch; ch[1] = base;
             ch[8] = done == T - 1u ? 1u : 0u;
         }
         __syncthreads();
         if (ch[8]) {   // (uniform) this workgroup finished the range
-            const uint32_t nch = ch[0], first = ch[1], nt = es[7];
-            const uint32_t w2c = (d - 1u) | ((depth + 1u) << 8);
-            for (uint32_t i = tid; i < nt; i += CG_BLOCK) {
-                const uint32_t cc = (nch == 2 && i >= ch[6]) ? 1u : 0u;
-                const uint32_t fb = first + (cc ? ch[6] : 0u);   // the child's first ticket
-                pqf_entry(Q, first + i, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c | ((first + i - fb) << 16), fb);
+            const uint32_t nch = ch[0], base = ch[1];
+            const uint32_t used = (nch > 0 ? ch[6] : 0u) + (nch > 1 ? ch[7] : 0u);
+            // split slots [base, base + T + 1): the children's tiles (their swap slots T + 1 on),
+            // then nops; swap slots [base + T + 1, base + 2 T + 2): the children's tiles publish
+            // their own, the rest are nops
+            const uint32_t w2c = (d - 1u) | ((depth + 1u) << 8) | ((T + 1u) << 16);
+            for (uint32_t i = tid; i < 2u * (T + 1u); i += CG_BLOCK) {
+                const uint32_t k = base + i;
+                if (k >= Q.cap) break;
+                if (i < used) {
+                    const uint32_t cc = (nch == 2 && i >= ch[6]) ? 1u : 0u;
+                    const uint32_t fb = base + (cc ? ch[6] : 0u);   // the child's first ticket
+                    pqf_entry(Q, k, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c, fb);
+                } else if (i < T + 1u || i >= T + 1u + used) {
+                    pqf_entry(Q, k, 0u, 1u, PQF_NOP, 0u);
+                }
             }
         }
         __syncthreads();   // (es and ch are rewritten for the next ticket)
@@ -3547,7 +3596,8 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(30, take((LG_PQ_HDR + 4 * PQ_EW * LG_PQ_CAP) * 4));   // PCL sort range lists
     // their look-back words: two sets (tickets, finished, one per tile) and the range counts
     place(31, take((2 * (2 + lg_pq_tmax(N)) + 2 * PQ_MAXR + 16) * 8));   // + lg_arrivals' words
-    place(32, take(PQF_HDR * 8 + lg_pqf_cap(N) * 40));   // lg_pq_flow: 16 + 8 + 8 + 4 + 4 B per ticket
+    place(32, take(PQF_HDR * 8 + lg_pqf_cap(N) * 40));   // lg_pq_flow: 16 + 8 + 8 + 8 B per ticket
+    place(33, take(N * 16));                               // lg_pq_flow: the lists' records
     return off;
 }
 }  // namespace
@@ -3577,6 +3627,7 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 30: S.pq = (uint32_t*)p; S.pq_cap = LG_PQ_CAP; break;
             case 31: S.pqst = (uint64_t*)p; S.pq_tmax = (uint32_t)lg_pq_tmax(std::max<uint32_t>(n, 1)); break;
             case 32: S.pqf = (uint64_t*)p; S.pqf_cap = (uint32_t)lg_pqf_cap(std::max<uint32_t>(n, 1)); break;
+            case 33: S.pqr = (uint64_t*)p; break;
 
             default: *arr[k - 16] = (uint32_t*)p; break;
         }

@@ -17,6 +17,8 @@ LEAF = 4096           # LG_PCL_LEAF
 TILE = 1 << 46        # PQ_RW_TILE
 RW_N = (1 << 23) - 1  # PQ_RW_N
 KIND_SWAP = 1 << 7
+NOP = 1 << 6
+SD_BASE = 39          # PQF_SD_BASE
 M32 = 0xFFFFFFFF
 
 
@@ -43,14 +45,20 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
     sd = Arr(cap)
     par = Arr(n + 2)
     cnt = Arr(n + 2)
+    recL = Arr(n + 2)
+    recR = Arr(n + 2)
     vst = Arr(n)
-    hdr = [0, 0, 0]        # tickets handed out, queued past T0, pend
-    st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0}
+    hdr = [0, 0, 0]        # tickets handed out, queued past T0, records in leaves
+    st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0, "nops": 0}
 
     def entry(k, f, e, w2, tb):
         assert 0 <= k < cap
+        assert ent[2 * k] == 0 and ent[2 * k + 1] == 0, "a ticket published twice"
         ent[2 * k] = (e << 32) | f
         ent[2 * k + 1] = (tb << 32) | w2
+
+    def push_leaf(f, e, d, b):
+        leaflist.append((f, e, d, b))
 
     # a workgroup is a generator: it yields when it waits (for an entry or a range word)
     def workgroup():
@@ -58,7 +66,7 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
             t = hdr[0]
             hdr[0] += 1
             st["tickets"] = max(st["tickets"], hdr[0])
-            f, e, w2, tb = 0, n, d0 | (t << 16), 0
+            f, e, w2, tb = 0, n, d0 | (T0 << 16), 0   # (range 0: its swap slots at [T0, 2 T0))
             if t >= T0:
                 if t >= cap:
                     return
@@ -67,15 +75,23 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
                     if a and b:
                         f, e, w2, tb = a & M32, a >> 32, b & M32, b >> 32
                         break
-                    if hdr[2] == 1:
+                    if hdr[2] >= n:
                         return
                     yield "entry"
-            d, depth = w2 & 0x7F, (w2 >> 8) & 0xFF
             assert f < e <= n, (f, e)
+            if w2 & NOP:
+                st["nops"] += 1
+                continue
+            d, depth = w2 & 0x3F, (w2 >> 8) & 0xFF
             swap_entry = (w2 & KIND_SWAP) != 0
             q = (w2 >> 16) if swap_entry else t - tb
+            off = 0 if swap_entry else w2 >> 16   # split entries: the range's swap slots at tb + off
             T = tiles(f, e)
             assert 0 <= q < T
+            if not swap_entry and q == 0:   # the children block, reserved as the range starts
+                base = 2 * T0 + hdr[1]
+                hdr[1] += 2 * (T + 1)
+                sd[tb] = sd[tb] + (min(base, cap) << SD_BASE)
             E, Eo = bufs[depth & 1], bufs[(depth + 1) & 1]
             a_, b_, c_ = f + 1, f + (e - f) // 2, e - 1
             m = _pb_median(a_, b_, c_, key(E[a_]), key(E[b_]), key(E[c_]))
@@ -84,10 +100,12 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
             xs = [f + 1 + q * PQ_T + tid for tid in range(PQ_T)]
             valid = [x < e for x in xs]
             rx = [E[x] if v else E[f] for x, v in zip(xs, valid)]
+            vx = [rf if x == m else r for x, r in zip(xs, rx)]
+            handed = hdr[0]
             gi = [0] * PQ_T
             li = [0] * PQ_T
             if not swap_entry:
-                k_ = [(key(rf) if x == m else key(r)) if v else 0 for x, r, v in zip(xs, rx, valid)]
+                k_ = [key(r) if v else 0 for r, v in zip(vx, valid)]
                 ge = [v and k >= p for k, v in zip(k_, valid)]
                 le = [v and k <= p for k, v in zip(k_, valid)]
                 tg, tl = sum(ge), sum(le)
@@ -102,22 +120,26 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
                     gi[i], li[i] = bg + rg, bl + rl
                     if ge[i]:
                         par[f + 1 + gi[i]] = xs[i]
+                        recL[f + 1 + gi[i]] = vx[i]
                         rg += 1
                     if le[i]:
                         cnt[f + 1 + li[i]] = xs[i]
+                        recR[f + 1 + li[i]] = vx[i]
                         rl += 1
                 rw[tb] = rw[tb] + (TILE | (tg << 23) | tl)
                 yield "split"
-                inline = hdr[0] >= tb + T and rng.random() >= defer_p
+                inline = handed >= tb + T and rng.random() >= defer_p
+                slot = tb + off + q           # the tile's swap slot
                 if not inline:
                     for i in range(PQ_T):
                         if valid[i]:
                             vst[xs[i]] = (gi[i] << 32) | li[i]
-                    kq = T0 + hdr[1]
-                    hdr[1] += 1
-                    entry(kq, f, e, (w2 & 0xFFFF) | KIND_SWAP | (q << 16), tb)
+                    if slot < cap:
+                        entry(slot, f, e, (w2 & 0xFFFF) | KIND_SWAP | (q << 16), tb)
                     st["deferred"] += 1
                     continue
+                if slot < cap:
+                    entry(slot, 0, 1, NOP, 0)
                 st["inline"] += 1
             else:
                 for i in range(PQ_T):
@@ -135,76 +157,87 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
                 x = xs[i]
                 if not valid[i]:
                     continue
-                vx = rf if x == m else rx[i]
-                k = key(vx)
+                k = key(vx[i])
                 ge, le = k >= p, k <= p
                 hasL = ge and gi[i] < nR
                 nx = hasL and gi[i] + 1 < min(nL, nR)
                 ri = (nR - 1 - li[i]) & M32
                 hasR = le and ri < nL
-                jj = cnt[f + 1 + (nR - 1 - gi[i] if hasL else 0)]
+                iR = f + 1 + (nR - 1 - gi[i] if hasL else 0)
+                iL = f + 1 + (ri if hasR else 0)
+                jj, rjj = cnt[iR], recR[iR]
                 l2 = par[f + 1 + (gi[i] + 1 if gi[i] + 1 < nL else 0)]
                 r2 = cnt[f + 1 + (nR - 2 - gi[i] if nx else 0)]
-                il = par[f + 1 + (ri if hasR else 0)]
-                partner, cutter, cut = x, False, 0
+                il, ril = par[iL], recL[iL]
+                rec, cutter, cut = vx[i], False, 0
                 if hasL:
                     if x < jj:
-                        partner = jj
+                        rec = rjj
+                        assert rjj == (rf if jj == m else E[jj]), "list record != the partner's"
                         if not nx or not l2 < r2:
                             cutter, cut = True, min(l2 if gi[i] + 1 < nL else M32, jj)
                     elif gi[i] == 0:
                         cutter, cut = True, x
                 if hasR and il < x:
-                    partner = il
-                partner = min(max(partner, f), e - 1)
-                Eo[x] = vx if partner == x else (rf if partner == m else E[partner])
+                    rec = ril
+                    assert ril == (rf if il == m else E[il]), "list record != the partner's"
+                Eo[x] = rec
                 if cutter:
                     assert tcut == 0, "two cutters in a tile"
                     tcut = min(max(cut, f), e) + 1
             yield "swap"
-            # one add per tile: count (bits 0-15), cut + 1 (16-39); the last tile reads both
+            # one add per tile: count, and the cut from the cutter's tile; the base came first
             add = 1 | (tcut << 16)
-            assert not (tcut and (sd[tb] >> 16) & 0xFFFFFF), "two cutters in a range"
+            assert not (tcut and (sd[tb] >> 16) & 0x7FFFFF), "two cutters in a range"
             sd[tb] = sd[tb] + add
             tot = sd[tb]
             done = (tot & 0xFFFF) - 1
-            ch = [None] * 9
-            nch = nt = first = 0
+            base = (tot >> SD_BASE) & 0xFFFFFF
+            ch = [None] * 10
+            nch = 0
             if done == T - 1:
-                c = (tot >> 16) & 0xFFFFFF
-                assert c and not (c >> 31)
-                cut = (c & 0x7FFFFFFF) - 1
+                cw = 0 if tot >> 63 else (tot >> 16) & 0x7FFFFF
+                assert cw
+                fits = base + 2 * (T + 1) <= cap
+                cut = cw - 1
                 lo, hi = (f, cut), (cut, e)
-                tc = [0, 0]
-                rg_ = [False, False]
+                used = placed = 0
                 for cc in range(2):
-                    rg_[cc] = hi[cc] - lo[cc] > CUT and d > 1 and not (depth_cap and depth + 1 >= depth_cap)
-                    if rg_[cc]:
-                        tc[cc] = tiles(lo[cc], hi[cc])
-                if tc[0] + tc[1]:
-                    first = T0 + hdr[1]
-                    hdr[1] += tc[0] + tc[1]
-                    assert first + tc[0] + tc[1] <= cap
-                for cc in range(2):
-                    if rg_[cc]:
+                    tcc = tiles(lo[cc], hi[cc])
+                    r_ = hi[cc] - lo[cc] > CUT and d > 1 and not (depth_cap and depth + 1 >= depth_cap) and fits
+                    if r_:
                         ch[2 + 2 * nch] = lo[cc]
                         ch[3 + 2 * nch] = hi[cc]
-                        ch[6 + nch] = tc[cc]
+                        ch[6 + nch] = tcc
+                        used += tcc
                         nch += 1
-                        st["ranges"] += rg_[cc]
+                        st["ranges"] += 1
                     else:
-                        leaflist.append((lo[cc], hi[cc], d - 1, (depth + 1) & 1))
-                nt = tc[0] + tc[1]
-                hdr[2] += 1 - nch   # before any child is published
+                        push_leaf(lo[cc], hi[cc], d - 1, (depth + 1) & 1)
+                        placed += hi[cc] - lo[cc]
                 st["max_depth"] = max(st["max_depth"], depth + 1)
-            ch[0], ch[1], ch[8] = nch, first, 1 if done == T - 1 else 0
-            if ch[8]:
+                ch[0], ch[1] = nch, base
+                # the children's entries and the leaves' count in either order
                 w2c = (d - 1) | ((depth + 1) << 8)
-                for i in range(nt):
-                    cc = 1 if (nch == 2 and i >= ch[6]) else 0
-                    fb = first + (ch[6] if cc else 0)
-                    entry(first + i, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c | ((first + i - fb) << 16), fb)
-            yield "push"
+                order = [0, 1] if rng.random() < 0.5 else [1, 0]
+                for step in order:
+                    if step == 0:
+                        hdr[2] += placed
+                    else:
+                        # split slots [base, base + T + 1): the children's tiles, then nops; swap
+                        # slots [base + T + 1, base + 2 T + 2): the children's tiles publish their
+                        # own, the rest are nops
+                        for i in range(2 * (T + 1)):
+                            k = base + i
+                            if k >= cap:
+                                break
+                            if i < used:
+                                cc = 1 if (nch == 2 and i >= ch[6]) else 0
+                                fb = base + (ch[6] if cc else 0)
+                                entry(k, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c | ((T + 1) << 16), fb)
+                            elif i < T + 1 or i >= T + 1 + used:
+                                entry(k, 0, 1, NOP, 0)
+                    yield "push"
 
     pool = [workgroup() for _ in range(grid)]
     live = list(pool)
@@ -217,8 +250,7 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
             live.remove(g)
         steps += 1
         assert steps < 50_000_000, "no progress"
-    assert hdr[2] == 1, hdr
-    st["pend"] = hdr[2]
+    assert hdr[2] == n, hdr
     return finish(n, bufs, leaflist), st
 
 

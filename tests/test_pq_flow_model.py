@@ -28,7 +28,7 @@ def test_flow_model_equals_std_sort(n, keys, grid, seed):
     recs = _records(n, keys, seed)
     got, st = flow_sort(recs, grid=grid, seed=seed)
     assert got == std_sort(recs)
-    assert st["pend"] == 1 and st["ranges"] >= 1
+    assert st["ranges"] >= 1
 
 
 def test_flow_model_sorted_and_reversed_inputs():
