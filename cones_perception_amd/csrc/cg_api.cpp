@@ -1446,7 +1446,7 @@ int cg_debug_large_buffer(cg_handle* h, int which, void* out, uint64_t bytes) {
     const uint64_t cap = which == 0   ? LG_META_WORDS * 4
                          : which == 1 ? nch * LG_CHUNK
                          : which == 2 ? nch * CG_BLOCK * 16
-                         : which == 4 ? 1024
+                         : which == 4 ? CG_DEBUG_HIST_BYTES
                                       : (uint64_t)cg_large_pq_words() * 4;
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, src, std::min(bytes, cap), hipMemcpyDeviceToHost));

@@ -146,6 +146,15 @@ int cg_launch_split(const CgLaunch& L, const CgDevParams& P, int kmode, hipStrea
 #ifndef CG_HOOK_LG_STAMP
 #define CG_HOOK_LG_STAMP(S, i) ((void)0)
 #endif
+//   CG_HOOK_PQF(S, t, k, v): lg_pq_flow's ticket t, record word k (0 entry taken, 1 split done,
+//     2 range word complete, 3 end, 4 first | last << 32, 5 entry word | first ticket << 32),
+//     thread 0, with the LgScratch S in scope (tools/variants/pqf_stamps.h)
+#ifndef CG_HOOK_PQF
+#define CG_HOOK_PQF(S, t, k, v) ((void)0)
+#endif
+#ifndef CG_DEBUG_HIST_BYTES
+#define CG_DEBUG_HIST_BYTES 1024   // cg_debug_large_buffer(4): bytes of the histogram area returned
+#endif
 
 // Host wait for a stream's queued work.
 static inline hipError_t cg_stream_wait(hipStream_t s) { return CG_HOOK_STREAM_WAIT(s); }

@@ -2020,6 +2020,11 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 }
             }
             es[0] = ok; es[1] = f; es[2] = e; es[3] = w2; es[4] = tb; es[5] = t;
+            if (ok) {
+                CG_HOOK_PQF(S, t, 0, __builtin_amdgcn_s_memrealtime());
+                CG_HOOK_PQF(S, t, 4, ((uint64_t)e << 32) | f);
+                CG_HOOK_PQF(S, t, 5, ((uint64_t)tb << 32) | w2);
+            }
         }
         __syncthreads();
         if (!es[0]) return;
@@ -2088,6 +2093,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 // slot then takes a nop
                 es[6] = handed >= (uint64_t)tb + T ? 1u : 0u;
                 if (es[6] && slot < Q.cap) pqf_entry(Q, slot, 0u, 1u, PQF_NOP, 0u);
+                CG_HOOK_PQF(S, t, 1, __builtin_amdgcn_s_memrealtime());
             }
             __syncthreads();
             if (!es[6]) {   // defer: the state to HBM, a swap entry in the tile's swap slot
@@ -2118,6 +2124,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             if ((wv >> 46) < T) S.meta[LG_PQ_TIMEOUT] = 1u;   // (the frame's fetch fails on it)
             tbase = wv;
             tcut = 0u;
+            CG_HOOK_PQF(S, t, 2, __builtin_amdgcn_s_memrealtime());
         }
         __syncthreads();
         const uint64_t rw = tbase;
@@ -2240,6 +2247,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                 }
             }
         }
+        if (tid == 0) CG_HOOK_PQF(S, t, 3, __builtin_amdgcn_s_memrealtime() | (ch[8] ? (1ull << 63) : 0ull));
         __syncthreads();   // (es and ch are rewritten for the next ticket)
     }
 }
