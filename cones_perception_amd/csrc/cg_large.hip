@@ -1965,44 +1965,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
 // from the cutter's tile), the children block's base ticket (39-62, from the first tile as it
 // starts), a wait that gave up (63): one add per tile, the last one reads it all
 #define PQF_SD_BASE 39
-// A range of LG_PCL_CUT..LG_PCL_LEAF records as ONE ticket (PQF_TASK): its workgroup loads it
-// into LDS and partitions it there (pcl_block_sort's levels, WMAX = LG_PCL_CUT) down to the
-// leaves a chain of tile-split ranges would have cut, in place of those ranges' dependent
-// cross-workgroup steps (7-8 us each on C5, profiles/r6_pqf_stamps.txt). Its leaves go to the
-// leaf list with their records back in the range's buffer (PqfLeaf); ranges of <= 64 records
-// (one wave, pw_range64) and <= 16 (insertion) are sorted to the outputs here, as in lg_pcl_leaf.
-#ifndef PQF_TASKS
-#define PQF_TASKS 1
-#endif
-#define PQF_TASK (PQF_NOP | PQF_KIND_SWAP)
-struct PqfLeaf {
-    LgScratch S; uint64_t* Eh; uint32_t base, buf;
-    template <class P64, class OUT>
-    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
-        if (m <= PW_MAX) {
-            pw_range64(E, f, m, d, out);
-            return;
-        }
-        const uint32_t l = lane_id();
-        for (uint32_t i = l; i < m; i += 64) Eh[base + f + i] = E[f + i];   // (read by lg_pcl_leaf)
-        if (l == 0) pq_push(S, PQ_LEAFLIST, base + f, base + f + m, d, buf);
-    }
-};
-__device__ __forceinline__ void pqf_lds_task(const LgScratch& S, unsigned char* smem, lds_u32* Rl, uint64_t* E,
-                                             uint32_t f, uint32_t size, uint32_t d, uint32_t buf, uint64_t* kout,
-                                             uint32_t* vout) {
-    lds_u64* const El = (lds_u64*)(uint64_t*)smem;
-    lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * LG_PCL_LEAF);
-    const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4)};
-    for (uint32_t i = threadIdx.x; i < size; i += CG_BLOCK) El[i] = ld64(E + f + i);   // (this launch's swaps)
-    __syncthreads();
-    pcl_block_sort<8, PbLds, PqLeafOut, false, PqfLeaf, LG_PCL_CUT>(El, PqLeafOut{kout, vout, f}, size, d, PS, Rl,
-                                                                     nullptr, PqfLeaf{S, E, f, buf});
-}
-__global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap,
-                                                       uint64_t* kout, uint32_t* vout) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[PQF_TASKS ? LG_PCL_LDS : 16];
-    __shared__ uint32_t red[8 * WAVES];
+__global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0, uint64_t* E1, uint32_t depth_cap) {
     __shared__ uint32_t cg[WAVES], cl[WAVES];
     __shared__ uint64_t tbase;
     __shared__ uint32_t es[8];   // the ticket's entry: ok, f, e, w2, tb, t; then the inline decision
@@ -2040,8 +2003,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                             // (never expected) an entry that does not describe a range of this
                             // index_vector: the frame fails, no index is formed from it
                             if (!(f < e && e <= n && tb < Q.cap &&
-                                  ((w2 & PQF_NOP) ? (!(w2 & PQF_KIND_SWAP) || e - f <= LG_PCL_LEAF)
-                                                  : ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tb) < pqf_tiles(f, e)))) {
+                                  ((w2 & PQF_NOP) || ((w2 & PQF_KIND_SWAP) ? (w2 >> 16) : t - tb) < pqf_tiles(f, e)))) {
                                 S.meta[LG_PQ_TIMEOUT] = 1u;
                                 ok = 0;
                             }
@@ -2067,28 +2029,24 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
         __syncthreads();
         if (!es[0]) return;
         const uint32_t f = es[1], e = es[2], w2 = es[3], tb = es[4], t = es[5];
+        if (w2 & PQF_NOP) continue;   // (uniform) an unused slot of a children block
         const uint32_t d = w2 & 0x3fu, depth = (w2 >> 8) & 0xffu;
-        if ((w2 & PQF_TASK) == PQF_TASK) {   // (uniform) a range partitioned here, in LDS
-            if constexpr (PQF_TASKS) {
-                pqf_lds_task(S, smem, (lds_u32*)red, (depth & 1u) ? E1 : E0, f, e - f, d, depth & 1u, kout, vout);
-                // its records are all in leaves or sorted now (the stores need no order with
-                // this: the launch's end publishes them to lg_pcl_leaf)
-                if (tid == 0)
-                    __hip_atomic_fetch_add(&Q.hdr[PQF_DONE], (uint64_t)(e - f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                CG_HOOK_PQF(S, t, 3, __builtin_amdgcn_s_memrealtime());
-            }
-            continue;   // (pcl_block_sort ended with a barrier: es is read)
-        }
-        if (w2 & PQF_NOP) {   // (uniform) an unused slot of a children block
-            __syncthreads();   // (every thread has read es before it is rewritten)
-            continue;
-        }
         const bool swap_entry = (w2 & PQF_KIND_SWAP) != 0;
         const uint32_t q = swap_entry ? (w2 >> 16) : t - tb;
         const uint32_t off = swap_entry ? 0u : (w2 >> 16);   // a split entry: the range's swap slots at tb + off
         const uint32_t T = pqf_tiles(f, e);
         const uint64_t* const E = (depth & 1u) ? E1 : E0;
         uint64_t* const Eo = (depth & 1u) ? E0 : E1;
+        // the range's first tile reserves the block its children will be queued in as it starts
+        // (off the critical path; the base rides in the range's count word to the tile that ends
+        // the range): T + 1 slots for the children's tiles (they number at most T + 1), then T + 1
+        // for their swap slots
+        if (!swap_entry && q == 0 && tid == 0) {
+            const uint64_t base = 2ull * T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 2ull * ((uint64_t)T + 1ull),
+                                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&Q.sd[tb], min(base, (uint64_t)Q.cap) << PQF_SD_BASE, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
         // the median of three and this element's record in one batch of loads: x > f, and x's
         // virtual record is E[f] when x is the median (__move_median_to_first's swap)
         const uint32_t x = f + 1 + q * PQ_T + tid;
@@ -2131,17 +2089,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             if (tid == 0) {
                 __hip_atomic_fetch_add(&Q.rw[tb], PQ_RW_TILE | ((uint64_t)tg << 23) | tl, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                // the range's first tile reserves the block its children will be queued in, after
-                // its split (off the look-backs' path); the base rides in the range's count word,
-                // added before the tile's own count, to the tile that ends the range: T + 1 slots
-                // for the children's tickets (their tiles number at most T + 1), then T + 1 for
-                // their swap slots
-                if (q == 0) {
-                    const uint64_t base = 2ull * T0 + __hip_atomic_fetch_add(&Q.hdr[PQF_TAIL], 2ull * ((uint64_t)T + 1ull),
-                                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(&Q.sd[tb], min(base, (uint64_t)Q.cap) << PQF_SD_BASE, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                }
                 // the swaps here only when every ticket of the range is held (or done); the swap
                 // slot then takes a nop
                 es[6] = handed >= (uint64_t)tb + T ? 1u : 0u;
@@ -2260,11 +2207,9 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                         const bool rng = hi[cc] - lo[cc] > LG_PCL_CUT && d > 1 && !(depth_cap && depth + 1u >= depth_cap) &&
                                          fits;   // (a block past the capacity: the leaves finish it in HBM)
                         if (rng) {
-                            // (PQF_TASKS) a range that fits LDS: one ticket, partitioned there
-                            const bool task = PQF_TASKS && hi[cc] - lo[cc] <= LG_PCL_LEAF;
-                            ch[2 + 2 * nch] = lo[cc]; ch[3 + 2 * nch] = hi[cc] | (task ? 0x80000000u : 0u);
-                            ch[6 + nch] = task ? 1u : tcc;
-                            used += ch[6 + nch];
+                            ch[2 + 2 * nch] = lo[cc]; ch[3 + 2 * nch] = hi[cc];
+                            ch[6 + nch] = tcc;
+                            used += tcc;
                             nch++;
                         } else {
                             pq_push(S, PQ_LEAFLIST, lo[cc], hi[cc], d - 1u, (depth + 1u) & 1u);
@@ -2286,25 +2231,18 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
         if (ch[8]) {   // (uniform) this workgroup finished the range
             const uint32_t nch = ch[0], base = ch[1];
             const uint32_t used = (nch > 0 ? ch[6] : 0u) + (nch > 1 ? ch[7] : 0u);
-            // split slots [base, base + T + 1): the children's tiles (their swap slots T + 1 on)
-            // or tasks, then nops; swap slots [base + T + 1, base + 2 T + 2): the children's tiles
-            // publish their own, the rest (a task's too) are nops
+            // split slots [base, base + T + 1): the children's tiles (their swap slots T + 1 on),
+            // then nops; swap slots [base + T + 1, base + 2 T + 2): the children's tiles publish
+            // their own, the rest are nops
             const uint32_t w2c = (d - 1u) | ((depth + 1u) << 8) | ((T + 1u) << 16);
             for (uint32_t i = tid; i < 2u * (T + 1u); i += CG_BLOCK) {
                 const uint32_t k = base + i;
                 if (k >= Q.cap) break;
-                const uint32_t j = i < T + 1u ? i : i - (T + 1u);
-                const uint32_t cc = (nch == 2 && j >= ch[6]) ? 1u : 0u;
-                const bool task = j < used && (ch[3 + 2 * cc] >> 31);
-                if (i < T + 1u && j < used) {
-                    const uint32_t hi = ch[3 + 2 * cc] & 0x7fffffffu;
-                    if (task) {
-                        pqf_entry(Q, k, ch[2 + 2 * cc], hi, (w2c & 0xffffu) | PQF_TASK, 0u);
-                    } else {
-                        const uint32_t fb = base + (cc ? ch[6] : 0u);   // the child's first ticket
-                        pqf_entry(Q, k, ch[2 + 2 * cc], hi, w2c, fb);
-                    }
-                } else if (j >= used || task) {
+                if (i < used) {
+                    const uint32_t cc = (nch == 2 && i >= ch[6]) ? 1u : 0u;
+                    const uint32_t fb = base + (cc ? ch[6] : 0u);   // the child's first ticket
+                    pqf_entry(Q, k, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c, fb);
+                } else if (i < T + 1u || i >= T + 1u + used) {
                     pqf_entry(Q, k, 0u, 1u, PQF_NOP, 0u);
                 }
             }
@@ -3441,7 +3379,7 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     // kb[0]; route 5's level cap as a depth cap
     (void)levels;
     hipLaunchKernelGGL(lg_pq_flow, dim3(std::min<uint32_t>(LG_FLOW_GRID, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
-                       S.pcl_levels_cap, kb[0], vb2[0]);
+                       S.pcl_levels_cap);
     hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0, s, S,
                        kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],

@@ -1,17 +1,15 @@
 """Tile-by-tile model of cg_large.hip lg_pq_flow (the device-sized PCL partition as one dataflow
 launch) for tests/test_pq_flow_model.py: the same ticket queue, 16-byte entries (both halves'
 bit layouts), look-back counts, range words, inline / deferred swaps, cut word, the children's
-shared slots (ch[]), the block reserved by a range's first tile after its split, LDS tasks (ranges
-of CUT..LEAF records partitioned by one workgroup: pb_model.block_sort with wmax = CUT), the
-records-in-leaves count that ends the launch and the leaf list, with every array access bounds-checked
+shared slots (ch[]), the `pend` count and the leaf list, with every array access bounds-checked
 (pb_model.Arr). Workgroups are modelled as a pool that takes tickets in order; a random
 scheduler interleaves their steps (split, wait, swap, push) so that ranges of different depths
 run side by side as on the device. The leaves then go through std::sort's restatement with
 their budgets (their in-LDS sort is modelled in pb_model.block_sort). Returns the records and
-the statistics the kernel's design relies on (every ticket served, the count reaching n last)."""
+the statistics the kernel's design relies on (every ticket served, pend never 1 early)."""
 import random
 
-from pb_model import Arr, _lg, _pb_median, block_sort, key, std_sort, wave_sort
+from pb_model import Arr, _lg, _pb_median, key, std_sort
 
 PQ_T = 512
 CUT = 2048            # LG_PCL_CUT
@@ -20,8 +18,6 @@ TILE = 1 << 46        # PQ_RW_TILE
 RW_N = (1 << 23) - 1  # PQ_RW_N
 KIND_SWAP = 1 << 7
 NOP = 1 << 6
-TASK = NOP | KIND_SWAP  # a range of CUT..LEAF records, partitioned by one workgroup in LDS
-PW_MAX = 64
 SD_BASE = 39          # PQF_SD_BASE
 M32 = 0xFFFFFFFF
 
@@ -30,7 +26,7 @@ def tiles(f, e):
     return (e - f - 1 + PQ_T - 1) // PQ_T
 
 
-def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
+def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3):
     rng = random.Random(seed)
     n = len(E_in)
     d0 = 2 * _lg(n)
@@ -38,10 +34,9 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
     for i, r in enumerate(E_in):
         bufs[0][i] = r
     leaflist = []          # pq_push(PQ_LEAFLIST): (first, last, budget, buffer)
-    final = {}             # positions an LDS task sorted to the end (PqLeafOut)
     if n <= CUT:
         leaflist.append((0, n, d0, 0))
-        return finish(n, bufs, leaflist, final), {"tickets": 0}
+        return finish(n, bufs, leaflist), {"tickets": 0}
     T0 = tiles(0, n)
     cap = 2 * (2 * _lg(n) + 2) * (n // PQ_T + n // CUT + 2) + 1024
     ent = Arr(2 * cap)
@@ -54,7 +49,7 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
     recR = Arr(n + 2)
     vst = Arr(n)
     hdr = [0, 0, 0]        # tickets handed out, queued past T0, records in leaves
-    st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0, "nops": 0, "tasks": 0}
+    st = {"tickets": 0, "deferred": 0, "inline": 0, "ranges": 1, "max_depth": 0, "nops": 0}
 
     def entry(k, f, e, w2, tb):
         assert 0 <= k < cap
@@ -84,27 +79,6 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
                         return
                     yield "entry"
             assert f < e <= n, (f, e)
-            if w2 & TASK == TASK:   # pqf_lds_task: partitioned in LDS down to leaves of <= CUT
-                d, depth = w2 & 0x3F, (w2 >> 8) & 0xFF
-                assert CUT < e - f <= LEAF and d >= 1
-                E = bufs[depth & 1]
-                lo, wt = block_sort([E[i] for i in range(f, e)], depth0=d, wmax=CUT, defer=True)
-                for i, r in enumerate(lo):
-                    if r is not None:
-                        assert f + i not in final
-                        final[f + i] = r
-                for (tf, tm, td, trecs) in wt:   # PqfLeaf: one wave each
-                    if tm <= PW_MAX:
-                        for i, r in enumerate(wave_sort(trecs, td)):
-                            final[f + tf + i] = r
-                    else:
-                        for i, r in enumerate(trecs):
-                            E[f + tf + i] = r
-                        push_leaf(f + tf, f + tf + tm, td, depth & 1)
-                hdr[2] += e - f
-                st["tasks"] += 1
-                yield "task"
-                continue
             if w2 & NOP:
                 st["nops"] += 1
                 continue
@@ -114,6 +88,10 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
             off = 0 if swap_entry else w2 >> 16   # split entries: the range's swap slots at tb + off
             T = tiles(f, e)
             assert 0 <= q < T
+            if not swap_entry and q == 0:   # the children block, reserved as the range starts
+                base = 2 * T0 + hdr[1]
+                hdr[1] += 2 * (T + 1)
+                sd[tb] = sd[tb] + (min(base, cap) << SD_BASE)
             E, Eo = bufs[depth & 1], bufs[(depth + 1) & 1]
             a_, b_, c_ = f + 1, f + (e - f) // 2, e - 1
             m = _pb_median(a_, b_, c_, key(E[a_]), key(E[b_]), key(E[c_]))
@@ -149,10 +127,6 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
                         recR[f + 1 + li[i]] = vx[i]
                         rl += 1
                 rw[tb] = rw[tb] + (TILE | (tg << 23) | tl)
-                if q == 0:   # the children block, reserved by the first tile after its split
-                    base = 2 * T0 + hdr[1]
-                    hdr[1] += 2 * (T + 1)
-                    sd[tb] = sd[tb] + (min(base, cap) << SD_BASE)
                 yield "split"
                 inline = handed >= tb + T and rng.random() >= defer_p
                 slot = tb + off + q           # the tile's swap slot
@@ -223,7 +197,7 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
             nch = 0
             if done == T - 1:
                 cw = 0 if tot >> 63 else (tot >> 16) & 0x7FFFFF
-                assert cw and base >= 2 * T0, "the range ends before its block is reserved"
+                assert cw
                 fits = base + 2 * (T + 1) <= cap
                 cut = cw - 1
                 lo, hi = (f, cut), (cut, e)
@@ -232,11 +206,10 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
                     tcc = tiles(lo[cc], hi[cc])
                     r_ = hi[cc] - lo[cc] > CUT and d > 1 and not (depth_cap and depth + 1 >= depth_cap) and fits
                     if r_:
-                        tk_ = tasks and hi[cc] - lo[cc] <= LEAF
                         ch[2 + 2 * nch] = lo[cc]
-                        ch[3 + 2 * nch] = hi[cc] | (1 << 31 if tk_ else 0)
-                        ch[6 + nch] = 1 if tk_ else tcc
-                        used += ch[6 + nch]
+                        ch[3 + 2 * nch] = hi[cc]
+                        ch[6 + nch] = tcc
+                        used += tcc
                         nch += 1
                         st["ranges"] += 1
                     else:
@@ -258,17 +231,11 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
                             k = base + i
                             if k >= cap:
                                 break
-                            j = i if i < T + 1 else i - (T + 1)
-                            cc = 1 if (nch == 2 and j >= ch[6]) else 0
-                            task = j < used and ch[3 + 2 * cc] >> 31
-                            if i < T + 1 and j < used:
+                            if i < used:
+                                cc = 1 if (nch == 2 and i >= ch[6]) else 0
                                 fb = base + (ch[6] if cc else 0)
-                                hi_ = ch[3 + 2 * cc] & 0x7FFFFFFF
-                                if task:
-                                    entry(k, ch[2 + 2 * cc], hi_, w2c & 0xFFFF | TASK, 0)
-                                else:
-                                    entry(k, ch[2 + 2 * cc], hi_, w2c | ((T + 1) << 16), fb)
-                            elif j >= used or task:   # (a task's swap slot: nobody else publishes it)
+                                entry(k, ch[2 + 2 * cc], ch[3 + 2 * cc], w2c | ((T + 1) << 16), fb)
+                            elif i < T + 1 or i >= T + 1 + used:
                                 entry(k, 0, 1, NOP, 0)
                     yield "push"
 
@@ -284,15 +251,13 @@ def flow_sort(E_in, grid=8, seed=0, depth_cap=0, defer_p=0.3, tasks=True):
         steps += 1
         assert steps < 50_000_000, "no progress"
     assert hdr[2] == n, hdr
-    return finish(n, bufs, leaflist, final), st
+    return finish(n, bufs, leaflist), st
 
 
-def finish(n, bufs, leaflist, final):
+def finish(n, bufs, leaflist):
     """Every leaf sorted with its budget from the buffer its depth left it in (lg_pcl_leaf); the
     leaves must tile [0, n) exactly."""
     out = [None] * n
-    for i, r in final.items():
-        out[i] = r
     for (f, e, d, b) in leaflist:
         seg = [bufs[b][i] for i in range(f, e)]
         srt = std_sort(seg, depth0=d)

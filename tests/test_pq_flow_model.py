@@ -1,5 +1,5 @@
 """lg_pq_flow's queue and bookkeeping, modelled tile by tile on the CPU (tests/pqf_model.py):
-entries, look-back, range words, inline and deferred swaps, the children's slots, LDS tasks and
+entries, look-back, range words, inline and deferred swaps, the children's slots, `pend` and
 the leaf list, under random interleavings of the workgroups' steps and small grids (ranges with
 more tiles than workgroups take the deferred path). The result must be libstdc++'s std::sort
 permutation (pb_model.std_sort) and the launch must drain with every ticket served."""
@@ -43,14 +43,3 @@ def test_flow_model_depth_cap_route5():
     recs = _records(30000, 3000, 11)
     got, st = flow_sort(recs, grid=8, seed=11, depth_cap=1)
     assert got == std_sort(recs) and st["ranges"] == 1
-
-
-def test_flow_model_lds_tasks():
-    """Ranges of 2,049-4,096 records go to one workgroup as a task (PQF_TASK), partitioned in LDS
-    down to the leaves (pcl_block_sort, WMAX = LG_PCL_CUT); with tasks off every range is split
-    tile by tile. Both orders are std::sort's."""
-    recs = _records(30000, 4000, 13)
-    got, st = flow_sort(recs, grid=10, seed=13)
-    assert got == std_sort(recs) and st["tasks"] > 0
-    got0, st0 = flow_sort(recs, grid=10, seed=13, tasks=False)
-    assert got0 == got and st0["tasks"] == 0 and st0["ranges"] > st["ranges"] - st["tasks"]
