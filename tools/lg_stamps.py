@@ -30,6 +30,10 @@ print("lg_cluster_tail phases, us (median of %d frames):" % len(rows))
 for i in range(2, 13):
     print(f"  {names[i - 1]:12s} {statistics.median((t[:, i] - t[:, i - 1]) / 100.0):7.2f}")
 print(f"  total        {statistics.median((t[:, 12] - t[:, 1]) / 100.0):7.2f}")
+print("lg_decide_write, workgroup 0 (fold of the front's keys + thresholds, pass 2 + survivor loads + "
+      "look-back + bounds), then to the last arrival's fold end, us:")
+for nm, a0, a1 in (("fold+thr", 0, 13), ("pass2..bounds", 13, 14), ("to last fold end", 14, 15), ("total", 0, 15)):
+    print(f"  {nm:18s} {statistics.median((t[:, a1] - t[:, a0]) / 100.0):7.2f}")
 if (t[:, 64] > t[:, 8]).all():   # the CSR's three parts (stamps 64, 65)
     for nm, a0, a1 in (("csr counts", 8, 64), ("csr starts", 64, 65), ("csr place", 65, 9)):
         print(f"  {nm:12s} {statistics.median((t[:, a1] - t[:, a0]) / 100.0):7.2f}")
