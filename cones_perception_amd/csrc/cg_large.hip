@@ -938,7 +938,8 @@ __device__ void lg_grid_setup(const uint32_t* in, uint32_t* m, const CgDevParams
 #ifndef LG_PCL_CUT
 // the levels cut ranges longer than this; the leaves take up to LG_PCL_LEAF, so a range an
 // uneven last cut leaves between the two still sorts in LDS (4,096 against 2,048 on C5:
-// 271 / 268 us per frame, profiles/r5_c5_cut_ab.txt)
+// 271 / 268 us per frame, profiles/r5_c5_cut_ab.txt; with the flow launch 3,072 / 4,096 /
+// 2,048: 246-247 / 239-240 / 235-237 us, profiles/r6_c5_cut_ab.txt)
 #define LG_PCL_CUT 2048
 #endif
 #define LG_PQ_HDR 8            // [0..2] level list counts, [3] leaf count, [4] [5] level-0 nL / nR,
