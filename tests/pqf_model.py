@@ -1,12 +1,14 @@
 """Tile-by-tile model of cg_large.hip lg_pq_flow (the device-sized PCL partition as one dataflow
 launch) for tests/test_pq_flow_model.py: the same ticket queue, 16-byte entries (both halves'
 bit layouts), look-back counts, range words, inline / deferred swaps, cut word, the children's
-shared slots (ch[]), the `pend` count and the leaf list, with every array access bounds-checked
+shared slots (ch[]), the block reserved by a range's first tile, the records-in-leaves count that
+ends the launch and the leaf list, with every array access bounds-checked
 (pb_model.Arr). Workgroups are modelled as a pool that takes tickets in order; a random
 scheduler interleaves their steps (split, wait, swap, push) so that ranges of different depths
 run side by side as on the device. The leaves then go through std::sort's restatement with
 their budgets (their in-LDS sort is modelled in pb_model.block_sort). Returns the records and
-the statistics the kernel's design relies on (every ticket served, pend never 1 early)."""
+the statistics the kernel's design relies on (every ticket served, the records count reaching n
+only when every record is in a leaf)."""
 import random
 
 from pb_model import Arr, _lg, _pb_median, key, std_sort

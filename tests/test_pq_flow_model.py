@@ -1,7 +1,7 @@
 """lg_pq_flow's queue and bookkeeping, modelled tile by tile on the CPU (tests/pqf_model.py):
-entries, look-back, range words, inline and deferred swaps, the children's slots, `pend` and
-the leaf list, under random interleavings of the workgroups' steps and small grids (ranges with
-more tiles than workgroups take the deferred path). The result must be libstdc++'s std::sort
+entries, look-back, range words, inline and deferred swaps, the children's slots, the
+records-in-leaves count and the leaf list, under random interleavings of the workgroups' steps
+and small grids (ranges with more tiles than workgroups take the deferred path). The result must be libstdc++'s std::sort
 permutation (pb_model.std_sort) and the launch must drain with every ticket served."""
 import random
 
