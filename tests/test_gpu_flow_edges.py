@@ -41,7 +41,7 @@ def _grid_points(order):
 def _one_voxel():
     rng = np.random.default_rng(11)
     x = 3.0 + (0.1 + 0.8 * rng.random(N)) * LEAF
-    y = 0.5 + (0.1 + 0.8 * rng.random(N)) * LEAF
+    y = 0.52 + (0.1 + 0.8 * rng.random(N)) * LEAF
     z = 0.0 + (0.1 + 0.8 * rng.random(N)) * LEAF
     return np.stack([x, y, z, rng.random(N) * 100.0], axis=1).astype(np.float32)
 
@@ -51,7 +51,7 @@ def _three_voxels():
     rng = np.random.default_rng(13)
     v = np.arange(N) % 3
     x = 3.0 + (v * 5 + 0.1 + 0.8 * rng.random(N)) * LEAF
-    y = 0.5 + (0.1 + 0.8 * rng.random(N)) * LEAF
+    y = 0.52 + (0.1 + 0.8 * rng.random(N)) * LEAF
     z = 0.0 + (0.1 + 0.8 * rng.random(N)) * LEAF
     return np.stack([x, y, z, rng.random(N) * 100.0], axis=1).astype(np.float32)
 
