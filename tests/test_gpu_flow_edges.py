@@ -74,3 +74,27 @@ def test_flow_partition_edge_clouds(case):
     ref, _ = O.run(params, msg, O.MODE_DETECT)
     assert ref.n_filtered == N, ref.n_filtered   # every point reaches the voxel stage
     assert_same_detection(got, ref, f"flow edge {case}")
+
+
+@pytest.mark.parametrize("n_keep", [2048, 2049, 2561, 4097, 70_001])
+def test_flow_index_vector_lengths(n_keep):
+    """A 70,001-point cloud (the device-sized path) of which n_keep points reach the voxel stage
+    (the rest lie past distance_treshold_max): index_vectors at and just past one leaf (2,048:
+    no partition at all; 2,049: the smallest range the launch cuts), a few tiles, and nearly the
+    whole cloud. Random voxel keys with duplicates."""
+    params = cp.load_params("simulation")
+    rng = np.random.default_rng(n_keep)
+    n_all = 70_001
+    pts = np.zeros((n_all, 4), np.float32)
+    k = rng.integers(0, max(2, n_keep // 3), n_all)      # ~3 points per voxel
+    pts[:, 0] = 3.0 + ((k % 97) + 0.5) * LEAF
+    pts[:, 1] = -1.0 + (((k // 97) % 41) + 0.5) * LEAF
+    pts[:, 2] = -0.5 + ((k // (97 * 41)) + 0.5) * LEAF
+    pts[:, 3] = rng.random(n_all) * 100.0
+    far = rng.permutation(n_all)[: n_all - n_keep]
+    pts[far, 0] = 20.0                                    # past the 10 m filter
+    msg = cp.PointCloud2.from_xyzi(pts)
+    got = cp.ConeDetector(params).cloud_handler(msg)
+    ref, _ = O.run(params, msg, O.MODE_DETECT)
+    assert ref.n_filtered == n_keep, ref.n_filtered
+    assert_same_detection(got, ref, f"index_vector {n_keep}")
