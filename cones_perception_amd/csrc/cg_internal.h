@@ -225,7 +225,6 @@ struct LgScratch {
     uint64_t* pqf;            //   the dataflow partition's queue (lg_pq_flow): counters, entries,
     uint32_t pqf_cap;         //   look-back, range and count words for pqf_cap tickets
     uint64_t* pqr;            //   the records beside the L and R lists (2 N words)
-    uint64_t* mq;             // lg_pcl_leafmid: the mid ranges' entries as the leaves publish them
     uint32_t force_global;    // diagnostics: global backend even when M fits the LDS path
     uint32_t pcl_levels_cap;  // diagnostics: at most this many PCL partition levels (0: no cap)
     uint32_t force_wait_fail; // diagnostics (cg_debug_route 10): the first partition level reports

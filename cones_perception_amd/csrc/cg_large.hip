@@ -1796,12 +1796,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_level(LgScratch S, const uint6
 #define LG_FLOW_GRID 192
 #endif
 #define LG_CLEAR_FLOW 0x100u   // lg_pcl_leaf's clear_set for lg_pq_flow's words
-#ifndef LG_LEAFMID
-#define LG_LEAFMID 0   // 1: the leaves and their mid ranges in one launch (lg_pcl_leafmid); 0: two launches
-#endif
-#ifndef LG_LEAFMID_GRID
-#define LG_LEAFMID_GRID 512    // lg_pcl_leafmid's workgroups (one resident per CU: 99 KB of LDS)
-#endif
 #define PQF_HDR 48         // u64 words, the counters on lines of their own (they take every
                            // workgroup's atomics and polls): [PQF_TK] tickets handed out,
                            // [PQF_TAIL] tickets queued past range 0's, [PQF_DONE] records in leaves
@@ -1965,169 +1959,6 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pcl_mid(LgScratch S, uint64_t* E0
         pcl_block_sort<1, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS, Rl,
                                                             nullptr, wt);
     }
-}
-// The leaves and their mid ranges in ONE launch (flow mode), in place of lg_pcl_leaf then
-// lg_pcl_mid: a mid range starts as soon as its leaf has cut it, not after the slowest leaf.
-//   - workgroups take the leaves by ticket (counter [9] of lg_arrivals(S, 1)), so every leaf
-//     is held by a running workgroup; a leaf's 65-PQ_MID-record ranges are published (PqfMid):
-//     the wave stores their records sc1, waits vmcnt(0), reserves a slot (S.pq[PQ_MIDS]) and
-//     stores the entry (first | size, budget, buffer << 32, nonzero) sc1 into S.mq;
-//   - a workgroup without a leaf takes mid tickets (counter [10]) and polls its entry (sc1),
-//     then loads the range's records sc1; it leaves when every leaf is done (counter [11],
-//     added after the leaf's slot reservations returned) and no slot at or past its ticket
-//     was reserved;
-//   - waits go only to running workgroups (leaf holders) and are bounded (200 ms, then
-//     LG_PQ_TIMEOUT: the frame fails its fetch);
-//   - the launch's last workgroup (lg_last_arrival) zeroes the entries used, its tickets and
-//     lg_pq_flow's counters for the next frame.
-// (tests/test_leafmid_model.py models the queue under random interleavings.)
-#define LM_LEAF_TK 9
-#define LM_MID_TK 10
-#define LM_LEAVES_DONE 11
-struct PqfMid {
-    uint64_t* Eh; uint64_t* mq; uint32_t* count; uint32_t cap; uint32_t* fail; uint32_t base, buf;
-    template <class P64, class OUT>
-    __device__ __forceinline__ void operator()(P64 E, uint32_t f, uint32_t m, uint32_t d, OUT out) const {
-        if (m <= PW_MAX) {
-            pw_range64(E, f, m, d, out);
-            return;
-        }
-        const uint32_t l = lane_id();
-        for (uint32_t i = l; i < m; i += 64) st64(Eh + base + f + i, E[f + i]);
-        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0): the range's records are stored
-        if (l == 0) {
-            const uint32_t q = atomicAdd(count, 1u);
-            if (q < cap) st64(mq + q, ((uint64_t)(m | (d << 16) | (buf << 24)) << 32) | (base + f));
-            else *fail = 1u;   // (the capacity bounds every frame: never expected)
-        }
-    }
-};
-__global__ __launch_bounds__(CG_BLOCK) void lg_pcl_leafmid(LgScratch S, uint64_t* E0, uint64_t* E1, uint64_t* kout,
-                                                           uint32_t* vout) {
-    __shared__ __attribute__((aligned(16))) unsigned char smem[LG_PCL_LDS];
-    __shared__ uint32_t red[8 * WAVES];
-    __shared__ uint32_t tk, go, last;
-    __shared__ uint64_t ment;
-    const uint32_t tid = threadIdx.x;
-    uint32_t* const ctr = lg_arrivals(S, 1);
-    const uint32_t nleaf = min(S.pq[PQ_LEAFLIST], (uint32_t)LG_PQ_CAP);
-    const uint32_t mcap = S.meta[LG_PCL_N] / 65u + 2u;
-    uint32_t* const fail = S.meta + LG_PQ_TIMEOUT;
-    {   // lg_pq_flow's words of every ticket it handed out (as lg_pcl_leaf's LG_CLEAR_FLOW)
-        const PqfView Q = pqf_view(S);
-        const uint64_t n_ = S.meta[LG_PCL_N];
-        const uint64_t alloc = n_ > LG_PCL_CUT ? 2ull * ((n_ - 1 + PQ_T - 1) / PQ_T) + Q.hdr[PQF_TAIL] : 0ull;
-        const uint32_t used = (uint32_t)min(max(Q.hdr[PQF_TK], alloc), (uint64_t)Q.cap);
-        for (uint32_t i = blockIdx.x * CG_BLOCK + tid; i < used; i += gridDim.x * CG_BLOCK) {
-            Q.ent[2ull * i] = 0ull; Q.ent[2ull * i + 1] = 0ull;
-            Q.lb[i] = 0ull; Q.rw[i] = 0ull; Q.sd[i] = 0ull;
-        }
-    }
-    lds_u64* const El = (lds_u64*)(uint64_t*)smem;
-    lds_u32* const Rl = (lds_u32*)red;
-#if LG_LEAFMID_BLOCKIDX   // (diagnostic: the leaves by block index, as lg_pcl_leaf)
-    for (uint32_t b = blockIdx.x; b < nleaf; b += gridDim.x) {
-#else
-    for (;;) {   // leaves, by ticket
-        if (tid == 0) tk = atomicAdd(&ctr[LM_LEAF_TK], 1u);
-        __syncthreads();
-        // (the ticket and the leaf's words in scalar registers: the branches around the sort's
-        // barriers are then uniform to the compiler, as lg_pcl_leaf's blockIdx loop is)
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
-        if (b >= nleaf) break;   // (uniform)
-#endif
-        const uint32_t* ent = pq_list(S, PQ_LEAFLIST) + PQ_EW * b;
-        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)ent[0]);
-        const uint32_t last_ = (uint32_t)__builtin_amdgcn_readfirstlane((int)ent[1]);
-        const uint32_t depth = (uint32_t)__builtin_amdgcn_readfirstlane((int)ent[2]);
-        const uint32_t ebuf = (uint32_t)__builtin_amdgcn_readfirstlane((int)ent[3]);
-        const uint32_t size = last_ - first;
-        uint64_t* const E = ebuf ? E1 : E0;
-        if (size <= LG_PCL_LEAF) {
-            lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * LG_PCL_LEAF);
-            const PbScratch<PbLds> PS{w0, w0 + (LG_PCL_LEAF + 4), w0 + 2 * (LG_PCL_LEAF + 4), w0 + 3 * (LG_PCL_LEAF + 4)};
-            const PqLeafOut out{kout, vout, first};
-#if LG_LEAFMID == 2   // (diagnostic: the mid ranges to lg_pcl_mid's list, no mid loop)
-            const PqDefer wt{E, S.dsz, S.pq + PQ_MIDS, first, ebuf};
-#define LM_WT PqDefer
-#else
-            const PqfMid wt{E, S.mq, S.pq + PQ_MIDS, mcap, fail, first, ebuf};
-#define LM_WT PqfMid
-#endif
-            for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = E[first + i];
-            __syncthreads();
-            if (size <= CG_BLOCK)
-                pcl_block_sort<1, PbLds, PqLeafOut, false, LM_WT, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else if (size <= 2 * CG_BLOCK)
-                pcl_block_sort<2, PbLds, PqLeafOut, false, LM_WT, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else if (size <= 4 * CG_BLOCK)
-                pcl_block_sort<4, PbLds, PqLeafOut, false, LM_WT, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-            else pcl_block_sort<8, PbLds, PqLeafOut, false, LM_WT, PQ_MID>(El, out, size, depth, PS, Rl, nullptr, wt);
-#undef LM_WT
-        } else {   // the range's own span of the HBM arrays
-            Work W{};
-            W.KEY = (uint64_t*)S.vox + 2ull * first;
-            W.A = S.lab + first; W.PAR = S.par + first; W.CNT = S.cnt + first; W.UK = S.uk + first;
-            W.ORD = S.ord + first; W.LAB = (int32_t*)S.rank + first; W.OFF = S.off + first;
-            pcl_sort<2, false>(W, E + first, size, red, (int)depth);
-            for (uint32_t i = tid; i < size; i += CG_BLOCK) {
-                const uint64_t rr = W.KEY[i];
-                kout[first + i] = rr >> 32;
-                vout[first + i] = (uint32_t)rr;
-            }
-        }
-        __syncthreads();   // (every slot reservation of the leaf has returned)
-        if (tid == 0) atomicAdd(&ctr[LM_LEAVES_DONE], 1u);
-    }
-    for (; LG_LEAFMID != 2;) {   // mid ranges, by ticket, as the leaves publish them
-        if (tid == 0) {
-            const uint32_t m = atomicAdd(&ctr[LM_MID_TK], 1u);
-            uint32_t g = 0;
-            uint64_t en = 0;
-            const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-                if (m >= mcap) break;
-                en = ld64(S.mq + m);
-                if (en >> 32) { g = 1; break; }
-                // (the count is read after the leaves' count: a leaf adds to it only after its
-                // slot reservations returned)
-                if (ld_rlx(&ctr[LM_LEAVES_DONE]) >= nleaf && ld_rlx(S.pq + PQ_MIDS) <= m) break;
-                if (__builtin_amdgcn_s_memrealtime() - t_0 > PQ_WAIT_TICKS) { *fail = 1u; break; }   // (never expected)
-                __builtin_amdgcn_s_sleep(1);
-            }
-            go = g;
-            ment = en;
-        }
-        __syncthreads();
-        if (!__builtin_amdgcn_readfirstlane((int)go)) break;   // (uniform)
-        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ment);
-        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ment >> 32));
-        const uint32_t size = w1 & 0xffffu, depth = (w1 >> 16) & 0xffu, buf = w1 >> 24;
-        uint64_t* const E = buf ? E1 : E0;
-        lds_u32* const w0 = (lds_u32*)(uint32_t*)(smem + 8 * PQ_MID);
-        const PbScratch<PbLds> PS{w0, w0 + (PQ_MID + 4), w0 + 2 * (PQ_MID + 4), w0 + 3 * (PQ_MID + 4)};
-        for (uint32_t i = tid; i < size; i += CG_BLOCK) El[i] = ld64(E + first + i);   // (this launch's sc1 stores)
-        __syncthreads();
-        const PqDefer wt{E, nullptr, nullptr, first, buf};   // (every task here is <= 64 records)
-        if (size > CG_BLOCK)
-            pcl_block_sort<2, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS, Rl,
-                                                                nullptr, wt);
-        else
-            pcl_block_sort<1, PbLds, PqLeafOut, false, PqDefer>(El, PqLeafOut{kout, vout, first}, size, depth, PS, Rl,
-                                                                nullptr, wt);
-        __syncthreads();   // (ment and go are rewritten for the next ticket)
-    }
-    // the last workgroup out resets the entries, the tickets and lg_pq_flow's counters
-    if (tid == 0) {
-        __builtin_amdgcn_s_waitcnt(0x0070);
-        last = lg_last_arrival(ctr) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!__builtin_amdgcn_readfirstlane((int)last)) return;
-    const uint32_t nm = min(ld_rlx(S.pq + PQ_MIDS), mcap);
-    for (uint32_t i = tid; i < nm; i += CG_BLOCK) st64(S.mq + i, 0ull);
-    if (tid == 0) { st_rlx(&ctr[LM_LEAF_TK], 0u); st_rlx(&ctr[LM_MID_TK], 0u); st_rlx(&ctr[LM_LEAVES_DONE], 0u); }
-    if (tid < PQF_HDR && LG_LEAFMID != 2) S.pqf[tid] = 0ull;
 }
 #define PQF_WAIT_TICKS PQ_WAIT_TICKS
 #define PQF_SD_BAD 0xffffffffu   // tcut of a tile whose range wait gave up
@@ -3550,22 +3381,10 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     (void)levels;
     hipLaunchKernelGGL(lg_pq_flow, dim3(std::min<uint32_t>(LG_FLOW_GRID, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
                        S.pcl_levels_cap);
-#if LG_LEAFMID
-    hipLaunchKernelGGL(lg_pcl_leafmid, dim3(std::min<uint32_t>(LG_LEAFMID_GRID, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S,
-                       kb[1], kb[0], kb[0], vb2[0]);
-#if LG_LEAFMID == 2
+    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0, s, S,
+                       kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
                        kb[0], vb2[0], 1u);
-#endif
-#else
-#ifndef LG_LEAF_GRID_MAX
-#define LG_LEAF_GRID_MAX 1024
-#endif
-    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(LG_LEAF_GRID_MAX, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0,
-                       s, S, kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
-    hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
-                       kb[0], vb2[0], 1u);
-#endif
 #else
     // one launch per level (lg_pq_level); a level's tiles
     // number at most tb + its ranges (<= 2^lv), taken by at most 512 workgroups (more when a
@@ -3788,7 +3607,6 @@ uint64_t lg_walk(uint32_t n, F place) {
     place(31, take((2 * (2 + lg_pq_tmax(N)) + 2 * PQ_MAXR + 16) * 8));   // + lg_arrivals' words
     place(32, take(PQF_HDR * 8 + lg_pqf_cap(N) * 40));   // lg_pq_flow: 16 + 8 + 8 + 8 B per ticket
     place(33, take(N * 16));                               // lg_pq_flow: the lists' records
-    place(34, take((N / 65 + 2) * 8));                     // lg_pcl_leafmid: mid range entries
     return off;
 }
 }  // namespace
@@ -3819,7 +3637,6 @@ void cg_large_layout(uint8_t* base, uint32_t n, LgScratch& S) {
             case 31: S.pqst = (uint64_t*)p; S.pq_tmax = (uint32_t)lg_pq_tmax(std::max<uint32_t>(n, 1)); break;
             case 32: S.pqf = (uint64_t*)p; S.pqf_cap = (uint32_t)lg_pqf_cap(std::max<uint32_t>(n, 1)); break;
             case 33: S.pqr = (uint64_t*)p; break;
-            case 34: S.mq = (uint64_t*)p; break;
 
             default: *arr[k - 16] = (uint32_t*)p; break;
         }
