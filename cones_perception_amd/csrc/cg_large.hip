@@ -1302,6 +1302,10 @@ __device__ __forceinline__ uint32_t pq_find(const uint32_t* tp, uint32_t nr, uin
     }
     return lo;
 }
+#ifndef PQ_POLL_SLEEP
+#define PQ_POLL_SLEEP 1   // s_sleep between the partition's polls (look-back, entries, range words); 0 measured
+                          // no faster on C5 (236.1-236.3 against 234.3-236.7 us, profiles/r6_c5_poll_sleep_ab.txt)
+#endif
 // Decoupled look-back over tiles [lo, t) of one range, 64-bit status words: flags in bits
 // 62 / 63, the >= count in bits 32..61, the <= count in bits 0..31 (counts < 2^30).
 #define PQ_ST_A (1ull << 62)
@@ -1331,7 +1335,7 @@ __device__ __forceinline__ uint64_t pq_lookback(uint64_t* ts, uint32_t lo, uint3
                 if (l == 0) *fail = 1u;
                 break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(PQ_POLL_SLEEP);
             continue;
         }
         const uint64_t v = l <= first ? (w & PQ_ST_V) : 0ull;
@@ -2016,7 +2020,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
                             ok = 0;
                             break;
                         }
-                        __builtin_amdgcn_s_sleep(1);
+                        __builtin_amdgcn_s_sleep(PQ_POLL_SLEEP);
                     }
                 }
             }
@@ -2119,7 +2123,7 @@ __global__ __launch_bounds__(CG_BLOCK) void lg_pq_flow(LgScratch S, uint64_t* E0
             uint64_t wv = 0;
             // route 10 (tests) takes the expired path itself on range 0: no wait at all
             while (!(tb == 0 && S.force_wait_fail) && ((wv = ld64(&Q.rw[tb])) >> 46) < T) {
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(PQ_POLL_SLEEP);
                 if (__builtin_amdgcn_s_memrealtime() - t_0 > PQF_WAIT_TICKS) break;   // (never expected)
             }
             if ((wv >> 46) < T) S.meta[LG_PQ_TIMEOUT] = 1u;   // (the frame's fetch fails on it)
