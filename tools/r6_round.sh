@@ -7,7 +7,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
-tag=r6
+tag=${TAG:-r6}
 mkdir -p gpurun_out
 if [ "${1:-A}" = A ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.txt 2>&1 || { tail -20 gpurun_out/${tag}_smoke.txt; exit 1; }
