@@ -3385,8 +3385,11 @@ static int large_backend_dev(const CgLaunch& L, const CgDevParams& P, LgScratch 
     (void)levels;
     hipLaunchKernelGGL(lg_pq_flow, dim3(std::min<uint32_t>(LG_FLOW_GRID, tb + 64)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
                        S.pcl_levels_cap);
-    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(1024, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0, s, S,
-                       kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
+#ifndef LG_LEAF_GRID_MAX
+#define LG_LEAF_GRID_MAX 1024   // (256 / 128: no faster on C5, profiles/r6_c5_leaf_grid_ab.txt)
+#endif
+    hipLaunchKernelGGL(lg_pcl_leaf, dim3(std::min<uint32_t>(LG_LEAF_GRID_MAX, nmax / LG_PCL_CUT * 2 + 2)), dim3(CG_BLOCK), 0,
+                       s, S, kb[1], kb[0], kb[0], vb2[0], LG_CLEAR_FLOW);
     hipLaunchKernelGGL(lg_pcl_mid, dim3(std::min<uint32_t>(2048, nmax / 65 + 1)), dim3(CG_BLOCK), 0, s, S, kb[1], kb[0],
                        kb[0], vb2[0], 1u);
 #else
